@@ -1,0 +1,97 @@
+"""ctypes binding of libclipk.so (the C-ABI in include/clipk.h).
+
+There is no CPU fallback: if the library is missing or the device is not a gfx950
+GPU, every op raises. Build with ``python __graft_entry__.py`` (``build()``) or
+``make -C <pkg>/csrc``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libclipk.so")
+
+F32, F16, BF16 = 0, 1, 2
+EPI_BIAS, EPI_BIAS_RES, EPI_BIAS_QGELU, EPI_DQGELU, EPI_NONE = 0, 1, 2, 3, 4
+PROF_NONE, PROF_GEMM_FC, PROF_GEMM_ALL, PROF_ATTN, PROF_LN = 0, 1, 2, 3, 4
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_long
+_F = ctypes.c_float
+_S = ctypes.c_size_t
+_D = ctypes.c_double
+
+# name -> (restype, argtypes); must match include/clipk.h exactly
+SIGNATURES = {
+    "clipk_version": (ctypes.c_char_p, []),
+    "clipk_strerror": (ctypes.c_char_p, [_I]),
+    "clipk_device_arch_ok": (_I, []),
+    "clipk_gemm": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P, _I, _I, _P]),
+    "clipk_layernorm_fwd": (_I, [_I, _I, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P]),
+    "clipk_layernorm_bwd": (_I, [_I, _I, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P]),
+    "clipk_attention_fwd": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P]),
+    "clipk_attention_bwd": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _I, _P, _P, _I, _P]),
+    "clipk_im2col": (_I, [_I, _I, _I, _I, _I, _P, _P, _P]),
+    "clipk_vit_embed_ln": (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "clipk_prompt_assemble": (_I, [_I, _I, _I, _I, _P, _P, _P, _L, _L, _P, _P, _P, _P]),
+    "clipk_ctx_grad": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "clipk_cosine_logits_fwd": (_I, [_I, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P]),
+    "clipk_cosine_logits_bwd": (_I, [_I, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P]),
+    "clipk_ce_loss": (_I, [_I, _I, _P, _P, _P, _F, _I, _F, _P, _P, _P]),
+    "clipk_meta_net_fwd": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "clipk_meta_net_bwd": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "clipk_sgd_step": (_I, [_L, _P, _P, _P, _F, _F, _F, _I, _P]),
+    "clipk_cast": (_I, [_I, _L, _P, _P, _P]),
+    "clipk_encoder_create": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "clipk_encoder_destroy": (None, [_P]),
+    "clipk_text_saved_bytes": (_S, [_P, _I, _I]),
+    "clipk_text_ws_bytes": (_S, [_P, _I, _I]),
+    "clipk_text_forward": (_I, [_P, _I, _I, _P, _P, _P, _P, _S, _P, _S, _P]),
+    "clipk_text_bwd_ws_bytes": (_S, [_P, _I, _I]),
+    "clipk_text_backward": (_I, [_P, _I, _I, _P, _P, _P, _S, _P, _P, _S, _P]),
+    "clipk_vision_create": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "clipk_vit_ws_bytes": (_S, [_P, _I]),
+    "clipk_vit_forward": (_I, [_P, _I, _P, _P, _P, _S, _P]),
+    "clipk_prof_enable": (_I, [_I]),
+    "clipk_prof_read": (_I, [_P, _P, _P]),
+}
+
+_lib = None
+
+
+class ClipkError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libclipk.so and declare every C-ABI signature (no device calls)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.isfile(LIB_PATH):
+        raise ClipkError(f"{LIB_PATH} is missing: the HIP extension is not built "
+                         f"(run `python __graft_entry__.py` or `make -C csrc`). No CPU fallback exists.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def strerror(rc: int) -> str:
+    return load().clipk_strerror(rc).decode()
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise ClipkError(f"{what} failed: {strerror(rc)} (status {rc})")
+
+
+def call(name: str, *args):
+    rc = getattr(load(), name)(*args)
+    check(rc, name)
+    return rc

@@ -1,0 +1,404 @@
+// Multi-head self-attention core (head dim 64) for CLIP's nn.MultiheadAttention
+// (PromptSRC/clip/model.py:171,181-183): softmax(q k^T / 8 + mask) v with the causal
+// -inf-above-diagonal text mask (model.py:592-598) or no mask (vision).
+//
+// Input is the packed in_proj output row [(s*L+t), 3*W] (q | k | v, head h at columns
+// h*64 of each third), exactly what the QKV GEMM writes, so no reshuffle pass exists.
+//
+// Short sequences (text, L <= 64 after EOT truncation): G = 64/LP (seq, head) pairs per
+// wave, lane = query row; the pair's K/V rows staged once in LDS and read back as
+// 16-B broadcasts; scores for the whole row kept in registers (fully unrolled over LP);
+// exact two-pass softmax. Long sequences (vision, L up to 577): 256 query rows per
+// block, keys streamed through LDS in chunks of 64 with an online softmax.
+// Backward (text): lane = query row for dQ, lane = key row for dK/dV, recomputing
+// P from the saved log-sum-exp; D_i = dO_i . O_i from the saved forward output.
+#include "common.h"
+
+namespace clipk {
+
+constexpr float kScale = 0.125f;  // 1/sqrt(64)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__device__ __forceinline__ void load_row64(const T* p, float* out) {
+  constexpr int V = Vec16<T>::N;
+#pragma unroll
+  for (int c = 0; c < 64 / V; ++c) load16_f32<T>(p + c * V, out + c * V);
+}
+
+template <typename T>
+__device__ __forceinline__ void store_row64(T* p, const float* in) {
+  constexpr int V = Vec16<T>::N;
+#pragma unroll
+  for (int c = 0; c < 64 / V; ++c) store16_f32<T>(p + c * V, in + c * V);
+}
+
+__device__ __forceinline__ float dot64(const float* a, const float* b) {
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+  for (int d = 0; d < 64; d += 4) {
+    s0 = fmaf(a[d], b[d], s0);
+    s1 = fmaf(a[d + 1], b[d + 1], s1);
+    s2 = fmaf(a[d + 2], b[d + 2], s2);
+    s3 = fmaf(a[d + 3], b[d + 3], s3);
+  }
+  return (s0 + s1) + (s2 + s3);
+}
+
+// ------------------------------------------------------------------ forward, L <= LP <= 64
+template <int LP, typename T>
+__global__ __launch_bounds__(256) void attn_fwd_short(int nseq, int L, int H, int causal,
+                                                      const T* __restrict__ qkv, int ldq,
+                                                      T* __restrict__ out, int ldo,
+                                                      float* __restrict__ lse) {
+  constexpr int G = 64 / LP;
+  constexpr int V = Vec16<T>::N;
+  // per wave: G*LP = 64 rows of K then 64 rows of V, 64 elements each
+  __shared__ CLIPK_LDS_ALIGN T sk[4][64 * 64];
+  __shared__ CLIPK_LDS_ALIGN T sv[4][64 * 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = lane / LP, i = lane % LP;
+  const int pair = (blockIdx.x * 4 + w) * G + g;
+  const bool pair_ok = pair < nseq * H;
+  const int s = pair_ok ? pair / H : 0, h = pair_ok ? pair % H : 0;
+  const int W = H * 64;
+  const bool row_ok = pair_ok && i < L;
+  const size_t row = (size_t)s * L + (row_ok ? i : 0);
+  const T* qp = qkv + row * ldq + h * 64;
+
+  // stage own K/V rows
+  T* myk = &sk[w][lane * 64];
+  T* myv = &sv[w][lane * 64];
+  if (row_ok) {
+#pragma unroll
+    for (int c = 0; c < 64 / V; ++c) {
+      *reinterpret_cast<u32x4*>(myk + c * V) =
+          *reinterpret_cast<const u32x4*>(qp + W + c * V);
+      *reinterpret_cast<u32x4*>(myv + c * V) =
+          *reinterpret_cast<const u32x4*>(qp + 2 * W + c * V);
+    }
+  }
+  float q[64];
+  load_row64<T>(qp, q);
+#pragma unroll
+  for (int d = 0; d < 64; ++d) q[d] *= kScale;
+  __syncthreads();
+
+  const T* gk = &sk[w][g * LP * 64];
+  const T* gv = &sv[w][g * LP * 64];
+  float sc[LP];
+  float m = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < LP; ++j) {
+    if (j < L) {
+      float kr[64];
+      load_row64<T>(gk + j * 64, kr);
+      float v = dot64(q, kr);
+      if (causal && j > i) v = -INFINITY;
+      sc[j] = v;
+      m = fmaxf(m, v);
+    } else {
+      sc[j] = -INFINITY;
+    }
+  }
+  float l = 0.f;
+  float o[64];
+#pragma unroll
+  for (int d = 0; d < 64; ++d) o[d] = 0.f;
+#pragma unroll
+  for (int j = 0; j < LP; ++j) {
+    if (j < L) {
+      const float p = __expf(sc[j] - m);
+      l += p;
+      float vr[64];
+      load_row64<T>(gv + j * 64, vr);
+#pragma unroll
+      for (int d = 0; d < 64; ++d) o[d] = fmaf(p, vr[d], o[d]);
+    }
+  }
+  if (row_ok) {
+    const float inv = 1.0f / l;
+#pragma unroll
+    for (int d = 0; d < 64; ++d) o[d] *= inv;
+    store_row64<T>(out + row * ldo + h * 64, o);
+    if (lse) lse[row * H + h] = m + __logf(l);
+  }
+}
+
+// ------------------------------------------------------------------ forward, any L
+template <typename T>
+__global__ __launch_bounds__(256) void attn_fwd_long(int nseq, int L, int H, int causal,
+                                                     const T* __restrict__ qkv, int ldq,
+                                                     T* __restrict__ out, int ldo,
+                                                     float* __restrict__ lse) {
+  __shared__ CLIPK_LDS_ALIGN float sk[64 * 64];
+  __shared__ CLIPK_LDS_ALIGN float sv[64 * 64];
+  const int tid = threadIdx.x;
+  const int i = blockIdx.x * 256 + tid;
+  const int h = blockIdx.y, s = blockIdx.z;
+  const int W = H * 64;
+  const bool row_ok = i < L;
+  const size_t row = (size_t)s * L + (row_ok ? i : 0);
+  float q[64];
+  load_row64<T>(qkv + row * ldq + h * 64, q);
+#pragma unroll
+  for (int d = 0; d < 64; ++d) q[d] *= kScale;
+  float o[64];
+#pragma unroll
+  for (int d = 0; d < 64; ++d) o[d] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const int qmax = min(L, (int)(blockIdx.x + 1) * 256) - 1;
+  const int jend = causal ? qmax + 1 : L;
+  for (int j0 = 0; j0 < jend; j0 += 64) {
+    __syncthreads();
+    // cooperative load of 64 key/value rows (fp32 in LDS): thread -> (row, 16-element quarter)
+    {
+      const int r = tid >> 2, part = tid & 3;
+      const int jr = j0 + r;
+      float tk[16], tv[16];
+      if (jr < L) {
+        const T* base = qkv + ((size_t)s * L + jr) * ldq + h * 64 + part * 16;
+        constexpr int V = Vec16<T>::N;
+#pragma unroll
+        for (int c = 0; c < 16 / V; ++c) {
+          load16_f32<T>(base + W + c * V, tk + c * V);
+          load16_f32<T>(base + 2 * W + c * V, tv + c * V);
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) { tk[c] = 0.f; tv[c] = 0.f; }
+      }
+#pragma unroll
+      for (int c = 0; c < 16; c += 4) {
+        *reinterpret_cast<f32x4*>(&sk[r * 64 + part * 16 + c]) = (f32x4){tk[c], tk[c + 1], tk[c + 2], tk[c + 3]};
+        *reinterpret_cast<f32x4*>(&sv[r * 64 + part * 16 + c]) = (f32x4){tv[c], tv[c + 1], tv[c + 2], tv[c + 3]};
+      }
+    }
+    __syncthreads();
+    float sc[64];
+    float cm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+      const int jj = j0 + j;
+      float v = dot64(q, &sk[j * 64]);
+      if (jj >= L || (causal && jj > i)) v = -INFINITY;
+      sc[j] = v;
+      cm = fmaxf(cm, v);
+    }
+    const float mn = fmaxf(m, cm);
+    if (mn == -INFINITY) continue;  // fully masked chunk for this row
+    const float corr = __expf(m - mn);
+    l *= corr;
+#pragma unroll
+    for (int d = 0; d < 64; ++d) o[d] *= corr;
+    m = mn;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+      const float p = __expf(sc[j] - m);
+      l += p;
+      const float* vr = &sv[j * 64];
+#pragma unroll
+      for (int d = 0; d < 64; ++d) o[d] = fmaf(p, vr[d], o[d]);
+    }
+  }
+  if (row_ok) {
+    const float inv = 1.0f / l;
+#pragma unroll
+    for (int d = 0; d < 64; ++d) o[d] *= inv;
+    store_row64<T>(out + row * ldo + h * 64, o);
+    if (lse) lse[row * H + h] = m + __logf(l);
+  }
+}
+
+// ------------------------------------------------------------------ backward, L <= LP <= 64
+// qkv/out in T (forward dtype), dout/dqkv in TG (grad dtype).
+template <int LP, typename T, typename TG>
+__global__ __launch_bounds__(64) void attn_bwd_short(int nseq, int L, int H, int causal,
+                                                     const T* __restrict__ qkv, int ldq,
+                                                     const T* __restrict__ o_fwd, int ldof,
+                                                     const TG* __restrict__ dout, int lddo,
+                                                     const float* __restrict__ lse,
+                                                     TG* __restrict__ dqkv, int lddq) {
+  constexpr int G = 64 / LP;
+  __shared__ CLIPK_LDS_ALIGN float sq[64 * 64];   // scaled q rows, later reused
+  __shared__ CLIPK_LDS_ALIGN float sk[64 * 64];
+  __shared__ CLIPK_LDS_ALIGN float sv[64 * 64];
+  __shared__ CLIPK_LDS_ALIGN float sdo[64 * 64];
+  __shared__ float slse[64], sD[64];
+  const int lane = threadIdx.x;
+  const int g = lane / LP, i = lane % LP;
+  const int pair = blockIdx.x * G + g;
+  const bool pair_ok = pair < nseq * H;
+  const int s = pair_ok ? pair / H : 0, h = pair_ok ? pair % H : 0;
+  const int W = H * 64;
+  const bool row_ok = pair_ok && i < L;
+  const size_t row = (size_t)s * L + (row_ok ? i : 0);
+
+  float a[64], b[64];
+  // q (scaled) -> LDS, k -> LDS
+  load_row64<T>(qkv + row * ldq + h * 64, a);
+#pragma unroll
+  for (int d = 0; d < 64; ++d) a[d] *= kScale;
+  load_row64<T>(qkv + row * ldq + W + h * 64, b);
+#pragma unroll
+  for (int d = 0; d < 64; d += 4) {
+    *reinterpret_cast<f32x4*>(&sq[lane * 64 + d]) = (f32x4){a[d], a[d + 1], a[d + 2], a[d + 3]};
+    *reinterpret_cast<f32x4*>(&sk[lane * 64 + d]) = (f32x4){b[d], b[d + 1], b[d + 2], b[d + 3]};
+  }
+  // v -> LDS ; dO and D_i = dO_i . O_i
+  load_row64<T>(qkv + row * ldq + 2 * W + h * 64, b);
+#pragma unroll
+  for (int d = 0; d < 64; d += 4)
+    *reinterpret_cast<f32x4*>(&sv[lane * 64 + d]) = (f32x4){b[d], b[d + 1], b[d + 2], b[d + 3]};
+  float dO[64];
+  load_row64<TG>(dout + row * lddo + h * 64, dO);
+  load_row64<T>(o_fwd + row * ldof + h * 64, b);
+  const float Di = dot64(dO, b);
+#pragma unroll
+  for (int d = 0; d < 64; d += 4)
+    *reinterpret_cast<f32x4*>(&sdo[lane * 64 + d]) = (f32x4){dO[d], dO[d + 1], dO[d + 2], dO[d + 3]};
+  const float li = row_ok ? lse[row * H + h] : 0.f;
+  slse[lane] = li;
+  sD[lane] = Di;
+  __syncthreads();
+
+  // ---- phase 1: lane = query row i:  dq_i = sum_j P_ij (dP_ij - D_i) k_j / 8
+  const float* gq = &sq[g * LP * 64];
+  const float* gk = &sk[g * LP * 64];
+  const float* gv = &sv[g * LP * 64];
+  const float* gdo = &sdo[g * LP * 64];
+#pragma unroll
+  for (int d = 0; d < 64; ++d) b[d] = 0.f;  // dq accumulator
+  const float* qi = &sq[lane * 64];
+#pragma unroll
+  for (int j = 0; j < LP; ++j) {
+    if (j < L && !(causal && j > i)) {
+      const float p = __expf(dot64(qi, gk + j * 64) - li);
+      const float dp = dot64(dO, gv + j * 64);
+      const float ds = p * (dp - Di);
+      const float* kr = gk + j * 64;
+#pragma unroll
+      for (int d = 0; d < 64; ++d) b[d] = fmaf(ds, kr[d], b[d]);
+    }
+  }
+  if (row_ok) {
+#pragma unroll
+    for (int d = 0; d < 64; ++d) b[d] *= kScale;
+    store_row64<TG>(dqkv + row * lddq + h * 64, b);
+  }
+
+  // ---- phase 2: lane = key row j:  dv_j = sum_i P_ij dO_i ; dk_j = sum_i dS_ij q_i(scaled)
+  const int j = i;
+  const float* kj = &sk[lane * 64];
+  const float* vj = &sv[lane * 64];
+  float dv[64];
+#pragma unroll
+  for (int d = 0; d < 64; ++d) { dv[d] = 0.f; a[d] = 0.f; }  // a = dk accumulator
+  const float* glse = &slse[g * LP];
+  const float* gD = &sD[g * LP];
+#pragma unroll
+  for (int ii = 0; ii < LP; ++ii) {
+    if (ii < L && !(causal && j > ii)) {
+      const float* qr = gq + ii * 64;
+      const float* dor = gdo + ii * 64;
+      const float p = __expf(dot64(qr, kj) - glse[ii]);
+      const float dp = dot64(dor, vj);
+      const float ds = p * (dp - gD[ii]);
+#pragma unroll
+      for (int d = 0; d < 64; ++d) {
+        dv[d] = fmaf(p, dor[d], dv[d]);
+        a[d] = fmaf(ds, qr[d], a[d]);
+      }
+    }
+  }
+  if (row_ok) {
+    store_row64<TG>(dqkv + row * lddq + W + h * 64, a);
+    store_row64<TG>(dqkv + row * lddq + 2 * W + h * 64, dv);
+  }
+}
+
+template <typename T>
+static int launch_fwd(int nseq, int L, int H, int causal, const void* qkv, int ldq, void* out,
+                      int ldo, float* lse, hipStream_t st) {
+  const int pairs = nseq * H;
+  auto short_launch = [&](auto lp_tag) {
+    constexpr int LP = decltype(lp_tag)::value;
+    constexpr int G = 64 / LP;
+    const int blocks = (pairs + 4 * G - 1) / (4 * G);
+    hipLaunchKernelGGL((attn_fwd_short<LP, T>), dim3(blocks), dim3(256), 0, st, nseq, L, H, causal,
+                       (const T*)qkv, ldq, (T*)out, ldo, lse);
+  };
+  if (L <= 16) short_launch(std::integral_constant<int, 16>{});
+  else if (L <= 32) short_launch(std::integral_constant<int, 32>{});
+  else if (L <= 64) short_launch(std::integral_constant<int, 64>{});
+  else {
+    dim3 grid((L + 255) / 256, H, nseq);
+    hipLaunchKernelGGL((attn_fwd_long<T>), grid, dim3(256), 0, st, nseq, L, H, causal,
+                       (const T*)qkv, ldq, (T*)out, ldo, lse);
+  }
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+template <typename T, typename TG>
+static int launch_bwd(int nseq, int L, int H, int causal, const void* qkv, int ldq,
+                      const void* ofwd, int ldof, const void* dout, int lddo, const float* lse,
+                      void* dqkv, int lddq, hipStream_t st) {
+  const int pairs = nseq * H;
+  auto go = [&](auto lp_tag) {
+    constexpr int LP = decltype(lp_tag)::value;
+    constexpr int G = 64 / LP;
+    const int blocks = (pairs + G - 1) / G;
+    hipLaunchKernelGGL((attn_bwd_short<LP, T, TG>), dim3(blocks), dim3(64), 0, st, nseq, L, H,
+                       causal, (const T*)qkv, ldq, (const T*)ofwd, ldof, (const TG*)dout, lddo, lse,
+                       (TG*)dqkv, lddq);
+  };
+  if (L <= 16) go(std::integral_constant<int, 16>{});
+  else if (L <= 32) go(std::integral_constant<int, 32>{});
+  else if (L <= 64) go(std::integral_constant<int, 64>{});
+  else return CLIPK_ESHAPE;
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+}  // namespace clipk
+
+using namespace clipk;
+
+extern "C" int clipk_attention_fwd(int dtype, int nseq, int L, int heads, int causal,
+                                   const void* qkv, int ldqkv, void* out, int ldo, float* lse,
+                                   void* stream) {
+  if (!qkv || !out) return CLIPK_EINVAL;
+  if (nseq < 0 || L <= 0 || heads <= 0 || ldqkv < 3 * heads * 64 || ldo < heads * 64 || ldqkv % 8 ||
+      ldo % 8)
+    return CLIPK_ESHAPE;
+  if (nseq == 0) return CLIPK_OK;
+  hipStream_t st = (hipStream_t)stream;
+  switch (dtype) {
+    case CLIPK_F16: return launch_fwd<f16>(nseq, L, heads, causal, qkv, ldqkv, out, ldo, lse, st);
+    case CLIPK_BF16: return launch_fwd<bf16>(nseq, L, heads, causal, qkv, ldqkv, out, ldo, lse, st);
+    case CLIPK_F32: return launch_fwd<float>(nseq, L, heads, causal, qkv, ldqkv, out, ldo, lse, st);
+    default: return CLIPK_EDTYPE;
+  }
+}
+
+extern "C" int clipk_attention_bwd(int dtype, int grad_dtype, int nseq, int L, int heads,
+                                    int causal, const void* qkv, int ldqkv, const void* ofwd,
+                                    int ldof, const void* dout, int lddo, const float* lse,
+                                    void* dqkv, int lddqkv, void* stream) {
+  if (!qkv || !ofwd || !dout || !lse || !dqkv) return CLIPK_EINVAL;
+  if (nseq < 0 || L <= 0 || heads <= 0 || ldqkv < 3 * heads * 64 || lddqkv < 3 * heads * 64 ||
+      ldof < heads * 64 || lddo < heads * 64)
+    return CLIPK_ESHAPE;
+  if (L > 64) return CLIPK_ESHAPE;
+  if (nseq == 0) return CLIPK_OK;
+  hipStream_t st = (hipStream_t)stream;
+#define CLIPK_BWD(TT, TGG) \
+  return launch_bwd<TT, TGG>(nseq, L, heads, causal, qkv, ldqkv, ofwd, ldof, dout, lddo, lse, dqkv, lddqkv, st)
+  if (dtype == CLIPK_F16 && grad_dtype == CLIPK_BF16) CLIPK_BWD(f16, bf16);
+  if (dtype == CLIPK_F16 && grad_dtype == CLIPK_F16) CLIPK_BWD(f16, f16);
+  if (dtype == CLIPK_BF16 && grad_dtype == CLIPK_BF16) CLIPK_BWD(bf16, bf16);
+  if (dtype == CLIPK_F32 && grad_dtype == CLIPK_F32) CLIPK_BWD(float, float);
+#undef CLIPK_BWD
+  return CLIPK_EDTYPE;
+}

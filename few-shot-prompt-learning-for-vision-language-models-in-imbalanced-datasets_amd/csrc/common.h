@@ -1,0 +1,136 @@
+// Shared device helpers for the gfx950 (CDNA4) CoOp/CoCoOp kernels.
+// Written for wave64 / MFMA only: no CUDA shims, no dual-platform paths.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/clipk.h"
+
+typedef _Float16 f16;
+typedef __bf16 bf16;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+#define CLIPK_LDS_ALIGN __attribute__((aligned(16)))
+
+namespace clipk {
+
+constexpr int kWave = 64;
+
+template <typename T> struct DT;
+template <> struct DT<float> { static constexpr int id = CLIPK_F32; };
+template <> struct DT<f16>   { static constexpr int id = CLIPK_F16; };
+template <> struct DT<bf16>  { static constexpr int id = CLIPK_BF16; };
+
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(f16 x) { return (float)x; }
+__device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }
+
+template <typename T> __device__ __forceinline__ T from_f32(float x) { return (T)x; }
+
+// 16 bytes of T -> fp32 values (8 for 16-bit types, 4 for fp32).
+template <typename T> struct Vec16 {
+  static constexpr int N = 16 / sizeof(T);
+};
+
+// Load N=16/sizeof(T) elements as fp32 from a 16-byte aligned address.
+template <typename T>
+__device__ __forceinline__ void load16_f32(const T* p, float* out) {
+  if constexpr (sizeof(T) == 4) {
+    f32x4 v = *reinterpret_cast<const f32x4*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = v[i];
+  } else {
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    t8 v = *reinterpret_cast<const t8*>(p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out[i] = (float)v[i];
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void store16_f32(T* p, const float* in) {
+  if constexpr (sizeof(T) == 4) {
+    f32x4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = in[i];
+    *reinterpret_cast<f32x4*>(p) = v;
+  } else {
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    t8 v;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (T)in[i];
+    *reinterpret_cast<t8*>(p) = v;
+  }
+}
+
+// 4 consecutive elements (fp32 in registers) -> memory of type T.
+template <typename T>
+__device__ __forceinline__ void store4(T* p, float a, float b, float c, float d) {
+  if constexpr (sizeof(T) == 4) {
+    f32x4 v = {a, b, c, d};
+    *reinterpret_cast<f32x4*>(p) = v;
+  } else {
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    t4 v = {(T)a, (T)b, (T)c, (T)d};
+    *reinterpret_cast<t4*>(p) = v;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void load4(const T* p, float* o) {
+  if constexpr (sizeof(T) == 4) {
+    f32x4 v = *reinterpret_cast<const f32x4*>(p);
+    o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = v[3];
+  } else {
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    t4 v = *reinterpret_cast<const t4*>(p);
+    o[0] = (float)v[0]; o[1] = (float)v[1]; o[2] = (float)v[2]; o[3] = (float)v[3];
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Reductions inside aligned groups of G lanes (G power of two <= 64).
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = G / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <int G>
+__device__ __forceinline__ float group_max(float v) {
+#pragma unroll
+  for (int o = G / 2; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// QuickGELU (PromptSRC/clip/model.py:162-164): x * sigmoid(1.702 x), and its derivative.
+__device__ __forceinline__ float quick_gelu(float x) {
+  return x / (1.0f + __expf(-1.702f * x));
+}
+__device__ __forceinline__ float quick_gelu_grad(float x) {
+  float s = 1.0f / (1.0f + __expf(-1.702f * x));
+  return s + 1.702f * x * s * (1.0f - s);
+}
+
+}  // namespace clipk
+
+#define CLIPK_CHECK_LAUNCH()                                  \
+  do {                                                        \
+    hipError_t _e = hipGetLastError();                        \
+    if (_e != hipSuccess) return (int)_e;                     \
+  } while (0)

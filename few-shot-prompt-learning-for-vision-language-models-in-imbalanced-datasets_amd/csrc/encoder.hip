@@ -1,0 +1,434 @@
+// Native encoder runtime: the per-layer launch sequences of the CLIP text transformer
+// (forward + input-grad backward) and of the ViT (forward only), behind an opaque
+// handle that holds host-side pointer tables to caller-owned packed weights.
+//
+// Replaces the Python layer loop of Transformer.forward (PromptSRC/clip/model.py:361-367)
+// driven by TextEncoder.forward (trainers/coop.py:195-205) / VisionTransformer.forward
+// (model.py:401-431), and torch autograd's backward through the frozen text encoder.
+// All launches go to the caller's stream; no allocation, no host sync (graph-capturable).
+#include <vector>
+#include <array>
+#include <cstring>
+#include <new>
+
+#include "common.h"
+
+struct clipk_encoder {
+  int kind;  // 0 text, 1 vision
+  int W, layers, heads, E, act, grad;
+  int res, patch, Kp, Limg;
+  std::vector<std::array<const void*, 16>> lw;
+  std::array<const void*, 8> head;
+};
+
+namespace clipk {
+
+static inline size_t esize(int dt) { return dt == CLIPK_F32 ? 4 : 2; }
+static inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+struct Carver {
+  char* base;
+  size_t off = 0;
+  explicit Carver(void* b) : base((char*)b) {}
+  void* take(size_t bytes) {
+    void* p = base ? base + off : nullptr;
+    off += align_up(bytes);
+    return p;
+  }
+};
+
+// ---------------------------------------------------------------- profiling (bench roofline)
+struct ProfState {
+  int kind = CLIPK_PROF_NONE;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  std::vector<double> work;
+  size_t used = 0;
+};
+static ProfState g_prof;
+
+struct ProfScope {
+  bool on = false;
+  hipStream_t st;
+  size_t idx = 0;
+  ProfScope(int cls, hipStream_t s, double work) : st(s) {
+    if (g_prof.kind == CLIPK_PROF_NONE) return;
+    if (!(g_prof.kind == cls || (g_prof.kind == CLIPK_PROF_GEMM_ALL &&
+                                 (cls == CLIPK_PROF_GEMM_FC || cls == CLIPK_PROF_GEMM_ALL))))
+      return;
+    if (g_prof.used == g_prof.ev.size()) {
+      hipEvent_t a, b;
+      if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+      g_prof.ev.push_back({a, b});
+      g_prof.work.push_back(0.0);
+    }
+    idx = g_prof.used++;
+    g_prof.work[idx] = work;
+    on = hipEventRecord(g_prof.ev[idx].first, st) == hipSuccess;
+  }
+  ~ProfScope() {
+    if (on) (void)hipEventRecord(g_prof.ev[idx].second, st);
+  }
+};
+
+#define TRY(x)                 \
+  do {                         \
+    int _rc = (x);             \
+    if (_rc != CLIPK_OK) return _rc; \
+  } while (0)
+
+static int gemm(int in, int out, int epi, int M, int N, int K, const void* A, const void* B,
+                const float* bias, const float* res, void* o, void* o2, const void* aux, int auxdt,
+                hipStream_t st, int prof_cls) {
+  ProfScope ps(prof_cls, st, 2.0 * M * N * K);
+  return clipk_gemm(in, out, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, aux, auxdt, N, st);
+}
+
+// ---------------------------------------------------------------- text layout
+struct TextBufs {
+  // saved (per layer)
+  std::vector<float*> X, Xm, mean1, rstd1, mean2, rstd2, lse;
+  std::vector<void*> qkv, o, h;
+  float* Xf = nullptr;  // final layer output (== X[layers])
+  float *meanf = nullptr, *rstdf = nullptr;
+  // forward temporaries
+  void *xn = nullptr, *g = nullptr, *lnf = nullptr;
+  size_t saved_bytes = 0, ws_bytes = 0;
+};
+
+// save=1: per-layer activations live in `saved`; save=0: buffers are reused across layers
+static TextBufs text_layout(const clipk_encoder* e, int nseq, int L, void* saved, void* ws, bool save) {
+  TextBufs t;
+  const size_t rows = (size_t)nseq * L, W = e->W, H = e->heads, a = esize(e->act);
+  const int nl = e->layers;
+  Carver sv(saved), wk(ws);
+  Carver& S = save ? sv : wk;
+  t.X.resize(nl + 1); t.Xm.resize(nl); t.mean1.resize(nl); t.rstd1.resize(nl);
+  t.mean2.resize(nl); t.rstd2.resize(nl); t.lse.resize(nl); t.qkv.resize(nl); t.o.resize(nl);
+  t.h.resize(nl);
+  if (save) {
+    for (int l = 0; l <= nl; ++l) t.X[l] = (float*)S.take(rows * W * 4);
+    for (int l = 0; l < nl; ++l) {
+      t.Xm[l] = (float*)S.take(rows * W * 4);
+      t.mean1[l] = (float*)S.take(rows * 4); t.rstd1[l] = (float*)S.take(rows * 4);
+      t.mean2[l] = (float*)S.take(rows * 4); t.rstd2[l] = (float*)S.take(rows * 4);
+      t.lse[l] = (float*)S.take(rows * H * 4);
+      t.qkv[l] = S.take(rows * 3 * W * a);
+      t.o[l] = S.take(rows * W * a);
+      t.h[l] = S.take(rows * 4 * W * a);
+    }
+    t.meanf = (float*)S.take((size_t)nseq * 4);
+    t.rstdf = (float*)S.take((size_t)nseq * 4);
+  } else {
+    float* x0 = (float*)wk.take(rows * W * 4);
+    float* x1 = (float*)wk.take(rows * W * 4);
+    float* xm = (float*)wk.take(rows * W * 4);
+    void* q = wk.take(rows * 3 * W * a);
+    void* o = wk.take(rows * W * a);
+    for (int l = 0; l <= nl; ++l) t.X[l] = (l & 1) ? x1 : x0;
+    for (int l = 0; l < nl; ++l) {
+      t.Xm[l] = xm; t.qkv[l] = q; t.o[l] = o; t.h[l] = nullptr;
+      t.mean1[l] = t.rstd1[l] = t.mean2[l] = t.rstd2[l] = nullptr; t.lse[l] = nullptr;
+    }
+  }
+  t.Xf = t.X[nl];
+  t.xn = wk.take(rows * W * a);
+  t.g = wk.take(rows * 4 * W * a);
+  t.lnf = wk.take((size_t)nseq * W * a);
+  t.saved_bytes = save ? sv.off : 0;
+  t.ws_bytes = wk.off;
+  return t;
+}
+
+struct TextBwdBufs {
+  void *dtg, *dX_lp, *dh, *do_, *dqkv;
+  float *dlnf, *dxn;
+  size_t bytes;
+};
+
+static TextBwdBufs text_bwd_layout(const clipk_encoder* e, int nseq, int L, void* ws) {
+  TextBwdBufs b;
+  const size_t rows = (size_t)nseq * L, W = e->W, g = esize(e->grad);
+  Carver c(ws);
+  b.dtg = c.take((size_t)nseq * e->E * g);
+  b.dlnf = (float*)c.take((size_t)nseq * W * 4);
+  b.dX_lp = c.take(rows * W * g);
+  b.dh = c.take(rows * 4 * W * g);
+  b.dxn = (float*)c.take(rows * W * 4);
+  b.do_ = c.take(rows * W * g);
+  b.dqkv = c.take(rows * 3 * W * g);
+  b.bytes = c.off;
+  return b;
+}
+
+// one residual block forward (shared by text and vision)
+static int block_fwd(const clipk_encoder* e, const std::array<const void*, 16>& w, int nseq, int L,
+                     int causal, const float* X, float* Xm, float* Xo, void* xn, void* qkv, void* o,
+                     float* lse, void* h, void* g, float* m1, float* r1, float* m2, float* r2,
+                     hipStream_t st) {
+  const int W = e->W, rows = nseq * L, act = e->act;
+  TRY(clipk_layernorm_fwd(act, rows, W, X, W, nullptr, (const float*)w[0], (const float*)w[1], xn, W,
+                          m1, r1, st));
+  TRY(gemm(act, act, CLIPK_EPI_BIAS, rows, 3 * W, W, xn, w[2], (const float*)w[3], nullptr, qkv,
+           nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
+  {
+    ProfScope ps(CLIPK_PROF_ATTN, st, 0.0);
+    TRY(clipk_attention_fwd(act, nseq, L, e->heads, causal, qkv, 3 * W, o, W, lse, st));
+  }
+  TRY(gemm(act, CLIPK_F32, CLIPK_EPI_BIAS_RES, rows, W, W, o, w[4], (const float*)w[5], X, Xm,
+           nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
+  TRY(clipk_layernorm_fwd(act, rows, W, Xm, W, nullptr, (const float*)w[6], (const float*)w[7], xn, W,
+                          m2, r2, st));
+  TRY(gemm(act, act, CLIPK_EPI_BIAS_QGELU, rows, 4 * W, W, xn, w[8], (const float*)w[9], nullptr, g,
+           h, nullptr, 0, st, CLIPK_PROF_GEMM_FC));
+  TRY(gemm(act, CLIPK_F32, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo,
+           nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
+  return CLIPK_OK;
+}
+
+}  // namespace clipk
+
+using namespace clipk;
+
+extern "C" const char* clipk_version(void) { return "clipk 0.1.0 gfx950"; }
+
+extern "C" const char* clipk_strerror(int status) {
+  switch (status) {
+    case CLIPK_OK: return "ok";
+    case CLIPK_EINVAL: return "invalid argument (null pointer or bad enum)";
+    case CLIPK_ESHAPE: return "shape violates a kernel constraint";
+    case CLIPK_EDTYPE: return "unsupported dtype combination";
+    case CLIPK_EWORKSPACE: return "workspace too small";
+    default: return status > 0 ? hipGetErrorString((hipError_t)status) : "unknown error";
+  }
+}
+
+extern "C" int clipk_device_arch_ok(void) {
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, 0) != hipSuccess) return 0;
+  return std::strncmp(p.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+}
+
+extern "C" int clipk_encoder_create(int width, int layers, int heads, int embed, int act_dtype,
+                                    int grad_dtype, const void* const* layer_ptrs,
+                                    const void* const* head_ptrs, clipk_encoder** out) {
+  if (!layer_ptrs || !head_ptrs || !out) return CLIPK_EINVAL;
+  if (width <= 0 || width % 128 || layers <= 0 || heads * 64 != width || embed % 128 || embed <= 0)
+    return CLIPK_ESHAPE;
+  if (act_dtype < 0 || act_dtype > 2 || grad_dtype < 0 || grad_dtype > 2) return CLIPK_EDTYPE;
+  auto* e = new (std::nothrow) clipk_encoder();
+  if (!e) return CLIPK_EINVAL;
+  e->kind = 0; e->W = width; e->layers = layers; e->heads = heads; e->E = embed;
+  e->act = act_dtype; e->grad = grad_dtype; e->res = e->patch = e->Kp = e->Limg = 0;
+  e->lw.resize(layers);
+  for (int l = 0; l < layers; ++l)
+    for (int i = 0; i < 16; ++i) e->lw[l][i] = layer_ptrs[l * 16 + i];
+  for (int i = 0; i < 4; ++i) e->head[i] = head_ptrs[i];
+  for (int i = 4; i < 8; ++i) e->head[i] = nullptr;
+  *out = e;
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_vision_create(int width, int layers, int heads, int embed, int res, int patch,
+                                   int act_dtype, const void* const* layer_ptrs,
+                                   const void* const* head_ptrs, clipk_encoder** out) {
+  if (!layer_ptrs || !head_ptrs || !out) return CLIPK_EINVAL;
+  if (width <= 0 || width % 128 || layers <= 0 || heads * 64 != width || embed % 128 || patch <= 0 ||
+      res % patch)
+    return CLIPK_ESHAPE;
+  auto* e = new (std::nothrow) clipk_encoder();
+  if (!e) return CLIPK_EINVAL;
+  e->kind = 1; e->W = width; e->layers = layers; e->heads = heads; e->E = embed;
+  e->act = act_dtype; e->grad = act_dtype; e->res = res; e->patch = patch;
+  const int k = 3 * patch * patch;
+  const int kq = act_dtype == CLIPK_F32 ? 32 : 64;
+  e->Kp = (k + kq - 1) / kq * kq;
+  e->Limg = (res / patch) * (res / patch) + 1;
+  e->lw.resize(layers);
+  for (int l = 0; l < layers; ++l)
+    for (int i = 0; i < 16; ++i) e->lw[l][i] = layer_ptrs[l * 16 + i];
+  for (int i = 0; i < 8; ++i) e->head[i] = head_ptrs[i];
+  *out = e;
+  return CLIPK_OK;
+}
+
+extern "C" void clipk_encoder_destroy(clipk_encoder* enc) { delete enc; }
+
+extern "C" size_t clipk_text_saved_bytes(const clipk_encoder* e, int nseq, int L) {
+  if (!e) return 0;
+  return text_layout(e, nseq, L, nullptr, nullptr, true).saved_bytes;
+}
+
+extern "C" size_t clipk_text_ws_bytes(const clipk_encoder* e, int nseq, int L) {
+  if (!e) return 0;
+  TextBufs a = text_layout(e, nseq, L, nullptr, nullptr, true);
+  TextBufs b = text_layout(e, nseq, L, nullptr, nullptr, false);
+  return a.ws_bytes > b.ws_bytes ? a.ws_bytes : b.ws_bytes;
+}
+
+extern "C" int clipk_text_forward(const clipk_encoder* e, int nseq, int L, const float* x0,
+                                  const int* eot_rows, float* txt, void* saved, size_t saved_bytes,
+                                  void* ws, size_t ws_bytes, void* stream) {
+  if (!e || e->kind != 0 || !x0 || !eot_rows || !txt || !ws) return CLIPK_EINVAL;
+  if (nseq <= 0 || L <= 0 || L > 77) return CLIPK_ESHAPE;
+  const bool save = saved != nullptr;
+  TextBufs t = text_layout(e, nseq, L, saved, ws, save);
+  if (ws_bytes < t.ws_bytes || (save && saved_bytes < t.saved_bytes)) return CLIPK_EWORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int W = e->W, rows = nseq * L;
+  // layer-0 input: copy x0 into X[0] when saving (X[0] is needed for LN1 backward)
+  const float* cur = x0;
+  if (save) {
+    if (hipMemcpyAsync(t.X[0], x0, (size_t)rows * W * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
+      return (int)hipGetLastError();
+    cur = t.X[0];
+  }
+  for (int l = 0; l < e->layers; ++l) {
+    float* Xo = t.X[l + 1];
+    if (!save && Xo == cur) Xo = t.X[l];  // ping-pong (cur may be the caller's x0)
+    TRY(block_fwd(e, e->lw[l], nseq, L, 1, cur, t.Xm[l], Xo, t.xn, t.qkv[l], t.o[l], t.lse[l],
+                  save ? t.h[l] : nullptr, t.g, t.mean1[l], t.rstd1[l], t.mean2[l], t.rstd2[l], st));
+    cur = Xo;
+  }
+  // ln_final on the EOT rows only (exact: LayerNorm is per row), then @ text_projection
+  TRY(clipk_layernorm_fwd(e->act, nseq, W, cur, W, eot_rows, (const float*)e->head[0],
+                          (const float*)e->head[1], t.lnf, W, t.meanf, t.rstdf, st));
+  TRY(gemm(e->act, CLIPK_F32, CLIPK_EPI_NONE, nseq, e->E, W, t.lnf, e->head[2], nullptr, nullptr, txt,
+           nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
+  return CLIPK_OK;
+}
+
+extern "C" size_t clipk_text_bwd_ws_bytes(const clipk_encoder* e, int nseq, int L) {
+  if (!e) return 0;
+  return text_bwd_layout(e, nseq, L, nullptr).bytes;
+}
+
+extern "C" int clipk_text_backward(const clipk_encoder* e, int nseq, int L, const int* eot_rows,
+                                   const float* dtxt, const void* saved, size_t saved_bytes, float* dx0,
+                                   void* ws, size_t ws_bytes, void* stream) {
+  if (!e || e->kind != 0 || !eot_rows || !dtxt || !saved || !dx0 || !ws) return CLIPK_EINVAL;
+  if (!e->head[3]) return CLIPK_EINVAL;  // forward-only encoder
+  if (nseq <= 0 || L <= 0 || L > 64) return CLIPK_ESHAPE;
+  TextBufs t = text_layout(e, nseq, L, const_cast<void*>(saved), nullptr, true);
+  TextBwdBufs b = text_bwd_layout(e, nseq, L, ws);
+  if (saved_bytes < t.saved_bytes || ws_bytes < b.bytes) return CLIPK_EWORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int W = e->W, rows = nseq * L, gd = e->grad, act = e->act;
+  float* dX = dx0;
+  // d lnf = dtxt . P^T   (txt = lnf @ P, P = text_projection [W,E])
+  TRY(clipk_cast(gd, (long)nseq * e->E, dtxt, b.dtg, st));
+  TRY(gemm(gd, CLIPK_F32, CLIPK_EPI_NONE, nseq, W, e->E, b.dtg, e->head[3], nullptr, nullptr, b.dlnf,
+           nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
+  if (hipMemsetAsync(dX, 0, (size_t)rows * W * 4, st) != hipSuccess) return (int)hipGetLastError();
+  if (hipMemsetAsync(b.dX_lp, 0, (size_t)rows * W * esize(gd), st) != hipSuccess)
+    return (int)hipGetLastError();
+  TRY(clipk_layernorm_bwd(nseq, W, b.dlnf, W, t.Xf, W, eot_rows, (const float*)e->head[0], t.meanf,
+                          t.rstdf, nullptr, W, dX, b.dX_lp, gd, eot_rows, W, st));
+  for (int l = e->layers - 1; l >= 0; --l) {
+    const auto& w = e->lw[l];
+    if (!w[12] || !w[13] || !w[14] || !w[15]) return CLIPK_EINVAL;
+    // MLP: dg = dX . Wproj ; dh = dg * qgelu'(h)
+    TRY(gemm(gd, gd, CLIPK_EPI_DQGELU, rows, 4 * W, W, b.dX_lp, w[15], nullptr, nullptr, b.dh, nullptr,
+             t.h[l], act, st, CLIPK_PROF_GEMM_ALL));
+    TRY(gemm(gd, CLIPK_F32, CLIPK_EPI_NONE, rows, W, 4 * W, b.dh, w[14], nullptr, nullptr, b.dxn, nullptr,
+             nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
+    TRY(clipk_layernorm_bwd(rows, W, b.dxn, W, t.Xm[l], W, nullptr, (const float*)w[6], t.mean2[l],
+                            t.rstd2[l], dX, W, dX, b.dX_lp, gd, nullptr, W, st));
+    // attention: do = dXm . Wout ; dqkv ; dxn1 = dqkv . Win
+    TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, W, b.dX_lp, w[13], nullptr, nullptr, b.do_, nullptr,
+             nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
+    {
+      ProfScope ps(CLIPK_PROF_ATTN, st, 0.0);
+      TRY(clipk_attention_bwd(act, gd, nseq, L, e->heads, 1, t.qkv[l], 3 * W, t.o[l], W, b.do_, W,
+                              t.lse[l], b.dqkv, 3 * W, st));
+    }
+    TRY(gemm(gd, CLIPK_F32, CLIPK_EPI_NONE, rows, W, 3 * W, b.dqkv, w[12], nullptr, nullptr, b.dxn,
+             nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
+    TRY(clipk_layernorm_bwd(rows, W, b.dxn, W, t.X[l], W, nullptr, (const float*)w[0], t.mean1[l],
+                            t.rstd1[l], dX, W, dX, l > 0 ? b.dX_lp : nullptr, gd, nullptr, W, st));
+  }
+  return CLIPK_OK;
+}
+
+// ---------------------------------------------------------------- vision
+namespace clipk {
+struct VitBufs {
+  void *patches, *xn, *qkv, *o, *g, *cls;
+  float *pout, *x0, *x1, *xm;
+  size_t bytes;
+};
+static VitBufs vit_layout(const clipk_encoder* e, int B, void* ws) {
+  VitBufs v;
+  const size_t a = esize(e->act), D = e->W, L = e->Limg, rows = (size_t)B * L;
+  const size_t np = (size_t)B * (L - 1);
+  Carver c(ws);
+  v.patches = c.take(np * e->Kp * a);
+  v.pout = (float*)c.take(np * D * 4);
+  v.x0 = (float*)c.take(rows * D * 4);
+  v.x1 = (float*)c.take(rows * D * 4);
+  v.xm = (float*)c.take(rows * D * 4);
+  v.xn = c.take(rows * D * a);
+  v.qkv = c.take(rows * 3 * D * a);
+  v.o = c.take(rows * D * a);
+  v.g = c.take(rows * 4 * D * a);
+  v.cls = c.take((size_t)B * D * a);
+  v.bytes = c.off;
+  return v;
+}
+}  // namespace clipk
+
+extern "C" size_t clipk_vit_ws_bytes(const clipk_encoder* e, int B) {
+  if (!e || e->kind != 1) return 0;
+  return vit_layout(e, B, nullptr).bytes;
+}
+
+extern "C" int clipk_vit_forward(const clipk_encoder* e, int B, const float* img, float* feat,
+                                 void* ws, size_t ws_bytes, void* stream) {
+  if (!e || e->kind != 1 || !img || !feat || !ws) return CLIPK_EINVAL;
+  if (B <= 0) return CLIPK_ESHAPE;
+  VitBufs v = vit_layout(e, B, ws);
+  if (ws_bytes < v.bytes) return CLIPK_EWORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int D = e->W, L = e->Limg, np = B * (L - 1), act = e->act;
+  // head: 0 ln_pre_w 1 ln_pre_b 2 ln_post_w 3 ln_post_b 4 projT[E,D] 5 conv_w[D,Kp] 6 cls 7 pos
+  TRY(clipk_im2col(act, B, e->res, e->patch, e->Kp, img, v.patches, st));
+  TRY(gemm(act, CLIPK_F32, CLIPK_EPI_NONE, np, D, e->Kp, v.patches, e->head[5], nullptr, nullptr,
+           v.pout, nullptr, nullptr, 0, st, CLIPK_PROF_NONE));
+  TRY(clipk_vit_embed_ln(B, L, D, v.pout, (const float*)e->head[6], (const float*)e->head[7],
+                         (const float*)e->head[0], (const float*)e->head[1], v.x0, st));
+  float* cur = v.x0;
+  float* nxt = v.x1;
+  for (int l = 0; l < e->layers; ++l) {
+    TRY(block_fwd(e, e->lw[l], B, L, 0, cur, v.xm, nxt, v.xn, v.qkv, v.o, nullptr, nullptr, v.g,
+                  nullptr, nullptr, nullptr, nullptr, st));
+    float* t = cur; cur = nxt; nxt = t;
+  }
+  // ln_post on the CLS rows (row stride L*D), then @ proj
+  TRY(clipk_layernorm_fwd(act, B, D, cur, L * D, nullptr, (const float*)e->head[2],
+                          (const float*)e->head[3], v.cls, D, nullptr, nullptr, st));
+  TRY(gemm(act, CLIPK_F32, CLIPK_EPI_NONE, B, e->E, D, v.cls, e->head[4], nullptr, nullptr, feat,
+           nullptr, nullptr, 0, st, CLIPK_PROF_NONE));
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_prof_enable(int kind) {
+  g_prof.kind = kind;
+  g_prof.used = 0;
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_prof_read(double* total_ms, long* count, double* work) {
+  double tot = 0.0, wsum = 0.0;
+  for (size_t i = 0; i < g_prof.used; ++i) {
+    float ms = 0.f;
+    if (hipEventSynchronize(g_prof.ev[i].second) != hipSuccess) return (int)hipGetLastError();
+    if (hipEventElapsedTime(&ms, g_prof.ev[i].first, g_prof.ev[i].second) != hipSuccess)
+      return (int)hipGetLastError();
+    tot += ms;
+    wsum += g_prof.work[i];
+  }
+  if (total_ms) *total_ms = tot;
+  if (count) *count = (long)g_prof.used;
+  if (work) *work = wsum;
+  g_prof.used = 0;
+  return CLIPK_OK;
+}

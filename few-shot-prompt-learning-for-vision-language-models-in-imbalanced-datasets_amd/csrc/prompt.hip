@@ -1,0 +1,477 @@
+// Small HBM-bound kernels on the CoOp/CoCoOp path: patch extraction, ViT embedding +
+// ln_pre, prompt assembly (+pos) and its ctx gradient, cosine logits fwd/bwd, CE/focal
+// loss fwd+bwd, CoCoOp Meta-Net fwd/bwd, fused SGD, casts. One wave per row throughout,
+// float4 accesses, fixed-order (deterministic) reductions.
+#include "common.h"
+
+namespace clipk {
+
+// ---------------------------------------------------------------- im2col (conv1 as GEMM)
+// model.py:376,402: Conv2d(3, D, kernel=p, stride=p, bias=False)
+template <typename TO>
+__global__ __launch_bounds__(256) void im2col_kernel(int B, int R, int P, int Kp,
+                                                     const float* __restrict__ img,
+                                                     TO* __restrict__ out) {
+  const int G = R / P;
+  const long total = (long)B * G * G * Kp;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int k = (int)(e % Kp);
+    const long patch = e / Kp;
+    float v = 0.f;
+    if (k < 3 * P * P) {
+      const int b = (int)(patch / (G * G)), pi = (int)(patch % (G * G));
+      const int gy = pi / G, gx = pi % G;
+      const int c = k / (P * P), r = k % (P * P), ky = r / P, kx = r % P;
+      v = img[(((long)b * 3 + c) * R + gy * P + ky) * R + gx * P + kx];
+    }
+    out[e] = (TO)v;
+  }
+}
+
+// ---------------------------------------------------------------- ViT embed + ln_pre
+// model.py:405-420: x = cat(cls, patches) + pos; ln_pre(x). One wave per token row.
+__global__ __launch_bounds__(256) void vit_embed_ln_kernel(int B, int L, int D,
+                                                           const float* __restrict__ patch,
+                                                           const float* __restrict__ cls,
+                                                           const float* __restrict__ pos,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           float* __restrict__ x) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= B * L) return;
+  const int b = r / L, t = r % L;
+  const float* src = t == 0 ? cls : patch + ((size_t)b * (L - 1) + t - 1) * D;
+  const float* pp = pos + (size_t)t * D;
+  const int nv = D >> 2;
+  f32x4 v[4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = lane + i * 64;
+    if (c < nv) {
+      v[i] = reinterpret_cast<const f32x4*>(src)[c] + reinterpret_cast<const f32x4*>(pp)[c];
+      s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+    }
+  }
+  const float mu = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = lane + i * 64;
+    if (c < nv)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { const float d = v[i][k] - mu; q += d * d; }
+  }
+  const float rs = rsqrtf(wave_sum(q) / D + 1e-5f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = lane + i * 64;
+    if (c < nv) {
+      const f32x4 gg = reinterpret_cast<const f32x4*>(gamma)[c];
+      const f32x4 bb = reinterpret_cast<const f32x4*>(beta)[c];
+      f32x4 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = (v[i][k] - mu) * rs * gg[k] + bb[k];
+      reinterpret_cast<f32x4*>(x + (size_t)r * D)[c] = o;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- prompt assembly
+// PromptLearner.forward (coop.py:259-296 / cocoop.py:173-198) + TextEncoder pos add
+// (coop.py:197), truncated to L tokens. src_map[c*L+t] >= 0: fixed token-embedding row
+// (prefix / class-name / suffix), < 0: context slot (-1-m).
+__global__ __launch_bounds__(256) void prompt_assemble_kernel(int B, int C, int L, int W,
+                                                              const int* __restrict__ src_map,
+                                                              const float* __restrict__ emb,
+                                                              const float* __restrict__ ctx, long sb,
+                                                              long sc, const float* __restrict__ bias,
+                                                              const float* __restrict__ pos,
+                                                              float* __restrict__ x0) {
+  const int lane = threadIdx.x & 63;
+  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= (long)B * C * L) return;
+  const int t = (int)(r % L);
+  const long s = r / L;
+  const int c = (int)(s % C), b = (int)(s / C);
+  const int m = src_map[c * L + t];
+  const float* src = m >= 0 ? emb + ((size_t)c * 77 + m) * W : ctx + b * sb + c * sc + (size_t)(-1 - m) * W;
+  const bool add_bias = m < 0 && bias != nullptr;
+  const float* bp = bias + (size_t)b * W;
+  const float* pp = pos + (size_t)t * W;
+  float* dst = x0 + r * W;
+  for (int c4 = lane; c4 < W / 4; c4 += 64) {
+    f32x4 v = reinterpret_cast<const f32x4*>(src)[c4] + reinterpret_cast<const f32x4*>(pp)[c4];
+    if (add_bias) v += reinterpret_cast<const f32x4*>(bp)[c4];
+    reinterpret_cast<f32x4*>(dst)[c4] = v;
+  }
+}
+
+// d ctx: out[(b*(csc?C:1) + cc)*n_ctx + k][w] = sum_{c in group} dx0[((b*C+c)*L + ctx_pos[c*n_ctx+k])*W + w]
+__global__ __launch_bounds__(256) void ctx_grad_kernel(int B, int C, int L, int W, int n_ctx, int csc,
+                                                       const int* __restrict__ ctx_pos,
+                                                       const float* __restrict__ dx0,
+                                                       float* __restrict__ dctx) {
+  const int w = blockIdx.y * 256 + threadIdx.x;
+  if (w >= W) return;
+  const int o = blockIdx.x;  // output row
+  const int k = o % n_ctx;
+  const int grp = o / n_ctx;
+  int b, c0, c1;
+  if (csc) { b = grp / C; c0 = grp % C; c1 = c0 + 1; } else { b = grp; c0 = 0; c1 = C; }
+  float acc = 0.f;
+  for (int c = c0; c < c1; ++c) {
+    const int t = ctx_pos[c * n_ctx + k];
+    acc += dx0[(((size_t)b * C + c) * L + t) * W + w];
+  }
+  dctx[(size_t)o * W + w] = acc;
+}
+
+// ---------------------------------------------------------------- cosine logits
+// coop.py:356-363 / cocoop.py:238-251: logits = exp(logit_scale) * (imf/|imf|) . (txt/|txt|)
+__global__ __launch_bounds__(256) void cos_logits_fwd_kernel(int B, int C, int E, int per_image,
+                                                             float scale, const float* __restrict__ imf,
+                                                             const float* __restrict__ txt,
+                                                             float* __restrict__ logits,
+                                                             float* __restrict__ inv_t,
+                                                             float* __restrict__ inv_i) {
+  const int lane = threadIdx.x & 63;
+  const long pidx = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pidx >= (long)B * C) return;
+  const int b = (int)(pidx / C), c = (int)(pidx % C);
+  const long row = per_image ? pidx : c;
+  const float* ip = imf + (size_t)b * E;
+  const float* tp = txt + (size_t)row * E;
+  float d = 0.f, ti = 0.f, ii = 0.f;
+  for (int e = lane; e < E / 4; e += 64) {
+    const f32x4 a = reinterpret_cast<const f32x4*>(ip)[e];
+    const f32x4 t = reinterpret_cast<const f32x4*>(tp)[e];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { d += a[k] * t[k]; ti += t[k] * t[k]; ii += a[k] * a[k]; }
+  }
+  d = wave_sum(d); ti = wave_sum(ti); ii = wave_sum(ii);
+  const float it = rsqrtf(ti), iv = rsqrtf(ii);
+  if (lane == 0) {
+    logits[pidx] = scale * d * it * iv;
+    if (inv_t && (per_image || b == 0)) inv_t[row] = it;
+    if (inv_i && c == 0) inv_i[b] = iv;
+  }
+}
+
+// dtxt[row] = inv_t * (dy - y (y.dy)),  y = txt*inv_t,  dy = scale * sum_b dl[b,c] * imf_b*inv_i[b]
+__global__ __launch_bounds__(256) void cos_logits_bwd_kernel(int B, int C, int E, int per_image,
+                                                             float scale, const float* __restrict__ imf,
+                                                             const float* __restrict__ txt,
+                                                             const float* __restrict__ inv_t,
+                                                             const float* __restrict__ inv_i,
+                                                             const float* __restrict__ dl,
+                                                             float* __restrict__ dtxt) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long nrows = per_image ? (long)B * C : C;
+  if (row >= nrows) return;
+  const int c = (int)(row % C);
+  const int b0 = per_image ? (int)(row / C) : 0, b1 = per_image ? b0 + 1 : B;
+  const float it = inv_t[row];
+  const float* tp = txt + (size_t)row * E;
+  constexpr int MAXE = 16;  // E <= 1024
+  float dy[MAXE], y[MAXE];
+  float yd = 0.f;
+#pragma unroll
+  for (int q = 0; q < MAXE; ++q) { dy[q] = 0.f; y[q] = 0.f; }
+  for (int b = b0; b < b1; ++b) {
+    const float coef = scale * dl[(size_t)b * C + c] * inv_i[b];
+    const float* ip = imf + (size_t)b * E;
+#pragma unroll
+    for (int q = 0; q < MAXE; ++q) {
+      const int e = lane + q * 64;
+      if (e < E) dy[q] += coef * ip[e];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < MAXE; ++q) {
+    const int e = lane + q * 64;
+    if (e < E) { y[q] = tp[e] * it; yd += y[q] * dy[q]; }
+  }
+  yd = wave_sum(yd);
+  float* op = dtxt + (size_t)row * E;
+#pragma unroll
+  for (int q = 0; q < MAXE; ++q) {
+    const int e = lane + q * 64;
+    if (e < E) op[e] = it * (dy[q] - y[q] * yd);
+  }
+}
+
+// ---------------------------------------------------------------- CE / focal loss
+// nn.CrossEntropyLoss (mean) and MultiClassFocalLoss (coop.py:145-163): FL = a_y (1-p)^g ce.
+__global__ __launch_bounds__(64) void ce_loss_kernel(int B, int C, const float* __restrict__ logits,
+                                                     const int64_t* __restrict__ labels,
+                                                     const float* __restrict__ alpha, float gamma,
+                                                     int focal, float grad_scale,
+                                                     float* __restrict__ row_loss,
+                                                     float* __restrict__ dlogits) {
+  const int lane = threadIdx.x;
+  const int b = blockIdx.x;
+  const float* z = logits + (size_t)b * C;
+  const int y = (int)labels[b];
+  float mx = -INFINITY;
+  for (int c = lane; c < C; c += 64) mx = fmaxf(mx, z[c]);
+  mx = wave_max(mx);
+  float se = 0.f;
+  for (int c = lane; c < C; c += 64) se += __expf(z[c] - mx);
+  se = wave_sum(se);
+  const float lse = mx + __logf(se);
+  const float ce = lse - z[y];
+  float wgt = 1.f, loss = ce;
+  if (focal) {
+    const float p = __expf(-ce);
+    const float a = alpha ? alpha[y] : 1.f;
+    const float om = 1.f - p;
+    loss = a * powf(om, gamma) * ce;
+    wgt = a * (powf(om, gamma) + (gamma != 0.f ? gamma * p * powf(om, gamma - 1.f) * ce : 0.f));
+  }
+  if (lane == 0 && row_loss) row_loss[b] = loss;
+  if (dlogits) {
+    for (int c = lane; c < C; c += 64) {
+      const float pc = __expf(z[c] - lse);
+      dlogits[(size_t)b * C + c] = grad_scale * wgt * (pc - (c == y ? 1.f : 0.f));
+    }
+  }
+}
+
+// ---------------------------------------------------------------- Meta-Net (cocoop.py:139-143)
+__global__ __launch_bounds__(256) void meta_net_fwd_kernel(int V, int Hd, int Wd, const float* __restrict__ x,
+                                                           const float* __restrict__ w1,
+                                                           const float* __restrict__ b1,
+                                                           const float* __restrict__ w2,
+                                                           const float* __restrict__ b2,
+                                                           float* __restrict__ h, float* __restrict__ y) {
+  extern __shared__ float sh[];  // Hd floats
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const float* xb = x + (size_t)b * V;
+  for (int k = wv; k < Hd; k += 4) {
+    float a = 0.f;
+    for (int v = lane; v < V; v += 64) a += w1[(size_t)k * V + v] * xb[v];
+    a = wave_sum(a) + b1[k];
+    a = fmaxf(a, 0.f);
+    if (lane == 0) { sh[k] = a; if (h) h[(size_t)b * Hd + k] = a; }
+  }
+  __syncthreads();
+  for (int o = tid; o < Wd; o += 256) {
+    float a = b2[o];
+    for (int k = 0; k < Hd; ++k) a += w2[(size_t)o * Hd + k] * sh[k];
+    y[(size_t)b * Wd + o] = a;
+  }
+}
+
+// one block: dh = (dy W2) * (h > 0); dW2 = dy^T h; db2 = sum dy; dW1 = dh^T x; db1 = sum dh
+__global__ __launch_bounds__(256) void meta_net_bwd_kernel(int B, int V, int Hd, int Wd,
+                                                           const float* __restrict__ x,
+                                                           const float* __restrict__ h,
+                                                           const float* __restrict__ w2,
+                                                           const float* __restrict__ dy,
+                                                           float* __restrict__ dw1, float* __restrict__ db1,
+                                                           float* __restrict__ dw2, float* __restrict__ db2,
+                                                           float* __restrict__ dh) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // dh[b,k]
+  for (int bk = wv; bk < B * Hd; bk += 4) {
+    const int b = bk / Hd, k = bk % Hd;
+    float a = 0.f;
+    for (int o = lane; o < Wd; o += 64) a += dy[(size_t)b * Wd + o] * w2[(size_t)o * Hd + k];
+    a = wave_sum(a);
+    if (lane == 0) dh[bk] = h[bk] > 0.f ? a : 0.f;
+  }
+  // dW2, db2
+  for (int o = tid; o < Wd; o += 256) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += dy[(size_t)b * Wd + o];
+    db2[o] = s;
+    for (int k = 0; k < Hd; ++k) {
+      float a = 0.f;
+      for (int b = 0; b < B; ++b) a += dy[(size_t)b * Wd + o] * h[(size_t)b * Hd + k];
+      dw2[(size_t)o * Hd + k] = a;
+    }
+  }
+  __syncthreads();
+  for (int k = 0; k < Hd; ++k) {
+    if (tid == 0) {
+      float s = 0.f;
+      for (int b = 0; b < B; ++b) s += dh[(size_t)b * Hd + k];
+      db1[k] = s;
+    }
+    for (int v = tid; v < V; v += 256) {
+      float a = 0.f;
+      for (int b = 0; b < B; ++b) a += dh[(size_t)b * Hd + k] * x[(size_t)b * V + v];
+      dw1[(size_t)k * V + v] = a;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- SGD (optimizer.py:105-113)
+__global__ __launch_bounds__(256) void sgd_kernel(long n, float* __restrict__ p, const float* __restrict__ g,
+                                                  float* __restrict__ buf, float lr, float mom, float wd,
+                                                  int has_buf) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float d = g[i] + wd * p[i];
+    const float bb = has_buf ? mom * buf[i] + d : d;
+    buf[i] = bb;
+    p[i] -= lr * bb;
+  }
+}
+
+template <typename TO>
+__global__ __launch_bounds__(256) void cast_kernel(long n, const float* __restrict__ x, TO* __restrict__ y) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) y[i] = (TO)x[i];
+}
+
+static inline int grid_for(long n) {
+  long g = (n + 255) / 256;
+  return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+}  // namespace clipk
+
+using namespace clipk;
+
+extern "C" int clipk_im2col(int out_dtype, int B, int res, int patch, int Kp, const float* img,
+                            void* out, void* stream) {
+  if (!img || !out) return CLIPK_EINVAL;
+  if (B < 0 || patch <= 0 || res % patch || Kp < 3 * patch * patch) return CLIPK_ESHAPE;
+  const long total = (long)B * (res / patch) * (res / patch) * Kp;
+  if (total == 0) return CLIPK_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = grid_for(total);
+  switch (out_dtype) {
+    case CLIPK_F16: hipLaunchKernelGGL(im2col_kernel<f16>, grid, 256, 0, st, B, res, patch, Kp, img, (f16*)out); break;
+    case CLIPK_BF16: hipLaunchKernelGGL(im2col_kernel<bf16>, grid, 256, 0, st, B, res, patch, Kp, img, (bf16*)out); break;
+    case CLIPK_F32: hipLaunchKernelGGL(im2col_kernel<float>, grid, 256, 0, st, B, res, patch, Kp, img, (float*)out); break;
+    default: return CLIPK_EDTYPE;
+  }
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_vit_embed_ln(int B, int L, int width, const float* patch, const float* cls,
+                                  const float* pos, const float* gamma, const float* beta, float* x,
+                                  void* stream) {
+  if (!patch || !cls || !pos || !gamma || !beta || !x) return CLIPK_EINVAL;
+  if (B < 0 || L < 2 || width % 4 || width > 1024) return CLIPK_ESHAPE;
+  if (B == 0) return CLIPK_OK;
+  hipLaunchKernelGGL(vit_embed_ln_kernel, dim3((B * L + 3) / 4), dim3(256), 0, (hipStream_t)stream, B,
+                     L, width, patch, cls, pos, gamma, beta, x);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_prompt_assemble(int B, int C, int L, int W, const int* src_map,
+                                     const float* emb, const float* ctx, long ctx_sb, long ctx_sc,
+                                     const float* bias, const float* pos, float* x0, void* stream) {
+  if (!src_map || !emb || !ctx || !pos || !x0) return CLIPK_EINVAL;
+  if (B < 0 || C < 0 || L <= 0 || L > 77 || W % 4) return CLIPK_ESHAPE;
+  const long rows = (long)B * C * L;
+  if (rows == 0) return CLIPK_OK;
+  hipLaunchKernelGGL(prompt_assemble_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                     B, C, L, W, src_map, emb, ctx, ctx_sb, ctx_sc, bias, pos, x0);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_ctx_grad(int B, int C, int L, int W, int n_ctx, int csc, const int* ctx_pos,
+                              const float* dx0, float* dctx, void* stream) {
+  if (!ctx_pos || !dx0 || !dctx) return CLIPK_EINVAL;
+  if (B <= 0 || C <= 0 || L <= 0 || n_ctx <= 0 || W <= 0) return CLIPK_ESHAPE;
+  const int outs = (csc ? B * C : B) * n_ctx;
+  hipLaunchKernelGGL(ctx_grad_kernel, dim3(outs, (W + 255) / 256), dim3(256), 0, (hipStream_t)stream, B,
+                     C, L, W, n_ctx, csc, ctx_pos, dx0, dctx);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_cosine_logits_fwd(int B, int C, int E, int per_image, float scale,
+                                       const float* imf, const float* txt, float* logits,
+                                       float* inv_tnorm, float* inv_inorm, void* stream) {
+  if (!imf || !txt || !logits) return CLIPK_EINVAL;
+  if (B < 0 || C < 0 || E % 4 || E > 1024) return CLIPK_ESHAPE;
+  const long pairs = (long)B * C;
+  if (pairs == 0) return CLIPK_OK;
+  hipLaunchKernelGGL(cos_logits_fwd_kernel, dim3((pairs + 3) / 4), dim3(256), 0, (hipStream_t)stream, B,
+                     C, E, per_image, scale, imf, txt, logits, inv_tnorm, inv_inorm);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_cosine_logits_bwd(int B, int C, int E, int per_image, float scale,
+                                       const float* imf, const float* txt, const float* inv_tnorm,
+                                       const float* inv_inorm, const float* dlogits, float* dtxt,
+                                       void* stream) {
+  if (!imf || !txt || !inv_tnorm || !inv_inorm || !dlogits || !dtxt) return CLIPK_EINVAL;
+  if (B < 0 || C < 0 || E > 1024) return CLIPK_ESHAPE;
+  const long rows = per_image ? (long)B * C : C;
+  if (rows == 0) return CLIPK_OK;
+  hipLaunchKernelGGL(cos_logits_bwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, B,
+                     C, E, per_image, scale, imf, txt, inv_tnorm, inv_inorm, dlogits, dtxt);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_ce_loss(int B, int C, const float* logits, const int64_t* labels,
+                             const float* alpha, float gamma, int focal, float grad_scale,
+                             float* row_loss, float* dlogits, void* stream) {
+  if (!logits || !labels) return CLIPK_EINVAL;
+  if (B < 0 || C <= 0) return CLIPK_ESHAPE;
+  if (B == 0) return CLIPK_OK;
+  hipLaunchKernelGGL(ce_loss_kernel, dim3(B), dim3(64), 0, (hipStream_t)stream, B, C, logits, labels,
+                     alpha, gamma, focal, grad_scale, row_loss, dlogits);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_meta_net_fwd(int B, int V, int Hd, int Wd, const float* x, const float* w1,
+                                  const float* b1, const float* w2, const float* b2, float* h,
+                                  float* y, void* stream) {
+  if (!x || !w1 || !b1 || !w2 || !b2 || !y) return CLIPK_EINVAL;
+  if (B < 0 || V <= 0 || Hd <= 0 || Wd <= 0) return CLIPK_ESHAPE;
+  if (B == 0) return CLIPK_OK;
+  hipLaunchKernelGGL(meta_net_fwd_kernel, dim3(B), dim3(256), Hd * sizeof(float), (hipStream_t)stream,
+                     V, Hd, Wd, x, w1, b1, w2, b2, h, y);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_meta_net_bwd(int B, int V, int Hd, int Wd, const float* x, const float* h,
+                                  const float* w2, const float* dy, float* dw1, float* db1,
+                                  float* dw2, float* db2, float* dh_ws, void* stream) {
+  if (!x || !h || !w2 || !dy || !dw1 || !db1 || !dw2 || !db2 || !dh_ws) return CLIPK_EINVAL;
+  if (B <= 0 || V <= 0 || Hd <= 0 || Wd <= 0) return CLIPK_ESHAPE;
+  hipLaunchKernelGGL(meta_net_bwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, V, Hd, Wd, x,
+                     h, w2, dy, dw1, db1, dw2, db2, dh_ws);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_sgd_step(long n, float* p, const float* g, float* buf, float lr,
+                              float momentum, float weight_decay, int has_buf, void* stream) {
+  if (!p || !g || !buf) return CLIPK_EINVAL;
+  if (n < 0) return CLIPK_ESHAPE;
+  if (n == 0) return CLIPK_OK;
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, buf, lr,
+                     momentum, weight_decay, has_buf);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_cast(int out_dtype, long n, const float* x, void* y, void* stream) {
+  if (!x || !y) return CLIPK_EINVAL;
+  if (n <= 0) return n == 0 ? CLIPK_OK : CLIPK_ESHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  switch (out_dtype) {
+    case CLIPK_F16: hipLaunchKernelGGL(cast_kernel<f16>, grid_for(n), 256, 0, st, n, x, (f16*)y); break;
+    case CLIPK_BF16: hipLaunchKernelGGL(cast_kernel<bf16>, grid_for(n), 256, 0, st, n, x, (bf16*)y); break;
+    case CLIPK_F32: hipLaunchKernelGGL(cast_kernel<float>, grid_for(n), 256, 0, st, n, x, (float*)y); break;
+    default: return CLIPK_EDTYPE;
+  }
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}

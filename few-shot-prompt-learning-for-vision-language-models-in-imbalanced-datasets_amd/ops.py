@@ -1,0 +1,187 @@
+"""Tensor-level wrappers over the C-ABI: torch tensors in, device pointers + the
+current HIP stream out. torch is plumbing here (allocation, streams); every op's
+arithmetic runs in libclipk.so. Inputs are validated on the host and errors map to
+``ClipkError`` (RuntimeError) naming the op and status, mirroring the reference's
+Python exceptions at module level.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _native as N
+
+DT = {torch.float32: N.F32, torch.float16: N.F16, torch.bfloat16: N.BF16}
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _need(t, name, dtype=None, cuda=True):
+    if t is None:
+        raise N.ClipkError(f"{name} is required")
+    if cuda and not t.is_cuda:
+        raise N.ClipkError(f"{name} must be a CUDA(HIP) tensor; no CPU path exists")
+    if dtype is not None and t.dtype != dtype:
+        raise N.ClipkError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise N.ClipkError(f"{name} must be contiguous")
+    return t
+
+
+def gemm(a, b, epi=N.EPI_NONE, out_dtype=torch.float32, bias=None, res=None, aux=None,
+         want_out2=False, out=None):
+    """out[M,N] = epi(a[M,K] @ b[N,K]^T); returns out (and out2 for EPI_BIAS_QGELU)."""
+    _need(a, "A")
+    _need(b, "B", a.dtype)
+    M, K = a.shape
+    Nn = b.shape[0]
+    if b.shape[1] != K:
+        raise N.ClipkError(f"gemm K mismatch {tuple(a.shape)} x {tuple(b.shape)}^T")
+    if out is None:
+        out = torch.empty(M, Nn, device=a.device, dtype=out_dtype)
+    out2 = torch.empty_like(out) if want_out2 else None
+    if bias is not None:
+        _need(bias, "bias", torch.float32)
+    if res is not None:
+        _need(res, "res", torch.float32)
+    if aux is not None:
+        _need(aux, "aux")
+    N.call("clipk_gemm", DT[a.dtype], DT[out.dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias),
+           _p(res), Nn, _p(out), Nn, _p(out2), _p(aux), DT[aux.dtype] if aux is not None else 0, Nn,
+           _stream())
+    return (out, out2) if want_out2 else out
+
+
+def layernorm(x, w, b, out_dtype=torch.float32, rows=None, stats=False):
+    """LayerNorm over the last dim of fp32 x [R, W] (optionally on gathered rows)."""
+    _need(x, "x", torch.float32)
+    R, W = x.shape
+    n = R if rows is None else rows.numel()
+    out = torch.empty(n, W, device=x.device, dtype=out_dtype)
+    mean = torch.empty(n, device=x.device) if stats else None
+    rstd = torch.empty(n, device=x.device) if stats else None
+    if rows is not None:
+        _need(rows, "rows", torch.int32)
+    N.call("clipk_layernorm_fwd", DT[out_dtype], n, W, _p(x), W, _p(rows), _p(w), _p(b), _p(out), W,
+           _p(mean), _p(rstd), _stream())
+    return (out, mean, rstd) if stats else out
+
+
+def layernorm_bwd(dy, x, w, mean, rstd, dres=None, lp_dtype=None):
+    _need(dy, "dy", torch.float32)
+    R, W = dy.shape
+    dx = torch.empty_like(dy)
+    lp = torch.empty(R, W, device=dy.device, dtype=lp_dtype) if lp_dtype is not None else None
+    N.call("clipk_layernorm_bwd", R, W, _p(dy), W, _p(x), W, None, _p(w), _p(mean), _p(rstd),
+           _p(dres), W, _p(dx), _p(lp), DT[lp_dtype] if lp_dtype is not None else 0, None, W, _stream())
+    return (dx, lp) if lp is not None else dx
+
+
+def attention(qkv, nseq, L, heads, causal, lse=False):
+    _need(qkv, "qkv")
+    W = heads * 64
+    out = torch.empty(nseq * L, W, device=qkv.device, dtype=qkv.dtype)
+    l = torch.empty(nseq * L, heads, device=qkv.device) if lse else None
+    N.call("clipk_attention_fwd", DT[qkv.dtype], nseq, L, heads, int(causal), _p(qkv), 3 * W, _p(out),
+           W, _p(l), _stream())
+    return (out, l) if lse else out
+
+
+def attention_bwd(qkv, o, dout, lse, nseq, L, heads, causal, grad_dtype):
+    W = heads * 64
+    dqkv = torch.empty(nseq * L, 3 * W, device=qkv.device, dtype=grad_dtype)
+    N.call("clipk_attention_bwd", DT[qkv.dtype], DT[grad_dtype], nseq, L, heads, int(causal), _p(qkv),
+           3 * W, _p(o), W, _p(dout), W, _p(lse), _p(dqkv), 3 * W, _stream())
+    return dqkv
+
+
+def im2col(img, patch, Kp, out_dtype):
+    _need(img, "image", torch.float32)
+    B, _, R, _ = img.shape
+    G = R // patch
+    out = torch.empty(B * G * G, Kp, device=img.device, dtype=out_dtype)
+    N.call("clipk_im2col", DT[out_dtype], B, R, patch, Kp, _p(img), _p(out), _stream())
+    return out
+
+
+def prompt_assemble(B, C, L, src_map, emb, ctx, ctx_sb, ctx_sc, bias, pos):
+    W = emb.shape[-1]
+    x0 = torch.empty(B * C * L, W, device=emb.device, dtype=torch.float32)
+    N.call("clipk_prompt_assemble", B, C, L, W, _p(src_map), _p(emb), _p(ctx), ctx_sb, ctx_sc, _p(bias),
+           _p(pos), _p(x0), _stream())
+    return x0
+
+
+def ctx_grad(B, C, L, W, n_ctx, csc, ctx_pos, dx0):
+    outs = (B * C if csc else B) * n_ctx
+    d = torch.empty(outs, W, device=dx0.device, dtype=torch.float32)
+    N.call("clipk_ctx_grad", B, C, L, W, n_ctx, int(csc), _p(ctx_pos), _p(dx0), _p(d), _stream())
+    return d
+
+
+def cosine_logits(imf, txt, scale, per_image, C):
+    B, E = imf.shape
+    logits = torch.empty(B, C, device=imf.device)
+    inv_t = torch.empty(txt.shape[0], device=imf.device)
+    inv_i = torch.empty(B, device=imf.device)
+    N.call("clipk_cosine_logits_fwd", B, C, E, int(per_image), float(scale), _p(imf), _p(txt),
+           _p(logits), _p(inv_t), _p(inv_i), _stream())
+    return logits, inv_t, inv_i
+
+
+def cosine_logits_bwd(imf, txt, inv_t, inv_i, dlogits, scale, per_image):
+    B, C = dlogits.shape
+    E = imf.shape[1]
+    dtxt = torch.empty_like(txt)
+    N.call("clipk_cosine_logits_bwd", B, C, E, int(per_image), float(scale), _p(imf), _p(txt),
+           _p(inv_t), _p(inv_i), _p(dlogits.contiguous()), _p(dtxt), _stream())
+    return dtxt
+
+
+def ce_loss(logits, labels, alpha=None, gamma=2.0, focal=False, grad=True):
+    B, C = logits.shape
+    row = torch.empty(B, device=logits.device)
+    dl = torch.empty_like(logits) if grad else None
+    N.call("clipk_ce_loss", B, C, _p(logits), _p(labels), _p(alpha), float(gamma), int(focal),
+           1.0 / B, _p(row), _p(dl), _stream())
+    return row, dl
+
+
+def meta_net(x, w1, b1, w2, b2):
+    B, V = x.shape
+    Hd, Wd = w1.shape[0], w2.shape[0]
+    h = torch.empty(B, Hd, device=x.device)
+    y = torch.empty(B, Wd, device=x.device)
+    N.call("clipk_meta_net_fwd", B, V, Hd, Wd, _p(x), _p(w1), _p(b1), _p(w2), _p(b2), _p(h), _p(y),
+           _stream())
+    return h, y
+
+
+def meta_net_bwd(x, h, w2, dy, V, Hd, Wd):
+    B = x.shape[0]
+    dw1 = torch.empty(Hd, V, device=x.device)
+    db1 = torch.empty(Hd, device=x.device)
+    dw2 = torch.empty(Wd, Hd, device=x.device)
+    db2 = torch.empty(Wd, device=x.device)
+    dh = torch.empty(B, Hd, device=x.device)
+    N.call("clipk_meta_net_bwd", B, V, Hd, Wd, _p(x), _p(h), _p(w2), _p(dy.contiguous()), _p(dw1),
+           _p(db1), _p(dw2), _p(db2), _p(dh), _stream())
+    return dw1, db1, dw2, db2
+
+
+def sgd_step(p, g, buf, lr, momentum, weight_decay, has_buf):
+    N.call("clipk_sgd_step", p.numel(), _p(p), _p(g), _p(buf), float(lr), float(momentum),
+           float(weight_decay), int(has_buf), _stream())
+
+
+def cast(x, dtype):
+    y = torch.empty(x.shape, device=x.device, dtype=dtype)
+    N.call("clipk_cast", DT[dtype], x.numel(), _p(x.contiguous()), _p(y), _stream())
+    return y

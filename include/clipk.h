@@ -1,0 +1,203 @@
+/*
+ * clipk.h — C-ABI of the MI355X-native CoOp/CoCoOp hot path (libclipk.so).
+ *
+ * Plain pointers + sizes + a hipStream_t (passed as void*); no torch types.
+ * Every device pointer is owned by the caller (the torch caching allocator in
+ * the Python host). Kernels never allocate. Encoder handles hold only HOST-side
+ * pointer tables to caller-owned, packed, frozen weights.
+ *
+ * Return value: CLIPK_OK (0); a negative CLIPK_E* for bad arguments (checked on
+ * the host BEFORE any launch); a positive hipError_t from a failed launch.
+ *
+ * Reference interfaces replaced (PyTorch ops inside the reference hot path):
+ *   clipk_gemm            nn.Linear / MHA in_proj,out_proj / mlp.c_fc,c_proj / @proj
+ *                         (PromptSRC/clip/model.py:171-177, 429; trainers/coop.py:204)
+ *   clipk_layernorm_*     LayerNorm (model.py:153-159) fwd / input-grad bwd
+ *   clipk_attention_*     nn.MultiheadAttention SDPA core (model.py:181-183, mask 592-598)
+ *   clipk_im2col          VisionTransformer.conv1 patch embed as GEMM (model.py:376,402)
+ *   clipk_vit_embed_ln    cls cat + pos add + ln_pre (model.py:405-420)
+ *   clipk_prompt_assemble PromptLearner.forward cat + TextEncoder pos add
+ *                         (trainers/coop.py:259-296, cocoop.py:173-198, coop.py:197)
+ *   clipk_ctx_grad        autograd of that cat w.r.t. ctx (coop.py:265, cocoop.py:186-194)
+ *   clipk_cosine_logits_* CustomCLIP normalize + logit_scale.exp() * imf @ txt^T
+ *                         (coop.py:356-363, cocoop.py:238-251)
+ *   clipk_ce_loss         nn.CrossEntropyLoss / MultiClassFocalLoss fwd+bwd
+ *                         (coop.py:131-163,324; cocoop.py:66-101,233)
+ *   clipk_meta_net_*      CoCoOp Meta-Net Linear-ReLU-Linear (cocoop.py:139-143,182-185)
+ *   clipk_sgd_step        torch.optim.SGD momentum/wd step (dassl optim/optimizer.py:105-113)
+ *   clipk_text_*          TextEncoder.forward + its input-grad backward (coop.py:195-205)
+ *   clipk_vit_forward     VisionTransformer.forward (model.py:401-431), frozen, fwd only
+ */
+#ifndef CLIPK_H
+#define CLIPK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* element types */
+enum { CLIPK_F32 = 0, CLIPK_F16 = 1, CLIPK_BF16 = 2 };
+
+/* status codes (hipError_t values > 0 pass through) */
+enum {
+  CLIPK_OK = 0,
+  CLIPK_EINVAL = -1,     /* null pointer / bad enum */
+  CLIPK_ESHAPE = -2,     /* shape violates a kernel constraint */
+  CLIPK_EDTYPE = -3,     /* unsupported dtype combination */
+  CLIPK_EWORKSPACE = -4  /* workspace too small */
+};
+
+/* GEMM epilogues:  acc = A[M,K] . B[N,K]^T  (fp32 accumulate)                         */
+enum {
+  CLIPK_EPI_BIAS = 0,       /* out(out_dtype) = acc + bias                                */
+  CLIPK_EPI_BIAS_RES = 1,   /* out(f32)       = acc + bias + res(f32)                     */
+  CLIPK_EPI_BIAS_QGELU = 2, /* out = quickgelu(acc + bias); out2 (optional) = acc + bias */
+  CLIPK_EPI_DQGELU = 3,     /* out = acc * quickgelu'(aux)                                */
+  CLIPK_EPI_NONE = 4        /* out = acc                                                  */
+};
+
+const char* clipk_version(void);
+const char* clipk_strerror(int status);
+int clipk_device_arch_ok(void); /* 1 if device 0 is gfx950 */
+
+/* ---------------------------------------------------------------- primitives */
+/* Constraints: N % 128 == 0, K % 64 == 0 (16-bit) or K % 32 == 0 (f32); lda,ldb,ldo
+ * multiples of 8 elements; A/B of in_dtype; bias/res fp32; aux of aux_dtype. */
+int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, int K,
+               const void* A, int lda, const void* B, int ldb,
+               const float* bias, const float* res, int ldr,
+               void* out, int ldo, void* out2, const void* aux, int aux_dtype, int ldaux,
+               void* stream);
+
+/* y = LN(x[row]) for rows r in [0,rows): x row = in_rows ? in_rows[r] : r.
+ * out of out_dtype with row stride ldo; mean/rstd (optional, fp32 [rows]). width%64==0, <=1024 */
+int clipk_layernorm_fwd(int out_dtype, int rows, int width, const float* x, int ldx,
+                        const int* in_rows, const float* gamma, const float* beta,
+                        void* out, int ldo, float* mean, float* rstd, void* stream);
+
+/* dx = LN-input-grad(dy; x, gamma, mean, rstd) (+ dres). x row = x_rows ? x_rows[r] : r;
+ * outputs written at row out_rows ? out_rows[r] : r of dx (f32) and dx_lp (lp_dtype, optional). */
+int clipk_layernorm_bwd(int rows, int width, const float* dy, int lddy, const float* x, int ldx,
+                        const int* x_rows, const float* gamma, const float* mean, const float* rstd,
+                        const float* dres, int lddres, float* dx, void* dx_lp, int lp_dtype,
+                        const int* out_rows, int ldo, void* stream);
+
+/* Multi-head self-attention core on packed qkv rows [(s*L+t), 3*heads*64] (head dim 64):
+ * out[(s*L+t), h*64+d]; lse[(s*L+t)*heads + h] (optional) = logsumexp of scaled scores. */
+int clipk_attention_fwd(int dtype, int nseq, int L, int heads, int causal,
+                        const void* qkv, int ldqkv, void* out, int ldo, float* lse, void* stream);
+
+/* Input-grad backward of the attention core (L <= 64): dqkv (grad_dtype) from qkv and the
+ * saved forward output ofwd (dtype), dout (grad_dtype) and lse. */
+int clipk_attention_bwd(int dtype, int grad_dtype, int nseq, int L, int heads, int causal,
+                        const void* qkv, int ldqkv, const void* ofwd, int ldof, const void* dout,
+                        int lddo, const float* lse, void* dqkv, int lddqkv, void* stream);
+
+/* Patch extraction: img fp32 [B,3,R,R] -> out [B*G*G, Kp] (out_dtype), K index c*p*p+ky*p+kx,
+ * zero padded to Kp >= 3*p*p. */
+int clipk_im2col(int out_dtype, int B, int res, int patch, int Kp, const float* img, void* out,
+                 void* stream);
+
+/* x[b*L + t] = ln_pre( (t==0 ? cls : patch[b*(L-1) + t-1]) + pos[t] ), L = G*G+1, f32 out. */
+int clipk_vit_embed_ln(int B, int L, int width, const float* patch, const float* cls,
+                       const float* pos, const float* gamma, const float* beta, float* x,
+                       void* stream);
+
+/* Prompt assembly (+ positional embedding) for nseq = B*C sequences of length L:
+ *   s = b*C + c;  m = src_map[c*L + t]
+ *   x0[s*L+t] = (m >= 0 ? emb[(c*77 + m)*W] : ctx[b*ctx_sb + c*ctx_sc + (-1-m)*W] + bias[b*W]) + pos[t*W]
+ * bias may be NULL (CoOp). */
+int clipk_prompt_assemble(int B, int C, int L, int W, const int* src_map, const float* emb,
+                          const float* ctx, long ctx_sb, long ctx_sc, const float* bias,
+                          const float* pos, float* x0, void* stream);
+
+/* d ctx_shifted: dctx[b*out_sb + c*out_sc + k*W + w] = sum over c' in class group of
+ *   dx0[((b*C + c')*L + pos_of(c',k))*W + w]   where pos_of from ctx_pos[c'*n_ctx + k].
+ * csc != 0: one output per class (no sum over c). Deterministic fixed-order sums. */
+int clipk_ctx_grad(int B, int C, int L, int W, int n_ctx, int csc, const int* ctx_pos,
+                   const float* dx0, float* dctx, void* stream);
+
+/* logits[b,c] = scale * <imf[b], txt[row]> / |txt[row]| / |imf[b]|,
+ * row = per_image ? b*C + c : c.  tnorm[row] (optional out) = |txt[row]|. */
+int clipk_cosine_logits_fwd(int B, int C, int E, int per_image, float scale, const float* imf,
+                            const float* txt, float* logits, float* inv_tnorm, float* inv_inorm,
+                            void* stream);
+/* d txt[row] from dlogits (image side has no grad: frozen encoder). */
+int clipk_cosine_logits_bwd(int B, int C, int E, int per_image, float scale, const float* imf,
+                            const float* txt, const float* inv_tnorm, const float* inv_inorm,
+                            const float* dlogits, float* dtxt, void* stream);
+
+/* Row-wise CE / focal (gamma) loss with optional per-class alpha; writes per-row loss and
+ * dlogits = d(mean loss)/dlogits * grad_scale. */
+int clipk_ce_loss(int B, int C, const float* logits, const int64_t* labels, const float* alpha,
+                  float gamma, int focal, float grad_scale, float* row_loss, float* dlogits,
+                  void* stream);
+
+/* CoCoOp Meta-Net: h = relu(x W1^T + b1); y = h W2^T + b2. x [B,V], W1 [Hd,V], W2 [Wd,Hd]. */
+int clipk_meta_net_fwd(int B, int V, int Hd, int Wd, const float* x, const float* w1,
+                       const float* b1, const float* w2, const float* b2, float* h, float* y,
+                       void* stream);
+/* grads of W1,b1,W2,b2 from dy (x has no grad). dh_ws: caller scratch of B*Hd floats. */
+int clipk_meta_net_bwd(int B, int V, int Hd, int Wd, const float* x, const float* h,
+                       const float* w2, const float* dy, float* dw1, float* db1, float* dw2,
+                       float* db2, float* dh_ws, void* stream);
+
+/* p -= lr * (buf = momentum*buf + (g + wd*p)); first step (has_buf==0): buf = g + wd*p. */
+int clipk_sgd_step(long n, float* p, const float* g, float* buf, float lr, float momentum,
+                   float weight_decay, int has_buf, void* stream);
+
+/* Elementwise cast fp32 -> dtype. */
+int clipk_cast(int out_dtype, long n, const float* x, void* y, void* stream);
+
+/* ---------------------------------------------------------------- encoders */
+typedef struct clipk_encoder clipk_encoder;
+
+/* Per-layer weight table order (n_per_layer = 16):
+ *   0 ln1_w f32, 1 ln1_b f32, 2 in_w [3W,W] act, 3 in_b f32[3W], 4 out_w [W,W] act, 5 out_b,
+ *   6 ln2_w, 7 ln2_b, 8 fc_w [4W,W] act, 9 fc_b f32[4W], 10 proj_w [W,4W] act, 11 proj_b,
+ *   12 in_wT [W,3W] grad, 13 out_wT [W,W] grad, 14 fc_wT [W,4W] grad, 15 proj_wT [4W,W] grad
+ * (12..15 may be NULL for a forward-only encoder). Head: lnf_w, lnf_b (f32), projT [E,W] act,
+ * proj_grad [W,E] grad (NULL if forward-only).
+ * act_dtype: forward GEMM operand type; grad_dtype: backward GEMM operand type. */
+int clipk_encoder_create(int width, int layers, int heads, int embed, int act_dtype,
+                         int grad_dtype, const void* const* layer_ptrs, const void* const* head_ptrs,
+                         clipk_encoder** out);
+void clipk_encoder_destroy(clipk_encoder* enc);
+
+/* Text encoder forward over nseq sequences of length L (x0 fp32 [nseq*L, W], positional
+ * embedding already added). eot_rows[s] = s*L + EOT position of sequence s (int32, device).
+ * txt fp32 [nseq, E].
+ * If save != 0 the activations needed by clipk_text_backward stay in `saved`. */
+size_t clipk_text_saved_bytes(const clipk_encoder* enc, int nseq, int L);
+size_t clipk_text_ws_bytes(const clipk_encoder* enc, int nseq, int L);
+int clipk_text_forward(const clipk_encoder* enc, int nseq, int L, const float* x0, const int* eot_rows,
+                       float* txt, void* saved, size_t saved_bytes, void* ws, size_t ws_bytes,
+                       void* stream);
+size_t clipk_text_bwd_ws_bytes(const clipk_encoder* enc, int nseq, int L);
+int clipk_text_backward(const clipk_encoder* enc, int nseq, int L, const int* eot_rows,
+                        const float* dtxt, const void* saved, size_t saved_bytes, float* dx0,
+                        void* ws, size_t ws_bytes, void* stream);
+
+/* Vision transformer forward (frozen, no grad): img fp32 [B,3,R,R] -> feat fp32 [B,E].
+ * Head table for a vision encoder: ln_pre_w, ln_pre_b, ln_post_w, ln_post_b (f32),
+ * projT [E,D] act, conv_w [D,Kp] act, class_emb f32[D], pos f32[L,D]. */
+int clipk_vision_create(int width, int layers, int heads, int embed, int res, int patch,
+                        int act_dtype, const void* const* layer_ptrs,
+                        const void* const* head_ptrs, clipk_encoder** out);
+size_t clipk_vit_ws_bytes(const clipk_encoder* enc, int B);
+int clipk_vit_forward(const clipk_encoder* enc, int B, const float* img, float* feat, void* ws,
+                      size_t ws_bytes, void* stream);
+
+/* Per-kernel-class timing with hipEvents on the launch stream (bench.py roofline). */
+enum { CLIPK_PROF_NONE = 0, CLIPK_PROF_GEMM_FC = 1, CLIPK_PROF_GEMM_ALL = 2, CLIPK_PROF_ATTN = 3,
+       CLIPK_PROF_LN = 4 };
+int clipk_prof_enable(int kind);
+int clipk_prof_read(double* total_ms, long* count, double* flops_or_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CLIPK_H */

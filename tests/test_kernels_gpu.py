@@ -1,0 +1,197 @@
+"""Per-kernel numerics on the GPU: each HIP kernel vs a plain PyTorch fp32 reference of
+the same op (float kernels), through the C-ABI. Tolerances are stated per dtype:
+fp32 kernels (f32-input MFMA / fp32 VALU) 2e-5 relative-to-scale, fp16 1e-2, bf16 3e-2
+(all relative to the reference's max |value|)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from fsp_amd import ops, _native as N
+
+pytestmark = pytest.mark.gpu
+
+TOL = {torch.float32: 2e-5, torch.float16: 1e-2, torch.bfloat16: 3e-2}
+
+
+def close(out, ref, dtype, what):
+    out = out.float()
+    ref = ref.float()
+    scale = ref.abs().max().item() + 1e-12
+    err = (out - ref).abs().max().item() / scale
+    assert err <= TOL[dtype], f"{what}: rel err {err:.3e} > {TOL[dtype]} ({dtype})"
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,Nn,K", [(300, 384, 192), (128, 128, 64), (1, 256, 512), (517, 1536, 512)])
+def test_gemm_epilogues(dev, dtype, M, Nn, K):
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + Nn + K)
+    a = torch.randn(M, K, generator=g).to(dev)
+    b = (torch.randn(Nn, K, generator=g) / math.sqrt(K)).to(dev)
+    bias = torch.randn(Nn, generator=g).to(dev)
+    res = torch.randn(M, Nn, generator=g).to(dev)
+    A, Bm = a.to(dtype), b.to(dtype)
+    ref = A.float() @ Bm.float().t()
+    close(ops.gemm(A, Bm, N.EPI_NONE, torch.float32), ref, dtype, "none")
+    close(ops.gemm(A, Bm, N.EPI_BIAS, dtype, bias=bias), ref + bias, dtype, "bias")
+    close(ops.gemm(A, Bm, N.EPI_BIAS_RES, torch.float32, bias=bias, res=res), ref + bias + res, dtype, "res")
+    g_out, h_out = ops.gemm(A, Bm, N.EPI_BIAS_QGELU, dtype, bias=bias, want_out2=True)
+    hr = ref + bias
+    close(h_out, hr, dtype, "qgelu.h")
+    close(g_out, hr * torch.sigmoid(1.702 * hr), dtype, "qgelu.g")
+    aux = torch.randn(M, Nn, generator=g).to(dev).to(dtype)
+    s = torch.sigmoid(1.702 * aux.float())
+    dref = ref * (s + 1.702 * aux.float() * s * (1 - s))
+    close(ops.gemm(A, Bm, N.EPI_DQGELU, dtype, aux=aux), dref, dtype, "dqgelu")
+
+
+def test_gemm_identity_asymmetric(dev):
+    """A = I with an asymmetric B catches a transposed C write (guide §3)."""
+    K = 128
+    A = torch.eye(K, device=dev, dtype=torch.float16)
+    B = (torch.arange(256 * K, device=dev, dtype=torch.float32).reshape(256, K) % 97).to(torch.float16)
+    out = ops.gemm(A, B, N.EPI_NONE, torch.float32)
+    assert torch.equal(out, B.float().t()[:K])
+
+
+def test_gemm_rejects_bad_shapes(dev):
+    A = torch.randn(10, 64, device=dev, dtype=torch.float16)
+    B = torch.randn(100, 64, device=dev, dtype=torch.float16)  # N % 128 != 0
+    with pytest.raises(N.ClipkError):
+        ops.gemm(A, B)
+
+
+@pytest.mark.parametrize("W", [128, 512, 768, 1024])
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
+def test_layernorm_fwd_bwd(dev, W, dtype):
+    g = torch.Generator().manual_seed(W)
+    x = (torch.randn(37, W, generator=g) * 3 + 1).to(dev)
+    w = (1 + 0.1 * torch.randn(W, generator=g)).to(dev)
+    b = (0.1 * torch.randn(W, generator=g)).to(dev)
+    out, mean, rstd = ops.layernorm(x, w, b, dtype, stats=True)
+    xr = x.clone().requires_grad_(True)
+    ref = F.layer_norm(xr, (W,), w, b, 1e-5)
+    close(out, ref, dtype, "ln fwd")
+    dy = torch.randn(37, W, generator=g).to(dev)
+    dres = torch.randn(37, W, generator=g).to(dev)
+    ref.backward(dy)
+    dx = ops.layernorm_bwd(dy, x, w, mean, rstd, dres=dres)
+    close(dx, xr.grad + dres, torch.float32, "ln bwd")
+    rows = torch.tensor([3, 0, 36], device=dev, dtype=torch.int32)
+    og = ops.layernorm(x, w, b, torch.float32, rows=rows)
+    close(og, F.layer_norm(x[rows.long()], (W,), w, b, 1e-5), torch.float32, "ln gather")
+
+
+def attn_ref(qkv, nseq, L, H, causal):
+    W = H * 64
+    q, k, v = qkv.float().view(nseq, L, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = q @ k.transpose(-1, -2) / 8.0
+    if causal:
+        s = s + torch.full((L, L), float("-inf"), device=qkv.device).triu(1)
+    lse = torch.logsumexp(s, -1)
+    o = torch.softmax(s, -1) @ v
+    return o.permute(0, 2, 1, 3).reshape(nseq * L, W), lse.permute(0, 2, 1).reshape(nseq * L, H)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
+@pytest.mark.parametrize("nseq,L,H,causal", [(7, 11, 8, 1), (5, 23, 2, 1), (3, 50, 4, 1), (2, 77, 8, 1),
+                                             (2, 197, 12, 0), (1, 257, 2, 0), (3, 5, 2, 0)])
+def test_attention_fwd(dev, dtype, nseq, L, H, causal):
+    g = torch.Generator().manual_seed(L * H)
+    qkv = torch.randn(nseq * L, 3 * H * 64, generator=g).to(dev).to(dtype)
+    o, lse = ops.attention(qkv, nseq, L, H, causal, lse=True)
+    ro, rl = attn_ref(qkv, nseq, L, H, causal)
+    close(o, ro, dtype, "attn out")
+    close(lse, rl, torch.float16 if dtype != torch.float32 else dtype, "attn lse")
+
+
+@pytest.mark.parametrize("dtype,gdtype", [(torch.float16, torch.bfloat16), (torch.float32, torch.float32)])
+@pytest.mark.parametrize("nseq,L,H", [(6, 11, 8), (3, 23, 2), (2, 64, 2), (4, 5, 2)])
+def test_attention_bwd(dev, dtype, gdtype, nseq, L, H):
+    g = torch.Generator().manual_seed(L + 100 * H)
+    qkv = torch.randn(nseq * L, 3 * H * 64, generator=g).to(dev).to(dtype)
+    o, lse = ops.attention(qkv, nseq, L, H, 1, lse=True)
+    do = torch.randn(nseq * L, H * 64, generator=g).to(dev).to(gdtype)
+    dqkv = ops.attention_bwd(qkv, o, do, lse, nseq, L, H, 1, gdtype)
+    qr = qkv.float().clone().requires_grad_(True)
+    ro, _ = attn_ref(qr, nseq, L, H, 1)
+    ro.backward(do.float())
+    close(dqkv, qr.grad, gdtype if dtype != torch.float32 else dtype, "attn bwd")
+
+
+@pytest.mark.parametrize("patch,res", [(16, 32), (32, 64), (14, 28)])
+def test_im2col_patch_gemm(dev, patch, res):
+    g = torch.Generator().manual_seed(patch)
+    img = torch.randn(2, 3, res, res, generator=g).to(dev)
+    D = 128
+    w = (torch.randn(D, 3, patch, patch, generator=g) * 0.05).to(dev)
+    k = 3 * patch * patch
+    Kp = (k + 63) // 64 * 64
+    wp = torch.zeros(D, Kp, device=dev)
+    wp[:, :k] = w.reshape(D, k)
+    cols = ops.im2col(img, patch, Kp, torch.float32)
+    out = ops.gemm(cols, wp, N.EPI_NONE, torch.float32)
+    ref = F.conv2d(img, w, stride=patch).flatten(2).transpose(1, 2).reshape(-1, D)
+    close(out, ref, torch.float32, "patch embed")
+
+
+def test_cosine_logits_ce_focal(dev):
+    g = torch.Generator().manual_seed(0)
+    B, C, E = 5, 37, 512
+    imf = torch.randn(B, E, generator=g).to(dev)
+    for per_image in (0, 1):
+        txt = torch.randn(B * C if per_image else C, E, generator=g).to(dev).requires_grad_(True)
+        scale = 100.0
+        logits, inv_t, inv_i = ops.cosine_logits(imf, txt.detach(), scale, per_image, C)
+        tn = txt / txt.norm(dim=-1, keepdim=True)
+        ifn = imf / imf.norm(dim=-1, keepdim=True)
+        ref = scale * (torch.einsum("be,bce->bc", ifn, tn.view(B, C, E)) if per_image else ifn @ tn.t())
+        close(logits, ref, torch.float32, "logits")
+        y = torch.from_numpy(__import__("numpy").random.RandomState(1).randint(0, C, B)).to(dev)
+        alpha = torch.rand(C, generator=g).to(dev) + 0.5
+        for focal in (0, 1):
+            lr = ref.detach().clone().requires_grad_(True)
+            if focal:
+                ce = F.cross_entropy(lr, y, reduction="none")
+                loss = (alpha[y] * (1 - torch.exp(-ce)) ** 2 * ce).mean()
+            else:
+                loss = F.cross_entropy(lr, y)
+            loss.backward()
+            row, dl = ops.ce_loss(logits, y, alpha if focal else None, 2.0, bool(focal))
+            assert abs(row.mean().item() - loss.item()) < 1e-4 * max(1.0, abs(loss.item()))
+            close(dl, lr.grad, torch.float32, "dlogits")
+        txt.grad = None
+        dlg = torch.randn(B, C, generator=g).to(dev)
+        ref.backward(dlg)
+        dtxt = ops.cosine_logits_bwd(imf, txt.detach(), inv_t, inv_i, dlg, scale, per_image)
+        close(dtxt, txt.grad, torch.float32, "dtxt")
+
+
+def test_meta_net_and_sgd(dev):
+    g = torch.Generator().manual_seed(3)
+    B, V, Wd = 4, 512, 512
+    Hd = V // 16
+    x = torch.randn(B, V, generator=g).to(dev)
+    w1 = (torch.randn(Hd, V, generator=g) * 0.05).to(dev).requires_grad_(True)
+    b1 = (torch.randn(Hd, generator=g) * 0.05).to(dev).requires_grad_(True)
+    w2 = (torch.randn(Wd, Hd, generator=g) * 0.1).to(dev).requires_grad_(True)
+    b2 = (torch.randn(Wd, generator=g) * 0.05).to(dev).requires_grad_(True)
+    h, y = ops.meta_net(x, w1.detach(), b1.detach(), w2.detach(), b2.detach())
+    ref = torch.relu(x @ w1.t() + b1) @ w2.t() + b2
+    close(y, ref, torch.float32, "meta fwd")
+    dy = torch.randn(B, Wd, generator=g).to(dev)
+    ref.backward(dy)
+    dw1, db1, dw2, db2 = ops.meta_net_bwd(x, h, w2.detach(), dy, V, Hd, Wd)
+    for a, r, n in ((dw1, w1.grad, "dw1"), (db1, b1.grad, "db1"), (dw2, w2.grad, "dw2"), (db2, b2.grad, "db2")):
+        close(a, r, torch.float32, n)
+    p = torch.randn(1000, generator=g).to(dev)
+    gr = torch.randn(1000, generator=g).to(dev)
+    buf = torch.zeros_like(p)
+    pr = p.clone().requires_grad_(True)
+    opt = torch.optim.SGD([pr], lr=0.002, momentum=0.9, weight_decay=5e-4)
+    for step in range(3):
+        pr.grad = gr.clone()
+        opt.step()
+        ops.sgd_step(p, gr, buf, 0.002, 0.9, 5e-4, step > 0)
+    close(p, pr.detach(), torch.float32, "sgd")
