@@ -52,9 +52,9 @@ struct ProfScope {
   size_t idx = 0;
   ProfScope(int cls, hipStream_t s, double work) : st(s) {
     if (g_prof.kind == CLIPK_PROF_NONE) return;
-    if (!(g_prof.kind == cls || (g_prof.kind == CLIPK_PROF_GEMM_ALL &&
-                                 (cls == CLIPK_PROF_GEMM_FC || cls == CLIPK_PROF_GEMM_ALL))))
-      return;
+    if (cls == CLIPK_PROF_NONE) return;
+    const bool is_gemm = cls == CLIPK_PROF_GEMM_FC || cls == CLIPK_PROF_GEMM_ALL || cls == CLIPK_PROF_GEMM_DGELU;
+    if (!(g_prof.kind == cls || (g_prof.kind == CLIPK_PROF_GEMM_ALL && is_gemm))) return;
     if (g_prof.used == g_prof.ev.size()) {
       hipEvent_t a, b;
       if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
@@ -164,24 +164,25 @@ static TextBwdBufs text_bwd_layout(const clipk_encoder* e, int nseq, int L, void
 static int block_fwd(const clipk_encoder* e, const std::array<const void*, 16>& w, int nseq, int L,
                      int causal, const float* X, float* Xm, float* Xo, void* xn, void* qkv, void* o,
                      float* lse, void* h, void* g, float* m1, float* r1, float* m2, float* r2,
-                     hipStream_t st) {
+                     hipStream_t st, bool text) {
+  const int pg = text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE;
   const int W = e->W, rows = nseq * L, act = e->act;
   TRY(clipk_layernorm_fwd(act, rows, W, X, W, nullptr, (const float*)w[0], (const float*)w[1], xn, W,
                           m1, r1, st));
   TRY(gemm(act, act, CLIPK_EPI_BIAS, rows, 3 * W, W, xn, w[2], (const float*)w[3], nullptr, qkv,
-           nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
+           nullptr, nullptr, 0, st, pg));
   {
-    ProfScope ps(CLIPK_PROF_ATTN, st, 0.0);
+    ProfScope ps(text ? CLIPK_PROF_ATTN : CLIPK_PROF_NONE, st, 0.0);
     TRY(clipk_attention_fwd(act, nseq, L, e->heads, causal, qkv, 3 * W, o, W, lse, st));
   }
   TRY(gemm(act, CLIPK_F32, CLIPK_EPI_BIAS_RES, rows, W, W, o, w[4], (const float*)w[5], X, Xm,
-           nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
+           nullptr, nullptr, 0, st, pg));
   TRY(clipk_layernorm_fwd(act, rows, W, Xm, W, nullptr, (const float*)w[6], (const float*)w[7], xn, W,
                           m2, r2, st));
   TRY(gemm(act, act, CLIPK_EPI_BIAS_QGELU, rows, 4 * W, W, xn, w[8], (const float*)w[9], nullptr, g,
-           h, nullptr, 0, st, CLIPK_PROF_GEMM_FC));
+           h, nullptr, 0, st, text ? CLIPK_PROF_GEMM_FC : CLIPK_PROF_NONE));
   TRY(gemm(act, CLIPK_F32, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo,
-           nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
+           nullptr, nullptr, 0, st, pg));
   return CLIPK_OK;
 }
 
@@ -286,7 +287,7 @@ extern "C" int clipk_text_forward(const clipk_encoder* e, int nseq, int L, const
     float* Xo = t.X[l + 1];
     if (!save && Xo == cur) Xo = t.X[l];  // ping-pong (cur may be the caller's x0)
     TRY(block_fwd(e, e->lw[l], nseq, L, 1, cur, t.Xm[l], Xo, t.xn, t.qkv[l], t.o[l], t.lse[l],
-                  save ? t.h[l] : nullptr, t.g, t.mean1[l], t.rstd1[l], t.mean2[l], t.rstd2[l], st));
+                  save ? t.h[l] : nullptr, t.g, t.mean1[l], t.rstd1[l], t.mean2[l], t.rstd2[l], st, true));
     cur = Xo;
   }
   // ln_final on the EOT rows only (exact: LayerNorm is per row), then @ text_projection
@@ -328,7 +329,7 @@ extern "C" int clipk_text_backward(const clipk_encoder* e, int nseq, int L, cons
     if (!w[12] || !w[13] || !w[14] || !w[15]) return CLIPK_EINVAL;
     // MLP: dg = dX . Wproj ; dh = dg * qgelu'(h)
     TRY(gemm(gd, gd, CLIPK_EPI_DQGELU, rows, 4 * W, W, b.dX_lp, w[15], nullptr, nullptr, b.dh, nullptr,
-             t.h[l], act, st, CLIPK_PROF_GEMM_ALL));
+             t.h[l], act, st, CLIPK_PROF_GEMM_DGELU));
     TRY(gemm(gd, CLIPK_F32, CLIPK_EPI_NONE, rows, W, 4 * W, b.dh, w[14], nullptr, nullptr, b.dxn, nullptr,
              nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
     TRY(clipk_layernorm_bwd(rows, W, b.dxn, W, t.Xm[l], W, nullptr, (const float*)w[6], t.mean2[l],
@@ -399,7 +400,7 @@ extern "C" int clipk_vit_forward(const clipk_encoder* e, int B, const float* img
   float* nxt = v.x1;
   for (int l = 0; l < e->layers; ++l) {
     TRY(block_fwd(e, e->lw[l], B, L, 0, cur, v.xm, nxt, v.xn, v.qkv, v.o, nullptr, nullptr, v.g,
-                  nullptr, nullptr, nullptr, nullptr, st));
+                  nullptr, nullptr, nullptr, nullptr, st, false));
     float* t = cur; cur = nxt; nxt = t;
   }
   // ln_post on the CLS rows (row stride L*D), then @ proj

@@ -1,0 +1,123 @@
+"""Autograd Functions wiring the native kernels into the prompt learners, plus the
+host-side prompt layout tables. Every forward/backward body is a libclipk.so call;
+torch only allocates and sums a handful of [B, n_ctx, W] values.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .. import ops
+
+
+def prompt_layout(n_cls, n_ctx, name_lens, position, eot, truncate=True):
+    """Token-slot tables for PromptLearner.forward (coop.py:259-296).
+
+    Returns (src_map [C,L] int32, ctx_pos [C,n_ctx] int32, L):
+    src_map[c,t] >= 0 -> row of the class's token embedding (prefix/class/suffix),
+    src_map[c,t] < 0  -> context vector (-1 - m).
+    L = max(EOT)+1 when truncating: positions after the EOT never reach it under the
+    causal mask (model.py:592-598), so truncation is exact."""
+    L = int(max(eot)) + 1 if truncate else 77
+    src = np.zeros((n_cls, L), np.int32)
+    cpos = np.zeros((n_cls, max(n_ctx, 1)), np.int32)
+    for c in range(n_cls):
+        nl = int(name_lens[c]) if name_lens is not None else 0
+        if position == "end":
+            seq = [0] + [-1 - k for k in range(n_ctx)] + list(range(1 + n_ctx, 77))
+        elif position == "middle":
+            h = n_ctx // 2
+            seq = ([0] + [-1 - k for k in range(h)] + [1 + n_ctx + j for j in range(nl)]
+                   + [-1 - k for k in range(h, n_ctx)] + list(range(1 + n_ctx + nl, 77)))
+        elif position == "front":
+            seq = ([0] + [1 + n_ctx + j for j in range(nl)] + [-1 - k for k in range(n_ctx)]
+                   + list(range(1 + n_ctx + nl, 77)))
+        else:
+            raise ValueError("Unknown class_token_position")
+        assert len(seq) == 77
+        src[c] = seq[:L]
+        for t, m in enumerate(seq):
+            if m < 0:
+                if t >= L:
+                    raise ValueError("context slot past the EOT token")
+                cpos[c, -1 - m] = t
+    return src, cpos, L
+
+
+class PromptAssembleFn(torch.autograd.Function):
+    """x0[(b*C+c)*L+t] = prompt token (+ctx[+bias_b]) + pos[t]; grads to ctx (and bias)."""
+
+    @staticmethod
+    def forward(ctx, ctx_vec, bias, lay):
+        B = 1 if bias is None else bias.shape[0]
+        csc = ctx_vec.dim() == 3
+        W = ctx_vec.shape[-1]
+        sc = lay.n_ctx * W if csc else 0
+        x0 = ops.prompt_assemble(B, lay.n_cls, lay.L, lay.src_map, lay.emb, ctx_vec.contiguous(), 0, sc,
+                                 None if bias is None else bias.contiguous(), lay.pos)
+        ctx.lay, ctx.B, ctx.csc, ctx.shape, ctx.has_bias = lay, B, csc, ctx_vec.shape, bias is not None
+        return x0
+
+    @staticmethod
+    def backward(ctx, dx0):
+        lay = ctx.lay
+        W = ctx.shape[-1]
+        d = ops.ctx_grad(ctx.B, lay.n_cls, lay.L, W, lay.n_ctx, ctx.csc, lay.ctx_pos, dx0.contiguous())
+        if ctx.csc:
+            return d.view(ctx.shape), None, None
+        d = d.view(ctx.B, lay.n_ctx, W)
+        dctx = d.sum(0) if ctx.B > 1 else d[0]
+        dbias = d.sum(1) if ctx.has_bias else None
+        return dctx, dbias, None
+
+
+class CosineLogitsFn(torch.autograd.Function):
+    """logits = scale * cos(imf[b], txt[row]); row = b*C+c (per_image) or c."""
+
+    @staticmethod
+    def forward(ctx, imf, txt, scale, per_image, n_cls):
+        imf = imf.contiguous()
+        txt = txt.contiguous()
+        logits, inv_t, inv_i = ops.cosine_logits(imf, txt, scale, per_image, n_cls)
+        ctx.save_for_backward(imf, txt, inv_t, inv_i)
+        ctx.scale, ctx.per_image = scale, per_image
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        imf, txt, inv_t, inv_i = ctx.saved_tensors
+        dtxt = ops.cosine_logits_bwd(imf, txt, inv_t, inv_i, dlogits.contiguous(), ctx.scale, ctx.per_image)
+        return None, dtxt, None, None, None
+
+
+class CrossEntropyFn(torch.autograd.Function):
+    """mean CE (nn.CrossEntropyLoss) or MultiClassFocalLoss (coop.py:145-163), fused fwd+bwd."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, alpha, gamma, focal):
+        row, dl = ops.ce_loss(logits.contiguous(), labels, alpha, gamma, focal, grad=logits.requires_grad)
+        ctx.dl = dl
+        return row.mean()
+
+    @staticmethod
+    def backward(ctx, g):
+        return ctx.dl * g, None, None, None, None
+
+
+class MetaNetFn(torch.autograd.Function):
+    """CoCoOp meta_net (cocoop.py:139-143): Linear(V,V/16) -> ReLU -> Linear(V/16,W)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        x = x.contiguous()
+        h, y = ops.meta_net(x, w1.contiguous(), b1.contiguous(), w2.contiguous(), b2.contiguous())
+        ctx.save_for_backward(x, h, w2)
+        ctx.dims = (x.shape[1], w1.shape[0], w2.shape[0])
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, h, w2 = ctx.saved_tensors
+        V, Hd, Wd = ctx.dims
+        dw1, db1, dw2, db2 = ops.meta_net_bwd(x, h, w2.contiguous(), dy, V, Hd, Wd)
+        return None, dw1, db1, dw2, db2

@@ -1,0 +1,178 @@
+"""CoCoOp on the MI355X-native path — same registry name, cfg keys (TRAINER.COCOOP.*),
+module contract and checkpoint format as ``PromptSRC/trainers/cocoop.py``.
+
+The reference encodes the C class prompts once PER IMAGE in a Python loop
+(cocoop.py:247-251) after materialising [B, C, 77, W] prompts (cocoop.py:189-197).
+Here one launch sequence encodes all B*C conditional prompts at once: the Meta-Net
+bias is added inside the prompt-assembly kernel, the text encoder runs over
+B*C sequences truncated to L = max EOT + 1, and the per-image cosine logits come from
+one kernel. Large B*C is split into image chunks bounded by NATIVE.MAX_TEXT_ROWS.
+"""
+from __future__ import annotations
+
+import os.path as osp
+from collections import OrderedDict
+
+import torch
+import torch.nn as nn
+
+from ..engine.registry import TRAINER_REGISTRY
+from ..engine.trainer import TrainerX, load_clip
+from ..engine.optim import build_optimizer, build_lr_scheduler
+from ..clip.model import TextEncodeFn
+from ._fns import PromptAssembleFn, CosineLogitsFn, MetaNetFn
+from .losses import CrossEntropyLoss, MultiClassFocalLoss, focal_alpha
+from .prompt_base import init_prompts
+from .coop import TextEncoder  # noqa: F401  (same API-compatible text encoder)
+
+
+class MetaNet(nn.Module):
+    """nn.Sequential(linear1, relu, linear2) of cocoop.py:139-143 (same state-dict keys)."""
+
+    def __init__(self, vis_dim, ctx_dim):
+        super().__init__()
+        self.linear1 = nn.Linear(vis_dim, vis_dim // 16)
+        self.linear2 = nn.Linear(vis_dim // 16, ctx_dim)
+
+    def forward(self, x):
+        return MetaNetFn.apply(x, self.linear1.weight, self.linear1.bias, self.linear2.weight,
+                               self.linear2.bias)
+
+
+class PromptLearner(nn.Module):
+    def __init__(self, cfg, classnames, clip_model):
+        super().__init__()
+        c = cfg.TRAINER.COCOOP
+        clip_imsize = clip_model.visual.input_resolution
+        cfg_imsize = cfg.INPUT.SIZE[0]
+        assert cfg_imsize == clip_imsize, f"cfg_imsize({cfg_imsize}) != clip_imsize({clip_imsize})"
+        vis_dim = clip_model.visual.output_dim
+        ctx_dim = clip_model.arch.transformer_width
+        truncate = cfg.get("NATIVE", {}).get("TRUNCATE_PROMPTS", True)
+        ctx_vectors, self.prompt_prefix = init_prompts(self, classnames, clip_model, c.N_CTX, c.CTX_INIT,
+                                                       "end", False, truncate)
+        self.ctx = nn.Parameter(ctx_vectors)
+        self.meta_net = MetaNet(vis_dim, ctx_dim).to(ctx_vectors.device)
+
+    def assemble(self, im_features):
+        """im_features [B, V] (L2-normalised) -> x0 [B*C*L, W] with ctx + meta_net(imf_b)."""
+        bias = self.meta_net(im_features)
+        return PromptAssembleFn.apply(self.ctx, bias, self.layout)
+
+    def construct_prompts(self, ctx, prefix, suffix, label=None):
+        if label is not None:
+            prefix, suffix = prefix[label], suffix[label]
+        return torch.cat([prefix, ctx, suffix], dim=1)
+
+    def forward(self, im_features):
+        """API-compatible [B, C, 77, W] prompts (cocoop.py:173-198)."""
+        bias = self.meta_net(im_features).unsqueeze(1)
+        shifted = self.ctx.unsqueeze(0) + bias
+        out = [self.construct_prompts(s.unsqueeze(0).expand(self.n_cls, -1, -1), self.token_prefix,
+                                      self.token_suffix) for s in shifted]
+        return torch.stack(out, 0)
+
+
+class CustomCLIP(nn.Module):
+    def __init__(self, cfg, classnames, clip_model):
+        super().__init__()
+        self.cfg = cfg
+        self.prompt_learner = PromptLearner(cfg, classnames, clip_model)
+        self.tokenized_prompts = self.prompt_learner.tokenized_prompts
+        self.image_encoder = clip_model.visual
+        self.text_core = clip_model.text
+        self.text_encoder = TextEncoder(clip_model)
+        self.logit_scale = clip_model.logit_scale
+        self.logit_scale_value = clip_model.logit_scale_value
+        self.dtype = clip_model.dtype
+        self.max_rows = int(cfg.get("NATIVE", {}).get("MAX_TEXT_ROWS", 2_000_000))
+        self.use_focal_loss = cfg.TRAINER.COCOOP.get("USE_FOCAL_LOSS", False)
+        print(f">> USE_FOCAL_LOSS = {self.use_focal_loss}")
+        if self.use_focal_loss:
+            print(">> Use Focal Loss!")
+            per_class = getattr(cfg.DATASET, "PER_CLASS_SHOTS", None)
+            alpha = focal_alpha(per_class, len(classnames), zero_guard=False) \
+                if isinstance(per_class, (list, str)) else None
+            self.criterion = MultiClassFocalLoss(alpha=alpha, gamma=2, reduction="mean")
+        else:
+            print(">> Use Cross Entropy Loss!")
+            self.criterion = CrossEntropyLoss()
+
+    def logits_for(self, imf_n):
+        pl = self.prompt_learner
+        B = imf_n.shape[0]
+        x0 = pl.assemble(imf_n)
+        txt = TextEncodeFn.apply(x0, self.text_core, pl.layout.eot_rows(B), B * pl.n_cls, pl.layout.L)
+        return CosineLogitsFn.apply(imf_n, txt, self.logit_scale_value, 1, pl.n_cls)
+
+    def forward(self, image, label=None):
+        imf = self.image_encoder(image)
+        imf = imf / imf.norm(dim=-1, keepdim=True)
+        pl = self.prompt_learner
+        per_img = pl.n_cls * pl.layout.L
+        chunk = max(1, self.max_rows // per_img)
+        if imf.shape[0] <= chunk:
+            logits = self.logits_for(imf)
+        else:
+            logits = torch.cat([self.logits_for(imf[i:i + chunk]) for i in range(0, imf.shape[0], chunk)], 0)
+        if self.training and label is not None:
+            return self.criterion(logits, label)
+        return logits
+
+
+@TRAINER_REGISTRY.register()
+class CoCoOp(TrainerX):
+    """cocoop.py:262-370 trainer contract."""
+
+    def check_cfg(self, cfg):
+        assert cfg.TRAINER.COCOOP.PREC in ["fp16", "fp32", "amp", "bf16"]
+
+    def build_model(self):
+        cfg = self.cfg
+        classnames = self.dm.dataset.classnames
+        print(f"Loading CLIP (backbone: {cfg.MODEL.BACKBONE.NAME})")
+        clip_model = load_clip(cfg, cfg.TRAINER.COCOOP.PREC, self.device)
+        print("Building custom CLIP")
+        self.model = CustomCLIP(cfg, classnames, clip_model)
+        print("Turning off gradients in both the image and the text encoder")
+        for name, param in self.model.named_parameters():
+            if "prompt_learner" not in name:
+                param.requires_grad_(False)
+        enabled = {n for n, p in self.model.named_parameters() if p.requires_grad}
+        print(f"Parameters to be updated: {enabled}")
+        if cfg.MODEL.INIT_WEIGHTS:
+            self.load_pretrained_weights(self.model.prompt_learner, cfg.MODEL.INIT_WEIGHTS)
+        self.optim = build_optimizer(self.model.prompt_learner, cfg.OPTIM)
+        self.sched = build_lr_scheduler(self.optim, cfg.OPTIM)
+        self.register_model("prompt_learner", self.model.prompt_learner, self.optim, self.sched)
+
+    def forward_backward(self, batch):
+        image, label = self.parse_batch_train(batch)
+        loss = self.model(image, label)
+        self.optim.zero_grad()
+        loss.backward()
+        self.allreduce_grads(self.model.prompt_learner)
+        self.optim.step()
+        loss_summary = {"loss": loss.item()}
+        if (self.batch_idx + 1) == self.num_batches:
+            self.update_lr()
+        return loss_summary
+
+    def parse_batch_train(self, batch):
+        return batch["img"].to(self.device), batch["label"].to(self.device)
+
+    def load_model(self, directory, epoch=None):
+        if not directory:
+            print("Note that load_model() is skipped as no pretrained model is given")
+            return
+        model_file = "model-best.pth.tar" if epoch is None else f"model.pth.tar-{epoch}"
+        for name in self.get_model_names():
+            model_path = osp.join(directory, name, model_file)
+            if not osp.exists(model_path):
+                raise FileNotFoundError(f'Model not found at "{model_path}"')
+            checkpoint = self.load_checkpoint(model_path)
+            state_dict = checkpoint["state_dict"]
+            state_dict.pop("token_prefix", None)
+            state_dict.pop("token_suffix", None)
+            print(f'Loading weights to {name} from "{model_path}" (epoch = {checkpoint["epoch"]})')
+            self._models[name].load_state_dict(state_dict, strict=False)

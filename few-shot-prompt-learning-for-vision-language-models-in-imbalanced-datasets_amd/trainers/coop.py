@@ -1,0 +1,199 @@
+"""CoOp on the MI355X-native path — same registry name, cfg keys (TRAINER.COOP.*),
+module contract and checkpoint format as ``PromptSRC/trainers/coop.py``.
+
+Hot path per step (``CustomCLIP.forward_once``, coop.py:351-363):
+  image_encoder (native ViT fwd) -> PromptAssembleFn (ctx spliced into the class
+  token embeddings + pos) -> TextEncodeFn (native text transformer fwd, input-grad bwd)
+  -> CosineLogitsFn -> CE / focal (fused kernel) or logit NT-Xent.
+The text encoder runs once per step over the C class prompts (prompts are image
+independent in CoOp), truncated to L = max EOT + 1 tokens (exact under the causal mask).
+"""
+from __future__ import annotations
+
+import os.path as osp
+
+import torch
+import torch.nn as nn
+
+from ..engine.registry import TRAINER_REGISTRY
+from ..engine.trainer import TrainerX, load_clip
+from ..engine.optim import build_optimizer, build_lr_scheduler
+from ..engine.metrics import compute_accuracy
+from ..clip.model import TextEncodeFn
+from ._fns import PromptAssembleFn, CosineLogitsFn
+from .losses import CrossEntropyLoss, MultiClassFocalLoss, LogitsNTXentLoss, focal_alpha
+from .prompt_base import init_prompts
+
+
+class TextEncoder(nn.Module):
+    """API-compatible TextEncoder.forward(prompts [N,L,W], tokenized [N,77]) -> [N,E]
+    (coop.py:186-205) on the native encoder; gradients flow to ``prompts``."""
+
+    def __init__(self, clip_model):
+        super().__init__()
+        self.core = clip_model.text
+        self.positional_embedding = clip_model.positional_embedding
+        self.dtype = clip_model.dtype
+
+    def forward(self, prompts, tokenized_prompts):
+        N_, L77, W = prompts.shape
+        eot = tokenized_prompts.argmax(dim=-1)
+        L = int(eot.max().item()) + 1
+        x0 = (prompts[:, :L] + self.positional_embedding[:L]).reshape(N_ * L, W).contiguous()
+        rows = (torch.arange(N_, device=eot.device) * L + eot).to(torch.int32).to(prompts.device)
+        return TextEncodeFn.apply(x0, self.core, rows, N_, L)
+
+
+class PromptLearner(nn.Module):
+    """coop.py:207-296. forward() returns prompts [C,77,W] for API compatibility; the
+    trainer's fast path uses ``assemble()`` (fused slot splice, no [C,77,W] concat)."""
+
+    def __init__(self, cfg, classnames, clip_model):
+        super().__init__()
+        c = cfg.TRAINER.COOP
+        clip_imsize = clip_model.visual.input_resolution
+        cfg_imsize = cfg.INPUT.SIZE[0]
+        assert cfg_imsize == clip_imsize, f"cfg_imsize ({cfg_imsize}) must equal to clip_imsize ({clip_imsize})"
+        if c.CSC and not c.CTX_INIT:
+            print("Initializing class-specific contexts")
+        elif not c.CTX_INIT:
+            print("Initializing a generic context")
+        truncate = cfg.get("NATIVE", {}).get("TRUNCATE_PROMPTS", True)
+        ctx_vectors, self.prompt_prefix = init_prompts(
+            self, classnames, clip_model, c.N_CTX, c.CTX_INIT, c.CLASS_TOKEN_POSITION,
+            bool(c.CSC) and not c.CTX_INIT, truncate)
+        self.ctx = nn.Parameter(ctx_vectors)
+        self.class_token_position = c.CLASS_TOKEN_POSITION
+
+    def assemble(self):
+        """[C*L, W] fp32 text-encoder input (prompts + positional embedding), grad -> ctx."""
+        return PromptAssembleFn.apply(self.ctx, None, self.layout)
+
+    def forward(self):
+        ctx = self.ctx
+        if ctx.dim() == 2:
+            ctx = ctx.unsqueeze(0).expand(self.n_cls, -1, -1)
+        prefix, suffix = self.token_prefix, self.token_suffix
+        if self.class_token_position == "end":
+            return torch.cat([prefix, ctx, suffix], dim=1)
+        rows = []
+        for i in range(self.n_cls):
+            nl = self.name_lens[i]
+            cls_i, suf_i = suffix[i:i + 1, :nl], suffix[i:i + 1, nl:]
+            if self.class_token_position == "middle":
+                h = self.n_ctx // 2
+                rows.append(torch.cat([prefix[i:i + 1], ctx[i:i + 1, :h], cls_i, ctx[i:i + 1, h:], suf_i], 1))
+            elif self.class_token_position == "front":
+                rows.append(torch.cat([prefix[i:i + 1], cls_i, ctx[i:i + 1], suf_i], 1))
+            else:
+                raise ValueError("Unknown class_token_position")
+        return torch.cat(rows, dim=0)
+
+
+class CustomCLIP(nn.Module):
+    def __init__(self, cfg, classnames, clip_model):
+        super().__init__()
+        self.cfg = cfg
+        self.prompt_learner = PromptLearner(cfg, classnames, clip_model)
+        self.tokenized_prompts = self.prompt_learner.tokenized_prompts
+        self.image_encoder = clip_model.visual
+        self.text_encoder = TextEncoder(clip_model)
+        self.text_core = clip_model.text
+        self.logit_scale = clip_model.logit_scale
+        self.logit_scale_value = clip_model.logit_scale_value
+        self.dtype = clip_model.dtype
+        self.loss_type = cfg.TRAINER.COOP.get("LOSS_TYPE", "ce")
+        if self.loss_type == "simclr":
+            print(">> Using LogitsNTXentLoss (logit-based simclr)!")
+            self.criterion_simclr = LogitsNTXentLoss(temperature=0.07)
+        elif self.loss_type == "ce":
+            print(">> Using CE Loss!")
+            self.criterion_ce = CrossEntropyLoss()
+        elif self.loss_type == "focal":
+            print(">> Use Focal Loss!")
+            alpha = focal_alpha(cfg.DATASET.PER_CLASS_SHOTS, len(classnames), zero_guard=True)
+            self.criterion_ce = MultiClassFocalLoss(alpha=alpha, gamma=2, reduction="mean")
+        else:
+            raise ValueError(f"Unknown loss_type = {self.loss_type}")
+
+    def text_features(self):
+        pl = self.prompt_learner
+        x0 = pl.assemble()
+        return TextEncodeFn.apply(x0, self.text_core, pl.layout.eot_rows(1), pl.n_cls, pl.layout.L)
+
+    def forward_once(self, image):
+        imf = self.image_encoder(image)
+        txt = self.text_features()
+        return CosineLogitsFn.apply(imf, txt, self.logit_scale_value, 0, self.prompt_learner.n_cls)
+
+    def forward(self, img1, lbl=None, img2=None):
+        if self.loss_type == "simclr":
+            return self.criterion_simclr(self.forward_once(img1), self.forward_once(img2))
+        if self.loss_type in ("ce", "focal"):
+            logits = self.forward_once(img1)
+            if self.training and lbl is not None:
+                return self.criterion_ce(logits, lbl)
+            return logits
+        raise ValueError(f"Unsupported loss_type? {self.loss_type}")
+
+
+@TRAINER_REGISTRY.register()
+class CoOp(TrainerX):
+    """coop.py:396-510 trainer contract: build_model / forward_backward / parse_batch_train /
+    load_model. Multi-GPU: one process per GPU (see fsp_amd.dist), not nn.DataParallel."""
+
+    def check_cfg(self, cfg):
+        assert cfg.TRAINER.COOP.PREC in ["fp16", "fp32", "amp", "bf16"]
+
+    def build_model(self):
+        cfg = self.cfg
+        classnames = self.dm.dataset.classnames
+        clip_model = load_clip(cfg, cfg.TRAINER.COOP.PREC, self.device)
+        print("Building custom CLIP w. logit-simclr or CE")
+        self.model = CustomCLIP(cfg, classnames, clip_model)
+        for name, param in self.model.named_parameters():
+            if "prompt_learner" not in name:
+                param.requires_grad = False
+        if cfg.MODEL.INIT_WEIGHTS:
+            self.load_pretrained_weights(self.model.prompt_learner, cfg.MODEL.INIT_WEIGHTS)
+        self.optim = build_optimizer(self.model.prompt_learner, cfg.OPTIM)
+        self.sched = build_lr_scheduler(self.optim, cfg.OPTIM)
+        self.register_model("prompt_learner", self.model.prompt_learner, self.optim, self.sched)
+
+    def forward_backward(self, batch):
+        x1, lbl, x2 = self.parse_batch_train(batch)
+        loss = self.model(x1, lbl, x2)
+        self.optim.zero_grad()
+        loss.backward()
+        self.allreduce_grads(self.model.prompt_learner)
+        self.optim.step()
+        loss_summary = {"loss": loss.item()}
+        if lbl is not None and x2 is None and self.model.loss_type == "ce":
+            # coop.py:464-469: acc from a second forward AFTER the step
+            with torch.no_grad():
+                logits_eval = self.model(x1, lbl=None, img2=None)
+                loss_summary["acc"] = compute_accuracy(logits_eval, lbl)[0].item()
+        if (self.batch_idx + 1) == self.num_batches:
+            self.update_lr()
+        return loss_summary
+
+    def parse_batch_train(self, batch):
+        if self.cfg.TRAINER.COOP.LOSS_TYPE == "simclr":
+            return batch["img1"].to(self.device), None, batch["img2"].to(self.device)
+        return batch["img"].to(self.device), batch["label"].to(self.device), None
+
+    def load_model(self, directory, epoch=None):
+        if not directory:
+            print("no pretrained => skip")
+            return
+        model_file = "model-best.pth.tar" if not epoch else f"model.pth.tar-{epoch}"
+        for name in self.get_model_names():
+            model_path = osp.join(directory, name, model_file)
+            if not osp.exists(model_path):
+                raise FileNotFoundError(f"No model at {model_path}")
+            ckpt = self.load_checkpoint(model_path)
+            state_dict = ckpt["state_dict"]
+            state_dict.pop("token_prefix", None)
+            state_dict.pop("token_suffix", None)
+            print(f'Loading {name} from "{model_path}" (epoch={ckpt["epoch"]})')
+            self._models[name].load_state_dict(state_dict, strict=False)

@@ -193,7 +193,9 @@ int clipk_vit_forward(const clipk_encoder* enc, int B, const float* img, float* 
 
 /* Per-kernel-class timing with hipEvents on the launch stream (bench.py roofline). */
 enum { CLIPK_PROF_NONE = 0, CLIPK_PROF_GEMM_FC = 1, CLIPK_PROF_GEMM_ALL = 2, CLIPK_PROF_ATTN = 3,
-       CLIPK_PROF_LN = 4 };
+       CLIPK_PROF_LN = 4, CLIPK_PROF_GEMM_DGELU = 5 };
+/* GEMM_FC = text c_fc forward GEMMs; GEMM_DGELU = text c_proj input-grad GEMMs with the fused
+ * QuickGELU' epilogue; GEMM_ALL = every text GEMM; ATTN = text attention fwd+bwd. */
 int clipk_prof_enable(int kind);
 int clipk_prof_read(double* total_ms, long* count, double* flops_or_bytes);
 
