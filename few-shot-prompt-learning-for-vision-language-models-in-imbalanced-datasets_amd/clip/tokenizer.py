@@ -51,14 +51,15 @@ def find_vocab():
 
 @lru_cache()
 def _byte_alphabet():
-    """Map each byte 0..255 to a printable unicode char (GPT-2/CLIP byte-level scheme)."""
-    printable = set(range(0x21, 0x7F)) | set(range(0xA1, 0xAD)) | set(range(0xAE, 0x100))
-    table = {}
+    """Map each byte 0..255 to a printable unicode char (GPT-2/CLIP byte-level scheme).
+
+    Iteration order matters: the vocab lists the printable bytes first (in byte order),
+    then the remapped control/space bytes (256+n), exactly as the CLIP vocab does."""
+    printable = sorted(set(range(0x21, 0x7F)) | set(range(0xA1, 0xAD)) | set(range(0xAE, 0x100)))
+    table = {b: chr(b) for b in printable}
     extra = 0
     for b in range(256):
-        if b in printable:
-            table[b] = chr(b)
-        else:
+        if b not in table:
             table[b] = chr(256 + extra)
             extra += 1
     return table

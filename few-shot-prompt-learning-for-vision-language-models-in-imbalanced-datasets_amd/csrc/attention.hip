@@ -317,6 +317,161 @@ __global__ __launch_bounds__(64) void attn_bwd_short(int nseq, int L, int H, int
   }
 }
 
+// ------------------------------------------------------------------ backward, L <= 16, MFMA
+// One wave per (seq, head); 16x16 tiles (rows >= L zero-padded and masked).
+// S = Q K^T and S^T = K Q^T (and dP, dP^T) with v_mfma_f32_16x16x32; the score
+// accumulators are reused in registers as operands of the 16x16x16 products
+// (accumulator layout [4*(l>>4)+r][l&15] == the 16x16x16 B layout == transposed A layout):
+//   dV = P^T dO, dK = dS^T Q (layout-1 P/dS as A),  dQ = dS K (layout-2 dS as A);
+// the row-major dO/Q/K tiles feed those products through ds_read_b64_tr_b16 (hardware
+// transposed LDS read). D_i = rowsum(P o dP) is formed in registers (no saved O needed).
+// Backward math is bf16 x bf16 -> fp32 (the grad dtype); T is the forward operand type.
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+constexpr int TRS = 72;  // LDS row stride in 16-bit elements (64 + 8 pad, 8-byte aligned)
+
+__device__ __forceinline__ s16x8 ld_row16(const void* p, bool ok) {
+  if (!ok) return (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
+  return *reinterpret_cast<const s16x8*>(p);
+}
+
+// convert 8 elements of T (raw 16 B) to bf16 bits
+template <typename T>
+__device__ __forceinline__ s16x8 to_bf16x8(s16x8 v) {
+  if constexpr (__is_same(T, bf16)) {
+    return v;
+  } else {
+    f16x8 h = __builtin_bit_cast(f16x8, v);
+    bf16x8 b;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b[i] = (bf16)(float)h[i];
+    return __builtin_bit_cast(s16x8, b);
+  }
+}
+
+__device__ __forceinline__ f32x4 mfma32_bf16(s16x8 a, s16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16_bf16(s16x4 a, s16x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ s16x4 pack_bf16x4(float a, float b, float c, float d) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  bf16x4 v = {(bf16)a, (bf16)b, (bf16)c, (bf16)d};
+  return __builtin_bit_cast(s16x4, v);
+}
+__device__ __forceinline__ s16x4 tr_read(const short* tile, int rbase, int cbase, int lane) {
+  const int li = lane & 15;
+  const short* p = tile + (rbase + (li >> 2)) * TRS + cbase + 4 * (li & 3);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
+}
+
+template <typename T, typename TG>
+__global__ __launch_bounds__(256) void attn_bwd_mfma16(int nseq, int L, int H, int causal,
+                                                       const T* __restrict__ qkv, int ldq,
+                                                       const TG* __restrict__ dout, int lddo,
+                                                       const float* __restrict__ lse,
+                                                       TG* __restrict__ dqkv, int lddq) {
+  static_assert(__is_same(TG, bf16), "MFMA attention backward computes in bf16");
+  __shared__ CLIPK_LDS_ALIGN short tiles[4][3][16 * TRS];  // per wave: Q, K, dO (bf16)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int pair = blockIdx.x * 4 + w;
+  if (pair >= nseq * H) return;  // wave-uniform
+  const int s = pair / H, h = pair % H;
+  const int W = H * 64;
+  const size_t row0 = (size_t)s * L;
+  short* tQ = tiles[w][0];
+  short* tK = tiles[w][1];
+  short* tD = tiles[w][2];
+
+  // ---- fragments: row r16, 16-B chunk g4 (+4 for kk=1) of Q, K, V (T) and dO (TG)
+  const bool rok = r16 < L;
+  const T* qrow = qkv + (row0 + (rok ? r16 : 0)) * ldq + h * 64;
+  const TG* drow = dout + (row0 + (rok ? r16 : 0)) * lddo + h * 64;
+  s16x8 q[2], k[2], v[2], d[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int c = 8 * g4 + 32 * kk;
+    q[kk] = ld_row16(qrow + c, rok);
+    k[kk] = ld_row16(qrow + W + c, rok);
+    v[kk] = ld_row16(qrow + 2 * W + c, rok);
+    d[kk] = ld_row16(drow + c, rok);
+  }
+  // stage Q, K, dO (bf16) for the transposed reads
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int c = 8 * g4 + 32 * kk;
+    const s16x8 qb = to_bf16x8<T>(q[kk]), kb = to_bf16x8<T>(k[kk]);
+    *reinterpret_cast<s16x8*>(tQ + r16 * TRS + c) = qb;
+    *reinterpret_cast<s16x8*>(tK + r16 * TRS + c) = kb;
+    *reinterpret_cast<s16x8*>(tD + r16 * TRS + c) = d[kk];
+    v[kk] = to_bf16x8<T>(v[kk]);
+    q[kk] = qb;
+    k[kk] = kb;
+  }
+  // ---- scores in both layouts
+  f32x4 s1 = {0, 0, 0, 0}, s2 = {0, 0, 0, 0}, p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0};
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    s1 = mfma32_bf16(q[kk], k[kk], s1);  // S  [i=4g4+r][j=r16]
+    s2 = mfma32_bf16(k[kk], q[kk], s2);  // S^T[j=4g4+r][i=r16]
+    p1 = mfma32_bf16(d[kk], v[kk], p1);  // dP [i][j]
+    p2 = mfma32_bf16(v[kk], d[kk], p2);  // dP^T
+  }
+  // ---- layout 2 (i = r16, j = 4g4+r): P, D_i, dS
+  const float* lse_h = lse + h;
+  const float li2 = rok ? lse_h[(row0 + r16) * H] : 0.f;
+  float P2[4], dS2[4], Dsum = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = r16, j = 4 * g4 + r;
+    const bool ok = i < L && j < L && !(causal && j > i);
+    P2[r] = ok ? __expf(s2[r] * kScale - li2) : 0.f;
+    Dsum += P2[r] * p2[r];
+  }
+  Dsum += __shfl_xor(Dsum, 16, 64);
+  Dsum += __shfl_xor(Dsum, 32, 64);  // D_i for i = r16, in every lane of that column
+#pragma unroll
+  for (int r = 0; r < 4; ++r) dS2[r] = P2[r] * (p2[r] - Dsum);
+  // ---- layout 1 (i = 4g4+r, j = r16)
+  float P1[4], dS1[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = 4 * g4 + r, j = r16;
+    const bool ok = i < L && j < L && !(causal && j > i);
+    const float li = ok ? lse_h[(row0 + i) * H] : 0.f;
+    const float Di = __shfl(Dsum, i, 64);
+    P1[r] = ok ? __expf(s1[r] * kScale - li) : 0.f;
+    dS1[r] = P1[r] * (p1[r] - Di);
+  }
+  const s16x4 aP = pack_bf16x4(P1[0], P1[1], P1[2], P1[3]);     // A[m=j][k=i] = P[i][j]
+  const s16x4 aS = pack_bf16x4(dS1[0], dS1[1], dS1[2], dS1[3]); // A[m=j][k=i] = dS[i][j]
+  const s16x4 aT = pack_bf16x4(dS2[0], dS2[1], dS2[2], dS2[3]); // A[m=i][k=j] = dS[i][j]
+  // the tiles are wave-private: LDS ops of one wave complete in order; this wait also
+  // fences the compiler (no __syncthreads: waves of a partial block exit early above)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  TG* out = dqkv + h * 64;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const f32x4 z = {0, 0, 0, 0};
+    const f32x4 dv = mfma16_bf16(aP, tr_read(tD, 4 * g4, 16 * t, lane), z);  // [j][d]
+    const f32x4 dk = mfma16_bf16(aS, tr_read(tQ, 4 * g4, 16 * t, lane), z);  // [j][d]
+    const f32x4 dq = mfma16_bf16(aT, tr_read(tK, 4 * g4, 16 * t, lane), z);  // [i][d]
+    const int col = 16 * t + r16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * g4 + r;
+      if (row < L) {
+        TG* o = out + (row0 + row) * lddq + col;
+        o[0] = (TG)(dq[r] * kScale);
+        o[W] = (TG)(dk[r] * kScale);
+        o[2 * W] = (TG)dv[r];
+      }
+    }
+  }
+}
+
 template <typename T>
 static int launch_fwd(int nseq, int L, int H, int causal, const void* qkv, int ldq, void* out,
                       int ldo, float* lse, hipStream_t st) {
@@ -345,6 +500,14 @@ static int launch_bwd(int nseq, int L, int H, int causal, const void* qkv, int l
                       const void* ofwd, int ldof, const void* dout, int lddo, const float* lse,
                       void* dqkv, int lddq, hipStream_t st) {
   const int pairs = nseq * H;
+  if constexpr (__is_same(TG, bf16)) {
+    if (L <= 16) {
+      hipLaunchKernelGGL((attn_bwd_mfma16<T, TG>), dim3((pairs + 3) / 4), dim3(256), 0, st, nseq, L, H,
+                         causal, (const T*)qkv, ldq, (const TG*)dout, lddo, lse, (TG*)dqkv, lddq);
+      CLIPK_CHECK_LAUNCH();
+      return CLIPK_OK;
+    }
+  }
   auto go = [&](auto lp_tag) {
     constexpr int LP = decltype(lp_tag)::value;
     constexpr int G = 64 / LP;

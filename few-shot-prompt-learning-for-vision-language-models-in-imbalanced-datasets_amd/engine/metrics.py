@@ -23,9 +23,9 @@ def compute_accuracy(output, target, topk=(1,)):
     return res
 
 
-def macro_f1(y_true, y_pred, n_cls=None):
-    labels = np.unique(np.concatenate([y_true, y_pred])) if n_cls is None else None
-    labels = labels if labels is not None else np.unique(np.concatenate([y_true, y_pred]))
+def macro_f1(y_true, y_pred):
+    """sklearn f1_score(average='macro') over the labels present in y_true or y_pred."""
+    labels = np.unique(np.concatenate([y_true, y_pred]))
     f1s = []
     for c in labels:
         tp = np.sum((y_pred == c) & (y_true == c))

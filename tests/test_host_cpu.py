@@ -1,0 +1,162 @@
+"""CPU: host-side logic (no GPU compute): the C-ABI library loads and exports every
+symbol include/clipk.h declares, prompt slot tables reproduce the reference prompt
+layouts, tokenizer, config, registry, losses' alpha, metrics."""
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "clipk.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(clipk_\w+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    from fsp_amd import _native
+    lib = _native.load()
+    names = header_functions()
+    assert len(names) >= 30
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(names) == set(_native.SIGNATURES), set(names) ^ set(_native.SIGNATURES)
+    assert lib.clipk_version().decode().startswith("clipk")
+    assert "shape" in _native.strerror(-2)
+
+
+def test_missing_library_fails_loudly(monkeypatch):
+    from fsp_amd import _native
+    monkeypatch.setattr(_native, "_lib", None)
+    monkeypatch.setattr(_native, "LIB_PATH", "/nonexistent/libclipk.so")
+    with pytest.raises(_native.ClipkError):
+        _native.load()
+
+
+def test_ops_refuse_cpu_tensors():
+    from fsp_amd import ops, _native
+    with pytest.raises(_native.ClipkError):
+        ops.gemm(torch.zeros(4, 64, dtype=torch.float16), torch.zeros(128, 64, dtype=torch.float16))
+
+
+@pytest.mark.parametrize("position", ["end", "middle", "front"])
+@pytest.mark.parametrize("csc", [False, True])
+def test_prompt_layout_matches_reference_cat(position, csc):
+    from oracle import clip_oracle as O
+    from fsp_amd.trainers._fns import prompt_layout
+    rs = np.random.RandomState(0)
+    C, n_ctx, W = 6, 4, 8
+    name_lens = [1, 2, 3, 1, 4, 2]
+    eot = [1 + n_ctx + nl + 1 for nl in name_lens]
+    emb = torch.from_numpy(rs.randn(C, 77, W).astype(np.float32))
+    ctx = torch.from_numpy(rs.randn(*((C, n_ctx, W) if csc else (n_ctx, W))).astype(np.float32))
+    ref = O.coop_prompts(ctx, emb[:, :1], emb[:, 1 + n_ctx:], name_lens, position).numpy()
+    src, cpos, L = prompt_layout(C, n_ctx, name_lens, position, eot, truncate=True)
+    assert L == max(eot) + 1
+    out = np.zeros((C, L, W), np.float32)
+    for c in range(C):
+        for t in range(L):
+            m = src[c, t]
+            cv = ctx[c] if csc else ctx
+            out[c, t] = emb[c, m].numpy() if m >= 0 else cv[-1 - m].numpy()
+            if m < 0:
+                assert cpos[c, -1 - m] == t
+    np.testing.assert_array_equal(out, ref[:, :L])
+    # the EOT token sits at the tokenized argmax position in every layout
+    for c in range(C):
+        assert src[c, eot[c]] == eot[c]
+
+
+def test_tokenizer_matches_reference_probes():
+    from fsp_amd.clip.tokenizer import BPETokenizer, find_vocab
+    probes = json.load(open(os.path.join(ROOT, "tests", "golden", "tokenizer_probes.json")))
+    if find_vocab() is None:
+        pytest.skip("BPE vocab not available (reference checkout absent)")
+    tok = BPETokenizer()
+    for s, ids in probes.items():
+        assert tok.encode(s) == ids, s
+
+
+def test_tokenizer_fallback_table_covers_synthetic_prompts():
+    from fsp_amd.clip.tokenizer import BPETokenizer
+    tok = BPETokenizer.__new__(BPETokenizer)
+    tok.encoder = None
+    tok._fallback = json.load(open(os.path.join(
+        ROOT, "few-shot-prompt-learning-for-vision-language-models-in-imbalanced-datasets_amd", "clip",
+        "bpe_fallback.json")))
+    probes = json.load(open(os.path.join(ROOT, "tests", "golden", "tokenizer_probes.json")))
+    for s in ["X X X X class7.", "a photo of a class123.", "X " * 16 + "class999."]:
+        assert tok.encode(s) == probes[s]
+    with pytest.raises(KeyError):
+        tok.encode("a photo of a dog.")
+
+
+def test_tokenize_matches_golden_tokens():
+    from fsp_amd.clip.tokenizer import tokenize
+    from parity_util import load_fixture
+    meta, ref = load_fixture("cocoop_vitb16_c4")
+    names = [f"class{i}" for i in range(meta["n_cls"])]
+    toks = tokenize([meta["ctx_init"] + " " + n + "." for n in names])
+    np.testing.assert_array_equal(toks, ref["tokenized"])
+    with pytest.raises(RuntimeError):
+        tokenize("x " * 100)
+    assert tokenize("x " * 100, truncate=True)[0, -1] == 49407
+
+
+def test_config_merge_and_freeze(tmp_path):
+    from fsp_amd.engine.config import get_cfg_default
+    cfg = get_cfg_default()
+    y = tmp_path / "c.yaml"
+    y.write_text("TRAINER:\n  COCOOP:\n    N_CTX: 4\n    CTX_INIT: 'a photo of a'\nOPTIM:\n  LR: 0.002\n"
+                 "INPUT:\n  SIZE: (224, 224)\n")
+    cfg.merge_from_file(str(y))
+    cfg.merge_from_list(["TRAINER.COOP.CSC", "True", "DATASET.PER_CLASS_SHOTS", "[16, 1]", "OPTIM.MAX_EPOCH", "5"])
+    assert cfg.TRAINER.COCOOP.N_CTX == 4 and cfg.TRAINER.COOP.CSC is True
+    assert cfg.DATASET.PER_CLASS_SHOTS == [16, 1] and cfg.OPTIM.MAX_EPOCH == 5
+    assert cfg.TRAINER.COOP.get("LOSS_TYPE", "ce") == "ce"
+    cfg.freeze()
+    with pytest.raises(AttributeError):
+        cfg.SEED = 3
+
+
+def test_registry_semantics():
+    from fsp_amd.engine.registry import Registry, TRAINER_REGISTRY
+    import fsp_amd.trainers  # noqa: F401
+    assert {"CoOp", "CoCoOp"} <= set(TRAINER_REGISTRY.registered_names())
+    r = Registry("X")
+
+    @r.register()
+    class A:
+        pass
+    with pytest.raises(KeyError):
+        r.register(A)
+    with pytest.raises(KeyError):
+        r.get("B")
+
+
+def test_focal_alpha_semantics():
+    from fsp_amd.trainers.losses import focal_alpha
+    assert focal_alpha([4, 1, 2, 0, 3], 5, zero_guard=True)[3] == 0.0
+    with pytest.raises(ZeroDivisionError):
+        focal_alpha([4, 0], 2, zero_guard=False)
+    assert focal_alpha("[2,2]", 2, True) == [1.0, 1.0]
+    assert focal_alpha([], 2, True) is None
+
+
+def test_metrics_match_sklearn():
+    from sklearn.metrics import f1_score
+    from fsp_amd.engine.metrics import macro_f1, compute_accuracy, base_new_accuracy
+    rs = np.random.RandomState(0)
+    y, p = rs.randint(0, 7, 200), rs.randint(0, 7, 200)
+    assert abs(macro_f1(y, p) - f1_score(y, p, average="macro")) < 1e-12
+    logits = torch.from_numpy(rs.randn(10, 5))
+    lab = torch.from_numpy(rs.randint(0, 5, 10))
+    acc = compute_accuracy(logits, lab)[0].item()
+    assert abs(acc - 100 * (logits.argmax(1) == lab).double().mean().item()) < 1e-4
+    b, n, hm = base_new_accuracy(np.array([0, 1, 3, 3]), np.array([0, 2, 3, 2]), 2)
+    assert b == 100.0 and abs(n - 100 / 3) < 1e-9 and abs(hm - 2 * 100 * (100 / 3) / (100 + 100 / 3)) < 1e-9
