@@ -5,9 +5,10 @@
 // the input-grad GEMMs (pre-packed once, so backward is the same "NT" form).
 //
 // gfx950 design:
-//  * 256 threads = 4 waves (2x2), block tile 128x128, K staged 128 bytes per row
-//    (64 halfs or 32 floats) into a 2-stage LDS ring by global_load_lds_dwordx4 (glds):
-//    one wave-instruction = 8 rows x 128 B = 1 KiB, lane-linear in LDS.
+//  * Block tiles 256x256 / 256x128 (8 waves) for the large-M text GEMMs, 128x128
+//    (4 waves) otherwise; K staged 128 bytes per row (64 halfs or 32 floats) into a 2-stage
+//    LDS ring by global_load_lds_dwordx4 (glds): one wave-instruction = 8 rows x 128 B
+//    = 1 KiB, lane-linear in LDS.
 //  * LDS image row-swizzled on the SOURCE address (glds writes lane-linear): physical
 //    16-B chunk p = c ^ ((row >> 1) & 7). With rows = lane&15 read by ds_read_b128 this
 //    puts each 16-lane group on 16 distinct 16-B slots of the 256-B bank row (no conflict).
@@ -17,16 +18,14 @@
 //    float4 bias/residual loads.
 //  * XCD-aware bijective block remap: consecutive tiles of one A row-panel run on one XCD
 //    so the panel is fetched from HBM once and re-read from that XCD's L2.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace clipk {
 
-constexpr int GEMM_BM = 128;
-constexpr int GEMM_BN = 128;
-constexpr int GEMM_ROWB = 128;                         // bytes per staged row (BK)
-constexpr int GEMM_OPB = GEMM_BM * GEMM_ROWB;          // 16 KiB per operand per stage
-constexpr int GEMM_STAGEB = 2 * GEMM_OPB;              // A + B
-constexpr int GEMM_LDS = 2 * GEMM_STAGEB;              // 2 stages = 64 KiB
+constexpr int GEMM_ROWB = 128;  // bytes per staged row (BK = 64 halfs / 32 floats)
+constexpr int GEMM_NMIN = 128;  // N granularity accepted by the C-ABI
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -63,121 +62,238 @@ __device__ __forceinline__ void glds16(const char* src, char* lds_wave_base) {
       (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-template <typename T, typename TO, typename TX, int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
-  __shared__ CLIPK_LDS_ALIGN char smem[GEMM_LDS];
+// Block tile BM x BN, WM x WN waves (each (BM/WM) x (BN/WN) = TM x TN 16x16 sub-tiles),
+// 2-stage LDS ring, one barrier per 128-byte K step. PERSIST: the grid is sized to the
+// CU count and each block walks an XCD-contiguous run of tiles; the last K step of a tile
+// prefetches the first stage of the next tile, so that load overlaps the epilogue.
+template <typename T, typename TO, typename TX, int EPI, int BM, int BN, int WM, int WN, bool PERSIST>
+__global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int OPA = BM * GEMM_ROWB, OPB = BN * GEMM_ROWB, STAGE = OPA + OPB;
+  constexpr int IA = BM / 8 / NW, IB = BN / 8 / NW;  // glds (8 rows x 128 B) per wave per stage
+  static_assert(IA >= 1 && IB >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile/wave mismatch");
+  __shared__ CLIPK_LDS_ALIGN char smem[2 * STAGE];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
-  // ---- XCD-aware bijective tile remap (tiles of one A row-panel share an XCD).
-  const int ntn = g.N / GEMM_BN;
-  const int ntm = (g.M + GEMM_BM - 1) / GEMM_BM;
+  // ---- XCD-aware bijective tile split: XCD group x owns tiles [t_beg, t_end) (row-panel
+  // major, so the tiles sharing an A panel run on one XCD and re-read it from its L2).
+  const int ntn = g.N / BN;
+  const int ntm = (g.M + BM - 1) / BM;
   const int nwg = ntm * ntn;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int m0 = (wgid / ntn) * GEMM_BM;
-  const int n0 = (wgid % ntn) * GEMM_BN;
+  const int t_beg = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  const int t_end = t_beg + (xcd < r ? q + 1 : q);
+  const int t_step = PERSIST ? (int)(gridDim.x >> 3) : 1;
+  int tile = t_beg + (bid >> 3);
+  if (tile >= t_end) return;  // block-uniform
 
-  // ---- staging addresses: this wave stages rows [w*32, w*32+32) of A and of B.
   const size_t esz = sizeof(T);
-  const char* srcA[4];
-  const char* srcB[4];
+  const int nk = (int)((size_t)g.K * esz / GEMM_ROWB);
+  const char* srcA[IA];
+  const char* srcB[IB];
+  auto set_tile = [&](int t) {
+    const int tm0 = (t / ntn) * BM, tn0 = (t % ntn) * BN;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = w * 32 + i * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ ((row >> 1) & 7);
-    int ga = m0 + row;
-    ga = ga < g.M ? ga : g.M - 1;
-    srcA[i] = g.A + ((size_t)ga * g.lda) * esz + c * 16;
-    srcB[i] = g.B + ((size_t)(n0 + row) * g.ldb) * esz + c * 16;
-  }
-  auto stage = [&](int s, int kt) {
-    char* base = smem + s * GEMM_STAGEB;
-    const size_t koff = (size_t)kt * GEMM_ROWB;
+    for (int i = 0; i < IA; ++i) {
+      const int row = (w * IA + i) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);  // source-side swizzle
+      int ga = tm0 + row;
+      ga = ga < g.M ? ga : g.M - 1;
+      srcA[i] = g.A + ((size_t)ga * g.lda) * esz + c * 16;
+    }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      glds16(srcA[i] + koff, base + (w * 32 + i * 8) * GEMM_ROWB);
-      glds16(srcB[i] + koff, base + GEMM_OPB + (w * 32 + i * 8) * GEMM_ROWB);
+    for (int i = 0; i < IB; ++i) {
+      const int row = (w * IB + i) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      srcB[i] = g.B + ((size_t)(tn0 + row) * g.ldb) * esz + c * 16;
     }
   };
+  auto stage = [&](int s, int kt) {
+    char* base = smem + s * STAGE;
+    const size_t koff = (size_t)kt * GEMM_ROWB;
+#pragma unroll
+    for (int i = 0; i < IA; ++i) glds16(srcA[i] + koff, base + (w * IA + i) * 8 * GEMM_ROWB);
+#pragma unroll
+    for (int i = 0; i < IB; ++i) glds16(srcB[i] + koff, base + OPA + (w * IB + i) * 8 * GEMM_ROWB);
+  };
 
-  const int wm = w >> 1, wn = w & 1;
+  const int wm = w / WN, wn = w % WN;
   const int fr = lane & 15;         // fragment row within a 16-row sub-tile
   const int fq = lane >> 4;         // 16-B chunk within a 64-B k-window
-  const int sw = (fr >> 1) & 7;     // row swizzle (row base is a multiple of 16)
+  const int sw = (fr >> 1) & 7;     // row swizzle (sub-tile row base is a multiple of 16)
+  constexpr bool HAS_BIAS = EPI == CLIPK_EPI_BIAS || EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_BIAS_QGELU;
 
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const int nk = (int)((size_t)g.K * esz / GEMM_ROWB);
+  set_tile(tile);
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  int it = 0;  // global K-step counter (LDS buffer = it & 1)
 
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
-    const char* As = smem + cur * GEMM_STAGEB + (wm * 64 + fr) * GEMM_ROWB;
-    const char* Bs = smem + cur * GEMM_STAGEB + GEMM_OPB + (wn * 64 + fr) * GEMM_ROWB;
+  while (true) {
+    const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+    const int next = tile + t_step;
+    const bool has_next = PERSIST && next < t_end;
+    f32x4 acc[TM][TN];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int p = ((kk * 4 + fq) ^ sw) * 16;
-      u32x4 a[4], b[4];
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const u32x4*>(As + i * 16 * GEMM_ROWB + p);
+      for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    for (int kt = 0; kt < nk; ++kt, ++it) {
+      const int cur = it & 1;
+      const bool last = kt + 1 == nk;
+      if (!last) {
+        stage(cur ^ 1, kt + 1);
+      } else if (has_next) {
+        set_tile(next);
+        stage(cur ^ 1, 0);  // next tile's first stage flies during this tile's epilogue
+      }
+      const char* As = smem + cur * STAGE + (wm * (BM / WM) + fr) * GEMM_ROWB;
+      const char* Bs = smem + cur * STAGE + OPA + (wn * (BN / WN) + fr) * GEMM_ROWB;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const u32x4*>(Bs + j * 16 * GEMM_ROWB + p);
+      for (int kk = 0; kk < 2; ++kk) {
+        const int p = ((kk * 4 + fq) ^ sw) * 16;
+        u32x4 a[TM], b[TN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const u32x4*>(Bs + j * 16 * GEMM_ROWB + p);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mma<T>(b[j], a[i], acc[i][j]);
+        for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const u32x4*>(As + i * 16 * GEMM_ROWB + p);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mma<T>(b[j], a[i], acc[i][j]);
+      }
+      if (!last) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
     }
+
+    // ---- epilogue: lane holds C[m][n..n+3] per sub-tile; operands (bias, residual, aux)
+    // are loaded up front per chunk of 4 sub-tile rows so their HBM latencies overlap.
+    const int nb = n0 + wn * (BN / WN) + fq * 4;
+    f32x4 bia[TN];
+    if constexpr (HAS_BIAS) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bia[j] = *reinterpret_cast<const f32x4*>(g.bias + nb + j * 16);
+    }
+    constexpr int EC = (EPI == CLIPK_EPI_BIAS_RES && TM * TN > 16) ? 2 : 4;  // rows per chunk
+#pragma unroll
+    for (int ic = 0; ic < TM; ic += EC) {
+      int mrow[EC];
+#pragma unroll
+      for (int i = 0; i < EC; ++i) mrow[i] = m0 + wm * (BM / WM) + (ic + i) * 16 + fr;
+      f32x4 ext[EC][TN];
+      if constexpr (EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU) {
+#pragma unroll
+        for (int i = 0; i < EC; ++i) {
+          const int mc = mrow[i] < g.M ? mrow[i] : g.M - 1;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            if constexpr (EPI == CLIPK_EPI_BIAS_RES) {
+              ext[i][j] = *reinterpret_cast<const f32x4*>(g.res + (size_t)mc * g.ldr + nb + j * 16);
+            } else {
+              float hv[4];
+              load4<TX>((const TX*)g.aux + (size_t)mc * g.ldaux + nb + j * 16, hv);
+              ext[i][j] = (f32x4){hv[0], hv[1], hv[2], hv[3]};
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < EC; ++i) {
+        const int m = mrow[i];
+        if (m >= g.M) continue;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = nb + j * 16;
+          f32x4 v = acc[ic + i][j];
+          if constexpr (HAS_BIAS) v += bia[j];
+          if constexpr (EPI == CLIPK_EPI_BIAS_RES) {
+            *reinterpret_cast<f32x4*>((float*)g.out + (size_t)m * g.ldo + n) = v + ext[i][j];
+          } else if constexpr (EPI == CLIPK_EPI_BIAS_QGELU) {
+            if (g.out2) store4<TO>((TO*)g.out2 + (size_t)m * g.ldo + n, v[0], v[1], v[2], v[3]);
+            store4<TO>((TO*)g.out + (size_t)m * g.ldo + n, quick_gelu(v[0]), quick_gelu(v[1]),
+                       quick_gelu(v[2]), quick_gelu(v[3]));
+          } else if constexpr (EPI == CLIPK_EPI_DQGELU) {
+            const f32x4 hv = ext[i][j];
+            store4<TO>((TO*)g.out + (size_t)m * g.ldo + n, v[0] * quick_gelu_grad(hv[0]),
+                       v[1] * quick_gelu_grad(hv[1]), v[2] * quick_gelu_grad(hv[2]),
+                       v[3] * quick_gelu_grad(hv[3]));
+          } else {
+            store4<TO>((TO*)g.out + (size_t)m * g.ldo + n, v[0], v[1], v[2], v[3]);
+          }
+        }
+      }
+    }
+    if (!has_next) break;
+    tile = next;
+    ++it;  // the last K step of this tile was it-1; the prefetched stage is buffer it & 1
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+}
 
-  // ---- epilogue: lane holds C[m][n..n+3]
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + wm * 64 + i * 16 + fr;
-    if (m >= g.M) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + fq * 4;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if constexpr (EPI == CLIPK_EPI_BIAS || EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_BIAS_QGELU) {
-        f32x4 bb = *reinterpret_cast<const f32x4*>(g.bias + n);
-        v[0] += bb[0]; v[1] += bb[1]; v[2] += bb[2]; v[3] += bb[3];
-      }
-      if constexpr (EPI == CLIPK_EPI_BIAS_RES) {
-        const f32x4 rr = *reinterpret_cast<const f32x4*>(g.res + (size_t)m * g.ldr + n);
-        f32x4 o = {v[0] + rr[0], v[1] + rr[1], v[2] + rr[2], v[3] + rr[3]};
-        *reinterpret_cast<f32x4*>((float*)g.out + (size_t)m * g.ldo + n) = o;
-      } else if constexpr (EPI == CLIPK_EPI_BIAS_QGELU) {
-        if (g.out2) store4<TO>((TO*)g.out2 + (size_t)m * g.ldo + n, v[0], v[1], v[2], v[3]);
-        store4<TO>((TO*)g.out + (size_t)m * g.ldo + n, quick_gelu(v[0]), quick_gelu(v[1]),
-                   quick_gelu(v[2]), quick_gelu(v[3]));
-      } else if constexpr (EPI == CLIPK_EPI_DQGELU) {
-        float h[4];
-        load4<TX>((const TX*)g.aux + (size_t)m * g.ldaux + n, h);
-        store4<TO>((TO*)g.out + (size_t)m * g.ldo + n, v[0] * quick_gelu_grad(h[0]),
-                   v[1] * quick_gelu_grad(h[1]), v[2] * quick_gelu_grad(h[2]),
-                   v[3] * quick_gelu_grad(h[3]));
-      } else {
-        store4<TO>((TO*)g.out + (size_t)m * g.ldo + n, v[0], v[1], v[2], v[3]);
-      }
-    }
+// Tile configurations: 0 = 128x128 (4 waves, 64 KiB LDS, 2 blocks/CU),
+// 1 = 256x256 (8 waves, 128 KiB, persistent when the grid exceeds 2 waves of CUs),
+// 2 = 256x128 (8 waves, 96 KiB), 3 = 256x256 non-persistent (benchmark knob).
+static int g_force_cfg = -2;  // -2: unread, -1: auto
+static int pick_cfg(int M, int N, int esz) {
+  if (g_force_cfg == -2) {
+    const char* e = getenv("CLIPK_GEMM_CFG");
+    g_force_cfg = e ? atoi(e) : -1;
   }
+  if (esz == 4) return 0;  // fp32 parity path: one configuration
+  if (g_force_cfg >= 0) {
+    if ((g_force_cfg == 1 || g_force_cfg == 3) && N % 256 == 0) return g_force_cfg;
+    if (g_force_cfg == 2) return 2;
+    return 0;
+  }
+  if (M >= 4096 && N % 256 == 0) return 1;  // measured best for every text GEMM shape
+  return 0;
+}
+
+static int g_num_cus = 0;
+static int num_cus() {
+  if (!g_num_cus) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      g_num_cus = n;
+    else
+      g_num_cus = 256;
+  }
+  return g_num_cus;
 }
 
 template <typename T, typename TO, typename TX, int EPI>
 static int launch_gemm(const GemmArgs& g, hipStream_t st) {
-  const int nwg = ((g.M + GEMM_BM - 1) / GEMM_BM) * (g.N / GEMM_BN);
-  hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI>), dim3(nwg), dim3(256), 0, st, g);
+  const int cfg = pick_cfg(g.M, g.N, (int)sizeof(T));
+  if constexpr (sizeof(T) == 4) {
+    const int nwg = ((g.M + 127) / 128) * (g.N / 128);
+    hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 128, 2, 2, false>), dim3(nwg), dim3(256), 0, st, g);
+  } else {
+    if (cfg == 1 || cfg == 3) {
+      const int nwg = ((g.M + 255) / 256) * (g.N / 256);
+      const int cus = num_cus();
+      if (cfg == 1 && nwg > 2 * cus) {
+        // persistent: one 8-wave block per CU, grid a multiple of 8 (XCD groups)
+        const int grid = (cus / 8) * 8;
+        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 256, 2, 4, true>), dim3(grid), dim3(512), 0, st, g);
+      } else {
+        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 256, 2, 4, false>), dim3(nwg), dim3(512), 0, st, g);
+      }
+    } else if (cfg == 2) {
+      const int nwg = ((g.M + 255) / 256) * (g.N / 128);
+      hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 128, 4, 2, false>), dim3(nwg), dim3(512), 0, st, g);
+    } else {
+      const int nwg = ((g.M + 127) / 128) * (g.N / 128);
+      hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 128, 2, 2, false>), dim3(nwg), dim3(256), 0, st, g);
+    }
+  }
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
 }
@@ -226,7 +342,7 @@ extern "C" int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, in
   if (!A || !B || !out) return CLIPK_EINVAL;
   if (M <= 0) return M == 0 ? CLIPK_OK : CLIPK_ESHAPE;
   const int esz = in_dtype == CLIPK_F32 ? 4 : 2;
-  if (N <= 0 || K <= 0 || N % GEMM_BN != 0 || (K * esz) % GEMM_ROWB != 0) return CLIPK_ESHAPE;
+  if (N <= 0 || K <= 0 || N % GEMM_NMIN != 0 || (K * esz) % GEMM_ROWB != 0) return CLIPK_ESHAPE;
   if (lda < K || ldb < K || (lda * esz) % 16 || (ldb * esz) % 16 || ldo < N || ldo % 4)
     return CLIPK_ESHAPE;
   if ((epi == CLIPK_EPI_BIAS || epi == CLIPK_EPI_BIAS_RES || epi == CLIPK_EPI_BIAS_QGELU) && !bias)
@@ -242,4 +358,11 @@ extern "C" int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, in
     case CLIPK_F32: return dispatch_out<float>(out_dtype, epi, aux_dtype, g, st);
     default: return CLIPK_EDTYPE;
   }
+}
+
+// Benchmark knob: force a tile configuration (-1 = automatic choice).
+extern "C" int clipk_gemm_set_config(int cfg) {
+  if (cfg < -1 || cfg > 3) return CLIPK_EINVAL;
+  g_force_cfg = cfg;
+  return CLIPK_OK;
 }

@@ -72,6 +72,10 @@ int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, int K,
                void* out, int ldo, void* out2, const void* aux, int aux_dtype, int ldaux,
                void* stream);
 
+/* Benchmark knob: force the 16-bit GEMM tile configuration (0: 128x128, 1: 256x256,
+ * 2: 256x128; -1 = automatic by shape). Not needed for normal use. */
+int clipk_gemm_set_config(int cfg);
+
 /* y = LN(x[row]) for rows r in [0,rows): x row = in_rows ? in_rows[r] : r.
  * out of out_dtype with row stride ldo; mean/rstd (optional, fp32 [rows]). width%64==0, <=1024 */
 int clipk_layernorm_fwd(int out_dtype, int rows, int width, const float* x, int ldx,
