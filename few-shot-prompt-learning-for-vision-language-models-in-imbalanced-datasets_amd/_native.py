@@ -31,7 +31,7 @@ SIGNATURES = {
     "clipk_gemm": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P, _I, _I, _P]),
     "clipk_gemm_set_config": (_I, [_I]),
     "clipk_layernorm_fwd": (_I, [_I, _I, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P]),
-    "clipk_layernorm_bwd": (_I, [_I, _I, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P]),
+    "clipk_layernorm_bwd": (_I, [_I, _I, _I, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P]),
     "clipk_attention_fwd": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P]),
     "clipk_attention_bwd": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _I, _P, _P, _I, _P]),
     "clipk_im2col": (_I, [_I, _I, _I, _I, _I, _P, _P, _P]),

@@ -472,6 +472,133 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma16(int nseq, int L, int H, i
   }
 }
 
+// ------------------------------------------------------------------ forward, MFMA (any L)
+// Flash-style forward on MFMA for 16-bit operands: block = 4 waves = 64 query rows of one
+// (seq, head); keys streamed through LDS in chunks of 64 (K and V tiles, row-major).
+// Per 16-key sub-chunk: S^T = K Q^T (16x16x32; query on the lane, keys in registers),
+// online softmax per query, O += P V (16x16x16 with P from the S^T registers as the A
+// operand and V through ds_read_b64_tr_b16).
+template <typename T>
+__device__ __forceinline__ f32x4 mfma32_t(s16x8 a, s16x8 b, f32x4 c) {
+  if constexpr (__is_same(T, f16))
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+template <typename T>
+__device__ __forceinline__ f32x4 mfma16_t(s16x4 a, s16x4 b, f32x4 c) {
+  if constexpr (__is_same(T, f16)) {
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    return __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h4, a), __builtin_bit_cast(h4, b), c, 0, 0, 0);
+  } else {
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+  }
+}
+template <typename T>
+__device__ __forceinline__ s16x4 pack4(float a, float b, float c, float d) {
+  typedef T t4 __attribute__((ext_vector_type(4)));
+  t4 v = {(T)a, (T)b, (T)c, (T)d};
+  return __builtin_bit_cast(s16x4, v);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_fwd_mfma(int nseq, int L, int H, int causal,
+                                                     const T* __restrict__ qkv, int ldq,
+                                                     T* __restrict__ out, int ldo,
+                                                     float* __restrict__ lse) {
+  __shared__ CLIPK_LDS_ALIGN short sK[64 * TRS];
+  __shared__ CLIPK_LDS_ALIGN short sV[64 * TRS];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int h = blockIdx.y, s = blockIdx.z;
+  const int W = H * 64;
+  const size_t row0 = (size_t)s * L;
+  const int q0 = blockIdx.x * 64 + w * 16;
+  // Q fragments (B operand of S^T = K Q^T): row q0+r16, 16-B chunks g4 and g4+4
+  const int qr = q0 + r16;
+  const bool qok = qr < L;
+  const T* qp = qkv + (row0 + (qok ? qr : 0)) * ldq + h * 64;
+  s16x8 qf[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) qf[kk] = ld_row16(qp + 8 * g4 + 32 * kk, qok);
+
+  f32x4 o[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) o[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;  // for query r16 (replicated over g4)
+  const int qmax = min(L, (int)(blockIdx.x + 1) * 64) - 1;
+  const int kend = causal ? qmax + 1 : L;
+  for (int k0 = 0; k0 < kend; k0 += 64) {
+    __syncthreads();
+    // cooperative load: 64 rows x 128 B of K and of V (2 x 16 B per thread each)
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int idx = it * 256 + tid;
+      const int rr = idx >> 3, ch = idx & 7;
+      const int kr = k0 + rr;
+      const bool ok = kr < L;
+      const T* base = qkv + (row0 + (ok ? kr : 0)) * ldq + h * 64 + ch * 8;
+      *reinterpret_cast<s16x8*>(sK + rr * TRS + ch * 8) = ld_row16(base + W, ok);
+      *reinterpret_cast<s16x8*>(sV + rr * TRS + ch * 8) = ld_row16(base + 2 * W, ok);
+    }
+    __syncthreads();
+    const int nsub = min(4, (kend - k0 + 15) / 16);
+    for (int sc = 0; sc < nsub; ++sc) {
+      f32x4 st = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const s16x8 kf = *reinterpret_cast<const s16x8*>(sK + (sc * 16 + r16) * TRS + 8 * g4 + 32 * kk);
+        st = mfma32_t<T>(kf, qf[kk], st);  // st[r] = S[q = r16][key = k0 + sc*16 + 4g4 + r]
+      }
+      float sv[4], mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + sc * 16 + 4 * g4 + r;
+        float v = st[r] * kScale;
+        if (key >= L || (causal && key > qr)) v = -INFINITY;
+        sv[r] = v;
+        mx = fmaxf(mx, v);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m, mx);
+      const float corr = mn == -INFINITY ? 1.f : __expf(m - mn);
+      float p[4], ps = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        p[r] = mn == -INFINITY ? 0.f : __expf(sv[r] - mn);
+        ps += p[r];
+      }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      l = l * corr + ps;
+      m = mn;
+      // rescale O rows (query 4g4+r) by that query's corr
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float c = __shfl(corr, 4 * g4 + r, 64);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) o[t][r] *= c;
+      }
+      const s16x4 pa = pack4<T>(p[0], p[1], p[2], p[3]);  // A[m=query r16][k=key 4g4+jj]
+#pragma unroll
+      for (int t = 0; t < 4; ++t) o[t] = mfma16_t<T>(pa, tr_read(sV, sc * 16 + 4 * g4, 16 * t, lane), o[t]);
+    }
+  }
+  // normalise and store rows q0 + 4g4 + r
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int q = q0 + 4 * g4 + r;
+    const float inv = 1.0f / __shfl(l, 4 * g4 + r, 64);
+    if (q < L) {
+      T* op = out + (row0 + q) * ldo + h * 64 + r16;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) op[16 * t] = (T)(o[t][r] * inv);
+    }
+  }
+  if (lse && g4 == 0 && qok) lse[(row0 + qr) * H + h] = m + __logf(l);
+}
+
 template <typename T>
 static int launch_fwd(int nseq, int L, int H, int causal, const void* qkv, int ldq, void* out,
                       int ldo, float* lse, hipStream_t st) {
@@ -483,6 +610,15 @@ static int launch_fwd(int nseq, int L, int H, int causal, const void* qkv, int l
     hipLaunchKernelGGL((attn_fwd_short<LP, T>), dim3(blocks), dim3(256), 0, st, nseq, L, H, causal,
                        (const T*)qkv, ldq, (T*)out, ldo, lse);
   };
+  if constexpr (sizeof(T) == 2) {
+    if (L > 16) {  // MFMA flash forward (vision L = 50..577, text 16 < L <= 77)
+      dim3 grid((L + 63) / 64, H, nseq);
+      hipLaunchKernelGGL((attn_fwd_mfma<T>), grid, dim3(256), 0, st, nseq, L, H, causal, (const T*)qkv, ldq,
+                         (T*)out, ldo, lse);
+      CLIPK_CHECK_LAUNCH();
+      return CLIPK_OK;
+    }
+  }
   if (L <= 16) short_launch(std::integral_constant<int, 16>{});
   else if (L <= 32) short_launch(std::integral_constant<int, 32>{});
   else if (L <= 64) short_launch(std::integral_constant<int, 64>{});

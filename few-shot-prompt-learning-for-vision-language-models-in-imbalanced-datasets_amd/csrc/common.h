@@ -119,11 +119,13 @@ __device__ __forceinline__ float group_max(float v) {
 }
 
 // QuickGELU (PromptSRC/clip/model.py:162-164): x * sigmoid(1.702 x), and its derivative.
+// v_exp_f32 + v_rcp_f32 (1 ulp) instead of an IEEE division: these run per output element
+// in the GEMM epilogues, where a full-precision divide costed ~10 VALU instructions.
 __device__ __forceinline__ float quick_gelu(float x) {
-  return x / (1.0f + __expf(-1.702f * x));
+  return x * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * x));
 }
 __device__ __forceinline__ float quick_gelu_grad(float x) {
-  float s = 1.0f / (1.0f + __expf(-1.702f * x));
+  const float s = __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * x));
   return s + 1.702f * x * s * (1.0f - s);
 }
 

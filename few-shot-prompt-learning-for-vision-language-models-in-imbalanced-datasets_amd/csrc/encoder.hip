@@ -140,8 +140,8 @@ static TextBufs text_layout(const clipk_encoder* e, int nseq, int L, void* saved
 }
 
 struct TextBwdBufs {
-  void *dtg, *dX_lp, *dh, *do_, *dqkv;
-  float *dlnf, *dxn;
+  void *dtg, *dX_lp, *dh, *do_, *dqkv, *dxn;  // dxn: LN-output grads in the grad dtype
+  float* dlnf;
   size_t bytes;
 };
 
@@ -153,7 +153,7 @@ static TextBwdBufs text_bwd_layout(const clipk_encoder* e, int nseq, int L, void
   b.dlnf = (float*)c.take((size_t)nseq * W * 4);
   b.dX_lp = c.take(rows * W * g);
   b.dh = c.take(rows * 4 * W * g);
-  b.dxn = (float*)c.take(rows * W * 4);
+  b.dxn = c.take(rows * W * g);
   b.do_ = c.take(rows * W * g);
   b.dqkv = c.take(rows * 3 * W * g);
   b.bytes = c.off;
@@ -322,7 +322,7 @@ extern "C" int clipk_text_backward(const clipk_encoder* e, int nseq, int L, cons
   if (hipMemsetAsync(dX, 0, (size_t)rows * W * 4, st) != hipSuccess) return (int)hipGetLastError();
   if (hipMemsetAsync(b.dX_lp, 0, (size_t)rows * W * esize(gd), st) != hipSuccess)
     return (int)hipGetLastError();
-  TRY(clipk_layernorm_bwd(nseq, W, b.dlnf, W, t.Xf, W, eot_rows, (const float*)e->head[0], t.meanf,
+  TRY(clipk_layernorm_bwd(CLIPK_F32, nseq, W, b.dlnf, W, t.Xf, W, eot_rows, (const float*)e->head[0], t.meanf,
                           t.rstdf, nullptr, W, dX, b.dX_lp, gd, eot_rows, W, st));
   for (int l = e->layers - 1; l >= 0; --l) {
     const auto& w = e->lw[l];
@@ -330,9 +330,9 @@ extern "C" int clipk_text_backward(const clipk_encoder* e, int nseq, int L, cons
     // MLP: dg = dX . Wproj ; dh = dg * qgelu'(h)
     TRY(gemm(gd, gd, CLIPK_EPI_DQGELU, rows, 4 * W, W, b.dX_lp, w[15], nullptr, nullptr, b.dh, nullptr,
              t.h[l], act, st, CLIPK_PROF_GEMM_DGELU));
-    TRY(gemm(gd, CLIPK_F32, CLIPK_EPI_NONE, rows, W, 4 * W, b.dh, w[14], nullptr, nullptr, b.dxn, nullptr,
+    TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, 4 * W, b.dh, w[14], nullptr, nullptr, b.dxn, nullptr,
              nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
-    TRY(clipk_layernorm_bwd(rows, W, b.dxn, W, t.Xm[l], W, nullptr, (const float*)w[6], t.mean2[l],
+    TRY(clipk_layernorm_bwd(gd, rows, W, b.dxn, W, t.Xm[l], W, nullptr, (const float*)w[6], t.mean2[l],
                             t.rstd2[l], dX, W, dX, b.dX_lp, gd, nullptr, W, st));
     // attention: do = dXm . Wout ; dqkv ; dxn1 = dqkv . Win
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, W, b.dX_lp, w[13], nullptr, nullptr, b.do_, nullptr,
@@ -342,9 +342,9 @@ extern "C" int clipk_text_backward(const clipk_encoder* e, int nseq, int L, cons
       TRY(clipk_attention_bwd(act, gd, nseq, L, e->heads, 1, t.qkv[l], 3 * W, t.o[l], W, b.do_, W,
                               t.lse[l], b.dqkv, 3 * W, st));
     }
-    TRY(gemm(gd, CLIPK_F32, CLIPK_EPI_NONE, rows, W, 3 * W, b.dqkv, w[12], nullptr, nullptr, b.dxn,
+    TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, 3 * W, b.dqkv, w[12], nullptr, nullptr, b.dxn,
              nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
-    TRY(clipk_layernorm_bwd(rows, W, b.dxn, W, t.X[l], W, nullptr, (const float*)w[0], t.mean1[l],
+    TRY(clipk_layernorm_bwd(gd, rows, W, b.dxn, W, t.X[l], W, nullptr, (const float*)w[0], t.mean1[l],
                             t.rstd1[l], dX, W, dX, l > 0 ? b.dX_lp : nullptr, gd, nullptr, W, st));
   }
   return CLIPK_OK;

@@ -237,6 +237,153 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
   }
 }
 
+// 256x256 persistent GEMM with a 4-stage LDS ring of 32-deep K steps (64-B rows) and
+// counted vmcnt: three stages (96 KiB) stay in flight while one is consumed, instead of the
+// 2-stage ring's single 64 KiB stage per barrier. The stage stream runs across tile
+// boundaries, so the next tile's first stages load during this tile's epilogue.
+// 64-B rows: physical chunk p = c ^ (((row >> 3) & 1) * 3) makes the ds_read_b128 16-lane
+// groups (rows fr, chunk fq) conflict-free; glds writes lane-linear, so the swizzle is
+// applied on the source address.
+template <typename T, typename TO, typename TX, int EPI>
+__global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g) {
+  constexpr int BM = 256, BN = 256, WM = 2, WN = 4, TM = 8, TN = 4, ROW = 64, NST = 4;
+  constexpr int OPA = BM * ROW, STAGE = (BM + BN) * ROW;  // 32 KiB per stage
+  __shared__ CLIPK_LDS_ALIGN char smem[NST * STAGE];      // 128 KiB
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ntn = g.N / BN;
+  const int ntm = (g.M + BM - 1) / BM;
+  const int nwg = ntm * ntn;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int t_beg = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int t_end = t_beg + (xcd < r8 ? q8 + 1 : q8);
+  const int t_step = gridDim.x >> 3;
+  const int t0 = t_beg + (bid >> 3);
+  if (t0 >= t_end) return;  // block-uniform
+  const int ntiles = (t_end - t0 + t_step - 1) / t_step;
+  const size_t esz = sizeof(T);
+  const int nk = (int)((size_t)g.K * esz / ROW);
+  const int total = ntiles * nk;
+
+  // ---- issue the 4 glds (2 A + 2 B, 16 rows x 64 B each) of stage q of this block's stream
+  auto issue = [&](int q) {
+    const int j = q / nk, kt = q - j * nk;
+    const int t = t0 + j * t_step;
+    const int tm0 = (t / ntn) * BM, tn0 = (t % ntn) * BN;
+    char* base = smem + (q & (NST - 1)) * STAGE;
+    const size_t koff = (size_t)kt * ROW;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (w * 2 + i) * 16 + (lane >> 2);
+      const int c = (lane & 3) ^ (((row >> 3) & 1) * 3);
+      int ga = tm0 + row;
+      ga = ga < g.M ? ga : g.M - 1;
+      glds16(g.A + ((size_t)ga * g.lda) * esz + koff + c * 16, base + (w * 2 + i) * 16 * ROW);
+      glds16(g.B + ((size_t)(tn0 + row) * g.ldb) * esz + koff + c * 16, base + OPA + (w * 2 + i) * 16 * ROW);
+    }
+  };
+
+  const int wm = w / WN, wn = w % WN;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int pch = (fq ^ (((fr >> 3) & 1) * 3)) * 16;  // physical chunk byte offset
+  constexpr bool HAS_BIAS = EPI == CLIPK_EPI_BIAS || EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_BIAS_QGELU;
+
+  issue(0);
+  if (total > 1) issue(1);
+  if (total > 2) issue(2);
+  f32x4 acc[TM][TN];
+  for (int q = 0; q < total; ++q) {
+    const int j = q / nk, kt = q - j * nk;
+    if (kt == 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < TN; ++jj) acc[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    // stage q landed (this wave): younger stages q+1, q+2 may stay in flight
+    const int younger = min(2, total - 1 - q);
+    if (kt == 0 && q > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // epilogue stores
+    else if (younger == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage q visible to all waves; stage q-1's buffer is free
+    if (q + 3 < total) issue(q + 3);
+    const char* As = smem + (q & (NST - 1)) * STAGE + (wm * (BM / WM) + fr) * ROW + pch;
+    const char* Bs = smem + (q & (NST - 1)) * STAGE + OPA + (wn * (BN / WN) + fr) * ROW + pch;
+    u32x4 a[TM], b[TN];
+#pragma unroll
+    for (int jj = 0; jj < TN; ++jj) b[jj] = *reinterpret_cast<const u32x4*>(Bs + jj * 16 * ROW);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const u32x4*>(As + i * 16 * ROW);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < TN; ++jj) acc[i][jj] = mma<T>(b[jj], a[i], acc[i][jj]);
+
+    if (kt != nk - 1) continue;
+    // ---- epilogue of tile t (same math as gemm_nt_kernel)
+    const int t = t0 + j * t_step;
+    const int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
+    const int nb = n0 + wn * (BN / WN) + fq * 4;
+    f32x4 bia[TN];
+    if constexpr (HAS_BIAS) {
+#pragma unroll
+      for (int jj = 0; jj < TN; ++jj) bia[jj] = *reinterpret_cast<const f32x4*>(g.bias + nb + jj * 16);
+    }
+    constexpr int EC = (EPI == CLIPK_EPI_BIAS_RES) ? 2 : 4;
+#pragma unroll
+    for (int ic = 0; ic < TM; ic += EC) {
+      int mrow[EC];
+#pragma unroll
+      for (int i = 0; i < EC; ++i) mrow[i] = m0 + wm * (BM / WM) + (ic + i) * 16 + fr;
+      f32x4 ext[EC][TN];
+      if constexpr (EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU) {
+#pragma unroll
+        for (int i = 0; i < EC; ++i) {
+          const int mc = mrow[i] < g.M ? mrow[i] : g.M - 1;
+#pragma unroll
+          for (int jj = 0; jj < TN; ++jj) {
+            if constexpr (EPI == CLIPK_EPI_BIAS_RES) {
+              ext[i][jj] = *reinterpret_cast<const f32x4*>(g.res + (size_t)mc * g.ldr + nb + jj * 16);
+            } else {
+              float hv[4];
+              load4<TX>((const TX*)g.aux + (size_t)mc * g.ldaux + nb + jj * 16, hv);
+              ext[i][jj] = (f32x4){hv[0], hv[1], hv[2], hv[3]};
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < EC; ++i) {
+        const int m = mrow[i];
+        if (m >= g.M) continue;
+#pragma unroll
+        for (int jj = 0; jj < TN; ++jj) {
+          const int n = nb + jj * 16;
+          f32x4 v = acc[ic + i][jj];
+          if constexpr (HAS_BIAS) v += bia[jj];
+          if constexpr (EPI == CLIPK_EPI_BIAS_RES) {
+            *reinterpret_cast<f32x4*>((float*)g.out + (size_t)m * g.ldo + n) = v + ext[i][jj];
+          } else if constexpr (EPI == CLIPK_EPI_BIAS_QGELU) {
+            if (g.out2) store4<TO>((TO*)g.out2 + (size_t)m * g.ldo + n, v[0], v[1], v[2], v[3]);
+            store4<TO>((TO*)g.out + (size_t)m * g.ldo + n, quick_gelu(v[0]), quick_gelu(v[1]),
+                       quick_gelu(v[2]), quick_gelu(v[3]));
+          } else if constexpr (EPI == CLIPK_EPI_DQGELU) {
+            const f32x4 hv = ext[i][jj];
+            store4<TO>((TO*)g.out + (size_t)m * g.ldo + n, v[0] * quick_gelu_grad(hv[0]),
+                       v[1] * quick_gelu_grad(hv[1]), v[2] * quick_gelu_grad(hv[2]),
+                       v[3] * quick_gelu_grad(hv[3]));
+          } else {
+            store4<TO>((TO*)g.out + (size_t)m * g.ldo + n, v[0], v[1], v[2], v[3]);
+          }
+        }
+      }
+    }
+  }
+}
+
 // Tile configurations: 0 = 128x128 (4 waves, 64 KiB LDS, 2 blocks/CU),
 // 1 = 256x256 (8 waves, 128 KiB, persistent when the grid exceeds 2 waves of CUs),
 // 2 = 256x128 (8 waves, 96 KiB), 3 = 256x256 non-persistent (benchmark knob).
@@ -248,7 +395,7 @@ static int pick_cfg(int M, int N, int esz) {
   }
   if (esz == 4) return 0;  // fp32 parity path: one configuration
   if (g_force_cfg >= 0) {
-    if ((g_force_cfg == 1 || g_force_cfg == 3) && N % 256 == 0) return g_force_cfg;
+    if ((g_force_cfg == 1 || g_force_cfg == 3 || g_force_cfg == 4) && N % 256 == 0) return g_force_cfg;
     if (g_force_cfg == 2) return 2;
     return 0;
   }
@@ -276,7 +423,12 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
     const int nwg = ((g.M + 127) / 128) * (g.N / 128);
     hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 128, 2, 2, false>), dim3(nwg), dim3(256), 0, st, g);
   } else {
-    if (cfg == 1 || cfg == 3) {
+    if (cfg == 4) {
+      const int cus = num_cus();
+      const int nwg = ((g.M + 255) / 256) * (g.N / 256);
+      const int grid = nwg < cus ? ((nwg + 7) / 8) * 8 : (cus / 8) * 8;
+      hipLaunchKernelGGL((gemm_ring_kernel<T, TO, TX, EPI>), dim3(grid), dim3(512), 0, st, g);
+    } else if (cfg == 1 || cfg == 3) {
       const int nwg = ((g.M + 255) / 256) * (g.N / 256);
       const int cus = num_cus();
       if (cfg == 1 && nwg > 2 * cus) {
@@ -362,7 +514,7 @@ extern "C" int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, in
 
 // Benchmark knob: force a tile configuration (-1 = automatic choice).
 extern "C" int clipk_gemm_set_config(int cfg) {
-  if (cfg < -1 || cfg > 3) return CLIPK_EINVAL;
+  if (cfg < -1 || cfg > 4) return CLIPK_EINVAL;
   g_force_cfg = cfg;
   return CLIPK_OK;
 }

@@ -65,8 +65,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int width, const 
 }
 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)) + dres,   g = dy * gamma
-template <typename TL>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int width, const float* __restrict__ dy,
+template <typename TL, typename TD>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int width, const TD* __restrict__ dy,
                                                      int lddy, const float* __restrict__ x, int ldx,
                                                      const int* __restrict__ x_rows,
                                                      const float* __restrict__ gamma,
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int width, const 
   const int orow = out_rows ? out_rows[r] : r;
   const float mu = mean[r], rs = rstd[r];
   const float* xp = x + (size_t)xr * ldx;
-  const float* dp = dy + (size_t)r * lddy;
+  const TD* dp = dy + (size_t)r * lddy;
   const int nv = width >> 2;
   f32x4 gv[LN_MAXV], xh[LN_MAXV];
   float s1 = 0.f, s2 = 0.f;
@@ -91,7 +91,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int width, const 
     const int c = lane + i * 64;
     if (c < nv) {
       const f32x4 xv = reinterpret_cast<const f32x4*>(xp)[c];
-      const f32x4 dv = reinterpret_cast<const f32x4*>(dp)[c];
+      float dva[4];
+      load4<TD>(dp + c * 4, dva);
+      const f32x4 dv = {dva[0], dva[1], dva[2], dva[3]};
       const f32x4 gg = reinterpret_cast<const f32x4*>(gamma)[c];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -157,8 +159,31 @@ extern "C" int clipk_layernorm_fwd(int out_dtype, int rows, int width, const flo
   return CLIPK_OK;
 }
 
-extern "C" int clipk_layernorm_bwd(int rows, int width, const float* dy, int lddy, const float* x,
-                                   int ldx, const int* x_rows, const float* gamma,
+template <typename TD>
+static int ln_bwd_launch(int rows, int width, const void* dy, int lddy, const float* x, int ldx,
+                         const int* x_rows, const float* gamma, const float* mean, const float* rstd,
+                         const float* dres, int lddres, float* dx, void* dx_lp, int lp_dtype,
+                         const int* out_rows, int ldo, hipStream_t st) {
+  dim3 grid((rows + 3) / 4), block(256);
+  const TD* d = (const TD*)dy;
+  if (!dx_lp || lp_dtype == CLIPK_F32) {
+    hipLaunchKernelGGL((ln_bwd_kernel<float, TD>), grid, block, 0, st, rows, width, d, lddy, x, ldx,
+                       x_rows, gamma, mean, rstd, dres, lddres, dx, (float*)dx_lp, out_rows, ldo);
+  } else if (lp_dtype == CLIPK_BF16) {
+    hipLaunchKernelGGL((ln_bwd_kernel<bf16, TD>), grid, block, 0, st, rows, width, d, lddy, x, ldx,
+                       x_rows, gamma, mean, rstd, dres, lddres, dx, (bf16*)dx_lp, out_rows, ldo);
+  } else if (lp_dtype == CLIPK_F16) {
+    hipLaunchKernelGGL((ln_bwd_kernel<f16, TD>), grid, block, 0, st, rows, width, d, lddy, x, ldx,
+                       x_rows, gamma, mean, rstd, dres, lddres, dx, (f16*)dx_lp, out_rows, ldo);
+  } else {
+    return CLIPK_EDTYPE;
+  }
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_layernorm_bwd(int dy_dtype, int rows, int width, const void* dy, int lddy,
+                                   const float* x, int ldx, const int* x_rows, const float* gamma,
                                    const float* mean, const float* rstd, const float* dres,
                                    int lddres, float* dx, void* dx_lp, int lp_dtype,
                                    const int* out_rows, int ldo, void* stream) {
@@ -167,20 +192,18 @@ extern "C" int clipk_layernorm_bwd(int rows, int width, const float* dy, int ldd
       lddy < width || (dres && lddres < width))
     return CLIPK_ESHAPE;
   if (rows == 0) return CLIPK_OK;
-  dim3 grid((rows + 3) / 4), block(256);
   hipStream_t st = (hipStream_t)stream;
-  if (!dx_lp || lp_dtype == CLIPK_F32) {
-    hipLaunchKernelGGL(ln_bwd_kernel<float>, grid, block, 0, st, rows, width, dy, lddy, x, ldx,
-                       x_rows, gamma, mean, rstd, dres, lddres, dx, (float*)dx_lp, out_rows, ldo);
-  } else if (lp_dtype == CLIPK_BF16) {
-    hipLaunchKernelGGL(ln_bwd_kernel<bf16>, grid, block, 0, st, rows, width, dy, lddy, x, ldx,
-                       x_rows, gamma, mean, rstd, dres, lddres, dx, (bf16*)dx_lp, out_rows, ldo);
-  } else if (lp_dtype == CLIPK_F16) {
-    hipLaunchKernelGGL(ln_bwd_kernel<f16>, grid, block, 0, st, rows, width, dy, lddy, x, ldx,
-                       x_rows, gamma, mean, rstd, dres, lddres, dx, (f16*)dx_lp, out_rows, ldo);
-  } else {
-    return CLIPK_EDTYPE;
+  switch (dy_dtype) {
+    case CLIPK_F32:
+      return ln_bwd_launch<float>(rows, width, dy, lddy, x, ldx, x_rows, gamma, mean, rstd, dres, lddres,
+                                  dx, dx_lp, lp_dtype, out_rows, ldo, st);
+    case CLIPK_BF16:
+      return ln_bwd_launch<bf16>(rows, width, dy, lddy, x, ldx, x_rows, gamma, mean, rstd, dres, lddres,
+                                 dx, dx_lp, lp_dtype, out_rows, ldo, st);
+    case CLIPK_F16:
+      return ln_bwd_launch<f16>(rows, width, dy, lddy, x, ldx, x_rows, gamma, mean, rstd, dres, lddres,
+                                dx, dx_lp, lp_dtype, out_rows, ldo, st);
+    default:
+      return CLIPK_EDTYPE;
   }
-  CLIPK_CHECK_LAUNCH();
-  return CLIPK_OK;
 }

@@ -109,23 +109,31 @@ __global__ __launch_bounds__(256) void prompt_assemble_kernel(int B, int C, int 
 }
 
 // d ctx: out[(b*(csc?C:1) + cc)*n_ctx + k][w] = sum_{c in group} dx0[((b*C+c)*L + ctx_pos[c*n_ctx+k])*W + w]
+// Block = (output row, 64 columns); wave v sums classes c = v, v+4, ... in order, then the 4
+// partials are added in a fixed order (deterministic).
 __global__ __launch_bounds__(256) void ctx_grad_kernel(int B, int C, int L, int W, int n_ctx, int csc,
                                                        const int* __restrict__ ctx_pos,
                                                        const float* __restrict__ dx0,
                                                        float* __restrict__ dctx) {
-  const int w = blockIdx.y * 256 + threadIdx.x;
-  if (w >= W) return;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int wcol = blockIdx.y * 64 + lane;
   const int o = blockIdx.x;  // output row
   const int k = o % n_ctx;
   const int grp = o / n_ctx;
   int b, c0, c1;
   if (csc) { b = grp / C; c0 = grp % C; c1 = c0 + 1; } else { b = grp; c0 = 0; c1 = C; }
   float acc = 0.f;
-  for (int c = c0; c < c1; ++c) {
-    const int t = ctx_pos[c * n_ctx + k];
-    acc += dx0[(((size_t)b * C + c) * L + t) * W + w];
+  if (wcol < W) {
+#pragma unroll 4
+    for (int c = c0 + wv; c < c1; c += 4) {
+      const int t = ctx_pos[c * n_ctx + k];
+      acc += dx0[(((size_t)b * C + c) * L + t) * W + wcol];
+    }
   }
-  dctx[(size_t)o * W + w] = acc;
+  red[wv][lane] = acc;
+  __syncthreads();
+  if (wv == 0 && wcol < W) dctx[(size_t)o * W + wcol] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
 // ---------------------------------------------------------------- cosine logits
@@ -383,7 +391,7 @@ extern "C" int clipk_ctx_grad(int B, int C, int L, int W, int n_ctx, int csc, co
   if (!ctx_pos || !dx0 || !dctx) return CLIPK_EINVAL;
   if (B <= 0 || C <= 0 || L <= 0 || n_ctx <= 0 || W <= 0) return CLIPK_ESHAPE;
   const int outs = (csc ? B * C : B) * n_ctx;
-  hipLaunchKernelGGL(ctx_grad_kernel, dim3(outs, (W + 255) / 256), dim3(256), 0, (hipStream_t)stream, B,
+  hipLaunchKernelGGL(ctx_grad_kernel, dim3(outs, (W + 63) / 64), dim3(256), 0, (hipStream_t)stream, B,
                      C, L, W, n_ctx, csc, ctx_pos, dx0, dctx);
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;

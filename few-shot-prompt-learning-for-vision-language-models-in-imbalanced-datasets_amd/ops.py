@@ -75,11 +75,11 @@ def layernorm(x, w, b, out_dtype=torch.float32, rows=None, stats=False):
 
 
 def layernorm_bwd(dy, x, w, mean, rstd, dres=None, lp_dtype=None):
-    _need(dy, "dy", torch.float32)
+    _need(dy, "dy")
     R, W = dy.shape
-    dx = torch.empty_like(dy)
+    dx = torch.empty(R, W, device=dy.device, dtype=torch.float32)
     lp = torch.empty(R, W, device=dy.device, dtype=lp_dtype) if lp_dtype is not None else None
-    N.call("clipk_layernorm_bwd", R, W, _p(dy), W, _p(x), W, None, _p(w), _p(mean), _p(rstd),
+    N.call("clipk_layernorm_bwd", DT[dy.dtype], R, W, _p(dy), W, _p(x), W, None, _p(w), _p(mean), _p(rstd),
            _p(dres), W, _p(dx), _p(lp), DT[lp_dtype] if lp_dtype is not None else 0, None, W, _stream())
     return (dx, lp) if lp is not None else dx
 

@@ -82,9 +82,9 @@ int clipk_layernorm_fwd(int out_dtype, int rows, int width, const float* x, int 
                         const int* in_rows, const float* gamma, const float* beta,
                         void* out, int ldo, float* mean, float* rstd, void* stream);
 
-/* dx = LN-input-grad(dy; x, gamma, mean, rstd) (+ dres). x row = x_rows ? x_rows[r] : r;
+/* dx = LN-input-grad(dy; x, gamma, mean, rstd) (+ dres). dy of dy_dtype; x row = x_rows ? x_rows[r] : r;
  * outputs written at row out_rows ? out_rows[r] : r of dx (f32) and dx_lp (lp_dtype, optional). */
-int clipk_layernorm_bwd(int rows, int width, const float* dy, int lddy, const float* x, int ldx,
+int clipk_layernorm_bwd(int dy_dtype, int rows, int width, const void* dy, int lddy, const float* x, int ldx,
                         const int* x_rows, const float* gamma, const float* mean, const float* rstd,
                         const float* dres, int lddres, float* dx, void* dx_lp, int lp_dtype,
                         const int* out_rows, int ldo, void* stream);

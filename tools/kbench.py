@@ -42,10 +42,14 @@ def main():
         ("qkv bwd   N512  K1536 NONE f32", dict(a=rnd(M, 3 * W, dt=bf), b=rnd(W, 3 * W, dt=bf), epi=N.EPI_NONE, out=torch.float32)),
         ("plain     N2048 K512 NONE f16", dict(a=rnd(M, W), b=rnd(4 * W, W), epi=N.EPI_NONE, out=f16)),
     ]
-    for cfg in (3, 1, -1):
+    REF.clear()
+    for cfg in (0, 1, 4):
         N.load().clipk_gemm_set_config(cfg)
         print(f"--- gemm config {cfg}")
         run_gemms(shapes, M, res, dev)
+
+
+REF = {}
 
 
 def run_gemms(shapes, M, res, dev):
@@ -55,6 +59,13 @@ def run_gemms(shapes, M, res, dev):
         bias = torch.randn(b.shape[0], device=dev) if c.get("bias") else None
         r = res if c.get("res") else None
         fn = lambda: ops.gemm(a, b, c["epi"], c["out"], bias=bias, res=r, aux=c.get("aux"), want_out2=c.get("out2", False))
+        o = fn()
+        o = o[0] if isinstance(o, tuple) else o
+        if name not in REF:
+            REF[name] = o.float().clone()
+            err = 0.0
+        else:
+            err = ((o.float() - REF[name]).abs().max() / (REF[name].abs().max() + 1e-30)).item()
         ms = timeit(fn)
         fl = 2.0 * M * b.shape[0] * a.shape[1]
         nbytes = a.numel() * a.element_size() + M * b.shape[0] * torch.empty(0, dtype=c["out"]).element_size() * (2 if c.get("out2") else 1)
@@ -63,7 +74,7 @@ def run_gemms(shapes, M, res, dev):
         if c.get("aux") is not None:
             nbytes += c["aux"].numel() * 2
         tot += ms
-        print(f"{name:34s} {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF/s  {nbytes/ms/1e6:7.1f} GB/s(min bytes)")
+        print(f"{name:34s} {ms*1e3:8.1f} us  {fl/ms/1e9:7.1f} TF/s  {nbytes/ms/1e6:7.1f} GB/s(min bytes)  err-vs-cfg0 {err:.1e}")
     print(f"sum {tot*1e3:.1f} us")
 
 
