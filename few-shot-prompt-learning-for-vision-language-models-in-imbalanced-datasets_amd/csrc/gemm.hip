@@ -231,7 +231,8 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
     }
     if (!has_next) break;
     tile = next;
-    ++it;  // the last K step of this tile was it-1; the prefetched stage is buffer it & 1
+    // the K loop left `it` one past this tile's last step: buffer it & 1 holds the
+    // next tile's prefetched first stage
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }

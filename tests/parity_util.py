@@ -69,7 +69,8 @@ def run_native(meta, arrays, prec, cocoop=False, dev="cuda", truncate=True):
     model = mod.CustomCLIP(cfg, names, clip)
     pl = model.prompt_learner
     with torch.no_grad():
-        pl.ctx.copy_(torch.from_numpy(arrays["ctx0"]).to(dev))
+        if arrays.get("ctx0") is not None:
+            pl.ctx.copy_(torch.from_numpy(arrays["ctx0"]).to(dev))
         if cocoop:
             mn = synth.make_meta_net(a.embed_dim, a.transformer_width, seed=4)
             for k, v in mn.items():
@@ -82,7 +83,8 @@ def run_native(meta, arrays, prec, cocoop=False, dev="cuda", truncate=True):
     img2 = torch.from_numpy(synth.make_images(B, a.image_resolution, seed=5)).to(dev)
     lbl = torch.from_numpy(synth.make_labels(B, meta["n_cls"], seed=2)).to(dev)
     out = {}
-    assert (pl.tokenized_prompts.numpy() == arrays["tokenized"]).all(), "tokenization differs"
+    if arrays.get("tokenized") is not None:
+        assert (pl.tokenized_prompts.numpy() == arrays["tokenized"]).all(), "tokenization differs"
     model.eval()
     with torch.no_grad():
         out["image_features"] = model.image_encoder(img).cpu().numpy()

@@ -195,3 +195,32 @@ def test_meta_net_and_sgd(dev):
         opt.step()
         ops.sgd_step(p, gr, buf, 0.002, 0.9, 5e-4, step > 0)
     close(p, pr.detach(), torch.float32, "sgd")
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 3, 4])
+@pytest.mark.parametrize("Nn,K", [(2048, 512), (512, 2048)])
+def test_gemm_large_m_every_config(dev, cfg, Nn, K):
+    """Bench-scale M (persistent / ring paths engage when tiles > 2x CUs) vs torch fp32."""
+    lib = N.load()
+    M = 40000
+    g = torch.Generator(device="cpu").manual_seed(cfg * 31 + Nn)
+    A = torch.randn(M, K, generator=g).to(dev).to(torch.float16)
+    B = (torch.randn(Nn, K, generator=g) / math.sqrt(K)).to(dev).to(torch.float16)
+    bias = torch.randn(Nn, generator=g).to(dev)
+    res = torch.randn(M, Nn, generator=g).to(dev)
+    aux = torch.randn(M, Nn, generator=g).to(dev).to(torch.float16)
+    ref = A.float() @ B.float().t()
+    try:
+        N.check(lib.clipk_gemm_set_config(cfg), "set_config")
+        close(ops.gemm(A, B, N.EPI_NONE, torch.float32), ref, torch.float16, f"cfg{cfg} none")
+        close(ops.gemm(A, B, N.EPI_BIAS_RES, torch.float32, bias=bias, res=res), ref + bias + res,
+              torch.float16, f"cfg{cfg} res")
+        gq, hq = ops.gemm(A, B, N.EPI_BIAS_QGELU, torch.float16, bias=bias, want_out2=True)
+        close(hq, ref + bias, torch.float16, f"cfg{cfg} qgelu.h")
+        Ab, Bb = A.to(torch.bfloat16), B.to(torch.bfloat16)
+        refb = Ab.float() @ Bb.float().t()
+        s = torch.sigmoid(1.702 * aux.float())
+        close(ops.gemm(Ab, Bb, N.EPI_DQGELU, torch.bfloat16, aux=aux),
+              refb * (s + 1.702 * aux.float() * s * (1 - s)), torch.bfloat16, f"cfg{cfg} dqgelu")
+    finally:
+        lib.clipk_gemm_set_config(-1)

@@ -89,3 +89,56 @@ def test_coop_full(dev, name, prec):
 @pytest.mark.parametrize("name", FULL_COCOOP)
 def test_cocoop_full(dev, name, prec):
     _check(name, True, prec, dev)
+
+
+def _cocoop_oracle_logits_grad(arch, n_cls, batch, seed_img=1):
+    """CPU oracle (pinned by the golden vectors) for a CoCoOp configuration too large for
+    a committed fixture: logits, CE loss, d ctx."""
+    import torch
+    from oracle import clip_oracle as O
+    from fsp_amd.clip import synth
+    from fsp_amd.clip.tokenizer import tokenize
+    a = synth.ARCHS[arch]
+    p = O.as_torch_sd(synth.make_state_dict(arch, seed=0))
+    mp = {k: torch.from_numpy(v).requires_grad_(True)
+          for k, v in synth.make_meta_net(a.embed_dim, a.transformer_width, seed=4).items()}
+    names = synth.synthetic_classnames(n_cls)
+    tok = torch.from_numpy(tokenize(["a photo of a " + n + "." for n in names]).astype(np.int64))
+    emb = O.token_embed(p, tok)
+    ctx = emb[0, 1:5].clone().requires_grad_(True)
+    img = torch.from_numpy(synth.make_images(batch, a.image_resolution, seed=seed_img))
+    L = int(tok.argmax(-1).max()) + 1
+    logits = O.cocoop_logits(p, mp, img, ctx, emb[:, :1], emb[:, 5:], tok, L)
+    y = torch.from_numpy(synth.make_labels(batch, n_cls, seed=2))
+    loss = torch.nn.functional.cross_entropy(logits, y)
+    loss.backward()
+    return logits.detach().numpy(), float(loss.detach()), ctx.grad.numpy(), ctx.detach().numpy()
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_cocoop_large_rows_vs_oracle(dev, prec):
+    """tiny CLIP, C = 2000 classes x B = 3 images: 66k text rows, so the large-M GEMM
+    paths (persistent 256x256) run inside the full model; checked against the oracle."""
+    import torch
+    meta = {"arch": "tiny", "n_cls": 2000, "batch": 3, "n_ctx": 4, "ctx_init": "a photo of a", "focal": 0}
+    logits, loss, gctx, ctx0 = _cocoop_oracle_logits_grad("tiny", 2000, 3)
+    out = run_native(meta, {"ctx0": ctx0, "tokenized": None}, prec, cocoop=True, dev=str(dev))
+    if prec == "fp32":
+        assert float(np.abs(out["logits"] - logits).max()) <= 1e-3
+        assert rel_err(out["grad_ctx"], gctx) <= 1e-3
+    else:
+        assert float(np.abs(out["logits"] - logits).max()) <= 5e-2
+        assert cos_err(out["grad_ctx"].reshape(1, -1), gctx.reshape(1, -1)) <= 2e-3
+
+
+def test_bench_scale_fp16_matches_fp32(dev):
+    """The benchmark workload shape (ViT-B/16, C = 1000, n_ctx 4) at B = 2: the fp16 path
+    (large-M GEMM configurations) against the fp32 path (f32 MFMA, 128x128 tiles)."""
+    meta = {"arch": "ViT-B/16", "n_cls": 1000, "batch": 2, "n_ctx": 4, "ctx_init": "a photo of a", "focal": 0}
+    o32 = run_native(meta, {"ctx0": None, "tokenized": None}, "fp32", cocoop=True, dev=str(dev))
+    o16 = run_native(meta, {"ctx0": None, "tokenized": None}, "fp16", cocoop=True, dev=str(dev))
+    assert np.isfinite(o16["logits"]).all() and np.isfinite(o16["grad_ctx"]).all()
+    assert float(np.abs(o16["logits"] - o32["logits"]).max()) <= 5e-2
+    assert abs(o16["loss"] - o32["loss"]) <= 0.05
+    for k in [k for k in o32 if k.startswith("grad_")]:
+        assert cos_err(o16[k].reshape(1, -1), o32[k].reshape(1, -1)) <= 2e-3, k

@@ -56,7 +56,8 @@ def run_gemms(shapes, M, res, dev):
     tot = 0.0
     for name, c in shapes:
         a, b = c["a"], c["b"]
-        bias = torch.randn(b.shape[0], device=dev) if c.get("bias") else None
+        bias = torch.randn(b.shape[0], device=dev, generator=torch.Generator(device=dev).manual_seed(7)) \
+            if c.get("bias") else None
         r = res if c.get("res") else None
         fn = lambda: ops.gemm(a, b, c["epi"], c["out"], bias=bias, res=r, aux=c.get("aux"), want_out2=c.get("out2", False))
         o = fn()
