@@ -122,7 +122,8 @@ def main():
         trainer = CoCoOp(cfg, dm=dm)
     dist.broadcast_params([p for p in trainer.model.prompt_learner.parameters()])
     trainer.num_batches = 10 ** 9  # keep update_lr out of the timed loop (epoch boundary)
-    L = trainer.model.prompt_learner.layout.L
+    lay = trainer.model.prompt_learner.layout
+    L = lay.L
     batches = dm.train_loader_x
 
     def step(i):
@@ -192,8 +193,12 @@ def main():
         "config": {"workload": f"CoCoOp {args.arch} n_ctx=4 ctx_init='a photo of a', {args.classes} classes, "
                                f"{args.batch} images/GPU/step, train step fwd+bwd+SGD",
                    "model": f"CLIP {args.arch}", "global_batch": world * args.batch, "classes": args.classes,
-                   "seq_len": L, "parallelism": f"dp{world}"},
+                   "seq_len": L, "parallelism": f"dp{world}",
+                   "text_layout": ("shared-prefix packed, %d text rows/image (plain: %d)"
+                                   % (lay.rows_per_group, args.classes * L)) if lay.pack is not None
+                                  else f"plain [B*C, {L}]"},
         "eval_images_per_sec": round(eval_ips, 3) if eval_ips else None,
+        # reference-equivalent FLOPs (plain [B*C, L_eff] layout) per second, not executed FLOPs
         "model_tflops_per_gpu": round(step_flops * args.steps / tmax / 1e12, 2),
         "roofline": roof,
     }

@@ -38,6 +38,12 @@ SIGNATURES = {
     "clipk_vit_embed_ln": (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "clipk_prompt_assemble": (_I, [_I, _I, _I, _I, _P, _P, _P, _L, _L, _P, _P, _P, _P]),
     "clipk_ctx_grad": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "clipk_prompt_assemble_rows": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _L, _L, _P, _P, _P, _P]),
+    "clipk_ctx_grad_rows": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P]),
+    "clipk_attention_prefix_fwd": (_I, [_I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _P, _I, _P, _P]),
+    "clipk_attention_prefix_ws_bytes": (_S, [_I, _I, _I]),
+    "clipk_attention_prefix_bwd": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _P, _I, _P, _I, _P, _P,
+                                        _I, _P, _S, _P]),
     "clipk_cosine_logits_fwd": (_I, [_I, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P]),
     "clipk_cosine_logits_bwd": (_I, [_I, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P]),
     "clipk_ce_loss": (_I, [_I, _I, _P, _P, _P, _F, _I, _F, _P, _P, _P]),
@@ -52,6 +58,11 @@ SIGNATURES = {
     "clipk_text_forward": (_I, [_P, _I, _I, _P, _P, _P, _P, _S, _P, _S, _P]),
     "clipk_text_bwd_ws_bytes": (_S, [_P, _I, _I]),
     "clipk_text_backward": (_I, [_P, _I, _I, _P, _P, _P, _S, _P, _P, _S, _P]),
+    "clipk_text_packed_saved_bytes": (_S, [_P, _I, _I, _I]),
+    "clipk_text_packed_ws_bytes": (_S, [_P, _I, _I, _I]),
+    "clipk_text_packed_bwd_ws_bytes": (_S, [_P, _I, _I, _I]),
+    "clipk_text_forward_packed": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _S, _P, _S, _P]),
+    "clipk_text_backward_packed": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _S, _P, _P, _S, _P]),
     "clipk_vision_create": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "clipk_vit_ws_bytes": (_S, [_P, _I]),
     "clipk_vit_forward": (_I, [_P, _I, _P, _P, _P, _S, _P]),

@@ -134,49 +134,65 @@ class TextEncoderCore(_Encoder):
                 "clipk_encoder_create(text)")
         self.handle = h
 
-    def forward(self, x0, eot_rows, nseq, L, save):
+    def forward(self, x0, shape, save):
+        """x0 fp32 [shape.rows, W] -> txt fp32 [shape.nout, E] (+ saved arena if save)."""
         lib = N.load()
-        txt = torch.empty(nseq, self.E, device=x0.device, dtype=torch.float32)
-        wsb = lib.clipk_text_ws_bytes(self.handle, nseq, L)
+        h = self.handle
+        txt = torch.empty(shape.nout, self.E, device=x0.device, dtype=torch.float32)
+        if shape.packed:
+            dims = (shape.G, shape.C, shape.R)
+            wsb = lib.clipk_text_packed_ws_bytes(h, *dims)
+            sb = lib.clipk_text_packed_saved_bytes(h, *dims) if save else 0
+        else:
+            wsb = lib.clipk_text_ws_bytes(h, shape.nseq, shape.L)
+            sb = lib.clipk_text_saved_bytes(h, shape.nseq, shape.L) if save else 0
         ws = WORKSPACE.get(wsb, x0.device, "text_fwd")
-        saved = None
-        sb = 0
-        if save:
-            sb = lib.clipk_text_saved_bytes(self.handle, nseq, L)
-            saved = torch.empty(sb, dtype=torch.uint8, device=x0.device)
-        N.check(lib.clipk_text_forward(self.handle, nseq, L, ops._p(x0), ops._p(eot_rows), ops._p(txt),
-                                       ops._p(saved), sb, ops._p(ws), ws.numel(), ops._stream()),
-                "clipk_text_forward")
+        saved = torch.empty(sb, dtype=torch.uint8, device=x0.device) if save else None
+        tail = (ops._p(x0), ops._p(shape.eot_rows), ops._p(txt), ops._p(saved), sb, ops._p(ws), ws.numel(),
+                ops._stream())
+        if shape.packed:
+            N.check(lib.clipk_text_forward_packed(h, shape.G, shape.C, shape.P, shape.R, ops._p(shape.seg),
+                                                  shape.max_q, *tail), "clipk_text_forward_packed")
+        else:
+            N.check(lib.clipk_text_forward(h, shape.nseq, shape.L, *tail), "clipk_text_forward")
         return txt, saved
 
-    def backward(self, dtxt, eot_rows, nseq, L, saved):
+    def backward(self, dtxt, shape, saved):
         lib = N.load()
-        dx0 = torch.empty(nseq * L, self.W, device=dtxt.device, dtype=torch.float32)
-        wsb = lib.clipk_text_bwd_ws_bytes(self.handle, nseq, L)
+        h = self.handle
+        dx0 = torch.empty(shape.rows, self.W, device=dtxt.device, dtype=torch.float32)
+        if shape.packed:
+            wsb = lib.clipk_text_packed_bwd_ws_bytes(h, shape.G, shape.C, shape.R)
+        else:
+            wsb = lib.clipk_text_bwd_ws_bytes(h, shape.nseq, shape.L)
         ws = WORKSPACE.get(wsb, dtxt.device, "text_bwd")
-        N.check(lib.clipk_text_backward(self.handle, nseq, L, ops._p(eot_rows), ops._p(dtxt.contiguous()),
-                                        ops._p(saved), saved.numel(), ops._p(dx0), ops._p(ws), ws.numel(),
-                                        ops._stream()),
-                "clipk_text_backward")
+        tail = (ops._p(shape.eot_rows), ops._p(dtxt.contiguous()), ops._p(saved), saved.numel(), ops._p(dx0),
+                ops._p(ws), ws.numel(), ops._stream())
+        if shape.packed:
+            N.check(lib.clipk_text_backward_packed(h, shape.G, shape.C, shape.P, shape.R, ops._p(shape.seg),
+                                                   shape.max_q, *tail), "clipk_text_backward_packed")
+        else:
+            N.check(lib.clipk_text_backward(h, shape.nseq, shape.L, *tail), "clipk_text_backward")
         return dx0
 
 
 class TextEncodeFn(torch.autograd.Function):
-    """x0 [nseq*L, W] fp32 (prompts + positional embedding) -> text features [nseq, E]."""
+    """x0 fp32 [shape.rows, W] (prompts + positional embedding) -> text features
+    [shape.nout, E]; ``shape`` is a trainers.prompt_base.TextShape (plain or packed)."""
 
     @staticmethod
-    def forward(ctx, x0, core, eot_rows, nseq, L):
-        txt, saved = core.forward(x0.contiguous(), eot_rows, nseq, L, save=bool(ctx.needs_input_grad[0]))
-        ctx.core, ctx.eot_rows, ctx.nseq, ctx.L, ctx.saved_arena = core, eot_rows, nseq, L, saved
+    def forward(ctx, x0, core, shape):
+        txt, saved = core.forward(x0.contiguous(), shape, save=bool(ctx.needs_input_grad[0]))
+        ctx.core, ctx.shape, ctx.saved_arena = core, shape, saved
         return txt
 
     @staticmethod
     def backward(ctx, dtxt):
         if ctx.saved_arena is None:
             raise RuntimeError("text encoder backward without saved activations")
-        dx0 = ctx.core.backward(dtxt, ctx.eot_rows, ctx.nseq, ctx.L, ctx.saved_arena)
+        dx0 = ctx.core.backward(dtxt, ctx.shape, ctx.saved_arena)
         ctx.saved_arena = None
-        return dx0, None, None, None, None
+        return dx0, None, None
 
 
 class VisionEncoder(nn.Module, _Encoder):

@@ -96,9 +96,9 @@ struct TextBufs {
 };
 
 // save=1: per-layer activations live in `saved`; save=0: buffers are reused across layers
-static TextBufs text_layout(const clipk_encoder* e, int nseq, int L, void* saved, void* ws, bool save) {
+static TextBufs text_layout(const clipk_encoder* e, size_t rows, int nout, void* saved, void* ws, bool save) {
   TextBufs t;
-  const size_t rows = (size_t)nseq * L, W = e->W, H = e->heads, a = esize(e->act);
+  const size_t W = e->W, H = e->heads, a = esize(e->act);
   const int nl = e->layers;
   Carver sv(saved), wk(ws);
   Carver& S = save ? sv : wk;
@@ -116,8 +116,8 @@ static TextBufs text_layout(const clipk_encoder* e, int nseq, int L, void* saved
       t.o[l] = S.take(rows * W * a);
       t.h[l] = S.take(rows * 4 * W * a);
     }
-    t.meanf = (float*)S.take((size_t)nseq * 4);
-    t.rstdf = (float*)S.take((size_t)nseq * 4);
+    t.meanf = (float*)S.take((size_t)nout * 4);
+    t.rstdf = (float*)S.take((size_t)nout * 4);
   } else {
     float* x0 = (float*)wk.take(rows * W * 4);
     float* x1 = (float*)wk.take(rows * W * 4);
@@ -133,7 +133,7 @@ static TextBufs text_layout(const clipk_encoder* e, int nseq, int L, void* saved
   t.Xf = t.X[nl];
   t.xn = wk.take(rows * W * a);
   t.g = wk.take(rows * 4 * W * a);
-  t.lnf = wk.take((size_t)nseq * W * a);
+  t.lnf = wk.take((size_t)nout * W * a);
   t.saved_bytes = save ? sv.off : 0;
   t.ws_bytes = wk.off;
   return t;
@@ -142,38 +142,83 @@ static TextBufs text_layout(const clipk_encoder* e, int nseq, int L, void* saved
 struct TextBwdBufs {
   void *dtg, *dX_lp, *dh, *do_, *dqkv, *dxn;  // dxn: LN-output grads in the grad dtype
   float* dlnf;
+  void* part;  // shared-prefix attention: per-chunk prefix dK/dV partials
   size_t bytes;
 };
 
-static TextBwdBufs text_bwd_layout(const clipk_encoder* e, int nseq, int L, void* ws) {
+static TextBwdBufs text_bwd_layout(const clipk_encoder* e, size_t rows, int nout, size_t part_bytes,
+                                   void* ws) {
   TextBwdBufs b;
-  const size_t rows = (size_t)nseq * L, W = e->W, g = esize(e->grad);
+  const size_t W = e->W, g = esize(e->grad);
   Carver c(ws);
-  b.dtg = c.take((size_t)nseq * e->E * g);
-  b.dlnf = (float*)c.take((size_t)nseq * W * 4);
+  b.dtg = c.take((size_t)nout * e->E * g);
+  b.dlnf = (float*)c.take((size_t)nout * W * 4);
   b.dX_lp = c.take(rows * W * g);
   b.dh = c.take(rows * 4 * W * g);
   b.dxn = c.take(rows * W * g);
   b.do_ = c.take(rows * W * g);
   b.dqkv = c.take(rows * 3 * W * g);
+  b.part = part_bytes ? c.take(part_bytes) : nullptr;
   b.bytes = c.off;
   return b;
 }
 
+// Row structure of one encoder call: nseq plain sequences of length L (vision, unpacked
+// text), or the shared-prefix packed text layout (attention_prefix.hip).
+struct SeqShape {
+  int rows = 0, nout = 0;
+  int nseq = 0, L = 0, causal = 0;
+  bool packed = false;
+  int G = 0, C = 0, P = 0, R = 0, max_q = 0;
+  const int* seg = nullptr;
+  static SeqShape plain(int nseq, int L, int causal) {
+    SeqShape s;
+    s.rows = nseq * L; s.nout = nseq; s.nseq = nseq; s.L = L; s.causal = causal;
+    return s;
+  }
+  static SeqShape prefix(int G, int C, int P, int R, const int* seg, int max_q) {
+    SeqShape s;
+    s.rows = G * R; s.nout = G * C; s.packed = true; s.causal = 1;
+    s.G = G; s.C = C; s.P = P; s.R = R; s.seg = seg; s.max_q = max_q;
+    return s;
+  }
+  size_t part_bytes(int heads) const { return packed ? clipk_attention_prefix_ws_bytes(G, C, heads) : 0; }
+};
+
+static int attn_fwd(const clipk_encoder* e, const SeqShape& sh, const void* qkv, void* o, float* lse,
+                    hipStream_t st) {
+  const int W = e->W;
+  if (sh.packed)
+    return clipk_attention_prefix_fwd(e->act, sh.G, sh.C, sh.P, sh.R, sh.seg, sh.max_q, e->heads, qkv, 3 * W,
+                                      o, W, lse, st);
+  return clipk_attention_fwd(e->act, sh.nseq, sh.L, e->heads, sh.causal, qkv, 3 * W, o, W, lse, st);
+}
+
+static int attn_bwd(const clipk_encoder* e, const SeqShape& sh, const void* qkv, const void* o,
+                    const void* dout, const float* lse, void* dqkv, void* part, hipStream_t st) {
+  const int W = e->W;
+  if (sh.packed)
+    return clipk_attention_prefix_bwd(e->act, e->grad, sh.G, sh.C, sh.P, sh.R, sh.seg, sh.max_q, e->heads,
+                                      qkv, 3 * W, o, W, dout, W, lse, dqkv, 3 * W, part,
+                                      sh.part_bytes(e->heads), st);
+  return clipk_attention_bwd(e->act, e->grad, sh.nseq, sh.L, e->heads, sh.causal, qkv, 3 * W, o, W, dout, W,
+                             lse, dqkv, 3 * W, st);
+}
+
 // one residual block forward (shared by text and vision)
-static int block_fwd(const clipk_encoder* e, const std::array<const void*, 16>& w, int nseq, int L,
-                     int causal, const float* X, float* Xm, float* Xo, void* xn, void* qkv, void* o,
+static int block_fwd(const clipk_encoder* e, const std::array<const void*, 16>& w, const SeqShape& sh,
+                     const float* X, float* Xm, float* Xo, void* xn, void* qkv, void* o,
                      float* lse, void* h, void* g, float* m1, float* r1, float* m2, float* r2,
                      hipStream_t st, bool text) {
   const int pg = text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE;
-  const int W = e->W, rows = nseq * L, act = e->act;
+  const int W = e->W, rows = sh.rows, act = e->act;
   TRY(clipk_layernorm_fwd(act, rows, W, X, W, nullptr, (const float*)w[0], (const float*)w[1], xn, W,
                           m1, r1, st));
   TRY(gemm(act, act, CLIPK_EPI_BIAS, rows, 3 * W, W, xn, w[2], (const float*)w[3], nullptr, qkv,
            nullptr, nullptr, 0, st, pg));
   {
     ProfScope ps(text ? CLIPK_PROF_ATTN : CLIPK_PROF_NONE, st, 0.0);
-    TRY(clipk_attention_fwd(act, nseq, L, e->heads, causal, qkv, 3 * W, o, W, lse, st));
+    TRY(attn_fwd(e, sh, qkv, o, lse, st));
   }
   TRY(gemm(act, CLIPK_F32, CLIPK_EPI_BIAS_RES, rows, W, W, o, w[4], (const float*)w[5], X, Xm,
            nullptr, nullptr, 0, st, pg));
@@ -254,28 +299,15 @@ extern "C" int clipk_vision_create(int width, int layers, int heads, int embed, 
 
 extern "C" void clipk_encoder_destroy(clipk_encoder* enc) { delete enc; }
 
-extern "C" size_t clipk_text_saved_bytes(const clipk_encoder* e, int nseq, int L) {
-  if (!e) return 0;
-  return text_layout(e, nseq, L, nullptr, nullptr, true).saved_bytes;
-}
+namespace clipk {
 
-extern "C" size_t clipk_text_ws_bytes(const clipk_encoder* e, int nseq, int L) {
-  if (!e) return 0;
-  TextBufs a = text_layout(e, nseq, L, nullptr, nullptr, true);
-  TextBufs b = text_layout(e, nseq, L, nullptr, nullptr, false);
-  return a.ws_bytes > b.ws_bytes ? a.ws_bytes : b.ws_bytes;
-}
-
-extern "C" int clipk_text_forward(const clipk_encoder* e, int nseq, int L, const float* x0,
-                                  const int* eot_rows, float* txt, void* saved, size_t saved_bytes,
-                                  void* ws, size_t ws_bytes, void* stream) {
-  if (!e || e->kind != 0 || !x0 || !eot_rows || !txt || !ws) return CLIPK_EINVAL;
-  if (nseq <= 0 || L <= 0 || L > 77) return CLIPK_ESHAPE;
+static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const float* x0, const int* eot_rows,
+                             float* txt, void* saved, size_t saved_bytes, void* ws, size_t ws_bytes,
+                             hipStream_t st) {
   const bool save = saved != nullptr;
-  TextBufs t = text_layout(e, nseq, L, saved, ws, save);
+  TextBufs t = text_layout(e, sh.rows, sh.nout, saved, ws, save);
   if (ws_bytes < t.ws_bytes || (save && saved_bytes < t.saved_bytes)) return CLIPK_EWORKSPACE;
-  hipStream_t st = (hipStream_t)stream;
-  const int W = e->W, rows = nseq * L;
+  const int W = e->W, rows = sh.rows;
   // layer-0 input: copy x0 into X[0] when saving (X[0] is needed for LN1 backward)
   const float* cur = x0;
   if (save) {
@@ -286,43 +318,34 @@ extern "C" int clipk_text_forward(const clipk_encoder* e, int nseq, int L, const
   for (int l = 0; l < e->layers; ++l) {
     float* Xo = t.X[l + 1];
     if (!save && Xo == cur) Xo = t.X[l];  // ping-pong (cur may be the caller's x0)
-    TRY(block_fwd(e, e->lw[l], nseq, L, 1, cur, t.Xm[l], Xo, t.xn, t.qkv[l], t.o[l], t.lse[l],
+    TRY(block_fwd(e, e->lw[l], sh, cur, t.Xm[l], Xo, t.xn, t.qkv[l], t.o[l], t.lse[l],
                   save ? t.h[l] : nullptr, t.g, t.mean1[l], t.rstd1[l], t.mean2[l], t.rstd2[l], st, true));
     cur = Xo;
   }
   // ln_final on the EOT rows only (exact: LayerNorm is per row), then @ text_projection
-  TRY(clipk_layernorm_fwd(e->act, nseq, W, cur, W, eot_rows, (const float*)e->head[0],
+  TRY(clipk_layernorm_fwd(e->act, sh.nout, W, cur, W, eot_rows, (const float*)e->head[0],
                           (const float*)e->head[1], t.lnf, W, t.meanf, t.rstdf, st));
-  TRY(gemm(e->act, CLIPK_F32, CLIPK_EPI_NONE, nseq, e->E, W, t.lnf, e->head[2], nullptr, nullptr, txt,
+  TRY(gemm(e->act, CLIPK_F32, CLIPK_EPI_NONE, sh.nout, e->E, W, t.lnf, e->head[2], nullptr, nullptr, txt,
            nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
   return CLIPK_OK;
 }
 
-extern "C" size_t clipk_text_bwd_ws_bytes(const clipk_encoder* e, int nseq, int L) {
-  if (!e) return 0;
-  return text_bwd_layout(e, nseq, L, nullptr).bytes;
-}
-
-extern "C" int clipk_text_backward(const clipk_encoder* e, int nseq, int L, const int* eot_rows,
-                                   const float* dtxt, const void* saved, size_t saved_bytes, float* dx0,
-                                   void* ws, size_t ws_bytes, void* stream) {
-  if (!e || e->kind != 0 || !eot_rows || !dtxt || !saved || !dx0 || !ws) return CLIPK_EINVAL;
-  if (!e->head[3]) return CLIPK_EINVAL;  // forward-only encoder
-  if (nseq <= 0 || L <= 0 || L > 64) return CLIPK_ESHAPE;
-  TextBufs t = text_layout(e, nseq, L, const_cast<void*>(saved), nullptr, true);
-  TextBwdBufs b = text_bwd_layout(e, nseq, L, ws);
+static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const int* eot_rows,
+                              const float* dtxt, const void* saved, size_t saved_bytes, float* dx0,
+                              void* ws, size_t ws_bytes, hipStream_t st) {
+  TextBufs t = text_layout(e, sh.rows, sh.nout, const_cast<void*>(saved), nullptr, true);
+  TextBwdBufs b = text_bwd_layout(e, sh.rows, sh.nout, sh.part_bytes(e->heads), ws);
   if (saved_bytes < t.saved_bytes || ws_bytes < b.bytes) return CLIPK_EWORKSPACE;
-  hipStream_t st = (hipStream_t)stream;
-  const int W = e->W, rows = nseq * L, gd = e->grad, act = e->act;
+  const int W = e->W, rows = sh.rows, nout = sh.nout, gd = e->grad, act = e->act;
   float* dX = dx0;
   // d lnf = dtxt . P^T   (txt = lnf @ P, P = text_projection [W,E])
-  TRY(clipk_cast(gd, (long)nseq * e->E, dtxt, b.dtg, st));
-  TRY(gemm(gd, CLIPK_F32, CLIPK_EPI_NONE, nseq, W, e->E, b.dtg, e->head[3], nullptr, nullptr, b.dlnf,
+  TRY(clipk_cast(gd, (long)nout * e->E, dtxt, b.dtg, st));
+  TRY(gemm(gd, CLIPK_F32, CLIPK_EPI_NONE, nout, W, e->E, b.dtg, e->head[3], nullptr, nullptr, b.dlnf,
            nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
   if (hipMemsetAsync(dX, 0, (size_t)rows * W * 4, st) != hipSuccess) return (int)hipGetLastError();
   if (hipMemsetAsync(b.dX_lp, 0, (size_t)rows * W * esize(gd), st) != hipSuccess)
     return (int)hipGetLastError();
-  TRY(clipk_layernorm_bwd(CLIPK_F32, nseq, W, b.dlnf, W, t.Xf, W, eot_rows, (const float*)e->head[0], t.meanf,
+  TRY(clipk_layernorm_bwd(CLIPK_F32, nout, W, b.dlnf, W, t.Xf, W, eot_rows, (const float*)e->head[0], t.meanf,
                           t.rstdf, nullptr, W, dX, b.dX_lp, gd, eot_rows, W, st));
   for (int l = e->layers - 1; l >= 0; --l) {
     const auto& w = e->lw[l];
@@ -339,8 +362,7 @@ extern "C" int clipk_text_backward(const clipk_encoder* e, int nseq, int L, cons
              nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
     {
       ProfScope ps(CLIPK_PROF_ATTN, st, 0.0);
-      TRY(clipk_attention_bwd(act, gd, nseq, L, e->heads, 1, t.qkv[l], 3 * W, t.o[l], W, b.do_, W,
-                              t.lse[l], b.dqkv, 3 * W, st));
+      TRY(attn_bwd(e, sh, t.qkv[l], t.o[l], b.do_, t.lse[l], b.dqkv, b.part, st));
     }
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, 3 * W, b.dqkv, w[12], nullptr, nullptr, b.dxn,
              nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
@@ -348,6 +370,90 @@ extern "C" int clipk_text_backward(const clipk_encoder* e, int nseq, int L, cons
                             t.rstd1[l], dX, W, dX, l > 0 ? b.dX_lp : nullptr, gd, nullptr, W, st));
   }
   return CLIPK_OK;
+}
+
+static size_t text_ws_bytes(const clipk_encoder* e, size_t rows, int nout) {
+  TextBufs a = text_layout(e, rows, nout, nullptr, nullptr, true);
+  TextBufs b = text_layout(e, rows, nout, nullptr, nullptr, false);
+  return a.ws_bytes > b.ws_bytes ? a.ws_bytes : b.ws_bytes;
+}
+
+}  // namespace clipk
+
+extern "C" size_t clipk_text_saved_bytes(const clipk_encoder* e, int nseq, int L) {
+  if (!e || nseq <= 0 || L <= 0) return 0;
+  return text_layout(e, (size_t)nseq * L, nseq, nullptr, nullptr, true).saved_bytes;
+}
+
+extern "C" size_t clipk_text_ws_bytes(const clipk_encoder* e, int nseq, int L) {
+  if (!e || nseq <= 0 || L <= 0) return 0;
+  return text_ws_bytes(e, (size_t)nseq * L, nseq);
+}
+
+extern "C" int clipk_text_forward(const clipk_encoder* e, int nseq, int L, const float* x0,
+                                  const int* eot_rows, float* txt, void* saved, size_t saved_bytes,
+                                  void* ws, size_t ws_bytes, void* stream) {
+  if (!e || e->kind != 0 || !x0 || !eot_rows || !txt || !ws) return CLIPK_EINVAL;
+  if (nseq <= 0 || L <= 0 || L > 77) return CLIPK_ESHAPE;
+  return text_forward_impl(e, SeqShape::plain(nseq, L, 1), x0, eot_rows, txt, saved, saved_bytes, ws,
+                           ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" size_t clipk_text_bwd_ws_bytes(const clipk_encoder* e, int nseq, int L) {
+  if (!e || nseq <= 0 || L <= 0) return 0;
+  return text_bwd_layout(e, (size_t)nseq * L, nseq, 0, nullptr).bytes;
+}
+
+extern "C" int clipk_text_backward(const clipk_encoder* e, int nseq, int L, const int* eot_rows,
+                                   const float* dtxt, const void* saved, size_t saved_bytes, float* dx0,
+                                   void* ws, size_t ws_bytes, void* stream) {
+  if (!e || e->kind != 0 || !eot_rows || !dtxt || !saved || !dx0 || !ws) return CLIPK_EINVAL;
+  if (!e->head[3]) return CLIPK_EINVAL;  // forward-only encoder
+  if (nseq <= 0 || L <= 0 || L > 64) return CLIPK_ESHAPE;
+  return text_backward_impl(e, SeqShape::plain(nseq, L, 1), eot_rows, dtxt, saved, saved_bytes, dx0, ws,
+                            ws_bytes, (hipStream_t)stream);
+}
+
+static bool packed_ok(int G, int C, int P, int R, int max_q) {
+  return G > 0 && C > 0 && P >= 1 && P <= 16 && max_q >= 1 && max_q <= 16 && R >= P + C &&
+         R <= P + C * max_q && (long)G * R < (1L << 31);
+}
+
+extern "C" size_t clipk_text_packed_saved_bytes(const clipk_encoder* e, int G, int C, int R) {
+  if (!e || G <= 0 || C <= 0 || R <= 0) return 0;
+  return text_layout(e, (size_t)G * R, G * C, nullptr, nullptr, true).saved_bytes;
+}
+
+extern "C" size_t clipk_text_packed_ws_bytes(const clipk_encoder* e, int G, int C, int R) {
+  if (!e || G <= 0 || C <= 0 || R <= 0) return 0;
+  return text_ws_bytes(e, (size_t)G * R, G * C);
+}
+
+extern "C" size_t clipk_text_packed_bwd_ws_bytes(const clipk_encoder* e, int G, int C, int R) {
+  if (!e || G <= 0 || C <= 0 || R <= 0) return 0;
+  return text_bwd_layout(e, (size_t)G * R, G * C, clipk_attention_prefix_ws_bytes(G, C, e->heads), nullptr)
+      .bytes;
+}
+
+extern "C" int clipk_text_forward_packed(const clipk_encoder* e, int G, int C, int P, int R, const int* seg,
+                                         int max_q, const float* x0, const int* eot_rows, float* txt,
+                                         void* saved, size_t saved_bytes, void* ws, size_t ws_bytes,
+                                         void* stream) {
+  if (!e || e->kind != 0 || !seg || !x0 || !eot_rows || !txt || !ws) return CLIPK_EINVAL;
+  if (!packed_ok(G, C, P, R, max_q)) return CLIPK_ESHAPE;
+  return text_forward_impl(e, SeqShape::prefix(G, C, P, R, seg, max_q), x0, eot_rows, txt, saved,
+                           saved_bytes, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int clipk_text_backward_packed(const clipk_encoder* e, int G, int C, int P, int R,
+                                          const int* seg, int max_q, const int* eot_rows,
+                                          const float* dtxt, const void* saved, size_t saved_bytes,
+                                          float* dx0, void* ws, size_t ws_bytes, void* stream) {
+  if (!e || e->kind != 0 || !seg || !eot_rows || !dtxt || !saved || !dx0 || !ws) return CLIPK_EINVAL;
+  if (!e->head[3]) return CLIPK_EINVAL;
+  if (!packed_ok(G, C, P, R, max_q)) return CLIPK_ESHAPE;
+  return text_backward_impl(e, SeqShape::prefix(G, C, P, R, seg, max_q), eot_rows, dtxt, saved, saved_bytes,
+                            dx0, ws, ws_bytes, (hipStream_t)stream);
 }
 
 // ---------------------------------------------------------------- vision
@@ -399,7 +505,7 @@ extern "C" int clipk_vit_forward(const clipk_encoder* e, int B, const float* img
   float* cur = v.x0;
   float* nxt = v.x1;
   for (int l = 0; l < e->layers; ++l) {
-    TRY(block_fwd(e, e->lw[l], B, L, 0, cur, v.xm, nxt, v.xn, v.qkv, v.o, nullptr, nullptr, v.g,
+    TRY(block_fwd(e, e->lw[l], SeqShape::plain(B, L, 0), cur, v.xm, nxt, v.xn, v.qkv, v.o, nullptr, nullptr, v.g,
                   nullptr, nullptr, nullptr, nullptr, st, false));
     float* t = cur; cur = nxt; nxt = t;
   }

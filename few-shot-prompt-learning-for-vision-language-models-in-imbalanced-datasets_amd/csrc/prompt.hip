@@ -136,6 +136,59 @@ __global__ __launch_bounds__(256) void ctx_grad_kernel(int B, int C, int L, int 
   if (wv == 0 && wcol < W) dctx[(size_t)o * W + wcol] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
+// Shared-prefix packed prompts (see attention_prefix.hip): group g's row r holds token
+// (c, t) = (row_tab[r] / L, row_tab[r] % L); same splice as prompt_assemble_kernel.
+__global__ __launch_bounds__(256) void prompt_assemble_rows_kernel(int G, int R, int L, int W,
+                                                                   const int* __restrict__ row_tab,
+                                                                   const int* __restrict__ src_map,
+                                                                   const float* __restrict__ emb,
+                                                                   const float* __restrict__ ctx, long sb,
+                                                                   long sc, const float* __restrict__ bias,
+                                                                   const float* __restrict__ pos,
+                                                                   float* __restrict__ x0) {
+  const int lane = threadIdx.x & 63;
+  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= (long)G * R) return;
+  const int g = (int)(r / R);
+  const int ct = row_tab[r % R];
+  const int c = ct / L, t = ct % L;
+  const int m = src_map[ct];
+  const float* src = m >= 0 ? emb + ((size_t)c * 77 + m) * W : ctx + g * sb + c * sc + (size_t)(-1 - m) * W;
+  const bool add_bias = m < 0 && bias != nullptr;
+  const float* bp = bias + (size_t)g * W;
+  const float* pp = pos + (size_t)t * W;
+  float* dst = x0 + r * W;
+  for (int c4 = lane; c4 < W / 4; c4 += 64) {
+    f32x4 v = reinterpret_cast<const f32x4*>(src)[c4] + reinterpret_cast<const f32x4*>(pp)[c4];
+    if (add_bias) v += reinterpret_cast<const f32x4*>(bp)[c4];
+    reinterpret_cast<f32x4*>(dst)[c4] = v;
+  }
+}
+
+// d ctx on packed prompts: out[g*n_ctx + k] = sum of dx0 over the group rows listed for
+// slot k (slot_rows[slot_ptr[k] .. slot_ptr[k+1]); a shared prefix row is listed once,
+// since its gradient already sums every class). Fixed-order 4-wave reduction.
+__global__ __launch_bounds__(256) void ctx_grad_rows_kernel(int R, int W, int n_ctx,
+                                                            const int* __restrict__ slot_ptr,
+                                                            const int* __restrict__ slot_rows,
+                                                            const float* __restrict__ dx0,
+                                                            float* __restrict__ dctx) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int wcol = blockIdx.y * 64 + lane;
+  const int o = blockIdx.x;
+  const int k = o % n_ctx, g = o / n_ctx;
+  float acc = 0.f;
+  if (wcol < W) {
+    const int e = slot_ptr[k + 1];
+#pragma unroll 4
+    for (int i = slot_ptr[k] + wv; i < e; i += 4) acc += dx0[((size_t)g * R + slot_rows[i]) * W + wcol];
+  }
+  red[wv][lane] = acc;
+  __syncthreads();
+  if (wv == 0 && wcol < W) dctx[(size_t)o * W + wcol] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
 // ---------------------------------------------------------------- cosine logits
 // coop.py:356-363 / cocoop.py:238-251: logits = exp(logit_scale) * (imf/|imf|) . (txt/|txt|)
 __global__ __launch_bounds__(256) void cos_logits_fwd_kernel(int B, int C, int E, int per_image,
@@ -393,6 +446,30 @@ extern "C" int clipk_ctx_grad(int B, int C, int L, int W, int n_ctx, int csc, co
   const int outs = (csc ? B * C : B) * n_ctx;
   hipLaunchKernelGGL(ctx_grad_kernel, dim3(outs, (W + 63) / 64), dim3(256), 0, (hipStream_t)stream, B,
                      C, L, W, n_ctx, csc, ctx_pos, dx0, dctx);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_prompt_assemble_rows(int G, int R, int C, int L, int W, const int* row_tab,
+                                          const int* src_map, const float* emb, const float* ctx,
+                                          long ctx_sg, long ctx_sc, const float* bias, const float* pos,
+                                          float* x0, void* stream) {
+  if (!row_tab || !src_map || !emb || !ctx || !pos || !x0) return CLIPK_EINVAL;
+  if (G < 0 || R < 0 || C <= 0 || L <= 0 || L > 77 || W % 4) return CLIPK_ESHAPE;
+  const long rows = (long)G * R;
+  if (rows == 0) return CLIPK_OK;
+  hipLaunchKernelGGL(prompt_assemble_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                     G, R, L, W, row_tab, src_map, emb, ctx, ctx_sg, ctx_sc, bias, pos, x0);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_ctx_grad_rows(int G, int R, int W, int n_ctx, const int* slot_ptr,
+                                   const int* slot_rows, const float* dx0, float* dctx, void* stream) {
+  if (!slot_ptr || !slot_rows || !dx0 || !dctx) return CLIPK_EINVAL;
+  if (G <= 0 || R <= 0 || n_ctx <= 0 || W <= 0) return CLIPK_ESHAPE;
+  hipLaunchKernelGGL(ctx_grad_rows_kernel, dim3(G * n_ctx, (W + 63) / 64), dim3(256), 0, (hipStream_t)stream,
+                     R, W, n_ctx, slot_ptr, slot_rows, dx0, dctx);
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
 }

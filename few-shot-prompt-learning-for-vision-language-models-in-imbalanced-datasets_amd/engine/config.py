@@ -122,5 +122,5 @@ def get_cfg_default() -> CfgNode:
         },
         # MI355X-native knobs (not in the reference): prompt truncation to the EOT and the
         # max rows per text-encoder launch chunk (memory bound for large B*C).
-        "NATIVE": {"TRUNCATE_PROMPTS": True, "MAX_TEXT_ROWS": 2_000_000},
+        "NATIVE": {"TRUNCATE_PROMPTS": True, "SHARED_PREFIX": True, "MAX_TEXT_ROWS": 2_000_000},
     })

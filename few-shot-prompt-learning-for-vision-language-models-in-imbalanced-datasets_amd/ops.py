@@ -119,6 +119,42 @@ def prompt_assemble(B, C, L, src_map, emb, ctx, ctx_sb, ctx_sc, bias, pos):
     return x0
 
 
+def prompt_assemble_rows(G, R, C, L, row_tab, src_map, emb, ctx, ctx_sg, ctx_sc, bias, pos):
+    W = emb.shape[-1]
+    x0 = torch.empty(G * R, W, device=emb.device, dtype=torch.float32)
+    N.call("clipk_prompt_assemble_rows", G, R, C, L, W, _p(row_tab), _p(src_map), _p(emb), _p(ctx), ctx_sg,
+           ctx_sc, _p(bias), _p(pos), _p(x0), _stream())
+    return x0
+
+
+def ctx_grad_rows(G, R, W, n_ctx, slot_ptr, slot_rows, dx0):
+    d = torch.empty(G * n_ctx, W, device=dx0.device, dtype=torch.float32)
+    N.call("clipk_ctx_grad_rows", G, R, W, n_ctx, _p(slot_ptr), _p(slot_rows), _p(dx0), _p(d), _stream())
+    return d
+
+
+def attention_prefix(qkv, G, C, P, R, seg, max_q, heads, lse=False):
+    """Shared-prefix packed causal attention (clipk_attention_prefix_fwd)."""
+    _need(qkv, "qkv")
+    _need(seg, "seg", torch.int32)
+    W = heads * 64
+    out = torch.zeros(G * R, W, device=qkv.device, dtype=qkv.dtype)
+    l = torch.zeros(G * R, heads, device=qkv.device) if lse else None
+    N.call("clipk_attention_prefix_fwd", DT[qkv.dtype], G, C, P, R, _p(seg), max_q, heads, _p(qkv), 3 * W,
+           _p(out), W, _p(l), _stream())
+    return (out, l) if lse else out
+
+
+def attention_prefix_bwd(qkv, o, dout, lse, G, C, P, R, seg, max_q, heads, grad_dtype):
+    W = heads * 64
+    dqkv = torch.zeros(G * R, 3 * W, device=qkv.device, dtype=grad_dtype)
+    nb = N.load().clipk_attention_prefix_ws_bytes(G, C, heads)
+    ws = torch.empty(nb, dtype=torch.uint8, device=qkv.device)
+    N.call("clipk_attention_prefix_bwd", DT[qkv.dtype], DT[grad_dtype], G, C, P, R, _p(seg), max_q, heads,
+           _p(qkv), 3 * W, _p(o), W, _p(dout), W, _p(lse), _p(dqkv), 3 * W, _p(ws), nb, _stream())
+    return dqkv
+
+
 def ctx_grad(B, C, L, W, n_ctx, csc, ctx_pos, dx0):
     outs = (B * C if csc else B) * n_ctx
     d = torch.empty(outs, W, device=dx0.device, dtype=torch.float32)

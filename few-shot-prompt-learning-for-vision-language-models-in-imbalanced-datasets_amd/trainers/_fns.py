@@ -45,7 +45,8 @@ def prompt_layout(n_cls, n_ctx, name_lens, position, eot, truncate=True):
 
 
 class PromptAssembleFn(torch.autograd.Function):
-    """x0[(b*C+c)*L+t] = prompt token (+ctx[+bias_b]) + pos[t]; grads to ctx (and bias)."""
+    """x0[(b*C+c)*L+t] = prompt token (+ctx[+bias_b]) + pos[t] (or the shared-prefix packed
+    rows, PromptLayout.pack); grads to ctx (and bias)."""
 
     @staticmethod
     def forward(ctx, ctx_vec, bias, lay):
@@ -53,8 +54,13 @@ class PromptAssembleFn(torch.autograd.Function):
         csc = ctx_vec.dim() == 3
         W = ctx_vec.shape[-1]
         sc = lay.n_ctx * W if csc else 0
-        x0 = ops.prompt_assemble(B, lay.n_cls, lay.L, lay.src_map, lay.emb, ctx_vec.contiguous(), 0, sc,
-                                 None if bias is None else bias.contiguous(), lay.pos)
+        bias_c = None if bias is None else bias.contiguous()
+        if lay.pack is not None:  # shared-prefix packed rows [B*R, W]
+            x0 = ops.prompt_assemble_rows(B, lay.R, lay.n_cls, lay.L, lay.row_tab, lay.src_map, lay.emb,
+                                          ctx_vec.contiguous(), 0, sc, bias_c, lay.pos)
+        else:
+            x0 = ops.prompt_assemble(B, lay.n_cls, lay.L, lay.src_map, lay.emb, ctx_vec.contiguous(), 0, sc,
+                                     bias_c, lay.pos)
         ctx.lay, ctx.B, ctx.csc, ctx.shape, ctx.has_bias = lay, B, csc, ctx_vec.shape, bias is not None
         return x0
 
@@ -62,7 +68,10 @@ class PromptAssembleFn(torch.autograd.Function):
     def backward(ctx, dx0):
         lay = ctx.lay
         W = ctx.shape[-1]
-        d = ops.ctx_grad(ctx.B, lay.n_cls, lay.L, W, lay.n_ctx, ctx.csc, lay.ctx_pos, dx0.contiguous())
+        if lay.pack is not None:
+            d = ops.ctx_grad_rows(ctx.B, lay.R, W, lay.n_ctx, lay.slot_ptr, lay.slot_rows, dx0.contiguous())
+        else:
+            d = ops.ctx_grad(ctx.B, lay.n_cls, lay.L, W, lay.n_ctx, ctx.csc, lay.ctx_pos, dx0.contiguous())
         if ctx.csc:
             return d.view(ctx.shape), None, None
         d = d.view(ctx.B, lay.n_ctx, W)

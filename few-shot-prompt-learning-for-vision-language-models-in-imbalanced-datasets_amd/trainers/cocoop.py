@@ -49,8 +49,9 @@ class PromptLearner(nn.Module):
         vis_dim = clip_model.visual.output_dim
         ctx_dim = clip_model.arch.transformer_width
         truncate = cfg.get("NATIVE", {}).get("TRUNCATE_PROMPTS", True)
+        shared = cfg.get("NATIVE", {}).get("SHARED_PREFIX", True)
         ctx_vectors, self.prompt_prefix = init_prompts(self, classnames, clip_model, c.N_CTX, c.CTX_INIT,
-                                                       "end", False, truncate)
+                                                       "end", False, truncate, shared)
         self.ctx = nn.Parameter(ctx_vectors)
         self.meta_net = MetaNet(vis_dim, ctx_dim).to(ctx_vectors.device)
 
@@ -102,14 +103,14 @@ class CustomCLIP(nn.Module):
         pl = self.prompt_learner
         B = imf_n.shape[0]
         x0 = pl.assemble(imf_n)
-        txt = TextEncodeFn.apply(x0, self.text_core, pl.layout.eot_rows(B), B * pl.n_cls, pl.layout.L)
+        txt = TextEncodeFn.apply(x0, self.text_core, pl.layout.shape(B))
         return CosineLogitsFn.apply(imf_n, txt, self.logit_scale_value, 1, pl.n_cls)
 
     def forward(self, image, label=None):
         imf = self.image_encoder(image)
         imf = imf / imf.norm(dim=-1, keepdim=True)
         pl = self.prompt_learner
-        per_img = pl.n_cls * pl.layout.L
+        per_img = pl.layout.rows_per_group
         chunk = max(1, self.max_rows // per_img)
         if imf.shape[0] <= chunk:
             logits = self.logits_for(imf)

@@ -22,7 +22,7 @@ from ..engine.metrics import compute_accuracy
 from ..clip.model import TextEncodeFn
 from ._fns import PromptAssembleFn, CosineLogitsFn
 from .losses import CrossEntropyLoss, MultiClassFocalLoss, LogitsNTXentLoss, focal_alpha
-from .prompt_base import init_prompts
+from .prompt_base import init_prompts, TextShape
 
 
 class TextEncoder(nn.Module):
@@ -41,7 +41,7 @@ class TextEncoder(nn.Module):
         L = int(eot.max().item()) + 1
         x0 = (prompts[:, :L] + self.positional_embedding[:L]).reshape(N_ * L, W).contiguous()
         rows = (torch.arange(N_, device=eot.device) * L + eot).to(torch.int32).to(prompts.device)
-        return TextEncodeFn.apply(x0, self.core, rows, N_, L)
+        return TextEncodeFn.apply(x0, self.core, TextShape(rows, nseq=N_, L=L))
 
 
 class PromptLearner(nn.Module):
@@ -59,9 +59,10 @@ class PromptLearner(nn.Module):
         elif not c.CTX_INIT:
             print("Initializing a generic context")
         truncate = cfg.get("NATIVE", {}).get("TRUNCATE_PROMPTS", True)
+        shared = cfg.get("NATIVE", {}).get("SHARED_PREFIX", True)
         ctx_vectors, self.prompt_prefix = init_prompts(
             self, classnames, clip_model, c.N_CTX, c.CTX_INIT, c.CLASS_TOKEN_POSITION,
-            bool(c.CSC) and not c.CTX_INIT, truncate)
+            bool(c.CSC) and not c.CTX_INIT, truncate, shared)
         self.ctx = nn.Parameter(ctx_vectors)
         self.class_token_position = c.CLASS_TOKEN_POSITION
 
@@ -119,7 +120,7 @@ class CustomCLIP(nn.Module):
     def text_features(self):
         pl = self.prompt_learner
         x0 = pl.assemble()
-        return TextEncodeFn.apply(x0, self.text_core, pl.layout.eot_rows(1), pl.n_cls, pl.layout.L)
+        return TextEncodeFn.apply(x0, self.text_core, pl.layout.shape(1))
 
     def forward_once(self, image):
         imf = self.image_encoder(image)

@@ -17,10 +17,66 @@ from ..clip.tokenizer import tokenize, default_tokenizer
 from ._fns import prompt_layout
 
 
+class TextShape:
+    """Row structure of one text-encoder call, as the native encoder takes it.
+
+    plain : nseq sequences of L rows (row s*L + t), eot_rows[s] = s*L + EOT_s.
+    packed: G groups of R rows sharing a P-row causal prefix (see shared_prefix_tables);
+            seg [C,2] int32 (first row, q_len) per class, eot_rows[g*C + c] absolute."""
+
+    def __init__(self, eot_rows, nseq=0, L=0, G=0, C=0, P=0, R=0, seg=None, max_q=0):
+        self.eot_rows = eot_rows
+        self.packed = seg is not None
+        self.nseq, self.L = nseq, L
+        self.G, self.C, self.P, self.R, self.seg, self.max_q = G, C, P, R, seg, max_q
+        self.rows = G * R if self.packed else nseq * L
+        self.nout = G * C if self.packed else nseq
+
+
+def shared_prefix_tables(src_map, ctx_pos, eot, n_ctx, csc, max_prefix=16, max_q=16):
+    """Packing tables for the shared causal prefix (attention_prefix.hip), or None.
+
+    The structural prefix = SOT + the context slots before the first class-name token
+    (position "end": 1 + n_ctx, "middle": 1 + n_ctx/2, "front": 1), identical for every
+    class when the context is shared (not CSC). Coincidentally equal class-name tokens are
+    NOT folded in, so the row count does not depend on the class-name vocabulary.
+    Under the causal mask those rows' states are the same for every class, and rows past a
+    class's EOT never reach its EOT row: packing [prefix][class rows P..EOT_c]... is exact."""
+    C, L = src_map.shape
+    if csc or n_ctx <= 0:
+        return None
+    P = 1
+    while P < L and src_map[0, P] < 0 and (src_map[:, P] == src_map[0, P]).all():
+        P += 1
+    P = min(P, max_prefix)
+    qlen = np.asarray(eot, np.int64) + 1 - P
+    if P < 2 or qlen.min() < 1 or qlen.max() > max_q:
+        return None
+    off = P + np.concatenate([[0], np.cumsum(qlen)[:-1]])
+    R = int(P + qlen.sum())
+    row_tab = np.empty(R, np.int32)
+    row_tab[:P] = np.arange(P)
+    for c in range(C):
+        row_tab[off[c]:off[c] + qlen[c]] = c * L + np.arange(P, P + qlen[c])
+    slot_ptr = [0]
+    slot_rows = []
+    for k in range(n_ctx):
+        t0 = int(ctx_pos[0, k])
+        if t0 < P and (ctx_pos[:, k] == t0).all():
+            slot_rows.append(t0)
+        else:
+            slot_rows.extend(int(off[c] + ctx_pos[c, k] - P) for c in range(C))
+        slot_ptr.append(len(slot_rows))
+    seg = np.stack([off, qlen], 1).astype(np.int32)
+    return {"P": P, "R": R, "seg": seg, "row_tab": row_tab, "max_q": int(qlen.max()),
+            "slot_ptr": np.asarray(slot_ptr, np.int32), "slot_rows": np.asarray(slot_rows, np.int32),
+            "eot_in_group": (off + qlen - 1).astype(np.int64)}
+
+
 class PromptLayout:
     """Device-resident slot tables for one (class set, n_ctx, position)."""
 
-    def __init__(self, n_cls, n_ctx, src_map, ctx_pos, L, eot, emb, pos):
+    def __init__(self, n_cls, n_ctx, src_map, ctx_pos, L, eot, emb, pos, csc=False, shared_prefix=True):
         self.n_cls, self.n_ctx, self.L = n_cls, n_ctx, L
         dev = emb.device
         self.src_map = torch.from_numpy(src_map).to(dev)
@@ -29,18 +85,46 @@ class PromptLayout:
         self.emb = emb
         self.pos = pos.contiguous()
         self._eot_rows = {}
+        self._shapes = {}
+        pk = shared_prefix_tables(src_map, ctx_pos, eot, n_ctx, csc) if shared_prefix else None
+        self.pack = None
+        if pk is not None:
+            self.pack = pk
+            self.P, self.R = pk["P"], pk["R"]
+            self.seg = torch.from_numpy(pk["seg"].reshape(-1).copy()).to(dev)
+            self.row_tab = torch.from_numpy(pk["row_tab"]).to(dev)
+            self.slot_ptr = torch.from_numpy(pk["slot_ptr"]).to(dev)
+            self.slot_rows = torch.from_numpy(pk["slot_rows"]).to(dev)
+
+    @property
+    def rows_per_group(self) -> int:
+        """Text rows one image (CoCoOp) / the class set (CoOp) costs."""
+        return self.R if self.pack is not None else self.n_cls * self.L
 
     def eot_rows(self, B: int) -> torch.Tensor:
-        """Global row index (b*C + c)*L + eot[c] of each sequence's EOT token."""
+        """Global row index of each sequence's EOT token, ordered (b, c)."""
         if B not in self._eot_rows:
             b = np.arange(B)[:, None]
-            rows = (b * self.n_cls + np.arange(self.n_cls)[None, :]) * self.L + self.eot[None, :]
+            if self.pack is not None:
+                rows = b * self.R + self.pack["eot_in_group"][None, :]
+            else:
+                rows = (b * self.n_cls + np.arange(self.n_cls)[None, :]) * self.L + self.eot[None, :]
             self._eot_rows[B] = torch.from_numpy(rows.reshape(-1).astype(np.int32)).to(self.emb.device)
         return self._eot_rows[B]
 
+    def shape(self, B: int) -> TextShape:
+        """TextShape for B groups (images for CoCoOp; 1 for CoOp)."""
+        if B not in self._shapes:
+            if self.pack is not None:
+                self._shapes[B] = TextShape(self.eot_rows(B), G=B, C=self.n_cls, P=self.P, R=self.R,
+                                            seg=self.seg, max_q=self.pack["max_q"])
+            else:
+                self._shapes[B] = TextShape(self.eot_rows(B), nseq=B * self.n_cls, L=self.L)
+        return self._shapes[B]
+
 
 def init_prompts(module: nn.Module, classnames, clip_model, n_ctx, ctx_init, position, csc,
-                 truncate: bool):
+                 truncate: bool, shared_prefix: bool = True):
     """Common __init__ body; returns (ctx_vectors, prompt_prefix)."""
     n_cls = len(classnames)
     W = clip_model.arch.transformer_width
@@ -75,7 +159,8 @@ def init_prompts(module: nn.Module, classnames, clip_model, n_ctx, ctx_init, pos
     eot = tokenized.argmax(dim=-1).numpy()
     src, cpos, L = prompt_layout(n_cls, n_ctx, name_lens, position, eot, truncate)
     module.layout = PromptLayout(n_cls, n_ctx, src, cpos, L, eot, emb.to(dev).contiguous(),
-                                 clip_model.positional_embedding.detach())
+                                 clip_model.positional_embedding.detach(), csc=csc,
+                                 shared_prefix=shared_prefix and truncate)
     module.n_cls, module.n_ctx = n_cls, n_ctx
     module.tokenized_prompts = tokenized
     module.name_lens = name_lens

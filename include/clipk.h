@@ -100,6 +100,23 @@ int clipk_attention_bwd(int dtype, int grad_dtype, int nseq, int L, int heads, i
                         const void* qkv, int ldqkv, const void* ofwd, int ldof, const void* dout,
                         int lddo, const float* lse, void* dqkv, int lddqkv, void* stream);
 
+/* Shared-prefix packed attention (text, causal). Rows of group g (stride R) hold the P
+ * prefix rows shared by all C sequences of the group, then each sequence's own rows:
+ * seg[2c], seg[2c+1] = (group-relative first row, q_len) of sequence c. Sequence c's
+ * queries see all P prefix keys plus its own keys causally; the prefix rows attend among
+ * themselves causally. 1 <= P <= 16, 1 <= q_len <= max_q <= 16. Exact restatement of the
+ * causal attention of the unpacked [C, L] prompts (attention_prefix.hip). */
+int clipk_attention_prefix_fwd(int dtype, int G, int C, int P, int R, const int* seg, int max_q,
+                               int heads, const void* qkv, int ldqkv, void* out, int ldo, float* lse,
+                               void* stream);
+/* Backward; ws >= clipk_attention_prefix_ws_bytes(G, C, heads) holds the per-chunk fp32
+ * partial dK/dV of the prefix rows (reduced in a fixed order). */
+size_t clipk_attention_prefix_ws_bytes(int G, int C, int heads);
+int clipk_attention_prefix_bwd(int dtype, int grad_dtype, int G, int C, int P, int R, const int* seg,
+                               int max_q, int heads, const void* qkv, int ldqkv, const void* ofwd,
+                               int ldof, const void* dout, int lddo, const float* lse, void* dqkv,
+                               int lddqkv, void* ws, size_t ws_bytes, void* stream);
+
 /* Patch extraction: img fp32 [B,3,R,R] -> out [B*G*G, Kp] (out_dtype), K index c*p*p+ky*p+kx,
  * zero padded to Kp >= 3*p*p. */
 int clipk_im2col(int out_dtype, int B, int res, int patch, int Kp, const float* img, void* out,
@@ -123,6 +140,16 @@ int clipk_prompt_assemble(int B, int C, int L, int W, const int* src_map, const 
  * csc != 0: one output per class (no sum over c). Deterministic fixed-order sums. */
 int clipk_ctx_grad(int B, int C, int L, int W, int n_ctx, int csc, const int* ctx_pos,
                    const float* dx0, float* dctx, void* stream);
+
+/* Packed-prompt assembly: x0[g*R + r] = token(c,t) (+ctx slot + bias[g]) + pos[t] with
+ * c*L + t = row_tab[r] and the src_map convention above (ctx offset g*ctx_sg + c*ctx_sc). */
+int clipk_prompt_assemble_rows(int G, int R, int C, int L, int W, const int* row_tab,
+                               const int* src_map, const float* emb, const float* ctx, long ctx_sg,
+                               long ctx_sc, const float* bias, const float* pos, float* x0,
+                               void* stream);
+/* dctx[(g*n_ctx + k)*W + w] = sum_{i in [slot_ptr[k], slot_ptr[k+1])} dx0[(g*R + slot_rows[i])*W + w]. */
+int clipk_ctx_grad_rows(int G, int R, int W, int n_ctx, const int* slot_ptr, const int* slot_rows,
+                        const float* dx0, float* dctx, void* stream);
 
 /* logits[b,c] = scale * <imf[b], txt[row]> / |txt[row]| / |imf[b]|,
  * row = per_image ? b*C + c : c.  tnorm[row] (optional out) = |txt[row]|. */
@@ -184,6 +211,20 @@ size_t clipk_text_bwd_ws_bytes(const clipk_encoder* enc, int nseq, int L);
 int clipk_text_backward(const clipk_encoder* enc, int nseq, int L, const int* eot_rows,
                         const float* dtxt, const void* saved, size_t saved_bytes, float* dx0,
                         void* ws, size_t ws_bytes, void* stream);
+
+/* Shared-prefix packed variant (see clipk_attention_prefix_fwd): G groups of R rows,
+ * C sequences per group, x0 fp32 [G*R, W]; eot_rows[g*C + c] = absolute EOT row;
+ * txt fp32 [G*C, E]. Exact: rows after a sequence's EOT and duplicated causal prefixes
+ * never influence the EOT features. */
+size_t clipk_text_packed_saved_bytes(const clipk_encoder* enc, int G, int C, int R);
+size_t clipk_text_packed_ws_bytes(const clipk_encoder* enc, int G, int C, int R);
+size_t clipk_text_packed_bwd_ws_bytes(const clipk_encoder* enc, int G, int C, int R);
+int clipk_text_forward_packed(const clipk_encoder* enc, int G, int C, int P, int R, const int* seg,
+                              int max_q, const float* x0, const int* eot_rows, float* txt, void* saved,
+                              size_t saved_bytes, void* ws, size_t ws_bytes, void* stream);
+int clipk_text_backward_packed(const clipk_encoder* enc, int G, int C, int P, int R, const int* seg,
+                               int max_q, const int* eot_rows, const float* dtxt, const void* saved,
+                               size_t saved_bytes, float* dx0, void* ws, size_t ws_bytes, void* stream);
 
 /* Vision transformer forward (frozen, no grad): img fp32 [B,3,R,R] -> feat fp32 [B,E].
  * Head table for a vision encoder: ln_pre_w, ln_pre_b, ln_post_w, ln_post_b (f32),

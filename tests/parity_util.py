@@ -28,13 +28,14 @@ def state_dict(arch):
     return _SD_CACHE[arch]
 
 
-def make_cfg(meta, prec, cocoop=False, truncate=True):
+def make_cfg(meta, prec, cocoop=False, truncate=True, shared=True):
     from fsp_amd.engine.config import get_cfg_default
     from fsp_amd.clip import synth
     a = synth.ARCHS[meta["arch"]]
     cfg = get_cfg_default()
     cfg.INPUT.SIZE = (a.image_resolution, a.image_resolution)
     cfg.NATIVE.TRUNCATE_PROMPTS = truncate
+    cfg.NATIVE.SHARED_PREFIX = shared
     if cocoop:
         cfg.TRAINER.COCOOP.N_CTX = meta["n_ctx"]
         cfg.TRAINER.COCOOP.CTX_INIT = meta["ctx_init"]
@@ -55,19 +56,20 @@ def make_cfg(meta, prec, cocoop=False, truncate=True):
     return cfg
 
 
-def run_native(meta, arrays, prec, cocoop=False, dev="cuda", truncate=True):
+def run_native(meta, arrays, prec, cocoop=False, dev="cuda", truncate=True, shared=True):
     """Returns dict with image_features, logits, loss, grads, ctx_after_step (numpy)."""
     from fsp_amd.clip import synth
     from fsp_amd.clip.model import build_model
     from fsp_amd.engine.optim import FusedSGD
     from fsp_amd.trainers import coop as C, cocoop as CC
     a = synth.ARCHS[meta["arch"]]
-    cfg = make_cfg(meta, prec, cocoop, truncate)
+    cfg = make_cfg(meta, prec, cocoop, truncate, shared)
     clip = build_model(state_dict(meta["arch"]), prec=prec, device=dev)
     names = synth.synthetic_classnames(meta["n_cls"])
     mod = CC if cocoop else C
     model = mod.CustomCLIP(cfg, names, clip)
     pl = model.prompt_learner
+    out = {"packed": pl.layout.pack is not None}
     with torch.no_grad():
         if arrays.get("ctx0") is not None:
             pl.ctx.copy_(torch.from_numpy(arrays["ctx0"]).to(dev))
@@ -82,7 +84,6 @@ def run_native(meta, arrays, prec, cocoop=False, dev="cuda", truncate=True):
     img = torch.from_numpy(synth.make_images(B, a.image_resolution, seed=1)).to(dev)
     img2 = torch.from_numpy(synth.make_images(B, a.image_resolution, seed=5)).to(dev)
     lbl = torch.from_numpy(synth.make_labels(B, meta["n_cls"], seed=2)).to(dev)
-    out = {}
     if arrays.get("tokenized") is not None:
         assert (pl.tokenized_prompts.numpy() == arrays["tokenized"]).all(), "tokenization differs"
     model.eval()

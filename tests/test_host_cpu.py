@@ -160,3 +160,45 @@ def test_metrics_match_sklearn():
     assert abs(acc - 100 * (logits.argmax(1) == lab).double().mean().item()) < 1e-4
     b, n, hm = base_new_accuracy(np.array([0, 1, 3, 3]), np.array([0, 2, 3, 2]), 2)
     assert b == 100.0 and abs(n - 100 / 3) < 1e-9 and abs(hm - 2 * 100 * (100 / 3) / (100 + 100 / 3)) < 1e-9
+
+
+@pytest.mark.parametrize("position,n_ctx,P_expect", [("end", 4, 5), ("end", 16, 16), ("middle", 8, 5),
+                                                     ("front", 4, None)])
+def test_shared_prefix_tables_reconstruct_prompts(position, n_ctx, P_expect):
+    """Packed rows (prefix once per group + each class's rows P..EOT) hold exactly the
+    reference prompt tokens; ctx slot row lists cover every packed row using the slot."""
+    from oracle import clip_oracle as O
+    from fsp_amd.trainers._fns import prompt_layout
+    from fsp_amd.trainers.prompt_base import shared_prefix_tables
+    rs = np.random.RandomState(1)
+    C, W = 7, 8
+    name_lens = [1, 2, 3, 1, 4, 2, 5]
+    eot = [1 + n_ctx + nl + 1 for nl in name_lens]
+    emb = torch.from_numpy(rs.randn(C, 77, W).astype(np.float32))
+    emb[:, 0] = emb[0, 0]  # SOT token embedding is class independent
+    ctx = torch.from_numpy(rs.randn(n_ctx, W).astype(np.float32))
+    ref = O.coop_prompts(ctx, emb[:, :1], emb[:, 1 + n_ctx:], name_lens, position).numpy()
+    src, cpos, L = prompt_layout(C, n_ctx, name_lens, position, eot, truncate=True)
+    pk = shared_prefix_tables(src, cpos, eot, n_ctx, csc=False)
+    if P_expect is None:
+        assert pk is None
+        return
+    P, R, seg, row_tab = pk["P"], pk["R"], pk["seg"], pk["row_tab"]
+    assert P == P_expect and R == P + sum(e + 1 - P for e in eot)
+    packed = np.zeros((R, W), np.float32)  # numpy restatement of clipk_prompt_assemble_rows
+    for r in range(R):
+        c, t = divmod(int(row_tab[r]), L)
+        m = src[c, t]
+        packed[r] = emb[c, m].numpy() if m >= 0 else ctx[-1 - m].numpy()
+    for c in range(C):
+        off, qn = seg[c]
+        assert off + qn - 1 == pk["eot_in_group"][c] and qn == eot[c] + 1 - P
+        seq = np.concatenate([packed[:P], packed[off:off + qn]])
+        np.testing.assert_array_equal(seq, ref[c, :eot[c] + 1])
+    for k in range(n_ctx):
+        rows = sorted(pk["slot_rows"][pk["slot_ptr"][k]:pk["slot_ptr"][k + 1]].tolist())
+        expect = sorted(r for r in range(R) if src.flat[row_tab[r]] == -1 - k)
+        assert rows == expect
+    # CSC contexts and over-long class suffixes fall back to the plain layout
+    assert shared_prefix_tables(src, cpos, eot, n_ctx, csc=True) is None
+    assert shared_prefix_tables(src, cpos, [e + 20 for e in eot], n_ctx, csc=False) is None

@@ -224,3 +224,98 @@ def test_gemm_large_m_every_config(dev, cfg, Nn, K):
               refb * (s + 1.702 * aux.float() * s * (1 - s)), torch.bfloat16, f"cfg{cfg} dqgelu")
     finally:
         lib.clipk_gemm_set_config(-1)
+
+
+def prefix_case(G, C, P, H, max_q, seed):
+    """Random shared-prefix packing: per-class q_len in [1, max_q], group stride R."""
+    g = torch.Generator().manual_seed(seed)
+    qlen = torch.randint(1, max_q + 1, (C,), generator=g)
+    qlen[0] = max_q
+    off = P + torch.cat([torch.zeros(1, dtype=torch.long), qlen.cumsum(0)[:-1]])
+    R = int(P + qlen.sum())
+    seg = torch.stack([off, qlen], 1).to(torch.int32).reshape(-1)
+    return R, seg, off.tolist(), qlen.tolist(), g
+
+
+def attn_prefix_ref(qkv, G, C, P, R, off, qlen, H):
+    """Unpacked restatement: each class sequence = [prefix rows, own rows], causal; the
+    prefix rows' outputs from the prefix alone. Gathers from qkv (autograd sums shares)."""
+    W = H * 64
+    out = [None] * (G * R)
+    lse = [None] * (G * R)
+    for g in range(G):
+        base = g * R
+        seqs = [list(range(base, base + P))] + [list(range(base, base + P)) + list(range(base + off[c], base + off[c] + qlen[c])) for c in range(C)]
+        dst = [list(range(base, base + P))] + [list(range(base + off[c], base + off[c] + qlen[c])) for c in range(C)]
+        for idx, d in zip(seqs, dst):
+            x = qkv[idx].float().view(len(idx), 3, H, 64).permute(1, 2, 0, 3)
+            s = x[0] @ x[1].transpose(-1, -2) / 8.0
+            Lq = len(idx)
+            s = s + torch.full((Lq, Lq), float("-inf"), device=qkv.device).triu(1)
+            o = (torch.softmax(s, -1) @ x[2]).permute(1, 0, 2).reshape(Lq, W)
+            l = torch.logsumexp(s, -1).t()
+            for i, r in enumerate(d):
+                out[r] = o[Lq - len(d) + i]
+                lse[r] = l[Lq - len(d) + i]
+    return torch.stack(out), torch.stack(lse)
+
+
+@pytest.mark.parametrize("dtype,gdtype", [(torch.float16, torch.bfloat16), (torch.bfloat16, torch.bfloat16),
+                                          (torch.float32, torch.float32)])
+@pytest.mark.parametrize("G,C,P,H,max_q", [(2, 37, 5, 8, 6), (1, 19, 16, 2, 7), (3, 16, 2, 4, 16), (2, 3, 9, 2, 1)])
+def test_attention_prefix_fwd_bwd(dev, dtype, gdtype, G, C, P, H, max_q):
+    R, seg, off, qlen, g = prefix_case(G, C, P, H, max_q, seed=G * 100 + C + P)
+    W = H * 64
+    qkv = torch.randn(G * R, 3 * W, generator=g).to(dev).to(dtype)
+    seg = seg.to(dev)
+    o, lse = ops.attention_prefix(qkv, G, C, P, R, seg, max_q, H, lse=True)
+    q32 = qkv.float().requires_grad_(True)
+    ro, rl = attn_prefix_ref(q32, G, C, P, R, off, qlen, H)
+    close(o, ro, dtype, "prefix attn out")
+    close(lse, rl, torch.float16 if dtype != torch.float32 else dtype, "prefix attn lse")
+    dout = torch.randn(G * R, W, generator=g).to(dev).to(gdtype)
+    (ro * dout.float()).sum().backward()
+    dq = ops.attention_prefix_bwd(qkv, o, dout, lse, G, C, P, R, seg, max_q, H, gdtype)
+    ref = q32.grad
+    for part, sl in (("dq", slice(0, W)), ("dk", slice(W, 2 * W)), ("dv", slice(2 * W, 3 * W))):
+        close(dq[:, sl], ref[:, sl], gdtype if dtype != torch.float32 else dtype, f"prefix attn {part}")
+
+
+def test_prompt_rows_and_ctx_grad_rows(dev):
+    """Packed assembly + slot-list ctx grad against torch on the same tables."""
+    from fsp_amd.trainers._fns import prompt_layout
+    from fsp_amd.trainers.prompt_base import shared_prefix_tables
+    C, n_ctx, W, G = 9, 4, 128, 3
+    name_lens = [1, 2, 3, 1, 4, 2, 5, 1, 2]
+    eot = [1 + n_ctx + nl + 1 for nl in name_lens]
+    src, cpos, L = prompt_layout(C, n_ctx, name_lens, "end", eot)
+    pk = shared_prefix_tables(src, cpos, eot, n_ctx, csc=False)
+    g = torch.Generator().manual_seed(3)
+    emb = torch.randn(C, 77, W, generator=g).to(dev)
+    ctx = torch.randn(n_ctx, W, generator=g).to(dev)
+    bias = torch.randn(G, W, generator=g).to(dev)
+    pos = torch.randn(77, W, generator=g).to(dev)
+    t = lambda a: torch.from_numpy(a).to(dev)
+    R = pk["R"]
+    x0 = ops.prompt_assemble_rows(G, R, C, L, t(pk["row_tab"]), t(src), emb, ctx, 0, 0, bias, pos)
+    ref = torch.empty(G * R, W, device=dev)
+    for gg in range(G):
+        for r in range(R):
+            c, tt = divmod(int(pk["row_tab"][r]), L)
+            m = int(src[c, tt])
+            ref[gg * R + r] = (emb[c, m] if m >= 0 else ctx[-1 - m] + bias[gg]) + pos[tt]
+    torch.testing.assert_close(x0, ref, rtol=0, atol=1e-6)
+    dx = torch.randn(G * R, W, generator=g).to(dev)
+    d = ops.ctx_grad_rows(G, R, W, n_ctx, t(pk["slot_ptr"]), t(pk["slot_rows"]), dx)
+    ctx_r = ctx.clone().requires_grad_(True)
+    bias_r = bias.clone().requires_grad_(True)
+    rows = []
+    for gg in range(G):
+        for r in range(R):
+            c, tt = divmod(int(pk["row_tab"][r]), L)
+            m = int(src[c, tt])
+            rows.append((ctx_r[-1 - m] + bias_r[gg]) if m < 0 else torch.zeros(W, device=dev))
+    (torch.stack(rows) * dx).sum().backward()
+    d = d.view(G, n_ctx, W)
+    torch.testing.assert_close(d.sum(0), ctx_r.grad, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(d.sum(1), bias_r.grad, rtol=1e-5, atol=1e-4)

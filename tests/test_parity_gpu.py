@@ -10,6 +10,9 @@ Tolerances (stated here):
   scale 100), |d loss| <= 0.05 (the same logit bound through a CE/focal loss, whose
   Lipschitz constant w.r.t. the max-norm of the logits is <= 2 * alpha_max here),
   gradient 1 - cos <= 2e-3.
+Every case runs twice: on the shared-prefix packed row layout (default; the prompt's
+SOT + context rows encoded once per image / class set, rows past each EOT dropped) and
+on the plain [B*C, L] layout (NATIVE.SHARED_PREFIX False); both against the same vectors.
 Accuracy/argmax parity is not asserted: with random weights the logits are clustered
  and argmax is ill-conditioned.
 """
@@ -30,9 +33,16 @@ FULL_COOP = ["coop_vitb32_c10", "coop_vitb16_c6_focal", "coop_vitl14_c4"]
 FULL_COCOOP = ["cocoop_vitb16_c4", "cocoop_vitl14_336_c3"]
 
 
-def _check(name, cocoop, prec, dev):
+SHOULD_PACK = {"coop_tiny_end_csc0_ce", "coop_tiny_middle_csc0_ce", "coop_tiny_end_focal", "coop_tiny_end_simclr",
+               "coop_tiny_ctxinit_ce", "coop_tinyp8_end_ce", "cocoop_tiny_ctxinit_ce", "cocoop_tiny_focal",
+               "coop_vitb32_c10", "coop_vitb16_c6_focal", "coop_vitl14_c4", "cocoop_vitb16_c4",
+               "cocoop_vitl14_336_c3"}
+
+
+def _check(name, cocoop, prec, dev, layout="packed"):
     meta, ref = load_fixture(name)
-    out = run_native(meta, ref, prec, cocoop=cocoop, dev=str(dev))
+    out = run_native(meta, ref, prec, cocoop=cocoop, dev=str(dev), shared=layout == "packed")
+    assert out["packed"] == (layout == "packed" and name in SHOULD_PACK), (name, layout, out["packed"])
     grads = [k for k in ref if k.startswith("grad_")]
     report = {}
     if prec == "fp32":
@@ -67,28 +77,32 @@ def _check(name, cocoop, prec, dev):
             assert cos_err(out["text_features"], ref["text_features"]) <= 5e-4
 
 
+@pytest.mark.parametrize("layout", ["packed", "plain"])
 @pytest.mark.parametrize("prec", ["fp32", "fp16"])
 @pytest.mark.parametrize("name", TINY_COOP)
-def test_coop_tiny(dev, name, prec):
-    _check(name, False, prec, dev)
+def test_coop_tiny(dev, name, prec, layout):
+    _check(name, False, prec, dev, layout)
 
 
+@pytest.mark.parametrize("layout", ["packed", "plain"])
 @pytest.mark.parametrize("prec", ["fp32", "fp16"])
 @pytest.mark.parametrize("name", TINY_COCOOP)
-def test_cocoop_tiny(dev, name, prec):
-    _check(name, True, prec, dev)
+def test_cocoop_tiny(dev, name, prec, layout):
+    _check(name, True, prec, dev, layout)
 
 
+@pytest.mark.parametrize("layout", ["packed", "plain"])
 @pytest.mark.parametrize("prec", ["fp32", "fp16"])
 @pytest.mark.parametrize("name", FULL_COOP)
-def test_coop_full(dev, name, prec):
-    _check(name, False, prec, dev)
+def test_coop_full(dev, name, prec, layout):
+    _check(name, False, prec, dev, layout)
 
 
+@pytest.mark.parametrize("layout", ["packed", "plain"])
 @pytest.mark.parametrize("prec", ["fp32", "fp16"])
 @pytest.mark.parametrize("name", FULL_COCOOP)
-def test_cocoop_full(dev, name, prec):
-    _check(name, True, prec, dev)
+def test_cocoop_full(dev, name, prec, layout):
+    _check(name, True, prec, dev, layout)
 
 
 def _cocoop_oracle_logits_grad(arch, n_cls, batch, seed_img=1):
@@ -116,13 +130,16 @@ def _cocoop_oracle_logits_grad(arch, n_cls, batch, seed_img=1):
 
 
 @pytest.mark.parametrize("prec", ["fp32", "fp16"])
-def test_cocoop_large_rows_vs_oracle(dev, prec):
+@pytest.mark.parametrize("layout", ["packed", "plain"])
+def test_cocoop_large_rows_vs_oracle(dev, prec, layout):
     """tiny CLIP, C = 2000 classes x B = 3 images: 66k text rows, so the large-M GEMM
     paths (persistent 256x256) run inside the full model; checked against the oracle."""
     import torch
     meta = {"arch": "tiny", "n_cls": 2000, "batch": 3, "n_ctx": 4, "ctx_init": "a photo of a", "focal": 0}
     logits, loss, gctx, ctx0 = _cocoop_oracle_logits_grad("tiny", 2000, 3)
-    out = run_native(meta, {"ctx0": ctx0, "tokenized": None}, prec, cocoop=True, dev=str(dev))
+    out = run_native(meta, {"ctx0": ctx0, "tokenized": None}, prec, cocoop=True, dev=str(dev),
+                     shared=layout == "packed")
+    assert out["packed"] == (layout == "packed")
     if prec == "fp32":
         assert float(np.abs(out["logits"] - logits).max()) <= 1e-3
         assert rel_err(out["grad_ctx"], gctx) <= 1e-3
@@ -132,11 +149,13 @@ def test_cocoop_large_rows_vs_oracle(dev, prec):
 
 
 def test_bench_scale_fp16_matches_fp32(dev):
-    """The benchmark workload shape (ViT-B/16, C = 1000, n_ctx 4) at B = 2: the fp16 path
-    (large-M GEMM configurations) against the fp32 path (f32 MFMA, 128x128 tiles)."""
+    """The benchmark workload shape (ViT-B/16, C = 1000, n_ctx 4) at B = 2: the fp16 packed
+    path (large-M GEMM configurations, shared-prefix attention) against the fp32 plain
+    path (f32 MFMA, 128x128 tiles, [B*C, L] rows)."""
     meta = {"arch": "ViT-B/16", "n_cls": 1000, "batch": 2, "n_ctx": 4, "ctx_init": "a photo of a", "focal": 0}
-    o32 = run_native(meta, {"ctx0": None, "tokenized": None}, "fp32", cocoop=True, dev=str(dev))
+    o32 = run_native(meta, {"ctx0": None, "tokenized": None}, "fp32", cocoop=True, dev=str(dev), shared=False)
     o16 = run_native(meta, {"ctx0": None, "tokenized": None}, "fp16", cocoop=True, dev=str(dev))
+    assert o16["packed"] and not o32["packed"]
     assert np.isfinite(o16["logits"]).all() and np.isfinite(o16["grad_ctx"]).all()
     assert float(np.abs(o16["logits"] - o32["logits"]).max()) <= 5e-2
     assert abs(o16["loss"] - o32["loss"]) <= 0.05
