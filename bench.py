@@ -159,8 +159,8 @@ def main():
             peak = PEAK[args.prec if args.prec != "fp16" else "bf16"]  # dgelu GEMM runs on bf16 operands
             roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(ach / peak, 4), "traffic": None,
-                    "kernel": "gemm_nt_kernel<bf16,bf16,f16,EPI_DQGELU> (text c_proj input-grad GEMM, "
-                              "M=B*C*L, N=4W, K=W)",
+                    "kernel": "gemm_nt_kernel<bf16,bf16,f16,EPI_DQGELU> (text c_proj input-grad GEMM fused with "
+                              "QuickGELU'(h), M=text rows, N=4W, K=W)",
                     "avg_launch_ms": round(avg_ms, 4), "launches": cnt.value,
                     "flops_per_launch": fl}
     tmax = dist.max_over_ranks(t)

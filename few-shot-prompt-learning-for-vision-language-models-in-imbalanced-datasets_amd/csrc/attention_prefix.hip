@@ -21,11 +21,23 @@
 // (g, h) are loaded once per wave and reused by every segment of the chunk. The backward
 // accumulates the prefix rows' dK/dV over the chunk in registers and writes one fp32
 // partial per chunk; prefix_kv_reduce sums the chunks in a fixed order (deterministic).
+#include <cstdlib>
+
 #include "attn_common.h"
 
 namespace clipk {
 
-constexpr int kSegChunk = 16;
+constexpr int kFwdBatch = 4, kBwdBatch = 2;  // segments whose loads are issued together
+constexpr int kSegChunk = 16;  // VALU kernels; MFMA kernels take the chunk as an argument (<= 16)
+
+// Segments per wave of the MFMA kernels (env CLIPK_PREFIX_FWD_CHUNK / _BWD_CHUNK, read once).
+static int chunk_env(const char* name, int def) {
+  const char* e = getenv(name);
+  const int v = e ? atoi(e) : def;
+  return v >= 1 && v <= 16 ? v : def;
+}
+static int fwd_chunk() { static int c = chunk_env("CLIPK_PREFIX_FWD_CHUNK", 16); return c; }
+static int bwd_chunk() { static int c = chunk_env("CLIPK_PREFIX_BWD_CHUNK", 16); return c; }
 
 __device__ __forceinline__ void seg_info(const int* __restrict__ seg, int g, int R, int P, int s,
                                          int& q0, int& qn, int& pre) {
@@ -38,13 +50,48 @@ __device__ __forceinline__ void seg_info(const int* __restrict__ seg, int g, int
   }
 }
 
+// The chunk's segment table in one VGPR (lane i holds seg[2*(s_begin-1) + i]), read back
+// with v_readlane: no dependent scalar-memory round trip inside the segment loop.
+__device__ __forceinline__ int load_seg_table(const int* __restrict__ seg, int C, int s_begin, int lane) {
+  const int idx = 2 * (s_begin - 1) + lane;
+  return (lane < 32 && idx >= 0 && idx < 2 * C) ? seg[idx] : 0;
+}
+__device__ __forceinline__ void seg_info_reg(int tab, int g, int R, int P, int s, int s_begin, int& q0,
+                                             int& qn, int& pre) {
+  if (s == 0) {
+    q0 = g * R; qn = P; pre = 0;
+  } else {
+    const int i = 2 * (s - s_begin);
+    q0 = g * R + __builtin_amdgcn_readlane(tab, i);
+    qn = min(__builtin_amdgcn_readlane(tab, i + 1), 16);
+    pre = P;
+  }
+}
+
+// Unconditional 16-B load (the caller clamps the row to a valid one) with the value
+// zeroed in lanes whose row is past the segment: no exec-masked branch around the load,
+// so the compiler can count the loads across the segment loop (vmcnt(N), not vmcnt(0)).
+__device__ __forceinline__ s16x8 ld16(const void* p) { return *reinterpret_cast<const s16x8*>(p); }
+__device__ __forceinline__ s16x8 sel16(s16x8 v, bool ok) {
+  const s16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+  return ok ? v : z;
+}
+
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // ------------------------------------------------------------------ forward, MFMA (16-bit)
+// Software-pipelined over the chunk's segments: the next segment's Q/K/V fragments are in
+// flight while the current one is computed (the per-segment work is too small to hide a
+// dependent HBM round trip otherwise).
+struct SegRows {
+  s16x8 q[2], k[2], v[2];
+  int q0, qn, pre;
+};
+
 template <typename T>
 __global__ __launch_bounds__(256) void attn_prefix_fwd_mfma(int G, int C, int P, int R,
                                                             const int* __restrict__ seg, int H,
-                                                            int nchunk, const T* __restrict__ qkv,
+                                                            int nchunk, int sc, const T* __restrict__ qkv,
                                                             int ldq, T* __restrict__ out, int ldo,
                                                             float* __restrict__ lse) {
   __shared__ CLIPK_LDS_ALIGN short tiles[4][2][16 * TRS];  // per wave: prefix V, own V
@@ -57,6 +104,25 @@ __global__ __launch_bounds__(256) void attn_prefix_fwd_mfma(int G, int C, int P,
   short* sVp = tiles[w][0];
   short* sVo = tiles[w][1];
 
+  const int s_begin = k * sc, s_end = min((k + 1) * sc, C + 1);
+  const int tab = load_seg_table(seg, C, s_begin, lane);
+  auto load = [&](int s, SegRows& f) {
+    seg_info_reg(tab, g, R, P, s, s_begin, f.q0, f.qn, f.pre);
+    const bool ok = r16 < f.qn;
+    const T* qp = qkv + ((size_t)f.q0 + min(r16, f.qn - 1)) * ldq + h * 64;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = 8 * g4 + 32 * kk;
+      f.q[kk] = ld16(qp + c);
+      f.k[kk] = ld16(qp + W + c);
+      f.v[kk] = ld16(qp + 2 * W + c);
+    }
+    (void)ok;
+  };
+
+  // Batches of kFwdBatch segments: all their loads issued up front (unconditional, rows
+  // and segment indices clamped), then the bodies; waits are counted inside one loop
+  // iteration (a load carried across the back edge gets a vmcnt(0) at the loop head).
   const bool pok = r16 < P;
   const T* pp = qkv + ((size_t)g * R + (pok ? r16 : 0)) * ldq + h * 64;
   s16x8 kp[2];
@@ -66,28 +132,23 @@ __global__ __launch_bounds__(256) void attn_prefix_fwd_mfma(int G, int C, int P,
     kp[kk] = ld_row16(pp + W + c, pok);
     *reinterpret_cast<s16x8*>(sVp + r16 * TRS + c) = ld_row16(pp + 2 * W + c, pok);
   }
-  const int s_end = min((k + 1) * kSegChunk, C + 1);
-  for (int s = k * kSegChunk; s < s_end; ++s) {
-    int q0, qn, pre;
-    seg_info(seg, g, R, P, s, q0, qn, pre);
+  auto body = [&](int s, SegRows& cur) {
+    const int q0 = cur.q0, qn = cur.qn, pre = cur.pre;
     const bool qok = r16 < qn;
-    const T* qp = qkv + ((size_t)q0 + (qok ? r16 : 0)) * ldq + h * 64;
-    s16x8 qf[2], ko[2], vo[2];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int c = 8 * g4 + 32 * kk;
-      qf[kk] = ld_row16(qp + c, qok);
-      ko[kk] = ld_row16(qp + W + c, qok);
-      vo[kk] = ld_row16(qp + 2 * W + c, qok);
+    for (int kk = 0; kk < 2; ++kk) {  // rows past the segment: zero (their loads were clamped)
+      cur.q[kk] = sel16(cur.q[kk], qok);
+      cur.k[kk] = sel16(cur.k[kk], qok);
+      cur.v[kk] = sel16(cur.v[kk], qok);
     }
     lds_fence();  // previous segment's transposed reads of sVo are done
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) *reinterpret_cast<s16x8*>(sVo + r16 * TRS + 8 * g4 + 32 * kk) = vo[kk];
+    for (int kk = 0; kk < 2; ++kk) *reinterpret_cast<s16x8*>(sVo + r16 * TRS + 8 * g4 + 32 * kk) = cur.v[kk];
     f32x4 sp = {0.f, 0.f, 0.f, 0.f}, so = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      sp = mfma32_t<T>(kp[kk], qf[kk], sp);  // sp[r] = S[query r16][prefix key 4g4+r]
-      so = mfma32_t<T>(ko[kk], qf[kk], so);  // so[r] = S[query r16][own key 4g4+r]
+      sp = mfma32_t<T>(kp[kk], cur.q[kk], sp);     // sp[r] = S[query r16][prefix key 4g4+r]
+      so = mfma32_t<T>(cur.k[kk], cur.q[kk], so);  // so[r] = S[query r16][own key 4g4+r]
     }
     float vp[4], vq[4], mx = -INFINITY;
 #pragma unroll
@@ -109,36 +170,46 @@ __global__ __launch_bounds__(256) void attn_prefix_fwd_mfma(int G, int C, int P,
     ps += __shfl_xor(ps, 16, 64);
     ps += __shfl_xor(ps, 32, 64);
     lds_fence();
-    const s16x4 ap = pack4<T>(ep[0], ep[1], ep[2], ep[3]);  // A[m=query r16][k=key 4g4+jj]
-    const s16x4 ao = pack4<T>(eo[0], eo[1], eo[2], eo[3]);
-    f32x4 o[4];
+    // O^T = V^T P^T: the transposed V read doubles as the A operand (A[m=d][k=key]) and the
+    // probabilities as B (B[k=key 4g4+jj][n=query r16]), so lane (r16, g4) ends up holding
+    // O[query r16][d = 16t + 4g4 .. +3]: one 8-byte store per 16 columns.
+    const s16x4 bp = pack4<T>(ep[0], ep[1], ep[2], ep[3]);
+    const s16x4 bo = pack4<T>(eo[0], eo[1], eo[2], eo[3]);
+    const float inv = 1.0f / ps;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      o[t] = mfma16_t<T>(ap, tr_read(sVp, 4 * g4, 16 * t, lane), (f32x4){0.f, 0.f, 0.f, 0.f});
-      o[t] = mfma16_t<T>(ao, tr_read(sVo, 4 * g4, 16 * t, lane), o[t]);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int q = 4 * g4 + r;
-      const float inv = 1.0f / __shfl(ps, q, 64);
-      if (q < qn) {
-        T* op = out + ((size_t)q0 + q) * ldo + h * 64 + r16;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) op[16 * t] = (T)(o[t][r] * inv);
-      }
+      f32x4 o = mfma16_t<T>(tr_read(sVp, 4 * g4, 16 * t, lane), bp, (f32x4){0.f, 0.f, 0.f, 0.f});
+      o = mfma16_t<T>(tr_read(sVo, 4 * g4, 16 * t, lane), bo, o);
+      if (qok) store4<T>(out + ((size_t)q0 + r16) * ldo + h * 64 + 16 * t + 4 * g4, o[0] * inv, o[1] * inv,
+                         o[2] * inv, o[3] * inv);
     }
     if (lse && g4 == 0 && qok) lse[((size_t)q0 + r16) * H + h] = mx + __logf(ps);
+  };
+  for (int s = s_begin; s < s_end; s += kFwdBatch) {
+    SegRows rr[kFwdBatch];
+#pragma unroll
+    for (int j = 0; j < kFwdBatch; ++j) load(min(s + j, s_end - 1), rr[j]);
+    __builtin_amdgcn_sched_barrier(0);  // every load of the batch issues before the first wait
+#pragma unroll
+    for (int j = 0; j < kFwdBatch; ++j)
+      if (s + j < s_end) body(s + j, rr[j]);
   }
 }
 
 // ------------------------------------------------------------------ backward, MFMA (bf16 math)
 // Per segment, with the two 16-key tiles (prefix, own) handled like attn_bwd_mfma16:
 // S / dP in both accumulator layouts, D_i = rowsum(P o dP) over both tiles in registers,
-// dV = P^T dO, dK = dS^T Q, dQ = dS_pre K_pre + dS_own K_own.
+// dV = P^T dO, dK = dS^T Q, dQ = dS_pre K_pre + dS_own K_own. Pipelined like the forward.
+struct SegRowsB {
+  s16x8 q[2], k[2], v[2], d[2];
+  float l2, l1[4];
+  int q0, qn, pre;
+};
+
 template <typename T, typename TG>
 __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int C, int P, int R,
                                                             const int* __restrict__ seg, int H,
-                                                            int nchunk, const T* __restrict__ qkv,
+                                                            int nchunk, int sc, const T* __restrict__ qkv,
                                                             int ldq, const TG* __restrict__ dout,
                                                             int lddo, const float* __restrict__ lse,
                                                             TG* __restrict__ dqkv, int lddq,
@@ -155,7 +226,31 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int C, int P,
   short* tKo = tiles[w][1];
   short* tQ = tiles[w][2];
   short* tD = tiles[w][3];
+  const float* lse_h = lse + h;
 
+  const int s_begin = k * sc, s_end = min((k + 1) * sc, C + 1);
+  const int tab = load_seg_table(seg, C, s_begin, lane);
+  auto load = [&](int s, SegRowsB& f) {
+    seg_info_reg(tab, g, R, P, s, s_begin, f.q0, f.qn, f.pre);
+    const bool ok = r16 < f.qn;
+    const size_t row = (size_t)f.q0 + min(r16, f.qn - 1);
+    const T* qp = qkv + row * ldq + h * 64;
+    const TG* dp = dout + row * lddo + h * 64;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = 8 * g4 + 32 * kk;
+      f.q[kk] = ld16(qp + c);
+      f.k[kk] = ld16(qp + W + c);
+      f.v[kk] = ld16(qp + 2 * W + c);
+      f.d[kk] = ld16(dp + c);
+    }
+    (void)ok;
+    f.l2 = lse_h[row * H];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) f.l1[r] = lse_h[((size_t)f.q0 + min(4 * g4 + r, f.qn - 1)) * H];
+  };
+
+  // batches of kBwdBatch segments, as in the forward
   const bool pok = r16 < P;
   const T* pp = qkv + ((size_t)g * R + (pok ? r16 : 0)) * ldq + h * 64;
   s16x8 kp[2], vp[2];
@@ -172,22 +267,16 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int C, int P,
     dkp[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
     dvp[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
   }
-  const float* lse_h = lse + h;
-  const int s_end = min((k + 1) * kSegChunk, C + 1);
-  for (int s = k * kSegChunk; s < s_end; ++s) {
-    int q0, qn, pre;
-    seg_info(seg, g, R, P, s, q0, qn, pre);
+  auto body = [&](int s, SegRowsB& cur) {
+    const int q0 = cur.q0, qn = cur.qn, pre = cur.pre;
     const bool qok = r16 < qn;
-    const T* qp = qkv + ((size_t)q0 + (qok ? r16 : 0)) * ldq + h * 64;
-    const TG* dp = dout + ((size_t)q0 + (qok ? r16 : 0)) * lddo + h * 64;
     s16x8 q[2], ko[2], vo[2], d[2];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int c = 8 * g4 + 32 * kk;
-      q[kk] = to_bf16x8<T>(ld_row16(qp + c, qok));
-      ko[kk] = to_bf16x8<T>(ld_row16(qp + W + c, qok));
-      vo[kk] = to_bf16x8<T>(ld_row16(qp + 2 * W + c, qok));
-      d[kk] = ld_row16(dp + c, qok);
+    for (int kk = 0; kk < 2; ++kk) {  // rows past the segment: zero (their loads were clamped)
+      q[kk] = to_bf16x8<T>(sel16(cur.q[kk], qok));
+      ko[kk] = to_bf16x8<T>(sel16(cur.k[kk], qok));
+      vo[kk] = to_bf16x8<T>(sel16(cur.v[kk], qok));
+      d[kk] = sel16(cur.d[kk], qok);
     }
     lds_fence();  // previous segment's transposed reads are done
 #pragma unroll
@@ -211,7 +300,7 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int C, int P,
       p2o = mfma32_bf16(vo[kk], d[kk], p2o);
     }
     // layout 2: i = r16, j = 4g4+r
-    const float li2 = qok ? lse_h[((size_t)q0 + r16) * H] : 0.f;
+    const float li2 = cur.l2;
     float P2p[4], P2o[4], Dsum = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -234,62 +323,66 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int C, int P,
     for (int r = 0; r < 4; ++r) {
       const int i = 4 * g4 + r;
       const bool iok = i < qn;
-      const float li = iok ? lse_h[((size_t)q0 + i) * H] : 0.f;
+      const float li = cur.l1[r];
       const float Di = __shfl(Dsum, i, 64);
       P1p[r] = (iok && r16 < pre) ? __expf(s1p[r] * kScale - li) : 0.f;
       P1o[r] = (iok && r16 <= i) ? __expf(s1o[r] * kScale - li) : 0.f;
       dS1p[r] = P1p[r] * (p1p[r] - Di);
       dS1o[r] = P1o[r] * (p1o[r] - Di);
     }
-    const s16x4 aPp = pack_bf16x4(P1p[0], P1p[1], P1p[2], P1p[3]);      // A[m=j][k=i]
-    const s16x4 aSp = pack_bf16x4(dS1p[0], dS1p[1], dS1p[2], dS1p[3]);
-    const s16x4 aPo = pack_bf16x4(P1o[0], P1o[1], P1o[2], P1o[3]);
-    const s16x4 aSo = pack_bf16x4(dS1o[0], dS1o[1], dS1o[2], dS1o[3]);
-    const s16x4 aTp = pack_bf16x4(dS2p[0], dS2p[1], dS2p[2], dS2p[3]);  // A[m=i][k=j]
-    const s16x4 aTo = pack_bf16x4(dS2o[0], dS2o[1], dS2o[2], dS2o[3]);
+    // Transposed products (operands swapped), so each lane holds 4 consecutive columns of
+    // one row: dV^T = dO^T P, dK^T = Q^T dS, dQ^T = K^T dS^T with the transposed LDS reads
+    // as A and the probability / dS registers as B. Lane (r16, g4), tile t: row r16,
+    // columns 16t + 4g4 .. +3.
+    const s16x4 bPp = pack_bf16x4(P1p[0], P1p[1], P1p[2], P1p[3]);      // B[k=i][n=j]
+    const s16x4 bSp = pack_bf16x4(dS1p[0], dS1p[1], dS1p[2], dS1p[3]);
+    const s16x4 bPo = pack_bf16x4(P1o[0], P1o[1], P1o[2], P1o[3]);
+    const s16x4 bSo = pack_bf16x4(dS1o[0], dS1o[1], dS1o[2], dS1o[3]);
+    const s16x4 bTp = pack_bf16x4(dS2p[0], dS2p[1], dS2p[2], dS2p[3]);  // B[k=j][n=i]
+    const s16x4 bTo = pack_bf16x4(dS2o[0], dS2o[1], dS2o[2], dS2o[3]);
     lds_fence();
     const bool own_is_prefix = s == 0;  // segment 0's keys are the prefix rows themselves
+    TG* orow = dqkv + ((size_t)q0 + r16) * lddq + h * 64 + 4 * g4;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const s16x4 bD = tr_read(tD, 4 * g4, 16 * t, lane);
-      const s16x4 bQ = tr_read(tQ, 4 * g4, 16 * t, lane);
-      dvp[t] = mfma16_bf16(aPp, bD, dvp[t]);
-      dkp[t] = mfma16_bf16(aSp, bQ, dkp[t]);
-      f32x4 dq = mfma16_bf16(aTp, tr_read(tKp, 4 * g4, 16 * t, lane), z);
-      dq = mfma16_bf16(aTo, tr_read(tKo, 4 * g4, 16 * t, lane), dq);
-      const f32x4 dvo = mfma16_bf16(aPo, bD, z);
-      const f32x4 dko = mfma16_bf16(aSo, bQ, z);
-      const int col = h * 64 + 16 * t + r16;
+      const s16x4 aD = tr_read(tD, 4 * g4, 16 * t, lane);
+      const s16x4 aQ = tr_read(tQ, 4 * g4, 16 * t, lane);
+      dvp[t] = mfma16_bf16(aD, bPp, dvp[t]);
+      dkp[t] = mfma16_bf16(aQ, bSp, dkp[t]);
+      f32x4 dq = mfma16_bf16(tr_read(tKp, 4 * g4, 16 * t, lane), bTp, z);
+      dq = mfma16_bf16(tr_read(tKo, 4 * g4, 16 * t, lane), bTo, dq);
+      const f32x4 dvo = mfma16_bf16(aD, bPo, z);
+      const f32x4 dko = mfma16_bf16(aQ, bSo, z);
       if (own_is_prefix) {
         dvp[t] += dvo;
         dkp[t] += dko;
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 4 * g4 + r;
-        if (row < qn) {
-          TG* o = dqkv + ((size_t)q0 + row) * lddq + col;
-          o[0] = (TG)(dq[r] * kScale);
-          if (!own_is_prefix) {
-            o[W] = (TG)(dko[r] * kScale);
-            o[2 * W] = (TG)dvo[r];
-          }
+      if (qok) {
+        store4<TG>(orow + 16 * t, dq[0] * kScale, dq[1] * kScale, dq[2] * kScale, dq[3] * kScale);
+        if (!own_is_prefix) {
+          store4<TG>(orow + W + 16 * t, dko[0] * kScale, dko[1] * kScale, dko[2] * kScale, dko[3] * kScale);
+          store4<TG>(orow + 2 * W + 16 * t, dvo[0], dvo[1], dvo[2], dvo[3]);
         }
       }
     }
+  };
+  for (int s = s_begin; s < s_end; s += kBwdBatch) {
+    SegRowsB rr[kBwdBatch];
+#pragma unroll
+    for (int j = 0; j < kBwdBatch; ++j) load(min(s + j, s_end - 1), rr[j]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < kBwdBatch; ++j)
+      if (s + j < s_end) body(s + j, rr[j]);
   }
   // this chunk's partial dK/dV of the prefix rows (fp32, [G][nchunk][16][2W])
   float* pb = part + ((size_t)g * nchunk + k) * 16 * (2 * W);
+  if (r16 < P) {
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int col = h * 64 + 16 * t + r16;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int j = 4 * g4 + r;
-      if (j < P) {
-        pb[(size_t)j * 2 * W + col] = dkp[t][r] * kScale;
-        pb[(size_t)j * 2 * W + W + col] = dvp[t][r];
-      }
+    for (int t = 0; t < 4; ++t) {
+      float* dst = pb + (size_t)r16 * 2 * W + h * 64 + 16 * t + 4 * g4;
+      *reinterpret_cast<f32x4*>(dst) = dkp[t] * kScale;
+      *reinterpret_cast<f32x4*>(dst + W) = dvp[t];
     }
   }
 }
@@ -555,17 +648,20 @@ __global__ __launch_bounds__(256) void prefix_kv_reduce(int P, int R, int W, int
   dqkv[((size_t)g * R + p) * lddq + W + col] = (TG)acc;
 }
 
-static inline int n_chunks(int C) { return (C + 1 + kSegChunk - 1) / kSegChunk; }
+static inline int n_chunks(int C, int sc = kSegChunk) { return (C + 1 + sc - 1) / sc; }
 
 template <typename T>
 static int prefix_fwd(int G, int C, int P, int R, const int* seg, int H, const void* qkv, int ldq,
                       void* out, int ldo, float* lse, hipStream_t st) {
-  const int nchunk = n_chunks(C);
-  const long waves = (long)G * nchunk * H;
   if constexpr (sizeof(T) == 2) {
+    const int sc = fwd_chunk();
+    const int nchunk = n_chunks(C, sc);
+    const long waves = (long)G * nchunk * H;
     hipLaunchKernelGGL((attn_prefix_fwd_mfma<T>), dim3((waves + 3) / 4), dim3(256), 0, st, G, C, P, R, seg,
-                       H, nchunk, (const T*)qkv, ldq, (T*)out, ldo, lse);
+                       H, nchunk, sc, (const T*)qkv, ldq, (T*)out, ldo, lse);
   } else {
+    const int nchunk = n_chunks(C);
+    const long waves = (long)G * nchunk * H;
     hipLaunchKernelGGL((attn_prefix_fwd_valu<T>), dim3(waves), dim3(64), 0, st, G, C, P, R, seg, H, nchunk,
                        (const T*)qkv, ldq, (T*)out, ldo, lse);
   }
@@ -577,11 +673,13 @@ template <typename T, typename TG>
 static int prefix_bwd(int G, int C, int P, int R, const int* seg, int H, const void* qkv, int ldq,
                       const void* ofwd, int ldof, const void* dout, int lddo, const float* lse,
                       void* dqkv, int lddq, float* part, hipStream_t st) {
-  const int nchunk = n_chunks(C);
+  constexpr bool mfma = __is_same(TG, bf16) && sizeof(T) == 2;
+  const int sc = mfma ? bwd_chunk() : kSegChunk;
+  const int nchunk = n_chunks(C, sc);
   const long waves = (long)G * nchunk * H;
-  if constexpr (__is_same(TG, bf16) && sizeof(T) == 2) {
+  if constexpr (mfma) {
     hipLaunchKernelGGL((attn_prefix_bwd_mfma<T, TG>), dim3((waves + 3) / 4), dim3(256), 0, st, G, C, P, R,
-                       seg, H, nchunk, (const T*)qkv, ldq, (const TG*)dout, lddo, lse, (TG*)dqkv, lddq,
+                       seg, H, nchunk, sc, (const T*)qkv, ldq, (const TG*)dout, lddo, lse, (TG*)dqkv, lddq,
                        part);
   } else {
     hipLaunchKernelGGL((attn_prefix_bwd_valu<T, TG>), dim3(waves), dim3(64), 0, st, G, C, P, R, seg, H,
@@ -606,7 +704,8 @@ static int prefix_shape_ok(int G, int C, int P, int R, int max_q, int heads) {
 
 extern "C" size_t clipk_attention_prefix_ws_bytes(int G, int C, int heads) {
   if (G <= 0 || C <= 0 || heads <= 0) return 0;
-  return (size_t)G * n_chunks(C) * 16 * 2 * heads * 64 * sizeof(float);
+  const int sc = bwd_chunk() < kSegChunk ? bwd_chunk() : kSegChunk;  // the larger chunk count of the two paths
+  return (size_t)G * n_chunks(C, sc) * 16 * 2 * heads * 64 * sizeof(float);
 }
 
 extern "C" int clipk_attention_prefix_fwd(int dtype, int G, int C, int P, int R, const int* seg,

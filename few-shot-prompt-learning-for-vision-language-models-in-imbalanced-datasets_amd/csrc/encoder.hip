@@ -350,7 +350,8 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
   for (int l = e->layers - 1; l >= 0; --l) {
     const auto& w = e->lw[l];
     if (!w[12] || !w[13] || !w[14] || !w[15]) return CLIPK_EINVAL;
-    // MLP: dg = dX . Wproj ; dh = dg * qgelu'(h)
+    // MLP: dg = dX . Wproj ; dh = dg * qgelu'(h)  (h saved in the act dtype: more precise
+    // than saving qgelu'(h), which rounds the saturated region)
     TRY(gemm(gd, gd, CLIPK_EPI_DQGELU, rows, 4 * W, W, b.dX_lp, w[15], nullptr, nullptr, b.dh, nullptr,
              t.h[l], act, st, CLIPK_PROF_GEMM_DGELU));
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, 4 * W, b.dh, w[14], nullptr, nullptr, b.dxn, nullptr,

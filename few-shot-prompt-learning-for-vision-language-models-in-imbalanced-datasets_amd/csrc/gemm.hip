@@ -26,6 +26,7 @@ namespace clipk {
 
 constexpr int GEMM_ROWB = 128;  // bytes per staged row (BK = 64 halfs / 32 floats)
 constexpr int GEMM_NMIN = 128;  // N granularity accepted by the C-ABI
+constexpr int EPI_SCRATCH = 16 * 64 * 4;  // per-wave epilogue transpose tile [16][64] fp32
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -62,6 +63,19 @@ __device__ __forceinline__ void glds16(const char* src, char* lds_wave_base) {
       (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
+// Raw register type of one lane's 4 epilogue operand values (residual f32, aux TX).
+template <int EPI, typename TX> struct ExtRaw { typedef f32x4 type; };
+template <> struct ExtRaw<CLIPK_EPI_DQGELU, f16> { typedef uint2 type; };
+template <> struct ExtRaw<CLIPK_EPI_DQGELU, bf16> { typedef uint2 type; };
+
+__device__ __forceinline__ f32x4 ext_f32(f32x4 v) { return v; }
+template <typename TX> __device__ __forceinline__ f32x4 ext_f32(f32x4 v) { return v; }
+template <typename TX> __device__ __forceinline__ f32x4 ext_f32(uint2 v) {
+  float o[4];
+  load4<TX>(reinterpret_cast<const TX*>(&v), o);
+  return (f32x4){o[0], o[1], o[2], o[3]};
+}
+
 // Block tile BM x BN, WM x WN waves (each (BM/WM) x (BN/WN) = TM x TN 16x16 sub-tiles),
 // 2-stage LDS ring, one barrier per 128-byte K step. PERSIST: the grid is sized to the
 // CU count and each block walks an XCD-contiguous run of tiles; the last K step of a tile
@@ -73,7 +87,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
   constexpr int OPA = BM * GEMM_ROWB, OPB = BN * GEMM_ROWB, STAGE = OPA + OPB;
   constexpr int IA = BM / 8 / NW, IB = BN / 8 / NW;  // glds (8 rows x 128 B) per wave per stage
   static_assert(IA >= 1 && IB >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile/wave mismatch");
-  __shared__ CLIPK_LDS_ALIGN char smem[2 * STAGE];
+  __shared__ CLIPK_LDS_ALIGN char smem[2 * STAGE + NW * EPI_SCRATCH];  // one array (see header)
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
@@ -125,6 +139,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
   const int fq = lane >> 4;         // 16-B chunk within a 64-B k-window
   const int sw = (fr >> 1) & 7;     // row swizzle (sub-tile row base is a multiple of 16)
   constexpr bool HAS_BIAS = EPI == CLIPK_EPI_BIAS || EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_BIAS_QGELU;
+  constexpr bool HAS_EXT = EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU;
 
   set_tile(tile);
   stage(0, 0);
@@ -142,6 +157,28 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+    const int nbase = n0 + wn * (BN / WN);
+    const int er = lane >> 4, ec = lane & 15;  // read-back: row er of each 4-row step, chunk ec
+    const int ncol = nbase + 4 * ec;
+    // residual / aux operands of group i+1 are loaded while group i is transposed and
+    // stored (raw, converted at use: a conversion right after the load would wait for it)
+    typedef typename ExtRaw<EPI, TX>::type XR;
+    XR ext_nxt[4];
+    auto load_ext = [&](int i, XR* dst) {
+      if constexpr (HAS_EXT) {
+        const int mg = m0 + wm * (BM / WM) + i * 16;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          int mc = mg + 4 * q + er;
+          mc = mc < g.M ? mc : g.M - 1;
+          if constexpr (EPI == CLIPK_EPI_BIAS_RES)
+            dst[q] = *reinterpret_cast<const XR*>(g.res + (size_t)mc * g.ldr + ncol);
+          else
+            dst[q] = *reinterpret_cast<const XR*>((const TX*)g.aux + (size_t)mc * g.ldaux + ncol);
+        }
+      }
+    };
+    // group 0's operands are loaded at the top of the last K step (its MFMAs hide them)
     for (int kt = 0; kt < nk; ++kt, ++it) {
       const int cur = it & 1;
       const bool last = kt + 1 == nk;
@@ -151,6 +188,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
         set_tile(next);
         stage(cur ^ 1, 0);  // next tile's first stage flies during this tile's epilogue
       }
+      if (last) load_ext(0, ext_nxt);
       const char* As = smem + cur * STAGE + (wm * (BM / WM) + fr) * GEMM_ROWB;
       const char* Bs = smem + cur * STAGE + OPA + (wn * (BN / WN) + fr) * GEMM_ROWB;
 #pragma unroll
@@ -172,60 +210,47 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
       }
     }
 
-    // ---- epilogue: lane holds C[m][n..n+3] per sub-tile; operands (bias, residual, aux)
-    // are loaded up front per chunk of 4 sub-tile rows so their HBM latencies overlap.
-    const int nb = n0 + wn * (BN / WN) + fq * 4;
-    f32x4 bia[TN];
-    if constexpr (HAS_BIAS) {
+    // ---- epilogue through a per-wave LDS scratch [16][64] fp32: the MFMA layout (lane =
+    // row fr, 4 columns per sub-tile) is transposed to row-major so that each store / residual
+    // / aux access instruction covers 4 rows x full 64-column runs (128 B of f16, 256 B of
+    // f32) instead of 16 rows x 32 B. 16-B chunk c of row r sits at chunk c ^ r (conflict-free
+    // on both the write and the read-back side).
+    static_assert(TN == 4, "epilogue transpose assumes 64 columns per wave");
+    f32x4 bia = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (HAS_BIAS) bia = *reinterpret_cast<const f32x4*>(g.bias + ncol);
+    float* scr = reinterpret_cast<float*>(smem + 2 * STAGE + w * EPI_SCRATCH);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bia[j] = *reinterpret_cast<const f32x4*>(g.bias + nb + j * 16);
-    }
-    constexpr int EC = (EPI == CLIPK_EPI_BIAS_RES && TM * TN > 16) ? 2 : 4;  // rows per chunk
+    for (int i = 0; i < TM; ++i) {
+      const int mg = m0 + wm * (BM / WM) + i * 16;  // first row of this 16-row group
+      XR ext[4];
 #pragma unroll
-    for (int ic = 0; ic < TM; ic += EC) {
-      int mrow[EC];
+      for (int q = 0; q < 4; ++q) ext[q] = ext_nxt[q];
+      if (i + 1 < TM) load_ext(i + 1, ext_nxt);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous group's read-back done
 #pragma unroll
-      for (int i = 0; i < EC; ++i) mrow[i] = m0 + wm * (BM / WM) + (ic + i) * 16 + fr;
-      f32x4 ext[EC][TN];
-      if constexpr (EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU) {
+      for (int j = 0; j < TN; ++j)
+        *reinterpret_cast<f32x4*>(scr + fr * 64 + (((4 * j + fq) ^ fr) << 2)) = acc[i][j];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private: no barrier needed
 #pragma unroll
-        for (int i = 0; i < EC; ++i) {
-          const int mc = mrow[i] < g.M ? mrow[i] : g.M - 1;
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            if constexpr (EPI == CLIPK_EPI_BIAS_RES) {
-              ext[i][j] = *reinterpret_cast<const f32x4*>(g.res + (size_t)mc * g.ldr + nb + j * 16);
-            } else {
-              float hv[4];
-              load4<TX>((const TX*)g.aux + (size_t)mc * g.ldaux + nb + j * 16, hv);
-              ext[i][j] = (f32x4){hv[0], hv[1], hv[2], hv[3]};
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < EC; ++i) {
-        const int m = mrow[i];
+      for (int q = 0; q < 4; ++q) {
+        const int rr = 4 * q + er;
+        const int m = mg + rr;
+        f32x4 v = *reinterpret_cast<const f32x4*>(scr + rr * 64 + ((ec ^ rr) << 2));
         if (m >= g.M) continue;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int n = nb + j * 16;
-          f32x4 v = acc[ic + i][j];
-          if constexpr (HAS_BIAS) v += bia[j];
-          if constexpr (EPI == CLIPK_EPI_BIAS_RES) {
-            *reinterpret_cast<f32x4*>((float*)g.out + (size_t)m * g.ldo + n) = v + ext[i][j];
-          } else if constexpr (EPI == CLIPK_EPI_BIAS_QGELU) {
-            if (g.out2) store4<TO>((TO*)g.out2 + (size_t)m * g.ldo + n, v[0], v[1], v[2], v[3]);
-            store4<TO>((TO*)g.out + (size_t)m * g.ldo + n, quick_gelu(v[0]), quick_gelu(v[1]),
-                       quick_gelu(v[2]), quick_gelu(v[3]));
-          } else if constexpr (EPI == CLIPK_EPI_DQGELU) {
-            const f32x4 hv = ext[i][j];
-            store4<TO>((TO*)g.out + (size_t)m * g.ldo + n, v[0] * quick_gelu_grad(hv[0]),
-                       v[1] * quick_gelu_grad(hv[1]), v[2] * quick_gelu_grad(hv[2]),
-                       v[3] * quick_gelu_grad(hv[3]));
-          } else {
-            store4<TO>((TO*)g.out + (size_t)m * g.ldo + n, v[0], v[1], v[2], v[3]);
-          }
+        if constexpr (HAS_BIAS) v += bia;
+        if constexpr (EPI == CLIPK_EPI_BIAS_RES) {
+          *reinterpret_cast<f32x4*>((float*)g.out + (size_t)m * g.ldo + ncol) = v + ext_f32(ext[q]);
+        } else if constexpr (EPI == CLIPK_EPI_BIAS_QGELU) {
+          if (g.out2) store4<TO>((TO*)g.out2 + (size_t)m * g.ldo + ncol, v[0], v[1], v[2], v[3]);
+          store4<TO>((TO*)g.out + (size_t)m * g.ldo + ncol, quick_gelu(v[0]), quick_gelu(v[1]),
+                     quick_gelu(v[2]), quick_gelu(v[3]));
+        } else if constexpr (EPI == CLIPK_EPI_DQGELU) {
+          const f32x4 hv = ext_f32<TX>(ext[q]);
+          store4<TO>((TO*)g.out + (size_t)m * g.ldo + ncol, v[0] * quick_gelu_grad(hv[0]),
+                     v[1] * quick_gelu_grad(hv[1]), v[2] * quick_gelu_grad(hv[2]),
+                     v[3] * quick_gelu_grad(hv[3]));
+        } else {
+          store4<TO>((TO*)g.out + (size_t)m * g.ldo + ncol, v[0], v[1], v[2], v[3]);
         }
       }
     }
@@ -235,153 +260,6 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
     // next tile's prefetched first stage
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-  }
-}
-
-// 256x256 persistent GEMM with a 4-stage LDS ring of 32-deep K steps (64-B rows) and
-// counted vmcnt: three stages (96 KiB) stay in flight while one is consumed, instead of the
-// 2-stage ring's single 64 KiB stage per barrier. The stage stream runs across tile
-// boundaries, so the next tile's first stages load during this tile's epilogue.
-// 64-B rows: physical chunk p = c ^ (((row >> 3) & 1) * 3) makes the ds_read_b128 16-lane
-// groups (rows fr, chunk fq) conflict-free; glds writes lane-linear, so the swizzle is
-// applied on the source address.
-template <typename T, typename TO, typename TX, int EPI>
-__global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g) {
-  constexpr int BM = 256, BN = 256, WM = 2, WN = 4, TM = 8, TN = 4, ROW = 64, NST = 4;
-  constexpr int OPA = BM * ROW, STAGE = (BM + BN) * ROW;  // 32 KiB per stage
-  __shared__ CLIPK_LDS_ALIGN char smem[NST * STAGE];      // 128 KiB
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int ntn = g.N / BN;
-  const int ntm = (g.M + BM - 1) / BM;
-  const int nwg = ntm * ntn;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int t_beg = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
-  const int t_end = t_beg + (xcd < r8 ? q8 + 1 : q8);
-  const int t_step = gridDim.x >> 3;
-  const int t0 = t_beg + (bid >> 3);
-  if (t0 >= t_end) return;  // block-uniform
-  const int ntiles = (t_end - t0 + t_step - 1) / t_step;
-  const size_t esz = sizeof(T);
-  const int nk = (int)((size_t)g.K * esz / ROW);
-  const int total = ntiles * nk;
-
-  // ---- issue the 4 glds (2 A + 2 B, 16 rows x 64 B each) of stage q of this block's stream
-  auto issue = [&](int q) {
-    const int j = q / nk, kt = q - j * nk;
-    const int t = t0 + j * t_step;
-    const int tm0 = (t / ntn) * BM, tn0 = (t % ntn) * BN;
-    char* base = smem + (q & (NST - 1)) * STAGE;
-    const size_t koff = (size_t)kt * ROW;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = (w * 2 + i) * 16 + (lane >> 2);
-      const int c = (lane & 3) ^ (((row >> 3) & 1) * 3);
-      int ga = tm0 + row;
-      ga = ga < g.M ? ga : g.M - 1;
-      glds16(g.A + ((size_t)ga * g.lda) * esz + koff + c * 16, base + (w * 2 + i) * 16 * ROW);
-      glds16(g.B + ((size_t)(tn0 + row) * g.ldb) * esz + koff + c * 16, base + OPA + (w * 2 + i) * 16 * ROW);
-    }
-  };
-
-  const int wm = w / WN, wn = w % WN;
-  const int fr = lane & 15, fq = lane >> 4;
-  const int pch = (fq ^ (((fr >> 3) & 1) * 3)) * 16;  // physical chunk byte offset
-  constexpr bool HAS_BIAS = EPI == CLIPK_EPI_BIAS || EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_BIAS_QGELU;
-
-  issue(0);
-  if (total > 1) issue(1);
-  if (total > 2) issue(2);
-  f32x4 acc[TM][TN];
-  for (int q = 0; q < total; ++q) {
-    const int j = q / nk, kt = q - j * nk;
-    if (kt == 0) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int jj = 0; jj < TN; ++jj) acc[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-    // stage q landed (this wave): younger stages q+1, q+2 may stay in flight
-    const int younger = min(2, total - 1 - q);
-    if (kt == 0 && q > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // epilogue stores
-    else if (younger == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // stage q visible to all waves; stage q-1's buffer is free
-    if (q + 3 < total) issue(q + 3);
-    const char* As = smem + (q & (NST - 1)) * STAGE + (wm * (BM / WM) + fr) * ROW + pch;
-    const char* Bs = smem + (q & (NST - 1)) * STAGE + OPA + (wn * (BN / WN) + fr) * ROW + pch;
-    u32x4 a[TM], b[TN];
-#pragma unroll
-    for (int jj = 0; jj < TN; ++jj) b[jj] = *reinterpret_cast<const u32x4*>(Bs + jj * 16 * ROW);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const u32x4*>(As + i * 16 * ROW);
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int jj = 0; jj < TN; ++jj) acc[i][jj] = mma<T>(b[jj], a[i], acc[i][jj]);
-
-    if (kt != nk - 1) continue;
-    // ---- epilogue of tile t (same math as gemm_nt_kernel)
-    const int t = t0 + j * t_step;
-    const int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
-    const int nb = n0 + wn * (BN / WN) + fq * 4;
-    f32x4 bia[TN];
-    if constexpr (HAS_BIAS) {
-#pragma unroll
-      for (int jj = 0; jj < TN; ++jj) bia[jj] = *reinterpret_cast<const f32x4*>(g.bias + nb + jj * 16);
-    }
-    constexpr int EC = (EPI == CLIPK_EPI_BIAS_RES) ? 2 : 4;
-#pragma unroll
-    for (int ic = 0; ic < TM; ic += EC) {
-      int mrow[EC];
-#pragma unroll
-      for (int i = 0; i < EC; ++i) mrow[i] = m0 + wm * (BM / WM) + (ic + i) * 16 + fr;
-      f32x4 ext[EC][TN];
-      if constexpr (EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU) {
-#pragma unroll
-        for (int i = 0; i < EC; ++i) {
-          const int mc = mrow[i] < g.M ? mrow[i] : g.M - 1;
-#pragma unroll
-          for (int jj = 0; jj < TN; ++jj) {
-            if constexpr (EPI == CLIPK_EPI_BIAS_RES) {
-              ext[i][jj] = *reinterpret_cast<const f32x4*>(g.res + (size_t)mc * g.ldr + nb + jj * 16);
-            } else {
-              float hv[4];
-              load4<TX>((const TX*)g.aux + (size_t)mc * g.ldaux + nb + jj * 16, hv);
-              ext[i][jj] = (f32x4){hv[0], hv[1], hv[2], hv[3]};
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < EC; ++i) {
-        const int m = mrow[i];
-        if (m >= g.M) continue;
-#pragma unroll
-        for (int jj = 0; jj < TN; ++jj) {
-          const int n = nb + jj * 16;
-          f32x4 v = acc[ic + i][jj];
-          if constexpr (HAS_BIAS) v += bia[jj];
-          if constexpr (EPI == CLIPK_EPI_BIAS_RES) {
-            *reinterpret_cast<f32x4*>((float*)g.out + (size_t)m * g.ldo + n) = v + ext[i][jj];
-          } else if constexpr (EPI == CLIPK_EPI_BIAS_QGELU) {
-            if (g.out2) store4<TO>((TO*)g.out2 + (size_t)m * g.ldo + n, v[0], v[1], v[2], v[3]);
-            store4<TO>((TO*)g.out + (size_t)m * g.ldo + n, quick_gelu(v[0]), quick_gelu(v[1]),
-                       quick_gelu(v[2]), quick_gelu(v[3]));
-          } else if constexpr (EPI == CLIPK_EPI_DQGELU) {
-            const f32x4 hv = ext[i][jj];
-            store4<TO>((TO*)g.out + (size_t)m * g.ldo + n, v[0] * quick_gelu_grad(hv[0]),
-                       v[1] * quick_gelu_grad(hv[1]), v[2] * quick_gelu_grad(hv[2]),
-                       v[3] * quick_gelu_grad(hv[3]));
-          } else {
-            store4<TO>((TO*)g.out + (size_t)m * g.ldo + n, v[0], v[1], v[2], v[3]);
-          }
-        }
-      }
-    }
   }
 }
 
@@ -396,7 +274,7 @@ static int pick_cfg(int M, int N, int esz) {
   }
   if (esz == 4) return 0;  // fp32 parity path: one configuration
   if (g_force_cfg >= 0) {
-    if ((g_force_cfg == 1 || g_force_cfg == 3 || g_force_cfg == 4) && N % 256 == 0) return g_force_cfg;
+    if ((g_force_cfg == 1 || g_force_cfg == 3) && N % 256 == 0) return g_force_cfg;
     if (g_force_cfg == 2) return 2;
     return 0;
   }
@@ -424,12 +302,7 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
     const int nwg = ((g.M + 127) / 128) * (g.N / 128);
     hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 128, 2, 2, false>), dim3(nwg), dim3(256), 0, st, g);
   } else {
-    if (cfg == 4) {
-      const int cus = num_cus();
-      const int nwg = ((g.M + 255) / 256) * (g.N / 256);
-      const int grid = nwg < cus ? ((nwg + 7) / 8) * 8 : (cus / 8) * 8;
-      hipLaunchKernelGGL((gemm_ring_kernel<T, TO, TX, EPI>), dim3(grid), dim3(512), 0, st, g);
-    } else if (cfg == 1 || cfg == 3) {
+    if (cfg == 1 || cfg == 3) {
       const int nwg = ((g.M + 255) / 256) * (g.N / 256);
       const int cus = num_cus();
       if (cfg == 1 && nwg > 2 * cus) {
@@ -515,7 +388,7 @@ extern "C" int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, in
 
 // Benchmark knob: force a tile configuration (-1 = automatic choice).
 extern "C" int clipk_gemm_set_config(int cfg) {
-  if (cfg < -1 || cfg > 4) return CLIPK_EINVAL;
+  if (cfg < -1 || cfg > 3) return CLIPK_EINVAL;
   g_force_cfg = cfg;
   return CLIPK_OK;
 }

@@ -326,48 +326,56 @@ __global__ __launch_bounds__(256) void meta_net_fwd_kernel(int V, int Hd, int Wd
   }
 }
 
-// one block: dh = (dy W2) * (h > 0); dW2 = dy^T h; db2 = sum dy; dW1 = dh^T x; db1 = sum dh
-__global__ __launch_bounds__(256) void meta_net_bwd_kernel(int B, int V, int Hd, int Wd,
-                                                           const float* __restrict__ x,
-                                                           const float* __restrict__ h,
-                                                           const float* __restrict__ w2,
-                                                           const float* __restrict__ dy,
-                                                           float* __restrict__ dw1, float* __restrict__ db1,
-                                                           float* __restrict__ dw2, float* __restrict__ db2,
-                                                           float* __restrict__ dh) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  // dh[b,k]
-  for (int bk = wv; bk < B * Hd; bk += 4) {
+// Meta-Net backward in two launches (every output element owned by one thread; fixed-order
+// sums over the batch, deterministic):
+//   A: waves [0, B*Hd): dh[b,k] = (dy[b] . W2[:,k]) * (h[b,k] > 0);
+//      threads after that: dW2[o,k] = sum_b dy[b,o] h[b,k], db2[o] = sum_b dy[b,o]
+//   B: dW1[k,v] = sum_b dh[b,k] x[b,v], db1[k] = sum_b dh[b,k]
+__global__ __launch_bounds__(256) void meta_net_bwd_a_kernel(int B, int Hd, int Wd, int nb_dh,
+                                                             const float* __restrict__ h,
+                                                             const float* __restrict__ w2,
+                                                             const float* __restrict__ dy,
+                                                             float* __restrict__ dw2, float* __restrict__ db2,
+                                                             float* __restrict__ dh) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  if ((int)blockIdx.x < nb_dh) {
+    const int bk = blockIdx.x * 4 + (tid >> 6);
+    if (bk >= B * Hd) return;
     const int b = bk / Hd, k = bk % Hd;
     float a = 0.f;
     for (int o = lane; o < Wd; o += 64) a += dy[(size_t)b * Wd + o] * w2[(size_t)o * Hd + k];
     a = wave_sum(a);
     if (lane == 0) dh[bk] = h[bk] > 0.f ? a : 0.f;
+    return;
   }
-  // dW2, db2
-  for (int o = tid; o < Wd; o += 256) {
-    float s = 0.f;
-    for (int b = 0; b < B; ++b) s += dy[(size_t)b * Wd + o];
-    db2[o] = s;
-    for (int k = 0; k < Hd; ++k) {
-      float a = 0.f;
-      for (int b = 0; b < B; ++b) a += dy[(size_t)b * Wd + o] * h[(size_t)b * Hd + k];
-      dw2[(size_t)o * Hd + k] = a;
-    }
+  const long i = (long)(blockIdx.x - nb_dh) * 256 + tid;
+  if (i >= (long)Wd * Hd) return;
+  const int o = (int)(i / Hd), k = (int)(i % Hd);
+  float a = 0.f, s = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float d = dy[(size_t)b * Wd + o];
+    a += d * h[(size_t)b * Hd + k];
+    s += d;
   }
-  __syncthreads();
-  for (int k = 0; k < Hd; ++k) {
-    if (tid == 0) {
-      float s = 0.f;
-      for (int b = 0; b < B; ++b) s += dh[(size_t)b * Hd + k];
-      db1[k] = s;
-    }
-    for (int v = tid; v < V; v += 256) {
-      float a = 0.f;
-      for (int b = 0; b < B; ++b) a += dh[(size_t)b * Hd + k] * x[(size_t)b * V + v];
-      dw1[(size_t)k * V + v] = a;
-    }
+  dw2[i] = a;
+  if (k == 0) db2[o] = s;
+}
+
+__global__ __launch_bounds__(256) void meta_net_bwd_b_kernel(int B, int V, int Hd,
+                                                             const float* __restrict__ x,
+                                                             const float* __restrict__ dh,
+                                                             float* __restrict__ dw1, float* __restrict__ db1) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)Hd * V) return;
+  const int k = (int)(i / V), v = (int)(i % V);
+  float a = 0.f, s = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float d = dh[(size_t)b * Hd + k];
+    a += d * x[(size_t)b * V + v];
+    s += d;
   }
+  dw1[i] = a;
+  if (v == 0) db1[k] = s;
 }
 
 // ---------------------------------------------------------------- SGD (optimizer.py:105-113)
@@ -530,8 +538,14 @@ extern "C" int clipk_meta_net_bwd(int B, int V, int Hd, int Wd, const float* x, 
                                   float* dw2, float* db2, float* dh_ws, void* stream) {
   if (!x || !h || !w2 || !dy || !dw1 || !db1 || !dw2 || !db2 || !dh_ws) return CLIPK_EINVAL;
   if (B <= 0 || V <= 0 || Hd <= 0 || Wd <= 0) return CLIPK_ESHAPE;
-  hipLaunchKernelGGL(meta_net_bwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, V, Hd, Wd, x,
-                     h, w2, dy, dw1, db1, dw2, db2, dh_ws);
+  hipStream_t st = (hipStream_t)stream;
+  const int nb_dh = (B * Hd + 3) / 4;
+  const long nw2 = (long)Wd * Hd, nw1 = (long)Hd * V;
+  hipLaunchKernelGGL(meta_net_bwd_a_kernel, dim3(nb_dh + (nw2 + 255) / 256), dim3(256), 0, st, B, Hd, Wd, nb_dh,
+                     h, w2, dy, dw2, db2, dh_ws);
+  CLIPK_CHECK_LAUNCH();
+  hipLaunchKernelGGL(meta_net_bwd_b_kernel, dim3((nw1 + 255) / 256), dim3(256), 0, st, B, V, Hd, x, dh_ws, dw1,
+                     db1);
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
 }

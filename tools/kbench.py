@@ -9,17 +9,21 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fsp_amd import ops, _native as N  # noqa: E402
 
 
-def timeit(fn, iters=20, warm=3):
+def timeit(fn, iters=10, warm=3, reps=int(os.environ.get("KB_REPS", 3))):
+    """min over `reps` rounds of the mean of `iters` back-to-back launches (ms)."""
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        fn()
-    e.record()
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / iters
+    best = float("inf")
+    for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        best = min(best, s.elapsed_time(e) / iters)
+    return best
 
 
 def main():
@@ -41,9 +45,12 @@ def main():
         ("out bwd   N512  K512 NONE bf16", dict(a=rnd(M, W, dt=bf), b=rnd(W, W, dt=bf), epi=N.EPI_NONE, out=bf)),
         ("qkv bwd   N512  K1536 NONE f32", dict(a=rnd(M, 3 * W, dt=bf), b=rnd(W, 3 * W, dt=bf), epi=N.EPI_NONE, out=torch.float32)),
         ("plain     N2048 K512 NONE f16", dict(a=rnd(M, W), b=rnd(4 * W, W), epi=N.EPI_NONE, out=f16)),
+        ("bias      N2048 K512 BIAS f16", dict(a=rnd(M, W), b=rnd(4 * W, W), epi=N.EPI_BIAS, out=f16, bias=True)),
+        ("qgelu     N2048 K512 QGELU f16", dict(a=rnd(M, W), b=rnd(4 * W, W), epi=N.EPI_BIAS_QGELU, out=f16, bias=True)),
+        ("plain32   N2048 K512 NONE f32", dict(a=rnd(M, W), b=rnd(4 * W, W), epi=N.EPI_NONE, out=torch.float32)),
     ]
     REF.clear()
-    for cfg in (0, 1, 4):
+    for cfg in [int(c) for c in os.environ.get("KB_CFGS", "0,1,2,3").split(",")]:
         N.load().clipk_gemm_set_config(cfg)
         print(f"--- gemm config {cfg}")
         run_gemms(shapes, M, res, dev)
@@ -101,6 +108,52 @@ def attn_ln(M, W, dev):
     print(f"attn fwd vision L197 B8 {ms*1e3:8.1f} us")
 
 
+def prefix_attn(dev):
+    """Shared-prefix packed attention at the bench shape (ViT-B/16 text, C=1000, P=5)."""
+    import ctypes
+    G, C, P, H = 8, 1000, 5, 8
+    W = H * 64
+    qlen = torch.full((C,), 6, dtype=torch.long)
+    qlen[:100] = 5
+    off = P + torch.cat([torch.zeros(1, dtype=torch.long), qlen.cumsum(0)[:-1]])
+    R = int(P + qlen.sum())
+    seg = torch.stack([off, qlen], 1).to(torch.int32).reshape(-1).to(dev)
+    qkv = (torch.randn(G * R, 3 * W, device=dev) * 0.5).to(torch.float16)
+    o, lse = ops.attention_prefix(qkv, G, C, P, R, seg, 6, H, lse=True)
+    ms = timeit(lambda: ops.attention_prefix(qkv, G, C, P, R, seg, 6, H, lse=True))
+    print(f"prefix attn fwd rows={G*R}  {ms*1e3:8.1f} us  {(qkv.numel()*2 + o.numel()*2)/ms/1e6:7.1f} GB/s")
+    dout = (torch.randn(G * R, W, device=dev) * 0.5).to(torch.bfloat16)
+    dq = torch.empty(G * R, 3 * W, device=dev, dtype=torch.bfloat16)
+    nb = N.load().clipk_attention_prefix_ws_bytes(G, C, H)
+    ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    fn = lambda: N.call("clipk_attention_prefix_bwd", N.F16, N.BF16, G, C, P, R, p(seg), 6, H, p(qkv), 3 * W,
+                        p(o), W, p(dout), W, p(lse), p(dq), 3 * W, p(ws), nb, st)
+    ms = timeit(fn)
+    print(f"prefix attn bwd rows={G*R}  {ms*1e3:8.1f} us  {(qkv.numel()*2*2 + dout.numel()*2)/ms/1e6:7.1f} GB/s")
+
+
+def torch_gemms(dev):
+    """hipBLASLt (torch.matmul) on the same shapes: a yardstick for the hand-written GEMM."""
+    M = int(os.environ.get("KB_M", 88000))
+    W = 512
+    for dt in (torch.float16, torch.bfloat16):
+        for (n, k) in ((3 * W, W), (W, W), (4 * W, W), (W, 4 * W)):
+            a = torch.randn(M, k, device=dev).to(dt)
+            b = torch.randn(n, k, device=dev).to(dt)
+            ms = timeit(lambda: a @ b.t())
+            print(f"torch {str(dt)[6:]:8s} N{n:<5d} K{k:<5d}  {ms*1e3:8.1f} us  {2*M*n*k/ms/1e9:7.1f} TF/s")
+
+
 if __name__ == "__main__":
-    main()
-    attn_ln(int(os.environ.get("KB_M", 88000)), 512, torch.device("cuda"))
+    only = os.environ.get("KB_ONLY", "gemm,attn,prefix").split(",")
+    dev = torch.device("cuda")
+    if "gemm" in only:
+        main()
+    if "attn" in only:
+        attn_ln(int(os.environ.get("KB_M", 88000)), 512, dev)
+    if "prefix" in only:
+        prefix_attn(dev)
+    if "torch" in only:
+        torch_gemms(dev)
