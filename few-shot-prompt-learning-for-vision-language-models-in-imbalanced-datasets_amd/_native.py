@@ -10,7 +10,7 @@ import ctypes
 import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "libclipk.so")
+LIB_PATH = os.environ.get("CLIPK_LIB", os.path.join(_PKG, "libclipk.so"))  # override: A/B builds
 
 F32, F16, BF16 = 0, 1, 2
 EPI_BIAS, EPI_BIAS_RES, EPI_BIAS_QGELU, EPI_DQGELU, EPI_NONE = 0, 1, 2, 3, 4
@@ -40,9 +40,9 @@ SIGNATURES = {
     "clipk_ctx_grad": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "clipk_prompt_assemble_rows": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _L, _L, _P, _P, _P, _P]),
     "clipk_ctx_grad_rows": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P]),
-    "clipk_attention_prefix_fwd": (_I, [_I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _P, _I, _P, _P]),
+    "clipk_attention_prefix_fwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _I, _P, _I, _P, _I, _P, _P]),
     "clipk_attention_prefix_ws_bytes": (_S, [_I, _I, _I]),
-    "clipk_attention_prefix_bwd": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _P, _I, _P, _I, _P, _P,
+    "clipk_attention_prefix_bwd": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I, _P, _I, _P, _I, _P, _P,
                                         _I, _P, _S, _P]),
     "clipk_cosine_logits_fwd": (_I, [_I, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P]),
     "clipk_cosine_logits_bwd": (_I, [_I, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P]),
@@ -60,9 +60,9 @@ SIGNATURES = {
     "clipk_text_backward": (_I, [_P, _I, _I, _P, _P, _P, _S, _P, _P, _S, _P]),
     "clipk_text_packed_saved_bytes": (_S, [_P, _I, _I, _I]),
     "clipk_text_packed_ws_bytes": (_S, [_P, _I, _I, _I]),
-    "clipk_text_packed_bwd_ws_bytes": (_S, [_P, _I, _I, _I]),
-    "clipk_text_forward_packed": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _S, _P, _S, _P]),
-    "clipk_text_backward_packed": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _S, _P, _P, _S, _P]),
+    "clipk_text_packed_bwd_ws_bytes": (_S, [_P, _I, _I, _I, _I]),
+    "clipk_text_forward_packed": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _S, _P, _S, _P]),
+    "clipk_text_backward_packed": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _S, _P, _P, _S, _P]),
     "clipk_vision_create": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "clipk_vit_ws_bytes": (_S, [_P, _I]),
     "clipk_vit_forward": (_I, [_P, _I, _P, _P, _P, _S, _P]),

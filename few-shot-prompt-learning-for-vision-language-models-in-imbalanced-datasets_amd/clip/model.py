@@ -151,8 +151,9 @@ class TextEncoderCore(_Encoder):
         tail = (ops._p(x0), ops._p(shape.eot_rows), ops._p(txt), ops._p(saved), sb, ops._p(ws), ws.numel(),
                 ops._stream())
         if shape.packed:
-            N.check(lib.clipk_text_forward_packed(h, shape.G, shape.C, shape.P, shape.R, ops._p(shape.seg),
-                                                  shape.max_q, *tail), "clipk_text_forward_packed")
+            N.check(lib.clipk_text_forward_packed(h, shape.G, shape.C, shape.P, shape.R, shape.ntiles,
+                                                  ops._p(shape.tiles), ops._p(shape.row_first), *tail),
+                    "clipk_text_forward_packed")
         else:
             N.check(lib.clipk_text_forward(h, shape.nseq, shape.L, *tail), "clipk_text_forward")
         return txt, saved
@@ -162,15 +163,16 @@ class TextEncoderCore(_Encoder):
         h = self.handle
         dx0 = torch.empty(shape.rows, self.W, device=dtxt.device, dtype=torch.float32)
         if shape.packed:
-            wsb = lib.clipk_text_packed_bwd_ws_bytes(h, shape.G, shape.C, shape.R)
+            wsb = lib.clipk_text_packed_bwd_ws_bytes(h, shape.G, shape.C, shape.R, shape.ntiles)
         else:
             wsb = lib.clipk_text_bwd_ws_bytes(h, shape.nseq, shape.L)
         ws = WORKSPACE.get(wsb, dtxt.device, "text_bwd")
         tail = (ops._p(shape.eot_rows), ops._p(dtxt.contiguous()), ops._p(saved), saved.numel(), ops._p(dx0),
                 ops._p(ws), ws.numel(), ops._stream())
         if shape.packed:
-            N.check(lib.clipk_text_backward_packed(h, shape.G, shape.C, shape.P, shape.R, ops._p(shape.seg),
-                                                   shape.max_q, *tail), "clipk_text_backward_packed")
+            N.check(lib.clipk_text_backward_packed(h, shape.G, shape.C, shape.P, shape.R, shape.ntiles,
+                                                   ops._p(shape.tiles), ops._p(shape.row_first), *tail),
+                    "clipk_text_backward_packed")
         else:
             N.check(lib.clipk_text_backward(h, shape.nseq, shape.L, *tail), "clipk_text_backward")
         return dx0

@@ -8,108 +8,96 @@
 // the EOT row that TextEncoder.forward reads (trainers/coop.py:201-203). The packed row
 // layout therefore stores, per group g (one image, or the whole class set for CoOp),
 //     [P prefix rows][class 0 rows P..eot_0][class 1 rows P..eot_1] ...
-// (group stride R rows), and attention runs over SEGMENTS:
-//     segment 0   : queries = the P prefix rows, keys = themselves (causal);
-//     segment 1+c : queries = class c's q_len rows, keys = the P prefix rows (all visible)
-//                   followed by its own rows (causal).
+// (group stride R rows). Attention: the prefix rows attend among themselves (causal); a
+// class row attends to all P prefix keys and causally to the rows of its own class.
 // Exactly the reference's math, on ~ (P + sum q_len) / (C * L) of the rows.
 //
-// seg[2c], seg[2c+1] = (group-relative first row, q_len) of class c; P <= 16, q_len <= 16
-// (one 16-row MFMA tile each; the host falls back to the plain layout otherwise).
+// Work unit = a TILE of at most 16 consecutive class rows holding whole classes (the host
+// packs consecutive classes greedily, so a 16-row MFMA tile carries ~16/q_len classes
+// instead of one): tiles[2t], tiles[2t+1] = (group-relative first row, rows). row_first[r]
+// = first row of the class that row r belongs to (the causal block-diagonal mask inside a
+// tile). Unit 0 of every group is the prefix tile itself (keys = its own rows).
 //
-// Work unit: one wave per (group, chunk of kSegChunk segments, head): the prefix K/V of
-// (g, h) are loaded once per wave and reused by every segment of the chunk. The backward
-// accumulates the prefix rows' dK/dV over the chunk in registers and writes one fp32
-// partial per chunk; prefix_kv_reduce sums the chunks in a fixed order (deterministic).
+// One wave per (group, chunk of units, head): the prefix K/V of (g, h) are loaded once per
+// wave and reused by every tile of the chunk. The backward accumulates the prefix rows'
+// dK/dV over the chunk in registers and writes one fp32 partial per chunk;
+// prefix_kv_reduce sums the chunks in a fixed order (deterministic).
 #include <cstdlib>
 
 #include "attn_common.h"
 
 namespace clipk {
 
-constexpr int kFwdBatch = 4, kBwdBatch = 2;  // segments whose loads are issued together
-constexpr int kSegChunk = 16;  // VALU kernels; MFMA kernels take the chunk as an argument (<= 16)
+// tiles whose loads are issued together (template parameter; env CLIPK_PREFIX_*_BATCH)
+constexpr int kValuChunk = 16;                // units per wave, VALU kernels
 
-// Segments per wave of the MFMA kernels (env CLIPK_PREFIX_FWD_CHUNK / _BWD_CHUNK, read once).
+// Units per wave of the MFMA kernels (env CLIPK_PREFIX_FWD_CHUNK / _BWD_CHUNK, read once).
 static int chunk_env(const char* name, int def) {
   const char* e = getenv(name);
   const int v = e ? atoi(e) : def;
   return v >= 1 && v <= 16 ? v : def;
 }
-static int fwd_chunk() { static int c = chunk_env("CLIPK_PREFIX_FWD_CHUNK", 16); return c; }
+static int fwd_chunk() { static int c = chunk_env("CLIPK_PREFIX_FWD_CHUNK", 8); return c; }
 static int bwd_chunk() { static int c = chunk_env("CLIPK_PREFIX_BWD_CHUNK", 16); return c; }
+static int fwd_batch() { static int c = chunk_env("CLIPK_PREFIX_FWD_BATCH", 1); return c; }
+static int bwd_batch() { static int c = chunk_env("CLIPK_PREFIX_BWD_BATCH", 2); return c; }
+static inline int n_chunks(int ntiles, int uc) { return (ntiles + 1 + uc - 1) / uc; }
 
-__device__ __forceinline__ void seg_info(const int* __restrict__ seg, int g, int R, int P, int s,
-                                         int& q0, int& qn, int& pre) {
-  if (s == 0) {
-    q0 = g * R; qn = P; pre = 0;
+// The chunk's tile table in one VGPR (lane i holds tiles[2*(u_begin-1) + i]), read back
+// with v_readlane: no dependent scalar-memory round trip inside the tile loop.
+__device__ __forceinline__ int load_tile_table(const int* __restrict__ tiles, int ntiles, int u_begin,
+                                               int lane) {
+  const int idx = 2 * (u_begin - 1) + lane;
+  return (lane < 32 && idx >= 0 && idx < 2 * ntiles) ? tiles[idx] : 0;
+}
+__device__ __forceinline__ void tile_info(int tab, int P, int u, int u_begin, int& t0, int& n, int& pre) {
+  if (u == 0) {
+    t0 = 0; n = P; pre = 0;
   } else {
-    q0 = g * R + seg[2 * (s - 1)];
-    qn = min(seg[2 * (s - 1) + 1], 16);
+    const int i = 2 * (u - u_begin);
+    t0 = __builtin_amdgcn_readlane(tab, i);
+    n = min(__builtin_amdgcn_readlane(tab, i + 1), 16);
     pre = P;
   }
 }
 
-// The chunk's segment table in one VGPR (lane i holds seg[2*(s_begin-1) + i]), read back
-// with v_readlane: no dependent scalar-memory round trip inside the segment loop.
-__device__ __forceinline__ int load_seg_table(const int* __restrict__ seg, int C, int s_begin, int lane) {
-  const int idx = 2 * (s_begin - 1) + lane;
-  return (lane < 32 && idx >= 0 && idx < 2 * C) ? seg[idx] : 0;
-}
-__device__ __forceinline__ void seg_info_reg(int tab, int g, int R, int P, int s, int s_begin, int& q0,
-                                             int& qn, int& pre) {
-  if (s == 0) {
-    q0 = g * R; qn = P; pre = 0;
-  } else {
-    const int i = 2 * (s - s_begin);
-    q0 = g * R + __builtin_amdgcn_readlane(tab, i);
-    qn = min(__builtin_amdgcn_readlane(tab, i + 1), 16);
-    pre = P;
-  }
-}
-
-// Unconditional 16-B load (the caller clamps the row to a valid one) with the value
-// zeroed in lanes whose row is past the segment: no exec-masked branch around the load,
-// so the compiler can count the loads across the segment loop (vmcnt(N), not vmcnt(0)).
+// Unconditional 16-B load: the caller clamps the row to a valid one (rows past the tile
+// are masked out of P / dS, never zeroed): no exec-masked branch around the load, so the
+// compiler counts the batch's loads (vmcnt(N)) instead of draining them.
 __device__ __forceinline__ s16x8 ld16(const void* p) { return *reinterpret_cast<const s16x8*>(p); }
-__device__ __forceinline__ s16x8 sel16(s16x8 v, bool ok) {
-  const s16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-  return ok ? v : z;
-}
-
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // ------------------------------------------------------------------ forward, MFMA (16-bit)
-// Software-pipelined over the chunk's segments: the next segment's Q/K/V fragments are in
-// flight while the current one is computed (the per-segment work is too small to hide a
-// dependent HBM round trip otherwise).
-struct SegRows {
+struct TileRows {
   s16x8 q[2], k[2], v[2];
-  int q0, qn, pre;
+  int t0, n, pre, first;  // first: this lane's row's class start, tile-relative
 };
 
-template <typename T>
-__global__ __launch_bounds__(256) void attn_prefix_fwd_mfma(int G, int C, int P, int R,
-                                                            const int* __restrict__ seg, int H,
-                                                            int nchunk, int sc, const T* __restrict__ qkv,
+template <typename T, int kFwdBatch>
+__global__ __launch_bounds__(256) void attn_prefix_fwd_mfma(int G, int P, int R, int ntiles,
+                                                            const int* __restrict__ tiles,
+                                                            const int* __restrict__ row_first, int H,
+                                                            int nchunk, int uc, const T* __restrict__ qkv,
                                                             int ldq, T* __restrict__ out, int ldo,
                                                             float* __restrict__ lse) {
-  __shared__ CLIPK_LDS_ALIGN short tiles[4][2][16 * TRS];  // per wave: prefix V, own V
+  __shared__ CLIPK_LDS_ALIGN short sm[4][2][16 * TRS];  // per wave: prefix V, own V
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
   const int wid = blockIdx.x * 4 + w;
   if (wid >= G * nchunk * H) return;  // wave-uniform; no block barriers below
   const int h = wid % H, k = (wid / H) % nchunk, g = wid / (H * nchunk);
   const int W = H * 64;
-  short* sVp = tiles[w][0];
-  short* sVo = tiles[w][1];
+  short* sVp = sm[w][0];
+  short* sVo = sm[w][1];
+  const int gR = g * R;
+  const T* qh = qkv + h * 64;
 
-  const int s_begin = k * sc, s_end = min((k + 1) * sc, C + 1);
-  const int tab = load_seg_table(seg, C, s_begin, lane);
-  auto load = [&](int s, SegRows& f) {
-    seg_info_reg(tab, g, R, P, s, s_begin, f.q0, f.qn, f.pre);
-    const bool ok = r16 < f.qn;
-    const T* qp = qkv + ((size_t)f.q0 + min(r16, f.qn - 1)) * ldq + h * 64;
+  const int u_begin = k * uc, u_end = min((k + 1) * uc, ntiles + 1);
+  const int tab = load_tile_table(tiles, ntiles, u_begin, lane);
+  auto load = [&](int u, TileRows& f) {
+    tile_info(tab, P, u, u_begin, f.t0, f.n, f.pre);
+    const int rl = f.t0 + min(r16, f.n - 1);
+    const T* qp = qh + (gR + rl) * ldq;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int c = 8 * g4 + 32 * kk;
@@ -117,14 +105,11 @@ __global__ __launch_bounds__(256) void attn_prefix_fwd_mfma(int G, int C, int P,
       f.k[kk] = ld16(qp + W + c);
       f.v[kk] = ld16(qp + 2 * W + c);
     }
-    (void)ok;
+    f.first = u == 0 ? 0 : row_first[rl] - f.t0;
   };
 
-  // Batches of kFwdBatch segments: all their loads issued up front (unconditional, rows
-  // and segment indices clamped), then the bodies; waits are counted inside one loop
-  // iteration (a load carried across the back edge gets a vmcnt(0) at the loop head).
   const bool pok = r16 < P;
-  const T* pp = qkv + ((size_t)g * R + (pok ? r16 : 0)) * ldq + h * 64;
+  const T* pp = qh + (gR + (pok ? r16 : 0)) * ldq;
   s16x8 kp[2];
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
@@ -132,16 +117,10 @@ __global__ __launch_bounds__(256) void attn_prefix_fwd_mfma(int G, int C, int P,
     kp[kk] = ld_row16(pp + W + c, pok);
     *reinterpret_cast<s16x8*>(sVp + r16 * TRS + c) = ld_row16(pp + 2 * W + c, pok);
   }
-  auto body = [&](int s, SegRows& cur) {
-    const int q0 = cur.q0, qn = cur.qn, pre = cur.pre;
-    const bool qok = r16 < qn;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {  // rows past the segment: zero (their loads were clamped)
-      cur.q[kk] = sel16(cur.q[kk], qok);
-      cur.k[kk] = sel16(cur.k[kk], qok);
-      cur.v[kk] = sel16(cur.v[kk], qok);
-    }
-    lds_fence();  // previous segment's transposed reads of sVo are done
+  auto body = [&](TileRows& cur) {
+    const int n = cur.n, pre = cur.pre, first = cur.first;
+    const bool qok = r16 < n;
+    lds_fence();  // previous tile's transposed reads of sVo are done
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) *reinterpret_cast<s16x8*>(sVo + r16 * TRS + 8 * g4 + 32 * kk) = cur.v[kk];
     f32x4 sp = {0.f, 0.f, 0.f, 0.f}, so = {0.f, 0.f, 0.f, 0.f};
@@ -155,7 +134,7 @@ __global__ __launch_bounds__(256) void attn_prefix_fwd_mfma(int G, int C, int P,
     for (int r = 0; r < 4; ++r) {
       const int key = 4 * g4 + r;
       vp[r] = key < pre ? sp[r] * kScale : -INFINITY;
-      vq[r] = (key <= r16 && key < qn) ? so[r] * kScale : -INFINITY;  // own key 0 always valid
+      vq[r] = (key <= r16 && key >= first) ? so[r] * kScale : -INFINITY;  // key == r16 always valid
       mx = fmaxf(mx, fmaxf(vp[r], vq[r]));
     }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
@@ -176,66 +155,73 @@ __global__ __launch_bounds__(256) void attn_prefix_fwd_mfma(int G, int C, int P,
     const s16x4 bp = pack4<T>(ep[0], ep[1], ep[2], ep[3]);
     const s16x4 bo = pack4<T>(eo[0], eo[1], eo[2], eo[3]);
     const float inv = 1.0f / ps;
+    T* orow = out + (gR + cur.t0 + r16) * ldo + h * 64 + 4 * g4;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       f32x4 o = mfma16_t<T>(tr_read(sVp, 4 * g4, 16 * t, lane), bp, (f32x4){0.f, 0.f, 0.f, 0.f});
       o = mfma16_t<T>(tr_read(sVo, 4 * g4, 16 * t, lane), bo, o);
-      if (qok) store4<T>(out + ((size_t)q0 + r16) * ldo + h * 64 + 16 * t + 4 * g4, o[0] * inv, o[1] * inv,
-                         o[2] * inv, o[3] * inv);
+      if (qok) store4<T>(orow + 16 * t, o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
     }
-    if (lse && g4 == 0 && qok) lse[((size_t)q0 + r16) * H + h] = mx + __logf(ps);
+    if (lse && g4 == 0 && qok) lse[(gR + cur.t0 + r16) * H + h] = mx + __logf(ps);
   };
-  for (int s = s_begin; s < s_end; s += kFwdBatch) {
-    SegRows rr[kFwdBatch];
+  // Batches of tiles: all their loads issued up front (unconditional, clamped), then the
+  // bodies; waits are counted inside one loop iteration (a load carried across the back
+  // edge gets a vmcnt(0) at the loop head).
+  for (int u = u_begin; u < u_end; u += kFwdBatch) {
+    TileRows rr[kFwdBatch];
 #pragma unroll
-    for (int j = 0; j < kFwdBatch; ++j) load(min(s + j, s_end - 1), rr[j]);
+    for (int j = 0; j < kFwdBatch; ++j) load(min(u + j, u_end - 1), rr[j]);
     __builtin_amdgcn_sched_barrier(0);  // every load of the batch issues before the first wait
 #pragma unroll
     for (int j = 0; j < kFwdBatch; ++j)
-      if (s + j < s_end) body(s + j, rr[j]);
+      if (u + j < u_end) body(rr[j]);
   }
 }
 
 // ------------------------------------------------------------------ backward, MFMA (bf16 math)
-// Per segment, with the two 16-key tiles (prefix, own) handled like attn_bwd_mfma16:
-// S / dP in both accumulator layouts, D_i = rowsum(P o dP) over both tiles in registers,
-// dV = P^T dO, dK = dS^T Q, dQ = dS_pre K_pre + dS_own K_own. Pipelined like the forward.
-struct SegRowsB {
+// Per tile, with the two 16-key tiles (prefix, own) handled like attn_bwd_mfma16: S / dP in
+// both accumulator layouts, D_i = rowsum(P o dP) over both key tiles in registers; then the
+// transposed products (operands swapped) dV^T = dO^T P, dK^T = Q^T dS, dQ^T = K^T dS^T so
+// that each lane holds 4 consecutive columns of one row for the stores.
+struct TileRowsB {
   s16x8 q[2], k[2], v[2], d[2];
   float l2, l1[4];
-  int q0, qn, pre;
+  int t0, n, pre, first2, first1[4];  // class starts (tile-relative) of rows r16 and 4g4+r
 };
 
-template <typename T, typename TG>
-__global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int C, int P, int R,
-                                                            const int* __restrict__ seg, int H,
-                                                            int nchunk, int sc, const T* __restrict__ qkv,
+template <typename T, typename TG, int kBwdBatch>
+__global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int P, int R, int ntiles,
+                                                            const int* __restrict__ tiles,
+                                                            const int* __restrict__ row_first, int H,
+                                                            int nchunk, int uc, const T* __restrict__ qkv,
                                                             int ldq, const TG* __restrict__ dout,
                                                             int lddo, const float* __restrict__ lse,
                                                             TG* __restrict__ dqkv, int lddq,
                                                             float* __restrict__ part) {
   static_assert(__is_same(TG, bf16), "MFMA attention backward computes in bf16");
-  __shared__ CLIPK_LDS_ALIGN short tiles[4][4][16 * TRS];  // per wave: K_pre, K_own, Q, dO
+  __shared__ CLIPK_LDS_ALIGN short sm[4][4][16 * TRS];  // per wave: K_pre, K_own, Q, dO
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
   const int wid = blockIdx.x * 4 + w;
   if (wid >= G * nchunk * H) return;  // wave-uniform
   const int h = wid % H, k = (wid / H) % nchunk, g = wid / (H * nchunk);
   const int W = H * 64;
-  short* tKp = tiles[w][0];
-  short* tKo = tiles[w][1];
-  short* tQ = tiles[w][2];
-  short* tD = tiles[w][3];
+  short* tKp = sm[w][0];
+  short* tKo = sm[w][1];
+  short* tQ = sm[w][2];
+  short* tD = sm[w][3];
+  const int gR = g * R;
+  const T* qh = qkv + h * 64;
+  const TG* dh = dout + h * 64;
   const float* lse_h = lse + h;
 
-  const int s_begin = k * sc, s_end = min((k + 1) * sc, C + 1);
-  const int tab = load_seg_table(seg, C, s_begin, lane);
-  auto load = [&](int s, SegRowsB& f) {
-    seg_info_reg(tab, g, R, P, s, s_begin, f.q0, f.qn, f.pre);
-    const bool ok = r16 < f.qn;
-    const size_t row = (size_t)f.q0 + min(r16, f.qn - 1);
-    const T* qp = qkv + row * ldq + h * 64;
-    const TG* dp = dout + row * lddo + h * 64;
+  const int u_begin = k * uc, u_end = min((k + 1) * uc, ntiles + 1);
+  const int tab = load_tile_table(tiles, ntiles, u_begin, lane);
+  auto load = [&](int u, TileRowsB& f) {
+    tile_info(tab, P, u, u_begin, f.t0, f.n, f.pre);
+    const int rl = f.t0 + min(r16, f.n - 1);
+    const T* qp = qh + (gR + rl) * ldq;
+    const TG* dp = dh + (gR + rl) * lddo;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int c = 8 * g4 + 32 * kk;
@@ -244,15 +230,18 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int C, int P,
       f.v[kk] = ld16(qp + 2 * W + c);
       f.d[kk] = ld16(dp + c);
     }
-    (void)ok;
-    f.l2 = lse_h[row * H];
+    f.l2 = lse_h[(gR + rl) * H];
+    f.first2 = u == 0 ? 0 : row_first[rl] - f.t0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) f.l1[r] = lse_h[((size_t)f.q0 + min(4 * g4 + r, f.qn - 1)) * H];
+    for (int r = 0; r < 4; ++r) {
+      const int ri = f.t0 + min(4 * g4 + r, f.n - 1);
+      f.l1[r] = lse_h[(gR + ri) * H];
+      f.first1[r] = u == 0 ? 0 : row_first[ri] - f.t0;
+    }
   };
 
-  // batches of kBwdBatch segments, as in the forward
   const bool pok = r16 < P;
-  const T* pp = qkv + ((size_t)g * R + (pok ? r16 : 0)) * ldq + h * 64;
+  const T* pp = qh + (gR + (pok ? r16 : 0)) * ldq;
   s16x8 kp[2], vp[2];
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
@@ -267,18 +256,18 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int C, int P,
     dkp[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
     dvp[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
   }
-  auto body = [&](int s, SegRowsB& cur) {
-    const int q0 = cur.q0, qn = cur.qn, pre = cur.pre;
-    const bool qok = r16 < qn;
-    s16x8 q[2], ko[2], vo[2], d[2];
+  auto body = [&](TileRowsB& cur, bool own_is_prefix) {
+    const int n = cur.n, pre = cur.pre;
+    const bool qok = r16 < n;
+    s16x8 q[2], ko[2], vo[2];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {  // rows past the segment: zero (their loads were clamped)
-      q[kk] = to_bf16x8<T>(sel16(cur.q[kk], qok));
-      ko[kk] = to_bf16x8<T>(sel16(cur.k[kk], qok));
-      vo[kk] = to_bf16x8<T>(sel16(cur.v[kk], qok));
-      d[kk] = sel16(cur.d[kk], qok);
+    for (int kk = 0; kk < 2; ++kk) {
+      q[kk] = to_bf16x8<T>(cur.q[kk]);
+      ko[kk] = to_bf16x8<T>(cur.k[kk]);
+      vo[kk] = to_bf16x8<T>(cur.v[kk]);
     }
-    lds_fence();  // previous segment's transposed reads are done
+    const s16x8* d = cur.d;
+    lds_fence();  // previous tile's transposed reads are done
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int c = 8 * g4 + 32 * kk;
@@ -299,14 +288,13 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int C, int P,
       p1o = mfma32_bf16(d[kk], vo[kk], p1o);
       p2o = mfma32_bf16(vo[kk], d[kk], p2o);
     }
-    // layout 2: i = r16, j = 4g4+r
-    const float li2 = cur.l2;
+    // layout 2: i = r16, j = 4g4+r  (rows past the tile are clamped copies: masked, not zeroed)
     float P2p[4], P2o[4], Dsum = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int j = 4 * g4 + r;
-      P2p[r] = (qok && j < pre) ? __expf(s2p[r] * kScale - li2) : 0.f;
-      P2o[r] = (qok && j <= r16) ? __expf(s2o[r] * kScale - li2) : 0.f;
+      P2p[r] = (qok && j < pre) ? __expf(s2p[r] * kScale - cur.l2) : 0.f;
+      P2o[r] = (qok && j <= r16 && j >= cur.first2) ? __expf(s2o[r] * kScale - cur.l2) : 0.f;
       Dsum += P2p[r] * p2p[r] + P2o[r] * p2o[r];
     }
     Dsum += __shfl_xor(Dsum, 16, 64);
@@ -322,18 +310,13 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int C, int P,
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = 4 * g4 + r;
-      const bool iok = i < qn;
-      const float li = cur.l1[r];
+      const bool iok = i < n;
       const float Di = __shfl(Dsum, i, 64);
-      P1p[r] = (iok && r16 < pre) ? __expf(s1p[r] * kScale - li) : 0.f;
-      P1o[r] = (iok && r16 <= i) ? __expf(s1o[r] * kScale - li) : 0.f;
+      P1p[r] = (iok && r16 < pre) ? __expf(s1p[r] * kScale - cur.l1[r]) : 0.f;
+      P1o[r] = (iok && r16 <= i && r16 >= cur.first1[r]) ? __expf(s1o[r] * kScale - cur.l1[r]) : 0.f;
       dS1p[r] = P1p[r] * (p1p[r] - Di);
       dS1o[r] = P1o[r] * (p1o[r] - Di);
     }
-    // Transposed products (operands swapped), so each lane holds 4 consecutive columns of
-    // one row: dV^T = dO^T P, dK^T = Q^T dS, dQ^T = K^T dS^T with the transposed LDS reads
-    // as A and the probability / dS registers as B. Lane (r16, g4), tile t: row r16,
-    // columns 16t + 4g4 .. +3.
     const s16x4 bPp = pack_bf16x4(P1p[0], P1p[1], P1p[2], P1p[3]);      // B[k=i][n=j]
     const s16x4 bSp = pack_bf16x4(dS1p[0], dS1p[1], dS1p[2], dS1p[3]);
     const s16x4 bPo = pack_bf16x4(P1o[0], P1o[1], P1o[2], P1o[3]);
@@ -341,8 +324,7 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int C, int P,
     const s16x4 bTp = pack_bf16x4(dS2p[0], dS2p[1], dS2p[2], dS2p[3]);  // B[k=j][n=i]
     const s16x4 bTo = pack_bf16x4(dS2o[0], dS2o[1], dS2o[2], dS2o[3]);
     lds_fence();
-    const bool own_is_prefix = s == 0;  // segment 0's keys are the prefix rows themselves
-    TG* orow = dqkv + ((size_t)q0 + r16) * lddq + h * 64 + 4 * g4;
+    TG* orow = dqkv + (gR + cur.t0 + r16) * lddq + h * 64 + 4 * g4;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const s16x4 aD = tr_read(tD, 4 * g4, 16 * t, lane);
@@ -353,7 +335,7 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int C, int P,
       dq = mfma16_bf16(tr_read(tKo, 4 * g4, 16 * t, lane), bTo, dq);
       const f32x4 dvo = mfma16_bf16(aD, bPo, z);
       const f32x4 dko = mfma16_bf16(aQ, bSo, z);
-      if (own_is_prefix) {
+      if (own_is_prefix) {  // the prefix tile's keys are the prefix rows themselves
         dvp[t] += dvo;
         dkp[t] += dko;
       }
@@ -366,14 +348,14 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int C, int P,
       }
     }
   };
-  for (int s = s_begin; s < s_end; s += kBwdBatch) {
-    SegRowsB rr[kBwdBatch];
+  for (int u = u_begin; u < u_end; u += kBwdBatch) {
+    TileRowsB rr[kBwdBatch];
 #pragma unroll
-    for (int j = 0; j < kBwdBatch; ++j) load(min(s + j, s_end - 1), rr[j]);
+    for (int j = 0; j < kBwdBatch; ++j) load(min(u + j, u_end - 1), rr[j]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < kBwdBatch; ++j)
-      if (s + j < s_end) body(s + j, rr[j]);
+      if (u + j < u_end) body(rr[j], u + j == 0);
   }
   // this chunk's partial dK/dV of the prefix rows (fp32, [G][nchunk][16][2W])
   float* pb = part + ((size_t)g * nchunk + k) * 16 * (2 * W);
@@ -388,11 +370,49 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int C, int P,
 }
 
 // ------------------------------------------------------------------ VALU versions (fp32 path)
-// One wave per (group, chunk, head); 4 segments in flight (lane group grp = lane>>4), lane
-// r16 = query row (forward, dQ) or key row (dK/dV). K/V rows staged in LDS as fp32.
+// One wave per (group, chunk of kValuChunk units, head); 4 tiles in flight (lane group
+// grp = lane>>4), lane r16 = row of the tile (query for the forward and dQ, key for dK/dV).
+// K/V rows staged in LDS as fp32.
+__device__ __forceinline__ void valu_unit(const int* __restrict__ tiles, const int* __restrict__ row_first,
+                                          int P, int u, int r16, int& t0, int& n, int& pre, int& first) {
+  if (u == 0) {
+    t0 = 0; n = P; pre = 0; first = 0;
+  } else {
+    t0 = tiles[2 * (u - 1)];
+    n = min(tiles[2 * (u - 1) + 1], 16);
+    pre = P;
+    first = row_first[t0 + min(r16, n - 1)] - t0;
+  }
+}
+
 template <typename T>
-__global__ __launch_bounds__(64) void attn_prefix_fwd_valu(int G, int C, int P, int R,
-                                                           const int* __restrict__ seg, int H,
+__device__ __forceinline__ void stage_prefix_f32(const T* __restrict__ qkv, int row0, int P, int ldq, int hW,
+                                                 int W, int lane, float* sKp, float* sVp) {
+  const int row = lane >> 2, qtr = lane & 3;  // 16 rows x 4 quarters of 16 values
+  float kv[16], vv[16];
+  if (row < P) {
+    const T* b = qkv + (size_t)(row0 + row) * ldq + hW + qtr * 16;
+    constexpr int V = Vec16<T>::N;
+#pragma unroll
+    for (int c = 0; c < 16 / V; ++c) {
+      load16_f32<T>(b + W + c * V, kv + c * V);
+      load16_f32<T>(b + 2 * W + c * V, vv + c * V);
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) { kv[c] = 0.f; vv[c] = 0.f; }
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    sKp[row * 64 + qtr * 16 + c] = kv[c];
+    sVp[row * 64 + qtr * 16 + c] = vv[c];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void attn_prefix_fwd_valu(int G, int P, int R, int ntiles,
+                                                           const int* __restrict__ tiles,
+                                                           const int* __restrict__ row_first, int H,
                                                            int nchunk, const T* __restrict__ qkv,
                                                            int ldq, T* __restrict__ out, int ldo,
                                                            float* __restrict__ lse) {
@@ -404,35 +424,16 @@ __global__ __launch_bounds__(64) void attn_prefix_fwd_valu(int G, int C, int P, 
   const int wid = blockIdx.x;
   const int h = wid % H, k = (wid / H) % nchunk, g = wid / (H * nchunk);
   const int W = H * 64;
-  {
-    const int row = lane >> 2, qtr = lane & 3;  // 16 rows x 4 quarters of 16 values
-    float kv[16], vv[16];
-    if (row < P) {
-      const T* b = qkv + ((size_t)g * R + row) * ldq + h * 64 + qtr * 16;
-      constexpr int V = Vec16<T>::N;
-#pragma unroll
-      for (int c = 0; c < 16 / V; ++c) {
-        load16_f32<T>(b + W + c * V, kv + c * V);
-        load16_f32<T>(b + 2 * W + c * V, vv + c * V);
-      }
-    } else {
-#pragma unroll
-      for (int c = 0; c < 16; ++c) { kv[c] = 0.f; vv[c] = 0.f; }
-    }
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      sKp[row * 64 + qtr * 16 + c] = kv[c];
-      sVp[row * 64 + qtr * 16 + c] = vv[c];
-    }
-  }
-  const int s_end = min((k + 1) * kSegChunk, C + 1);
-  for (int base = k * kSegChunk; base < s_end; base += 4) {
-    const int s = base + grp;
-    const bool active = s < s_end;
-    int q0 = 0, qn = 0, pre = 0;
-    if (active) seg_info(seg, g, R, P, s, q0, qn, pre);
-    const bool qok = active && r16 < qn;
-    const T* qp = qkv + ((size_t)q0 + (qok ? r16 : 0)) * ldq + h * 64;
+  stage_prefix_f32<T>(qkv, g * R, P, ldq, h * 64, W, lane, sKp, sVp);
+  const int u_end = min((k + 1) * kValuChunk, ntiles + 1);
+  for (int base = k * kValuChunk; base < u_end; base += 4) {
+    const int u = base + grp;
+    const bool active = u < u_end;
+    int t0 = 0, n = 1, pre = 0, first = 0;
+    if (active) valu_unit(tiles, row_first, P, u, r16, t0, n, pre, first);
+    const bool qok = active && r16 < n;
+    const size_t row = (size_t)g * R + t0 + min(r16, n - 1);
+    const T* qp = qkv + row * ldq + h * 64;
     float q[64], t64[64];
     load_row64<T>(qp, q);
 #pragma unroll
@@ -448,7 +449,7 @@ __global__ __launch_bounds__(64) void attn_prefix_fwd_valu(int G, int C, int P, 
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       sc[j] = j < pre ? dot64(q, &sKp[j * 64]) : -INFINITY;
-      sc[16 + j] = (j <= r16 && j < qn) ? dot64(q, &sK[grp][j * 64]) : -INFINITY;
+      sc[16 + j] = (j <= r16 && j >= first) ? dot64(q, &sK[grp][j * 64]) : -INFINITY;
       m = fmaxf(m, fmaxf(sc[j], sc[16 + j]));
     }
     float l = 0.f;
@@ -468,19 +469,19 @@ __global__ __launch_bounds__(64) void attn_prefix_fwd_valu(int G, int C, int P, 
       const float inv = 1.0f / l;
 #pragma unroll
       for (int dd = 0; dd < 64; ++dd) t64[dd] *= inv;
-      store_row64<T>(out + ((size_t)q0 + r16) * ldo + h * 64, t64);
-      if (lse) lse[((size_t)q0 + r16) * H + h] = m + __logf(l);
+      store_row64<T>(out + row * ldo + h * 64, t64);
+      if (lse) lse[row * H + h] = m + __logf(l);
     }
-    __syncthreads();  // sK/sV reused by the next 4 segments
+    __syncthreads();  // sK/sV reused by the next 4 tiles
   }
 }
 
 template <typename T, typename TG>
 __global__ __launch_bounds__(64) void attn_prefix_bwd_valu(
-    int G, int C, int P, int R, const int* __restrict__ seg, int H, int nchunk,
-    const T* __restrict__ qkv, int ldq, const T* __restrict__ o_fwd, int ldof,
-    const TG* __restrict__ dout, int lddo, const float* __restrict__ lse, TG* __restrict__ dqkv,
-    int lddq, float* __restrict__ part) {
+    int G, int P, int R, int ntiles, const int* __restrict__ tiles, const int* __restrict__ row_first, int H,
+    int nchunk, const T* __restrict__ qkv, int ldq, const T* __restrict__ o_fwd, int ldof,
+    const TG* __restrict__ dout, int lddo, const float* __restrict__ lse, TG* __restrict__ dqkv, int lddq,
+    float* __restrict__ part) {
   __shared__ CLIPK_LDS_ALIGN float sKp[16 * 64];
   __shared__ CLIPK_LDS_ALIGN float sVp[16 * 64];
   __shared__ CLIPK_LDS_ALIGN float sQ[4][16 * 64];   // scaled q
@@ -490,43 +491,24 @@ __global__ __launch_bounds__(64) void attn_prefix_bwd_valu(
   __shared__ CLIPK_LDS_ALIGN float sAk[4][16 * 64];  // prefix dK accumulators, per lane group
   __shared__ CLIPK_LDS_ALIGN float sAv[4][16 * 64];
   __shared__ float slse[4][16], sD[4][16];
+  __shared__ int sfirst[4][16];
   const int lane = threadIdx.x, grp = lane >> 4, r16 = lane & 15;
   const int wid = blockIdx.x;
   const int h = wid % H, k = (wid / H) % nchunk, g = wid / (H * nchunk);
   const int W = H * 64;
-  {
-    const int row = lane >> 2, qtr = lane & 3;
-    float kv[16], vv[16];
-    if (row < P) {
-      const T* b = qkv + ((size_t)g * R + row) * ldq + h * 64 + qtr * 16;
-      constexpr int V = Vec16<T>::N;
-#pragma unroll
-      for (int c = 0; c < 16 / V; ++c) {
-        load16_f32<T>(b + W + c * V, kv + c * V);
-        load16_f32<T>(b + 2 * W + c * V, vv + c * V);
-      }
-    } else {
-#pragma unroll
-      for (int c = 0; c < 16; ++c) { kv[c] = 0.f; vv[c] = 0.f; }
-    }
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      sKp[row * 64 + qtr * 16 + c] = kv[c];
-      sVp[row * 64 + qtr * 16 + c] = vv[c];
-    }
-  }
+  stage_prefix_f32<T>(qkv, g * R, P, ldq, h * 64, W, lane, sKp, sVp);
   for (int i = lane; i < 4 * 16 * 64; i += 64) {
     (&sAk[0][0])[i] = 0.f;
     (&sAv[0][0])[i] = 0.f;
   }
-  const int s_end = min((k + 1) * kSegChunk, C + 1);
-  for (int base = k * kSegChunk; base < s_end; base += 4) {
-    const int s = base + grp;
-    const bool active = s < s_end;
-    int q0 = 0, qn = 0, pre = 0;
-    if (active) seg_info(seg, g, R, P, s, q0, qn, pre);
-    const bool qok = active && r16 < qn;
-    const size_t row = (size_t)q0 + (qok ? r16 : 0);
+  const int u_end = min((k + 1) * kValuChunk, ntiles + 1);
+  for (int base = k * kValuChunk; base < u_end; base += 4) {
+    const int u = base + grp;
+    const bool active = u < u_end;
+    int t0 = 0, n = 1, pre = 0, first = 0;
+    if (active) valu_unit(tiles, row_first, P, u, r16, t0, n, pre, first);
+    const bool qok = active && r16 < n;
+    const size_t row = (size_t)g * R + t0 + min(r16, n - 1);
     const T* qp = qkv + row * ldq + h * 64;
     float a[64], dO[64];
     load_row64<T>(qp, a);
@@ -546,6 +528,7 @@ __global__ __launch_bounds__(64) void attn_prefix_bwd_valu(
     const float li = qok ? lse[row * H + h] : 0.f;
     slse[grp][r16] = li;
     sD[grp][r16] = Di;
+    sfirst[grp][r16] = first;
     __syncthreads();
     // phase 1 (lane = query): dq = sum_j P (dP - D) k_j / 8 over prefix + own keys
     {
@@ -553,7 +536,7 @@ __global__ __launch_bounds__(64) void attn_prefix_bwd_valu(
 #pragma unroll
       for (int dd = 0; dd < 64; ++dd) a[dd] = 0.f;
       for (int j = 0; j < 32; ++j) {
-        const bool ok = j < 16 ? j < pre : (j - 16 <= r16 && j - 16 < qn);
+        const bool ok = j < 16 ? j < pre : (j - 16 <= r16 && j - 16 >= first);
         if (!qok || !ok) continue;
         const float* kr = j < 16 ? &sKp[j * 64] : &sK[grp][(j - 16) * 64];
         const float* vr = j < 16 ? &sVp[j * 64] : &sV[grp][(j - 16) * 64];
@@ -568,14 +551,15 @@ __global__ __launch_bounds__(64) void attn_prefix_bwd_valu(
         store_row64<TG>(dqkv + row * lddq + h * 64, a);
       }
     }
-    // phase 2 (lane = own key j = r16): over queries i >= j of this segment
+    // phase 2 (lane = own key j = r16): over the queries i >= j of the same class
     {
       const float* kj = &sK[grp][r16 * 64];
       const float* vj = &sV[grp][r16 * 64];
       float dk[64], dv[64];
 #pragma unroll
       for (int dd = 0; dd < 64; ++dd) { dk[dd] = 0.f; dv[dd] = 0.f; }
-      for (int i = r16; i < qn; ++i) {
+      for (int i = r16; i < n; ++i) {
+        if (sfirst[grp][i] > r16) break;  // past this key's class
         const float* qr = &sQ[grp][i * 64];
         const float* dr = &sdO[grp][i * 64];
         const float p = __expf(dot64(qr, kj) - slse[grp][i]);
@@ -587,7 +571,7 @@ __global__ __launch_bounds__(64) void attn_prefix_bwd_valu(
         }
       }
       if (qok) {
-        if (s == 0) {  // segment 0's own keys are the prefix rows: accumulate
+        if (u == 0) {  // the prefix tile's own keys are the prefix rows: accumulate
 #pragma unroll
           for (int dd = 0; dd < 64; ++dd) {
             sAk[grp][r16 * 64 + dd] += dk[dd];
@@ -599,14 +583,14 @@ __global__ __launch_bounds__(64) void attn_prefix_bwd_valu(
         }
       }
     }
-    // phase 3 (lane = prefix key j = r16): partial over every query of this segment
+    // phase 3 (lane = prefix key j = r16): partial over every query of this tile
     if (active && r16 < pre) {
       const float* kj = &sKp[r16 * 64];
       const float* vj = &sVp[r16 * 64];
       float dk[64], dv[64];
 #pragma unroll
       for (int dd = 0; dd < 64; ++dd) { dk[dd] = 0.f; dv[dd] = 0.f; }
-      for (int i = 0; i < qn; ++i) {
+      for (int i = 0; i < n; ++i) {
         const float* qr = &sQ[grp][i * 64];
         const float* dr = &sdO[grp][i * 64];
         const float p = __expf(dot64(qr, kj) - slse[grp][i]);
@@ -623,7 +607,7 @@ __global__ __launch_bounds__(64) void attn_prefix_bwd_valu(
         sAv[grp][r16 * 64 + dd] += dv[dd];
       }
     }
-    __syncthreads();  // staging buffers reused by the next 4 segments
+    __syncthreads();  // staging buffers reused by the next 4 tiles
   }
   float* pb = part + ((size_t)g * nchunk + k) * 16 * (2 * W);
   for (int idx = lane; idx < P * 64; idx += 64) {
@@ -643,48 +627,64 @@ __global__ __launch_bounds__(256) void prefix_kv_reduce(int P, int R, int W, int
   const int col = blockIdx.y * 256 + threadIdx.x;
   if (col >= 2 * W) return;
   const float* src = part + ((size_t)g * nchunk * 16 + p) * 2 * W + col;
-  float acc = 0.f;
-  for (int k = 0; k < nchunk; ++k) acc += src[(size_t)k * 16 * 2 * W];
+  const size_t cs = (size_t)16 * 2 * W;  // chunk stride
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // 4 independent chains, fixed order
+  int k = 0;
+  for (; k + 4 <= nchunk; k += 4) {
+    a0 += src[k * cs];
+    a1 += src[(k + 1) * cs];
+    a2 += src[(k + 2) * cs];
+    a3 += src[(k + 3) * cs];
+  }
+  for (; k < nchunk; ++k) a0 += src[k * cs];
+  const float acc = (a0 + a1) + (a2 + a3);
   dqkv[((size_t)g * R + p) * lddq + W + col] = (TG)acc;
 }
 
-static inline int n_chunks(int C, int sc = kSegChunk) { return (C + 1 + sc - 1) / sc; }
-
 template <typename T>
-static int prefix_fwd(int G, int C, int P, int R, const int* seg, int H, const void* qkv, int ldq,
-                      void* out, int ldo, float* lse, hipStream_t st) {
+static int prefix_fwd(int G, int P, int R, int ntiles, const int* tiles, const int* row_first, int H,
+                      const void* qkv, int ldq, void* out, int ldo, float* lse, hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
-    const int sc = fwd_chunk();
-    const int nchunk = n_chunks(C, sc);
+    const int uc = fwd_chunk();
+    const int nchunk = n_chunks(ntiles, uc);
     const long waves = (long)G * nchunk * H;
-    hipLaunchKernelGGL((attn_prefix_fwd_mfma<T>), dim3((waves + 3) / 4), dim3(256), 0, st, G, C, P, R, seg,
-                       H, nchunk, sc, (const T*)qkv, ldq, (T*)out, ldo, lse);
+    const int b = fwd_batch();
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((waves + 3) / 4), dim3(256), 0, st, G, P, R, ntiles, tiles, row_first, H,
+                         nchunk, uc, (const T*)qkv, ldq, (T*)out, ldo, lse);
+    };
+    if (b == 1) go(attn_prefix_fwd_mfma<T, 1>);
+    else if (b == 2) go(attn_prefix_fwd_mfma<T, 2>);
+    else go(attn_prefix_fwd_mfma<T, 4>);
   } else {
-    const int nchunk = n_chunks(C);
+    const int nchunk = n_chunks(ntiles, kValuChunk);
     const long waves = (long)G * nchunk * H;
-    hipLaunchKernelGGL((attn_prefix_fwd_valu<T>), dim3(waves), dim3(64), 0, st, G, C, P, R, seg, H, nchunk,
-                       (const T*)qkv, ldq, (T*)out, ldo, lse);
+    hipLaunchKernelGGL((attn_prefix_fwd_valu<T>), dim3(waves), dim3(64), 0, st, G, P, R, ntiles, tiles,
+                       row_first, H, nchunk, (const T*)qkv, ldq, (T*)out, ldo, lse);
   }
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
 }
 
 template <typename T, typename TG>
-static int prefix_bwd(int G, int C, int P, int R, const int* seg, int H, const void* qkv, int ldq,
-                      const void* ofwd, int ldof, const void* dout, int lddo, const float* lse,
-                      void* dqkv, int lddq, float* part, hipStream_t st) {
+static int prefix_bwd(int G, int P, int R, int ntiles, const int* tiles, const int* row_first, int H,
+                      const void* qkv, int ldq, const void* ofwd, int ldof, const void* dout, int lddo,
+                      const float* lse, void* dqkv, int lddq, float* part, hipStream_t st) {
   constexpr bool mfma = __is_same(TG, bf16) && sizeof(T) == 2;
-  const int sc = mfma ? bwd_chunk() : kSegChunk;
-  const int nchunk = n_chunks(C, sc);
+  const int uc = mfma ? bwd_chunk() : kValuChunk;
+  const int nchunk = n_chunks(ntiles, uc);
   const long waves = (long)G * nchunk * H;
   if constexpr (mfma) {
-    hipLaunchKernelGGL((attn_prefix_bwd_mfma<T, TG>), dim3((waves + 3) / 4), dim3(256), 0, st, G, C, P, R,
-                       seg, H, nchunk, sc, (const T*)qkv, ldq, (const TG*)dout, lddo, lse, (TG*)dqkv, lddq,
-                       part);
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((waves + 3) / 4), dim3(256), 0, st, G, P, R, ntiles, tiles, row_first, H,
+                         nchunk, uc, (const T*)qkv, ldq, (const TG*)dout, lddo, lse, (TG*)dqkv, lddq, part);
+    };
+    if (bwd_batch() == 1) go(attn_prefix_bwd_mfma<T, TG, 1>);
+    else go(attn_prefix_bwd_mfma<T, TG, 2>);
   } else {
-    hipLaunchKernelGGL((attn_prefix_bwd_valu<T, TG>), dim3(waves), dim3(64), 0, st, G, C, P, R, seg, H,
-                       nchunk, (const T*)qkv, ldq, (const T*)ofwd, ldof, (const TG*)dout, lddo, lse,
-                       (TG*)dqkv, lddq, part);
+    hipLaunchKernelGGL((attn_prefix_bwd_valu<T, TG>), dim3(waves), dim3(64), 0, st, G, P, R, ntiles, tiles,
+                       row_first, H, nchunk, (const T*)qkv, ldq, (const T*)ofwd, ldof, (const TG*)dout, lddo,
+                       lse, (TG*)dqkv, lddq, part);
   }
   CLIPK_CHECK_LAUNCH();
   const int W = H * 64;
@@ -698,47 +698,48 @@ static int prefix_bwd(int G, int C, int P, int R, const int* seg, int H, const v
 
 using namespace clipk;
 
-static int prefix_shape_ok(int G, int C, int P, int R, int max_q, int heads) {
-  return G > 0 && C > 0 && P >= 1 && P <= 16 && max_q >= 1 && max_q <= 16 && R >= P + C && heads > 0;
+static int prefix_shape_ok(int G, int P, int R, int ntiles, int heads, int ldq) {
+  return G > 0 && P >= 1 && P <= 16 && ntiles >= 1 && R > P && heads > 0 &&
+         (long)G * R * (long)(ldq > 3 * heads * 64 ? ldq : 3 * heads * 64) < (1L << 31);  // int32 offsets
 }
 
-extern "C" size_t clipk_attention_prefix_ws_bytes(int G, int C, int heads) {
-  if (G <= 0 || C <= 0 || heads <= 0) return 0;
-  const int sc = bwd_chunk() < kSegChunk ? bwd_chunk() : kSegChunk;  // the larger chunk count of the two paths
-  return (size_t)G * n_chunks(C, sc) * 16 * 2 * heads * 64 * sizeof(float);
+extern "C" size_t clipk_attention_prefix_ws_bytes(int G, int ntiles, int heads) {
+  if (G <= 0 || ntiles <= 0 || heads <= 0) return 0;
+  const int uc = bwd_chunk() < kValuChunk ? bwd_chunk() : kValuChunk;  // the larger chunk count
+  return (size_t)G * n_chunks(ntiles, uc) * 16 * 2 * heads * 64 * sizeof(float);
 }
 
-extern "C" int clipk_attention_prefix_fwd(int dtype, int G, int C, int P, int R, const int* seg,
-                                          int max_q, int heads, const void* qkv, int ldqkv,
+extern "C" int clipk_attention_prefix_fwd(int dtype, int G, int P, int R, int ntiles, const int* tiles,
+                                          const int* row_first, int heads, const void* qkv, int ldqkv,
                                           void* out, int ldo, float* lse, void* stream) {
-  if (!seg || !qkv || !out) return CLIPK_EINVAL;
-  if (!prefix_shape_ok(G, C, P, R, max_q, heads) || ldqkv < 3 * heads * 64 || ldo < heads * 64 ||
+  if (!tiles || !row_first || !qkv || !out) return CLIPK_EINVAL;
+  if (!prefix_shape_ok(G, P, R, ntiles, heads, ldqkv) || ldqkv < 3 * heads * 64 || ldo < heads * 64 ||
       ldqkv % 8 || ldo % 8)
     return CLIPK_ESHAPE;
   hipStream_t st = (hipStream_t)stream;
   switch (dtype) {
-    case CLIPK_F16: return prefix_fwd<f16>(G, C, P, R, seg, heads, qkv, ldqkv, out, ldo, lse, st);
-    case CLIPK_BF16: return prefix_fwd<bf16>(G, C, P, R, seg, heads, qkv, ldqkv, out, ldo, lse, st);
-    case CLIPK_F32: return prefix_fwd<float>(G, C, P, R, seg, heads, qkv, ldqkv, out, ldo, lse, st);
+    case CLIPK_F16: return prefix_fwd<f16>(G, P, R, ntiles, tiles, row_first, heads, qkv, ldqkv, out, ldo, lse, st);
+    case CLIPK_BF16: return prefix_fwd<bf16>(G, P, R, ntiles, tiles, row_first, heads, qkv, ldqkv, out, ldo, lse, st);
+    case CLIPK_F32: return prefix_fwd<float>(G, P, R, ntiles, tiles, row_first, heads, qkv, ldqkv, out, ldo, lse, st);
     default: return CLIPK_EDTYPE;
   }
 }
 
-extern "C" int clipk_attention_prefix_bwd(int dtype, int grad_dtype, int G, int C, int P, int R,
-                                          const int* seg, int max_q, int heads, const void* qkv,
-                                          int ldqkv, const void* ofwd, int ldof, const void* dout,
-                                          int lddo, const float* lse, void* dqkv, int lddqkv,
-                                          void* ws, size_t ws_bytes, void* stream) {
-  if (!seg || !qkv || !ofwd || !dout || !lse || !dqkv || !ws) return CLIPK_EINVAL;
-  if (!prefix_shape_ok(G, C, P, R, max_q, heads) || ldqkv < 3 * heads * 64 ||
-      lddqkv < 3 * heads * 64 || ldof < heads * 64 || lddo < heads * 64)
+extern "C" int clipk_attention_prefix_bwd(int dtype, int grad_dtype, int G, int P, int R, int ntiles,
+                                          const int* tiles, const int* row_first, int heads,
+                                          const void* qkv, int ldqkv, const void* ofwd, int ldof,
+                                          const void* dout, int lddo, const float* lse, void* dqkv,
+                                          int lddqkv, void* ws, size_t ws_bytes, void* stream) {
+  if (!tiles || !row_first || !qkv || !ofwd || !dout || !lse || !dqkv || !ws) return CLIPK_EINVAL;
+  if (!prefix_shape_ok(G, P, R, ntiles, heads, lddqkv) || ldqkv < 3 * heads * 64 || lddqkv < 3 * heads * 64 ||
+      ldof < heads * 64 || lddo < heads * 64)
     return CLIPK_ESHAPE;
-  if (ws_bytes < clipk_attention_prefix_ws_bytes(G, C, heads)) return CLIPK_EWORKSPACE;
+  if (ws_bytes < clipk_attention_prefix_ws_bytes(G, ntiles, heads)) return CLIPK_EWORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)ws;
-#define CLIPK_PBWD(TT, TGG)                                                                      \
-  return prefix_bwd<TT, TGG>(G, C, P, R, seg, heads, qkv, ldqkv, ofwd, ldof, dout, lddo, lse, dqkv, \
-                             lddqkv, part, st)
+#define CLIPK_PBWD(TT, TGG)                                                                            \
+  return prefix_bwd<TT, TGG>(G, P, R, ntiles, tiles, row_first, heads, qkv, ldqkv, ofwd, ldof, dout, lddo, \
+                             lse, dqkv, lddqkv, part, st)
   if (dtype == CLIPK_F16 && grad_dtype == CLIPK_BF16) CLIPK_PBWD(f16, bf16);
   if (dtype == CLIPK_F16 && grad_dtype == CLIPK_F16) CLIPK_PBWD(f16, f16);
   if (dtype == CLIPK_BF16 && grad_dtype == CLIPK_BF16) CLIPK_PBWD(bf16, bf16);

@@ -169,28 +169,29 @@ struct SeqShape {
   int rows = 0, nout = 0;
   int nseq = 0, L = 0, causal = 0;
   bool packed = false;
-  int G = 0, C = 0, P = 0, R = 0, max_q = 0;
-  const int* seg = nullptr;
+  int G = 0, C = 0, P = 0, R = 0, ntiles = 0;
+  const int* tiles = nullptr;
+  const int* row_first = nullptr;
   static SeqShape plain(int nseq, int L, int causal) {
     SeqShape s;
     s.rows = nseq * L; s.nout = nseq; s.nseq = nseq; s.L = L; s.causal = causal;
     return s;
   }
-  static SeqShape prefix(int G, int C, int P, int R, const int* seg, int max_q) {
+  static SeqShape prefix(int G, int C, int P, int R, int ntiles, const int* tiles, const int* row_first) {
     SeqShape s;
     s.rows = G * R; s.nout = G * C; s.packed = true; s.causal = 1;
-    s.G = G; s.C = C; s.P = P; s.R = R; s.seg = seg; s.max_q = max_q;
+    s.G = G; s.C = C; s.P = P; s.R = R; s.ntiles = ntiles; s.tiles = tiles; s.row_first = row_first;
     return s;
   }
-  size_t part_bytes(int heads) const { return packed ? clipk_attention_prefix_ws_bytes(G, C, heads) : 0; }
+  size_t part_bytes(int heads) const { return packed ? clipk_attention_prefix_ws_bytes(G, ntiles, heads) : 0; }
 };
 
 static int attn_fwd(const clipk_encoder* e, const SeqShape& sh, const void* qkv, void* o, float* lse,
                     hipStream_t st) {
   const int W = e->W;
   if (sh.packed)
-    return clipk_attention_prefix_fwd(e->act, sh.G, sh.C, sh.P, sh.R, sh.seg, sh.max_q, e->heads, qkv, 3 * W,
-                                      o, W, lse, st);
+    return clipk_attention_prefix_fwd(e->act, sh.G, sh.P, sh.R, sh.ntiles, sh.tiles, sh.row_first, e->heads,
+                                      qkv, 3 * W, o, W, lse, st);
   return clipk_attention_fwd(e->act, sh.nseq, sh.L, e->heads, sh.causal, qkv, 3 * W, o, W, lse, st);
 }
 
@@ -198,8 +199,8 @@ static int attn_bwd(const clipk_encoder* e, const SeqShape& sh, const void* qkv,
                     const void* dout, const float* lse, void* dqkv, void* part, hipStream_t st) {
   const int W = e->W;
   if (sh.packed)
-    return clipk_attention_prefix_bwd(e->act, e->grad, sh.G, sh.C, sh.P, sh.R, sh.seg, sh.max_q, e->heads,
-                                      qkv, 3 * W, o, W, dout, W, lse, dqkv, 3 * W, part,
+    return clipk_attention_prefix_bwd(e->act, e->grad, sh.G, sh.P, sh.R, sh.ntiles, sh.tiles, sh.row_first,
+                                      e->heads, qkv, 3 * W, o, W, dout, W, lse, dqkv, 3 * W, part,
                                       sh.part_bytes(e->heads), st);
   return clipk_attention_bwd(e->act, e->grad, sh.nseq, sh.L, e->heads, sh.causal, qkv, 3 * W, o, W, dout, W,
                              lse, dqkv, 3 * W, st);
@@ -415,9 +416,8 @@ extern "C" int clipk_text_backward(const clipk_encoder* e, int nseq, int L, cons
                             ws_bytes, (hipStream_t)stream);
 }
 
-static bool packed_ok(int G, int C, int P, int R, int max_q) {
-  return G > 0 && C > 0 && P >= 1 && P <= 16 && max_q >= 1 && max_q <= 16 && R >= P + C &&
-         R <= P + C * max_q && (long)G * R < (1L << 31);
+static bool packed_ok(int G, int C, int P, int R, int ntiles) {
+  return G > 0 && C > 0 && P >= 1 && P <= 16 && ntiles >= 1 && R >= P + C && (long)G * R < (1L << 31);
 }
 
 extern "C" size_t clipk_text_packed_saved_bytes(const clipk_encoder* e, int G, int C, int R) {
@@ -430,31 +430,32 @@ extern "C" size_t clipk_text_packed_ws_bytes(const clipk_encoder* e, int G, int 
   return text_ws_bytes(e, (size_t)G * R, G * C);
 }
 
-extern "C" size_t clipk_text_packed_bwd_ws_bytes(const clipk_encoder* e, int G, int C, int R) {
-  if (!e || G <= 0 || C <= 0 || R <= 0) return 0;
-  return text_bwd_layout(e, (size_t)G * R, G * C, clipk_attention_prefix_ws_bytes(G, C, e->heads), nullptr)
+extern "C" size_t clipk_text_packed_bwd_ws_bytes(const clipk_encoder* e, int G, int C, int R, int ntiles) {
+  if (!e || G <= 0 || C <= 0 || R <= 0 || ntiles <= 0) return 0;
+  return text_bwd_layout(e, (size_t)G * R, G * C, clipk_attention_prefix_ws_bytes(G, ntiles, e->heads), nullptr)
       .bytes;
 }
 
-extern "C" int clipk_text_forward_packed(const clipk_encoder* e, int G, int C, int P, int R, const int* seg,
-                                         int max_q, const float* x0, const int* eot_rows, float* txt,
-                                         void* saved, size_t saved_bytes, void* ws, size_t ws_bytes,
-                                         void* stream) {
-  if (!e || e->kind != 0 || !seg || !x0 || !eot_rows || !txt || !ws) return CLIPK_EINVAL;
-  if (!packed_ok(G, C, P, R, max_q)) return CLIPK_ESHAPE;
-  return text_forward_impl(e, SeqShape::prefix(G, C, P, R, seg, max_q), x0, eot_rows, txt, saved,
+extern "C" int clipk_text_forward_packed(const clipk_encoder* e, int G, int C, int P, int R, int ntiles,
+                                         const int* tiles, const int* row_first, const float* x0,
+                                         const int* eot_rows, float* txt, void* saved, size_t saved_bytes,
+                                         void* ws, size_t ws_bytes, void* stream) {
+  if (!e || e->kind != 0 || !tiles || !row_first || !x0 || !eot_rows || !txt || !ws) return CLIPK_EINVAL;
+  if (!packed_ok(G, C, P, R, ntiles)) return CLIPK_ESHAPE;
+  return text_forward_impl(e, SeqShape::prefix(G, C, P, R, ntiles, tiles, row_first), x0, eot_rows, txt, saved,
                            saved_bytes, ws, ws_bytes, (hipStream_t)stream);
 }
 
-extern "C" int clipk_text_backward_packed(const clipk_encoder* e, int G, int C, int P, int R,
-                                          const int* seg, int max_q, const int* eot_rows,
+extern "C" int clipk_text_backward_packed(const clipk_encoder* e, int G, int C, int P, int R, int ntiles,
+                                          const int* tiles, const int* row_first, const int* eot_rows,
                                           const float* dtxt, const void* saved, size_t saved_bytes,
                                           float* dx0, void* ws, size_t ws_bytes, void* stream) {
-  if (!e || e->kind != 0 || !seg || !eot_rows || !dtxt || !saved || !dx0 || !ws) return CLIPK_EINVAL;
+  if (!e || e->kind != 0 || !tiles || !row_first || !eot_rows || !dtxt || !saved || !dx0 || !ws)
+    return CLIPK_EINVAL;
   if (!e->head[3]) return CLIPK_EINVAL;
-  if (!packed_ok(G, C, P, R, max_q)) return CLIPK_ESHAPE;
-  return text_backward_impl(e, SeqShape::prefix(G, C, P, R, seg, max_q), eot_rows, dtxt, saved, saved_bytes,
-                            dx0, ws, ws_bytes, (hipStream_t)stream);
+  if (!packed_ok(G, C, P, R, ntiles)) return CLIPK_ESHAPE;
+  return text_backward_impl(e, SeqShape::prefix(G, C, P, R, ntiles, tiles, row_first), eot_rows, dtxt, saved,
+                            saved_bytes, dx0, ws, ws_bytes, (hipStream_t)stream);
 }
 
 // ---------------------------------------------------------------- vision

@@ -133,25 +133,28 @@ def ctx_grad_rows(G, R, W, n_ctx, slot_ptr, slot_rows, dx0):
     return d
 
 
-def attention_prefix(qkv, G, C, P, R, seg, max_q, heads, lse=False):
-    """Shared-prefix packed causal attention (clipk_attention_prefix_fwd)."""
+def attention_prefix(qkv, G, P, R, tiles, row_first, heads, lse=False):
+    """Shared-prefix packed causal attention (clipk_attention_prefix_fwd); tiles int32
+    [ntiles*2] (first row, rows), row_first int32 [R]."""
     _need(qkv, "qkv")
-    _need(seg, "seg", torch.int32)
+    _need(tiles, "tiles", torch.int32)
+    _need(row_first, "row_first", torch.int32)
     W = heads * 64
     out = torch.zeros(G * R, W, device=qkv.device, dtype=qkv.dtype)
     l = torch.zeros(G * R, heads, device=qkv.device) if lse else None
-    N.call("clipk_attention_prefix_fwd", DT[qkv.dtype], G, C, P, R, _p(seg), max_q, heads, _p(qkv), 3 * W,
-           _p(out), W, _p(l), _stream())
+    N.call("clipk_attention_prefix_fwd", DT[qkv.dtype], G, P, R, tiles.numel() // 2, _p(tiles), _p(row_first),
+           heads, _p(qkv), 3 * W, _p(out), W, _p(l), _stream())
     return (out, l) if lse else out
 
 
-def attention_prefix_bwd(qkv, o, dout, lse, G, C, P, R, seg, max_q, heads, grad_dtype):
+def attention_prefix_bwd(qkv, o, dout, lse, G, P, R, tiles, row_first, heads, grad_dtype):
     W = heads * 64
+    nt = tiles.numel() // 2
     dqkv = torch.zeros(G * R, 3 * W, device=qkv.device, dtype=grad_dtype)
-    nb = N.load().clipk_attention_prefix_ws_bytes(G, C, heads)
+    nb = N.load().clipk_attention_prefix_ws_bytes(G, nt, heads)
     ws = torch.empty(nb, dtype=torch.uint8, device=qkv.device)
-    N.call("clipk_attention_prefix_bwd", DT[qkv.dtype], DT[grad_dtype], G, C, P, R, _p(seg), max_q, heads,
-           _p(qkv), 3 * W, _p(o), W, _p(dout), W, _p(lse), _p(dqkv), 3 * W, _p(ws), nb, _stream())
+    N.call("clipk_attention_prefix_bwd", DT[qkv.dtype], DT[grad_dtype], G, P, R, nt, _p(tiles), _p(row_first),
+           heads, _p(qkv), 3 * W, _p(o), W, _p(dout), W, _p(lse), _p(dqkv), 3 * W, _p(ws), nb, _stream())
     return dqkv
 
 

@@ -22,15 +22,36 @@ class TextShape:
 
     plain : nseq sequences of L rows (row s*L + t), eot_rows[s] = s*L + EOT_s.
     packed: G groups of R rows sharing a P-row causal prefix (see shared_prefix_tables);
-            seg [C,2] int32 (first row, q_len) per class, eot_rows[g*C + c] absolute."""
+            tiles [ntiles,2] int32 (first row, rows) of the <=16-row attention tiles,
+            row_first [R] int32, eot_rows[g*C + c] absolute."""
 
-    def __init__(self, eot_rows, nseq=0, L=0, G=0, C=0, P=0, R=0, seg=None, max_q=0):
+    def __init__(self, eot_rows, nseq=0, L=0, G=0, C=0, P=0, R=0, tiles=None, row_first=None):
         self.eot_rows = eot_rows
-        self.packed = seg is not None
+        self.packed = tiles is not None
         self.nseq, self.L = nseq, L
-        self.G, self.C, self.P, self.R, self.seg, self.max_q = G, C, P, R, seg, max_q
+        self.G, self.C, self.P, self.R = G, C, P, R
+        self.tiles, self.row_first = tiles, row_first
+        self.ntiles = 0 if tiles is None else tiles.numel() // 2
         self.rows = G * R if self.packed else nseq * L
         self.nout = G * C if self.packed else nseq
+
+
+def attention_tiles(off, qlen, R, max_rows=16):
+    """Attention work tiles of the packed layout: consecutive whole classes packed greedily
+    into windows of <= max_rows rows (so one 16-row MFMA tile carries ~16/q_len classes).
+    Returns (tiles [ntiles, 2] int32 = (first row, rows), row_first [R] int32 = first row of
+    each row's class; 0 for the prefix rows)."""
+    tiles, t0, rows = [], int(off[0]), 0
+    for c in range(len(qlen)):
+        if rows + int(qlen[c]) > max_rows:
+            tiles.append((t0, rows))
+            t0, rows = int(off[c]), 0
+        rows += int(qlen[c])
+    tiles.append((t0, rows))
+    row_first = np.zeros(R, np.int32)
+    for c in range(len(qlen)):
+        row_first[off[c]:off[c] + qlen[c]] = off[c]
+    return np.asarray(tiles, np.int32), row_first
 
 
 def shared_prefix_tables(src_map, ctx_pos, eot, n_ctx, csc, max_prefix=16, max_q=16):
@@ -68,7 +89,9 @@ def shared_prefix_tables(src_map, ctx_pos, eot, n_ctx, csc, max_prefix=16, max_q
             slot_rows.extend(int(off[c] + ctx_pos[c, k] - P) for c in range(C))
         slot_ptr.append(len(slot_rows))
     seg = np.stack([off, qlen], 1).astype(np.int32)
+    tiles, row_first = attention_tiles(off, qlen, R, max_q)
     return {"P": P, "R": R, "seg": seg, "row_tab": row_tab, "max_q": int(qlen.max()),
+            "tiles": np.asarray(tiles, np.int32), "row_first": row_first,
             "slot_ptr": np.asarray(slot_ptr, np.int32), "slot_rows": np.asarray(slot_rows, np.int32),
             "eot_in_group": (off + qlen - 1).astype(np.int64)}
 
@@ -91,7 +114,8 @@ class PromptLayout:
         if pk is not None:
             self.pack = pk
             self.P, self.R = pk["P"], pk["R"]
-            self.seg = torch.from_numpy(pk["seg"].reshape(-1).copy()).to(dev)
+            self.tiles = torch.from_numpy(pk["tiles"].reshape(-1).copy()).to(dev)
+            self.row_first = torch.from_numpy(pk["row_first"]).to(dev)
             self.row_tab = torch.from_numpy(pk["row_tab"]).to(dev)
             self.slot_ptr = torch.from_numpy(pk["slot_ptr"]).to(dev)
             self.slot_rows = torch.from_numpy(pk["slot_rows"]).to(dev)
@@ -117,7 +141,7 @@ class PromptLayout:
         if B not in self._shapes:
             if self.pack is not None:
                 self._shapes[B] = TextShape(self.eot_rows(B), G=B, C=self.n_cls, P=self.P, R=self.R,
-                                            seg=self.seg, max_q=self.pack["max_q"])
+                                            tiles=self.tiles, row_first=self.row_first)
             else:
                 self._shapes[B] = TextShape(self.eot_rows(B), nseq=B * self.n_cls, L=self.L)
         return self._shapes[B]

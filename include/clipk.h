@@ -101,21 +101,24 @@ int clipk_attention_bwd(int dtype, int grad_dtype, int nseq, int L, int heads, i
                         int lddo, const float* lse, void* dqkv, int lddqkv, void* stream);
 
 /* Shared-prefix packed attention (text, causal). Rows of group g (stride R) hold the P
- * prefix rows shared by all C sequences of the group, then each sequence's own rows:
- * seg[2c], seg[2c+1] = (group-relative first row, q_len) of sequence c. Sequence c's
- * queries see all P prefix keys plus its own keys causally; the prefix rows attend among
- * themselves causally. 1 <= P <= 16, 1 <= q_len <= max_q <= 16. Exact restatement of the
- * causal attention of the unpacked [C, L] prompts (attention_prefix.hip). */
-int clipk_attention_prefix_fwd(int dtype, int G, int C, int P, int R, const int* seg, int max_q,
-                               int heads, const void* qkv, int ldqkv, void* out, int ldo, float* lse,
-                               void* stream);
-/* Backward; ws >= clipk_attention_prefix_ws_bytes(G, C, heads) holds the per-chunk fp32
+ * prefix rows shared by all sequences of the group, then each sequence's own rows. The
+ * class rows are covered in order by ntiles tiles of <= 16 rows holding whole sequences:
+ * tiles[2t], tiles[2t+1] = (group-relative first row, rows); row_first[r] (r < R) = first
+ * row of the sequence that row r belongs to (0 for prefix rows). A class row attends to all
+ * P prefix keys plus the rows of its own sequence causally; the prefix rows attend among
+ * themselves causally. 1 <= P <= 16. Exact restatement of the causal attention of the
+ * unpacked [C, L] prompts (attention_prefix.hip). */
+int clipk_attention_prefix_fwd(int dtype, int G, int P, int R, int ntiles, const int* tiles,
+                               const int* row_first, int heads, const void* qkv, int ldqkv, void* out,
+                               int ldo, float* lse, void* stream);
+/* Backward; ws >= clipk_attention_prefix_ws_bytes(G, ntiles, heads) holds the per-chunk fp32
  * partial dK/dV of the prefix rows (reduced in a fixed order). */
-size_t clipk_attention_prefix_ws_bytes(int G, int C, int heads);
-int clipk_attention_prefix_bwd(int dtype, int grad_dtype, int G, int C, int P, int R, const int* seg,
-                               int max_q, int heads, const void* qkv, int ldqkv, const void* ofwd,
-                               int ldof, const void* dout, int lddo, const float* lse, void* dqkv,
-                               int lddqkv, void* ws, size_t ws_bytes, void* stream);
+size_t clipk_attention_prefix_ws_bytes(int G, int ntiles, int heads);
+int clipk_attention_prefix_bwd(int dtype, int grad_dtype, int G, int P, int R, int ntiles,
+                               const int* tiles, const int* row_first, int heads, const void* qkv,
+                               int ldqkv, const void* ofwd, int ldof, const void* dout, int lddo,
+                               const float* lse, void* dqkv, int lddqkv, void* ws, size_t ws_bytes,
+                               void* stream);
 
 /* Patch extraction: img fp32 [B,3,R,R] -> out [B*G*G, Kp] (out_dtype), K index c*p*p+ky*p+kx,
  * zero padded to Kp >= 3*p*p. */
@@ -218,13 +221,15 @@ int clipk_text_backward(const clipk_encoder* enc, int nseq, int L, const int* eo
  * never influence the EOT features. */
 size_t clipk_text_packed_saved_bytes(const clipk_encoder* enc, int G, int C, int R);
 size_t clipk_text_packed_ws_bytes(const clipk_encoder* enc, int G, int C, int R);
-size_t clipk_text_packed_bwd_ws_bytes(const clipk_encoder* enc, int G, int C, int R);
-int clipk_text_forward_packed(const clipk_encoder* enc, int G, int C, int P, int R, const int* seg,
-                              int max_q, const float* x0, const int* eot_rows, float* txt, void* saved,
-                              size_t saved_bytes, void* ws, size_t ws_bytes, void* stream);
-int clipk_text_backward_packed(const clipk_encoder* enc, int G, int C, int P, int R, const int* seg,
-                               int max_q, const int* eot_rows, const float* dtxt, const void* saved,
-                               size_t saved_bytes, float* dx0, void* ws, size_t ws_bytes, void* stream);
+size_t clipk_text_packed_bwd_ws_bytes(const clipk_encoder* enc, int G, int C, int R, int ntiles);
+int clipk_text_forward_packed(const clipk_encoder* enc, int G, int C, int P, int R, int ntiles,
+                              const int* tiles, const int* row_first, const float* x0,
+                              const int* eot_rows, float* txt, void* saved, size_t saved_bytes,
+                              void* ws, size_t ws_bytes, void* stream);
+int clipk_text_backward_packed(const clipk_encoder* enc, int G, int C, int P, int R, int ntiles,
+                               const int* tiles, const int* row_first, const int* eot_rows,
+                               const float* dtxt, const void* saved, size_t saved_bytes, float* dx0,
+                               void* ws, size_t ws_bytes, void* stream);
 
 /* Vision transformer forward (frozen, no grad): img fp32 [B,3,R,R] -> feat fp32 [B,E].
  * Head table for a vision encoder: ln_pre_w, ln_pre_b, ln_post_w, ln_post_b (f32),

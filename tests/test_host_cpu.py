@@ -199,6 +199,16 @@ def test_shared_prefix_tables_reconstruct_prompts(position, n_ctx, P_expect):
         rows = sorted(pk["slot_rows"][pk["slot_ptr"][k]:pk["slot_ptr"][k + 1]].tolist())
         expect = sorted(r for r in range(R) if src.flat[row_tab[r]] == -1 - k)
         assert rows == expect
+    # attention tiles: cover the class rows in order, <= 16 rows, whole classes only
+    tiles, rf = pk["tiles"], pk["row_first"]
+    starts = {int(o) for o, _ in seg}
+    assert tiles[0][0] == P and sum(int(n) for _, n in tiles) == R - P
+    for (t0, n), nxt in zip(tiles, list(tiles[1:]) + [(R, 0)]):
+        assert 1 <= n <= 16 and t0 + n == nxt[0] and t0 in starts and (t0 + n == R or t0 + n in starts)
+    for c in range(C):
+        off, qn = seg[c]
+        assert (rf[off:off + qn] == off).all()
+    assert (rf[:P] == 0).all()
     # CSC contexts and over-long class suffixes fall back to the plain layout
     assert shared_prefix_tables(src, cpos, eot, n_ctx, csc=True) is None
     assert shared_prefix_tables(src, cpos, [e + 20 for e in eot], n_ctx, csc=False) is None

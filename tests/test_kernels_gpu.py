@@ -227,14 +227,16 @@ def test_gemm_large_m_every_config(dev, cfg, Nn, K):
 
 
 def prefix_case(G, C, P, H, max_q, seed):
-    """Random shared-prefix packing: per-class q_len in [1, max_q], group stride R."""
+    """Random shared-prefix packing: per-class q_len in [1, max_q], group stride R, and the
+    host-side attention tiles (whole classes packed into <= 16-row windows)."""
+    from fsp_amd.trainers.prompt_base import attention_tiles
     g = torch.Generator().manual_seed(seed)
     qlen = torch.randint(1, max_q + 1, (C,), generator=g)
     qlen[0] = max_q
     off = P + torch.cat([torch.zeros(1, dtype=torch.long), qlen.cumsum(0)[:-1]])
     R = int(P + qlen.sum())
-    seg = torch.stack([off, qlen], 1).to(torch.int32).reshape(-1)
-    return R, seg, off.tolist(), qlen.tolist(), g
+    tiles, row_first = attention_tiles(off.numpy(), qlen.numpy(), R)
+    return R, torch.from_numpy(tiles.reshape(-1).copy()), torch.from_numpy(row_first), off.tolist(), qlen.tolist(), g
 
 
 def attn_prefix_ref(qkv, G, C, P, R, off, qlen, H):
@@ -262,20 +264,21 @@ def attn_prefix_ref(qkv, G, C, P, R, off, qlen, H):
 
 @pytest.mark.parametrize("dtype,gdtype", [(torch.float16, torch.bfloat16), (torch.bfloat16, torch.bfloat16),
                                           (torch.float32, torch.float32)])
-@pytest.mark.parametrize("G,C,P,H,max_q", [(2, 37, 5, 8, 6), (1, 19, 16, 2, 7), (3, 16, 2, 4, 16), (2, 3, 9, 2, 1)])
+@pytest.mark.parametrize("G,C,P,H,max_q", [(2, 37, 5, 8, 6), (1, 19, 16, 2, 7), (3, 16, 2, 4, 16), (2, 3, 9, 2, 1),
+                                           (2, 53, 5, 2, 3), (1, 40, 3, 2, 9)])
 def test_attention_prefix_fwd_bwd(dev, dtype, gdtype, G, C, P, H, max_q):
-    R, seg, off, qlen, g = prefix_case(G, C, P, H, max_q, seed=G * 100 + C + P)
+    R, tiles, row_first, off, qlen, g = prefix_case(G, C, P, H, max_q, seed=G * 100 + C + P)
     W = H * 64
     qkv = torch.randn(G * R, 3 * W, generator=g).to(dev).to(dtype)
-    seg = seg.to(dev)
-    o, lse = ops.attention_prefix(qkv, G, C, P, R, seg, max_q, H, lse=True)
+    tiles, row_first = tiles.to(dev), row_first.to(dev)
+    o, lse = ops.attention_prefix(qkv, G, P, R, tiles, row_first, H, lse=True)
     q32 = qkv.float().requires_grad_(True)
     ro, rl = attn_prefix_ref(q32, G, C, P, R, off, qlen, H)
     close(o, ro, dtype, "prefix attn out")
     close(lse, rl, torch.float16 if dtype != torch.float32 else dtype, "prefix attn lse")
     dout = torch.randn(G * R, W, generator=g).to(dev).to(gdtype)
     (ro * dout.float()).sum().backward()
-    dq = ops.attention_prefix_bwd(qkv, o, dout, lse, G, C, P, R, seg, max_q, H, gdtype)
+    dq = ops.attention_prefix_bwd(qkv, o, dout, lse, G, P, R, tiles, row_first, H, gdtype)
     ref = q32.grad
     for part, sl in (("dq", slice(0, W)), ("dk", slice(W, 2 * W)), ("dv", slice(2 * W, 3 * W))):
         close(dq[:, sl], ref[:, sl], gdtype if dtype != torch.float32 else dtype, f"prefix attn {part}")

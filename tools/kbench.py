@@ -117,18 +117,21 @@ def prefix_attn(dev):
     qlen[:100] = 5
     off = P + torch.cat([torch.zeros(1, dtype=torch.long), qlen.cumsum(0)[:-1]])
     R = int(P + qlen.sum())
-    seg = torch.stack([off, qlen], 1).to(torch.int32).reshape(-1).to(dev)
+    from fsp_amd.trainers.prompt_base import attention_tiles
+    tl, rf = attention_tiles(off.numpy(), qlen.numpy(), R)
+    tiles = torch.from_numpy(tl.reshape(-1).copy()).to(dev)
+    row_first = torch.from_numpy(rf).to(dev)
     qkv = (torch.randn(G * R, 3 * W, device=dev) * 0.5).to(torch.float16)
-    o, lse = ops.attention_prefix(qkv, G, C, P, R, seg, 6, H, lse=True)
-    ms = timeit(lambda: ops.attention_prefix(qkv, G, C, P, R, seg, 6, H, lse=True))
+    o, lse = ops.attention_prefix(qkv, G, P, R, tiles, row_first, H, lse=True)
+    ms = timeit(lambda: ops.attention_prefix(qkv, G, P, R, tiles, row_first, H, lse=True))
     print(f"prefix attn fwd rows={G*R}  {ms*1e3:8.1f} us  {(qkv.numel()*2 + o.numel()*2)/ms/1e6:7.1f} GB/s")
     dout = (torch.randn(G * R, W, device=dev) * 0.5).to(torch.bfloat16)
     dq = torch.empty(G * R, 3 * W, device=dev, dtype=torch.bfloat16)
-    nb = N.load().clipk_attention_prefix_ws_bytes(G, C, H)
+    nb = N.load().clipk_attention_prefix_ws_bytes(G, tiles.numel() // 2, H)
     ws = torch.empty(nb, dtype=torch.uint8, device=dev)
     p = lambda t: ctypes.c_void_p(t.data_ptr())
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    fn = lambda: N.call("clipk_attention_prefix_bwd", N.F16, N.BF16, G, C, P, R, p(seg), 6, H, p(qkv), 3 * W,
+    fn = lambda: N.call("clipk_attention_prefix_bwd", N.F16, N.BF16, G, P, R, tiles.numel() // 2, p(tiles), p(row_first), H, p(qkv), 3 * W,
                         p(o), W, p(dout), W, p(lse), p(dq), 3 * W, p(ws), nb, st)
     ms = timeit(fn)
     print(f"prefix attn bwd rows={G*R}  {ms*1e3:8.1f} us  {(qkv.numel()*2*2 + dout.numel()*2)/ms/1e6:7.1f} GB/s")
