@@ -30,6 +30,7 @@ SIGNATURES = {
     "clipk_device_arch_ok": (_I, []),
     "clipk_gemm": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P, _I, _I, _P]),
     "clipk_gemm_set_config": (_I, [_I]),
+    "clipk_gemm_stamps": (_I, [_P, _S]),
     "clipk_layernorm_fwd": (_I, [_I, _I, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P]),
     "clipk_layernorm_bwd": (_I, [_I, _I, _I, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P]),
     "clipk_attention_fwd": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P]),

@@ -19,6 +19,7 @@
 //  * XCD-aware bijective block remap: consecutive tiles of one A row-panel run on one XCD
 //    so the panel is fetched from HBM once and re-read from that XCD's L2.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -36,7 +37,9 @@ struct GemmArgs {
   const float* bias; const float* res; int ldr;
   void* out; int ldo; void* out2;
   const void* aux; int ldaux;
+  unsigned long long* stamp;  // diagnostic (CLIPK_GEMM_STAMP): per block/tile s_memrealtime marks
 };
+constexpr int STAMP_TILES = 8, STAMP_BLOCKS = 2048;
 
 template <typename T>
 __device__ __forceinline__ f32x4 mma(u32x4 a, u32x4 b, f32x4 c) {
@@ -63,30 +66,48 @@ __device__ __forceinline__ void glds16(const char* src, char* lds_wave_base) {
       (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-// Raw register type of one lane's 4 epilogue operand values (residual f32, aux TX).
-template <int EPI, typename TX> struct ExtRaw { typedef f32x4 type; };
-template <> struct ExtRaw<CLIPK_EPI_DQGELU, f16> { typedef uint2 type; };
-template <> struct ExtRaw<CLIPK_EPI_DQGELU, bf16> { typedef uint2 type; };
+// Raw bytes of one lane's epilogue operand run (residual f32 / aux TX, CW columns), kept
+// unconverted until use: a conversion right after the load would wait for it.
+template <int NB> struct Raw;
+template <> struct Raw<8> { uint2 v; };
+template <> struct Raw<16> { uint4 v; };
+template <> struct Raw<32> { uint4 v[2]; };
 
-__device__ __forceinline__ f32x4 ext_f32(f32x4 v) { return v; }
-template <typename TX> __device__ __forceinline__ f32x4 ext_f32(f32x4 v) { return v; }
-template <typename TX> __device__ __forceinline__ f32x4 ext_f32(uint2 v) {
-  float o[4];
-  load4<TX>(reinterpret_cast<const TX*>(&v), o);
-  return (f32x4){o[0], o[1], o[2], o[3]};
+template <int NB> __device__ __forceinline__ void ld_raw(const void* p, Raw<NB>& r) {
+  if constexpr (NB == 8) r.v = *reinterpret_cast<const uint2*>(p);
+  else if constexpr (NB == 16) r.v = *reinterpret_cast<const uint4*>(p);
+  else { r.v[0] = reinterpret_cast<const uint4*>(p)[0]; r.v[1] = reinterpret_cast<const uint4*>(p)[1]; }
+}
+template <typename TX, int CW, int NB>
+__device__ __forceinline__ void raw_f32(const Raw<NB>& r, float* o) {
+  static_assert(CW * (int)sizeof(TX) == NB, "raw run size");
+  const TX* e = reinterpret_cast<const TX*>(&r);
+#pragma unroll
+  for (int c = 0; c < CW; ++c) o[c] = to_f32(e[c]);
+}
+// CW (4 or 8) consecutive fp32 values -> TO in memory (one 8/16-B store).
+template <typename TO, int CW>
+__device__ __forceinline__ void store_run(TO* p, const float* v) {
+  if constexpr (CW == 8) store16_f32<TO>(p, v);
+  else store4<TO>(p, v[0], v[1], v[2], v[3]);
 }
 
 // Block tile BM x BN, WM x WN waves (each (BM/WM) x (BN/WN) = TM x TN 16x16 sub-tiles),
 // 2-stage LDS ring, one barrier per 128-byte K step. PERSIST: the grid is sized to the
 // CU count and each block walks an XCD-contiguous run of tiles; the last K step of a tile
 // prefetches the first stage of the next tile, so that load overlaps the epilogue.
-template <typename T, typename TO, typename TX, int EPI, int BM, int BN, int WM, int WN, bool PERSIST>
+template <typename T, typename TO, typename TX, int EPI, int BM, int BN, int WM, int WN, bool PERSIST,
+          int ROWB = GEMM_ROWB>
 __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
-  constexpr int OPA = BM * GEMM_ROWB, OPB = BN * GEMM_ROWB, STAGE = OPA + OPB;
-  constexpr int IA = BM / 8 / NW, IB = BN / 8 / NW;  // glds (8 rows x 128 B) per wave per stage
-  static_assert(IA >= 1 && IB >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile/wave mismatch");
+  constexpr int OPA = BM * ROWB, OPB = BN * ROWB, STAGE = OPA + OPB;
+  constexpr int RPI = 1024 / ROWB;   // rows per glds wave-instruction (64 lanes x 16 B)
+  constexpr int CPR = ROWB / 16;     // 16-B chunks per staged row
+  constexpr int KK = ROWB / 64;      // 64-B MFMA k-windows per K step
+  constexpr int IA = BM / RPI / NW, IB = BN / RPI / NW;  // glds per wave per stage
+  static_assert(ROWB == 128 || (ROWB == 64 && sizeof(T) == 2), "staged row is 128 B (or 64 B for 16-bit)");
+  static_assert(IA >= 1 && IB >= 1 && BM % (RPI * NW) == 0 && BN % (RPI * NW) == 0, "tile/wave mismatch");
   __shared__ CLIPK_LDS_ALIGN char smem[2 * STAGE + NW * EPI_SCRATCH];  // one array (see header)
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -105,39 +126,43 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
   if (tile >= t_end) return;  // block-uniform
 
   const size_t esz = sizeof(T);
-  const int nk = (int)((size_t)g.K * esz / GEMM_ROWB);
+  const int nk = (int)((size_t)g.K * esz / ROWB);
+  // source-side swizzle of 16-B chunk c in row r: 128-B rows c ^ ((r >> 1) & 7), 64-B rows
+  // c ^ ((r >> 2) & 3) -- either way 16 consecutive rows read at one chunk hit 16 distinct
+  // 16-B slots of the 256-B bank row
+  auto swz = [](int r) { return ROWB == 128 ? (r >> 1) & 7 : (r >> 2) & 3; };
   const char* srcA[IA];
   const char* srcB[IB];
   auto set_tile = [&](int t) {
     const int tm0 = (t / ntn) * BM, tn0 = (t % ntn) * BN;
 #pragma unroll
     for (int i = 0; i < IA; ++i) {
-      const int row = (w * IA + i) * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ ((row >> 1) & 7);  // source-side swizzle
+      const int row = (w * IA + i) * RPI + lane / CPR;
+      const int c = (lane % CPR) ^ swz(row);  // source-side swizzle
       int ga = tm0 + row;
       ga = ga < g.M ? ga : g.M - 1;
       srcA[i] = g.A + ((size_t)ga * g.lda) * esz + c * 16;
     }
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
-      const int row = (w * IB + i) * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      const int row = (w * IB + i) * RPI + lane / CPR;
+      const int c = (lane % CPR) ^ swz(row);
       srcB[i] = g.B + ((size_t)(tn0 + row) * g.ldb) * esz + c * 16;
     }
   };
   auto stage = [&](int s, int kt) {
     char* base = smem + s * STAGE;
-    const size_t koff = (size_t)kt * GEMM_ROWB;
+    const size_t koff = (size_t)kt * ROWB;
 #pragma unroll
-    for (int i = 0; i < IA; ++i) glds16(srcA[i] + koff, base + (w * IA + i) * 8 * GEMM_ROWB);
+    for (int i = 0; i < IA; ++i) glds16(srcA[i] + koff, base + (w * IA + i) * 1024);
 #pragma unroll
-    for (int i = 0; i < IB; ++i) glds16(srcB[i] + koff, base + OPA + (w * IB + i) * 8 * GEMM_ROWB);
+    for (int i = 0; i < IB; ++i) glds16(srcB[i] + koff, base + OPA + (w * IB + i) * 1024);
   };
 
   const int wm = w / WN, wn = w % WN;
   const int fr = lane & 15;         // fragment row within a 16-row sub-tile
   const int fq = lane >> 4;         // 16-B chunk within a 64-B k-window
-  const int sw = (fr >> 1) & 7;     // row swizzle (sub-tile row base is a multiple of 16)
+  const int sw = swz(fr);           // row swizzle (sub-tile row base is a multiple of 16)
   constexpr bool HAS_BIAS = EPI == CLIPK_EPI_BIAS || EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_BIAS_QGELU;
   constexpr bool HAS_EXT = EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU;
 
@@ -146,6 +171,10 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   int it = 0;  // global K-step counter (LDS buffer = it & 1)
+  int ti = 0;  // tiles done by this block (diagnostic stamps)
+  unsigned long long* stp = (g.stamp && threadIdx.x == 0 && bid < STAMP_BLOCKS)
+                                ? g.stamp + (size_t)bid * (STAMP_TILES * 3 + 4) : nullptr;
+  if (stp) { stp[0] = __builtin_amdgcn_s_memtime(); stp[1] = __builtin_amdgcn_s_memrealtime(); }
 
   while (true) {
     const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
@@ -158,26 +187,32 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
       for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
     const int nbase = n0 + wn * (BN / WN);
-    const int er = lane >> 4, ec = lane & 15;  // read-back: row er of each 4-row step, chunk ec
-    const int ncol = nbase + 4 * ec;
-    // residual / aux operands of group i+1 are loaded while group i is transposed and
-    // stored (raw, converted at use: a conversion right after the load would wait for it)
-    typedef typename ExtRaw<EPI, TX>::type XR;
-    XR ext_nxt[4];
+    // read-back geometry: each lane owns CW consecutive columns of one row, so every store /
+    // residual / aux instruction moves 16 B per lane (8 columns of a 16-bit output, 4 of fp32)
+    // and covers RPQ rows x 64 columns
+    constexpr int CW = sizeof(TO) == 2 ? 8 : 4;
+    constexpr int LPR = 64 / CW, RPQ = 64 / LPR, NQ = 16 / RPQ;
+    const int er = lane / LPR, ec = lane % LPR;
+    const int ncol = nbase + CW * ec;
+    // residual / aux operands of group i+1 are loaded while group i is transposed and stored
+    constexpr int XNB = CW * (EPI == CLIPK_EPI_BIAS_RES ? 4 : (int)sizeof(TX));
+    typedef Raw<XNB> XR;
+    XR ext_nxt[NQ];
     auto load_ext = [&](int i, XR* dst) {
       if constexpr (HAS_EXT) {
         const int mg = m0 + wm * (BM / WM) + i * 16;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          int mc = mg + 4 * q + er;
+        for (int q = 0; q < NQ; ++q) {
+          int mc = mg + RPQ * q + er;
           mc = mc < g.M ? mc : g.M - 1;
           if constexpr (EPI == CLIPK_EPI_BIAS_RES)
-            dst[q] = *reinterpret_cast<const XR*>(g.res + (size_t)mc * g.ldr + ncol);
+            ld_raw<XNB>(g.res + (size_t)mc * g.ldr + ncol, dst[q]);
           else
-            dst[q] = *reinterpret_cast<const XR*>((const TX*)g.aux + (size_t)mc * g.ldaux + ncol);
+            ld_raw<XNB>((const TX*)g.aux + (size_t)mc * g.ldaux + ncol, dst[q]);
         }
       }
     };
+    if (stp && ti < STAMP_TILES) stp[2 + 3 * ti] = __builtin_amdgcn_s_memrealtime();
     // group 0's operands are loaded at the top of the last K step (its MFMAs hide them)
     for (int kt = 0; kt < nk; ++kt, ++it) {
       const int cur = it & 1;
@@ -189,16 +224,16 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
         stage(cur ^ 1, 0);  // next tile's first stage flies during this tile's epilogue
       }
       if (last) load_ext(0, ext_nxt);
-      const char* As = smem + cur * STAGE + (wm * (BM / WM) + fr) * GEMM_ROWB;
-      const char* Bs = smem + cur * STAGE + OPA + (wn * (BN / WN) + fr) * GEMM_ROWB;
+      const char* As = smem + cur * STAGE + (wm * (BM / WM) + fr) * ROWB;
+      const char* Bs = smem + cur * STAGE + OPA + (wn * (BN / WN) + fr) * ROWB;
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
+      for (int kk = 0; kk < KK; ++kk) {
         const int p = ((kk * 4 + fq) ^ sw) * 16;
         u32x4 a[TM], b[TN];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const u32x4*>(Bs + j * 16 * GEMM_ROWB + p);
+        for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const u32x4*>(Bs + j * 16 * ROWB + p);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const u32x4*>(As + i * 16 * GEMM_ROWB + p);
+        for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const u32x4*>(As + i * 16 * ROWB + p);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -215,16 +250,25 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
     // / aux access instruction covers 4 rows x full 64-column runs (128 B of f16, 256 B of
     // f32) instead of 16 rows x 32 B. 16-B chunk c of row r sits at chunk c ^ r (conflict-free
     // on both the write and the read-back side).
-    static_assert(TN == 4, "epilogue transpose assumes 64 columns per wave");
-    f32x4 bia = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (HAS_BIAS) bia = *reinterpret_cast<const f32x4*>(g.bias + ncol);
+    if (stp && ti < STAMP_TILES) stp[3 + 3 * ti] = __builtin_amdgcn_s_memrealtime();
+    static_assert(TN == 4, "epilogue assumes 64 columns per wave");
+    float bia[CW];
+#pragma unroll
+    for (int c = 0; c < CW; ++c) bia[c] = 0.f;
+    if constexpr (HAS_BIAS) {
+#pragma unroll
+      for (int c = 0; c < CW; c += 4) {
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(g.bias + ncol + c);
+        bia[c] = b4[0]; bia[c + 1] = b4[1]; bia[c + 2] = b4[2]; bia[c + 3] = b4[3];
+      }
+    }
     float* scr = reinterpret_cast<float*>(smem + 2 * STAGE + w * EPI_SCRATCH);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int mg = m0 + wm * (BM / WM) + i * 16;  // first row of this 16-row group
-      XR ext[4];
+      XR ext[NQ];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) ext[q] = ext_nxt[q];
+      for (int q = 0; q < NQ; ++q) ext[q] = ext_nxt[q];
       if (i + 1 < TM) load_ext(i + 1, ext_nxt);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous group's read-back done
 #pragma unroll
@@ -232,29 +276,51 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
         *reinterpret_cast<f32x4*>(scr + fr * 64 + (((4 * j + fq) ^ fr) << 2)) = acc[i][j];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private: no barrier needed
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int rr = 4 * q + er;
+      for (int q = 0; q < NQ; ++q) {
+        const int rr = RPQ * q + er;
         const int m = mg + rr;
-        f32x4 v = *reinterpret_cast<const f32x4*>(scr + rr * 64 + ((ec ^ rr) << 2));
+        float v[CW];
+#pragma unroll
+        for (int c = 0; c < CW / 4; ++c) {  // 16-B chunk (CW/4)*ec + c of row rr sits at chunk ^ rr
+          const f32x4 t = *reinterpret_cast<const f32x4*>(scr + rr * 64 + ((((CW / 4) * ec + c) ^ rr) << 2));
+          v[4 * c] = t[0]; v[4 * c + 1] = t[1]; v[4 * c + 2] = t[2]; v[4 * c + 3] = t[3];
+        }
         if (m >= g.M) continue;
-        if constexpr (HAS_BIAS) v += bia;
+        if constexpr (HAS_BIAS) {
+#pragma unroll
+          for (int c = 0; c < CW; ++c) v[c] += bia[c];
+        }
         if constexpr (EPI == CLIPK_EPI_BIAS_RES) {
-          *reinterpret_cast<f32x4*>((float*)g.out + (size_t)m * g.ldo + ncol) = v + ext_f32(ext[q]);
+          float r[CW];
+          raw_f32<float, CW>(ext[q], r);
+#pragma unroll
+          for (int c = 0; c < CW; ++c) v[c] += r[c];
+          store_run<TO, CW>((TO*)g.out + (size_t)m * g.ldo + ncol, v);
         } else if constexpr (EPI == CLIPK_EPI_BIAS_QGELU) {
-          if (g.out2) store4<TO>((TO*)g.out2 + (size_t)m * g.ldo + ncol, v[0], v[1], v[2], v[3]);
-          store4<TO>((TO*)g.out + (size_t)m * g.ldo + ncol, quick_gelu(v[0]), quick_gelu(v[1]),
-                     quick_gelu(v[2]), quick_gelu(v[3]));
+          if (g.out2) store_run<TO, CW>((TO*)g.out2 + (size_t)m * g.ldo + ncol, v);
+#pragma unroll
+          for (int c = 0; c < CW; ++c) v[c] = quick_gelu(v[c]);
+          store_run<TO, CW>((TO*)g.out + (size_t)m * g.ldo + ncol, v);
         } else if constexpr (EPI == CLIPK_EPI_DQGELU) {
-          const f32x4 hv = ext_f32<TX>(ext[q]);
-          store4<TO>((TO*)g.out + (size_t)m * g.ldo + ncol, v[0] * quick_gelu_grad(hv[0]),
-                     v[1] * quick_gelu_grad(hv[1]), v[2] * quick_gelu_grad(hv[2]),
-                     v[3] * quick_gelu_grad(hv[3]));
+          float h[CW];
+          raw_f32<TX, CW>(ext[q], h);
+#pragma unroll
+          for (int c = 0; c < CW; ++c) v[c] *= quick_gelu_grad(h[c]);
+          store_run<TO, CW>((TO*)g.out + (size_t)m * g.ldo + ncol, v);
         } else {
-          store4<TO>((TO*)g.out + (size_t)m * g.ldo + ncol, v[0], v[1], v[2], v[3]);
+          store_run<TO, CW>((TO*)g.out + (size_t)m * g.ldo + ncol, v);
         }
       }
     }
-    if (!has_next) break;
+    if (stp && ti < STAMP_TILES) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      stp[4 + 3 * ti] = __builtin_amdgcn_s_memrealtime();
+    }
+    ++ti;
+    if (!has_next) {
+      if (stp) { stp[2 + 3 * STAMP_TILES] = __builtin_amdgcn_s_memtime(); stp[3 + 3 * STAMP_TILES] = __builtin_amdgcn_s_memrealtime(); }
+      break;
+    }
     tile = next;
     // the K loop left `it` one past this tile's last step: buffer it & 1 holds the
     // next tile's prefetched first stage
@@ -265,7 +331,11 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
 
 // Tile configurations: 0 = 128x128 (4 waves, 64 KiB LDS, 2 blocks/CU),
 // 1 = 256x256 (8 waves, 128 KiB, persistent when the grid exceeds 2 waves of CUs),
-// 2 = 256x128 (8 waves, 96 KiB), 3 = 256x256 non-persistent (benchmark knob).
+// 2 = 256x128 (8 waves, 96 KiB), 3 = 256x256 non-persistent (benchmark knob),
+// 4 = 256x128 / 5 = 128x256: 4 waves of 128x64, 64-B staged rows (48 KiB + 16 KiB epilogue
+// scratch), two blocks per CU, persistent over 2 x CUs blocks (benchmark knobs: measured
+// 5-25 % slower than 1 on every text shape -- a 32-deep K step halves the MFMA work per
+// barrier, and co-resident blocks did not overlap their epilogues).
 static int g_force_cfg = -2;  // -2: unread, -1: auto
 static int pick_cfg(int M, int N, int esz) {
   if (g_force_cfg == -2) {
@@ -274,12 +344,25 @@ static int pick_cfg(int M, int N, int esz) {
   }
   if (esz == 4) return 0;  // fp32 parity path: one configuration
   if (g_force_cfg >= 0) {
-    if ((g_force_cfg == 1 || g_force_cfg == 3) && N % 256 == 0) return g_force_cfg;
-    if (g_force_cfg == 2) return 2;
+    if ((g_force_cfg == 1 || g_force_cfg == 3 || g_force_cfg == 5) && N % 256 == 0) return g_force_cfg;
+    if (g_force_cfg == 2 || g_force_cfg == 4) return g_force_cfg;
     return 0;
   }
   if (M >= 4096 && N % 256 == 0) return 1;  // measured best for every text GEMM shape
   return 0;
+}
+
+static unsigned long long* g_stamp = nullptr;
+static int g_stamp_on = -1;
+static unsigned long long* gemm_stamp_buf() {
+  if (g_stamp_on < 0) g_stamp_on = getenv("CLIPK_GEMM_STAMP") ? 1 : 0;
+  if (!g_stamp_on) return nullptr;
+  if (!g_stamp) {
+    const size_t bytes = (size_t)STAMP_BLOCKS * (STAMP_TILES * 3 + 4) * 8;
+    if (hipMalloc((void**)&g_stamp, bytes) != hipSuccess) { g_stamp_on = 0; return nullptr; }
+    (void)hipMemset(g_stamp, 0, bytes);
+  }
+  return g_stamp;
 }
 
 static int g_num_cus = 0;
@@ -298,6 +381,7 @@ static int num_cus() {
 template <typename T, typename TO, typename TX, int EPI>
 static int launch_gemm(const GemmArgs& g, hipStream_t st) {
   const int cfg = pick_cfg(g.M, g.N, (int)sizeof(T));
+  const_cast<GemmArgs&>(g).stamp = gemm_stamp_buf();
   if constexpr (sizeof(T) == 4) {
     const int nwg = ((g.M + 127) / 128) * (g.N / 128);
     hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 128, 2, 2, false>), dim3(nwg), dim3(256), 0, st, g);
@@ -311,6 +395,23 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
         hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 256, 2, 4, true>), dim3(grid), dim3(512), 0, st, g);
       } else {
         hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 256, 2, 4, false>), dim3(nwg), dim3(512), 0, st, g);
+      }
+    } else if (cfg == 4 || cfg == 5) {
+      constexpr int R = 64;
+      const int nwg = cfg == 4 ? ((g.M + 255) / 256) * (g.N / 128) : ((g.M + 127) / 128) * (g.N / 256);
+      const int slots = 2 * num_cus();
+      const bool pers = nwg > slots;
+      const int grid = pers ? (slots / 8) * 8 : nwg;
+      if (cfg == 4) {
+        if (pers)
+          hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 128, 2, 2, true, R>), dim3(grid), dim3(256), 0, st, g);
+        else
+          hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 128, 2, 2, false, R>), dim3(grid), dim3(256), 0, st, g);
+      } else {
+        if (pers)
+          hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 256, 1, 4, true, R>), dim3(grid), dim3(256), 0, st, g);
+        else
+          hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 256, 1, 4, false, R>), dim3(grid), dim3(256), 0, st, g);
       }
     } else if (cfg == 2) {
       const int nwg = ((g.M + 255) / 256) * (g.N / 128);
@@ -376,7 +477,7 @@ extern "C" int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, in
   if (epi == CLIPK_EPI_BIAS_RES && (!res || ldr < N || ldr % 4)) return CLIPK_EINVAL;
   if (epi == CLIPK_EPI_DQGELU && (!aux || ldaux < N || ldaux % 4)) return CLIPK_EINVAL;
   GemmArgs g{(const char*)A, (const char*)B, M, N, K, lda, ldb, bias, res, ldr, out, ldo, out2, aux,
-             ldaux};
+             ldaux, nullptr};
   hipStream_t st = (hipStream_t)stream;
   switch (in_dtype) {
     case CLIPK_F16: return dispatch_out<f16>(out_dtype, epi, aux_dtype, g, st);
@@ -386,9 +487,21 @@ extern "C" int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, in
   }
 }
 
+// Diagnostic: copy the per-block stamps of the last launch (CLIPK_GEMM_STAMP set) to host
+// [STAMP_BLOCKS][4 + 3 * STAMP_TILES] u64: memtime0, realtime0, then per tile
+// (k-loop start, k-loop end, epilogue end) s_memrealtime (100 MHz), then memtime / realtime
+// at the block's end (effective shader clock).
+extern "C" int clipk_gemm_stamps(void* host, size_t bytes) {
+  const size_t need = (size_t)STAMP_BLOCKS * (STAMP_TILES * 3 + 4) * 8;
+  if (!g_stamp || !host || bytes < need) return CLIPK_EINVAL;
+  if (hipDeviceSynchronize() != hipSuccess) return (int)hipGetLastError();
+  if (hipMemcpy(host, g_stamp, need, hipMemcpyDeviceToHost) != hipSuccess) return (int)hipGetLastError();
+  return CLIPK_OK;
+}
+
 // Benchmark knob: force a tile configuration (-1 = automatic choice).
 extern "C" int clipk_gemm_set_config(int cfg) {
-  if (cfg < -1 || cfg > 3) return CLIPK_EINVAL;
+  if (cfg < -1 || cfg > 5) return CLIPK_EINVAL;
   g_force_cfg = cfg;
   return CLIPK_OK;
 }

@@ -73,8 +73,13 @@ int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, int K,
                void* stream);
 
 /* Benchmark knob: force the 16-bit GEMM tile configuration (0: 128x128, 1: 256x256,
- * 2: 256x128; -1 = automatic by shape). Not needed for normal use. */
+ * 2: 256x128, 3: 256x256 non-persistent, 4: 256x128 / 5: 128x256 two blocks per CU;
+ * -1 = automatic by shape). Not needed for normal use. */
 int clipk_gemm_set_config(int cfg);
+
+/* Diagnostic: per-block / per-tile s_memrealtime marks of the last GEMM launch, recorded
+ * only when the process runs with CLIPK_GEMM_STAMP set (synchronises the device). */
+int clipk_gemm_stamps(void* host, size_t bytes);
 
 /* y = LN(x[row]) for rows r in [0,rows): x row = in_rows ? in_rows[r] : r.
  * out of out_dtype with row stride ldo; mean/rstd (optional, fp32 [rows]). width%64==0, <=1024 */

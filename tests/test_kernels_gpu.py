@@ -197,7 +197,7 @@ def test_meta_net_and_sgd(dev):
     close(p, pr.detach(), torch.float32, "sgd")
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("Nn,K", [(2048, 512), (512, 2048)])
 def test_gemm_large_m_every_config(dev, cfg, Nn, K):
     """Bench-scale M (persistent / ring paths engage when tiles > 2x CUs) vs torch fp32."""
@@ -217,6 +217,9 @@ def test_gemm_large_m_every_config(dev, cfg, Nn, K):
               torch.float16, f"cfg{cfg} res")
         gq, hq = ops.gemm(A, B, N.EPI_BIAS_QGELU, torch.float16, bias=bias, want_out2=True)
         close(hq, ref + bias, torch.float16, f"cfg{cfg} qgelu.h")
+        hr = ref + bias
+        close(gq, hr * torch.sigmoid(1.702 * hr), torch.float16, f"cfg{cfg} qgelu.g")
+        close(ops.gemm(A, B, N.EPI_BIAS, torch.bfloat16, bias=bias), ref + bias, torch.bfloat16, f"cfg{cfg} bias bf16")
         Ab, Bb = A.to(torch.bfloat16), B.to(torch.bfloat16)
         refb = Ab.float() @ Bb.float().t()
         s = torch.sigmoid(1.702 * aux.float())

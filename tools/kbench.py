@@ -160,3 +160,23 @@ if __name__ == "__main__":
         prefix_attn(dev)
     if "torch" in only:
         torch_gemms(dev)
+
+
+def ksweep(dev):
+    """plain f16 GEMM M x N=2048 at K = 512 .. 4096: splits per-tile fixed cost (prologue,
+    epilogue, tail) from the per-K-step main-loop cost."""
+    M = int(os.environ.get("KB_M", 47160))
+    for cfg in [int(c) for c in os.environ.get("KB_CFGS", "-1").split(",")]:
+        N.load().clipk_gemm_set_config(cfg)
+        for odt in (torch.float16, torch.float32):
+            for k in (512, 1024, 2048, 4096):
+                a = (torch.randn(M, k, device=dev) * 0.5).half()
+                b = (torch.randn(2048, k, device=dev) * 0.5).half()
+                ms = timeit(lambda: ops.gemm(a, b, N.EPI_NONE, odt))
+                mt = timeit(lambda: a @ b.t()) if odt == torch.float16 else float("nan")
+                print(f"ksweep cfg{cfg} out {str(odt)[6:]} N2048 K{k:<5d} ours {ms*1e3:8.1f} us "
+                      f"{2*M*2048*k/ms/1e9:7.1f} TF/s | torch {mt*1e3:8.1f} us {2*M*2048*k/mt/1e9:7.1f} TF/s")
+
+
+if __name__ == "__main__" and "ksweep" in os.environ.get("KB_ONLY", ""):
+    ksweep(torch.device("cuda"))
