@@ -335,7 +335,10 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
 // 4 = 256x128 / 5 = 128x256: 4 waves of 128x64, 64-B staged rows (48 KiB + 16 KiB epilogue
 // scratch), two blocks per CU, persistent over 2 x CUs blocks (benchmark knobs: measured
 // 5-25 % slower than 1 on every text shape -- a 32-deep K step halves the MFMA work per
-// barrier, and co-resident blocks did not overlap their epilogues).
+// barrier, and co-resident blocks did not overlap their epilogues),
+// 6 = 192x256 (8 waves of 96x64, 112 KiB + scratch): 4/3 more row tiles, chosen when it
+// fills the last wave of CUs better than 256-row tiles (N = 512 at 47k rows: 1.45 -> 1.92
+// waves).
 static int g_force_cfg = -2;  // -2: unread, -1: auto
 static int pick_cfg(int M, int N, int esz) {
   if (g_force_cfg == -2) {
@@ -344,11 +347,18 @@ static int pick_cfg(int M, int N, int esz) {
   }
   if (esz == 4) return 0;  // fp32 parity path: one configuration
   if (g_force_cfg >= 0) {
-    if ((g_force_cfg == 1 || g_force_cfg == 3 || g_force_cfg == 5) && N % 256 == 0) return g_force_cfg;
+    if ((g_force_cfg == 1 || g_force_cfg == 3 || g_force_cfg == 5 || g_force_cfg == 6) && N % 256 == 0)
+      return g_force_cfg;
     if (g_force_cfg == 2 || g_force_cfg == 4) return g_force_cfg;
     return 0;
   }
-  if (M >= 4096 && N % 256 == 0) return 1;  // measured best for every text GEMM shape
+  if (M >= 4096 && N % 256 == 0) {
+    // 256- vs 192-row tiles: fraction of the last round of CU slots each leaves busy
+    const double cus = 256.0;
+    const double w256 = ((M + 255) / 256) * (N / 256) / cus, w192 = ((M + 191) / 192) * (N / 256) / cus;
+    const double e256 = w256 / __builtin_ceil(w256), e192 = w192 / __builtin_ceil(w192);
+    return e192 > e256 + 0.05 ? 6 : 1;
+  }
   return 0;
 }
 
@@ -396,6 +406,13 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
       } else {
         hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 256, 2, 4, false>), dim3(nwg), dim3(512), 0, st, g);
       }
+    } else if (cfg == 6) {
+      const int nwg = ((g.M + 191) / 192) * (g.N / 256);
+      const int cus = num_cus();
+      if (nwg > 2 * cus)
+        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 192, 256, 2, 4, true>), dim3((cus / 8) * 8), dim3(512), 0, st, g);
+      else
+        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 192, 256, 2, 4, false>), dim3(nwg), dim3(512), 0, st, g);
     } else if (cfg == 4 || cfg == 5) {
       constexpr int R = 64;
       const int nwg = cfg == 4 ? ((g.M + 255) / 256) * (g.N / 128) : ((g.M + 127) / 128) * (g.N / 256);
@@ -501,7 +518,7 @@ extern "C" int clipk_gemm_stamps(void* host, size_t bytes) {
 
 // Benchmark knob: force a tile configuration (-1 = automatic choice).
 extern "C" int clipk_gemm_set_config(int cfg) {
-  if (cfg < -1 || cfg > 5) return CLIPK_EINVAL;
+  if (cfg < -1 || cfg > 6) return CLIPK_EINVAL;
   g_force_cfg = cfg;
   return CLIPK_OK;
 }

@@ -197,7 +197,7 @@ def test_meta_net_and_sgd(dev):
     close(p, pr.detach(), torch.float32, "sgd")
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("Nn,K", [(2048, 512), (512, 2048)])
 def test_gemm_large_m_every_config(dev, cfg, Nn, K):
     """Bench-scale M (persistent / ring paths engage when tiles > 2x CUs) vs torch fp32."""

@@ -41,9 +41,9 @@ def main():
         ("fc fwd    N2048 K512 QGELU+h", dict(a=rnd(M, W), b=rnd(4 * W, W), epi=N.EPI_BIAS_QGELU, out=f16, bias=True, out2=True)),
         ("proj fwd  N512  K2048 BIAS_RES", dict(a=rnd(M, 4 * W), b=rnd(W, 4 * W), epi=N.EPI_BIAS_RES, out=torch.float32, bias=True, res=True)),
         ("dgelu bwd N2048 K512 DQGELU", dict(a=rnd(M, W, dt=bf), b=rnd(4 * W, W, dt=bf), epi=N.EPI_DQGELU, out=bf, aux=rnd(M, 4 * W))),
-        ("fc bwd    N512  K2048 NONE f32", dict(a=rnd(M, 4 * W, dt=bf), b=rnd(W, 4 * W, dt=bf), epi=N.EPI_NONE, out=torch.float32)),
+        ("fc bwd    N512  K2048 NONE bf16", dict(a=rnd(M, 4 * W, dt=bf), b=rnd(W, 4 * W, dt=bf), epi=N.EPI_NONE, out=bf)),
         ("out bwd   N512  K512 NONE bf16", dict(a=rnd(M, W, dt=bf), b=rnd(W, W, dt=bf), epi=N.EPI_NONE, out=bf)),
-        ("qkv bwd   N512  K1536 NONE f32", dict(a=rnd(M, 3 * W, dt=bf), b=rnd(W, 3 * W, dt=bf), epi=N.EPI_NONE, out=torch.float32)),
+        ("qkv bwd   N512  K1536 NONE bf16", dict(a=rnd(M, 3 * W, dt=bf), b=rnd(W, 3 * W, dt=bf), epi=N.EPI_NONE, out=bf)),
         ("plain     N2048 K512 NONE f16", dict(a=rnd(M, W), b=rnd(4 * W, W), epi=N.EPI_NONE, out=f16)),
         ("bias      N2048 K512 BIAS f16", dict(a=rnd(M, W), b=rnd(4 * W, W), epi=N.EPI_BIAS, out=f16, bias=True)),
         ("qgelu     N2048 K512 QGELU f16", dict(a=rnd(M, W), b=rnd(4 * W, W), epi=N.EPI_BIAS_QGELU, out=f16, bias=True)),
