@@ -37,6 +37,23 @@ def flops(arch, n_cls, L):
     return f_img, f_txt, b_txt
 
 
+ROOF_KERNEL = "gemm_nt_kernelIDF16bDF16bDF16_Li3ELi256ELi256"  # EPI_DQGELU bf16 persistent 256x256
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc", "traffic.json")
+
+
+def pmc_traffic(kernel_key):
+    """HBM bytes per launch of the roofline kernel from the committed PMC passes of this
+    workload (tools/pmc_bench.sh: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of
+    bench.py; FETCH_SIZE doubled per the gfx950 note, MI355X_MICROARCH.md HBM). None if absent."""
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+    except OSError:
+        return None
+    hits = [v["hbm_bytes"] for k, v in d.items() if kernel_key in k]
+    return hits[0] if hits else None
+
+
 def cpu_baseline(arch_name, n_ctx_init, n_cls_full, sample_cls, threads):
     """Time the CPU oracle (fp32 restatement of the reference, 77-token prompts) on a
     bounded sample: 1 image x sample_cls classes, fwd + bwd; scale text cost to n_cls_full."""
@@ -157,8 +174,15 @@ def main():
             fl = work.value / cnt.value
             ach = fl / (avg_ms * 1e-3) / 1e12
             peak = PEAK[args.prec if args.prec != "fp16" else "bf16"]  # dgelu GEMM runs on bf16 operands
+            traffic = pmc_traffic(ROOF_KERNEL) if (args.arch, args.classes, args.batch, args.prec) == \
+                ("ViT-B/16", 1000, 8, "fp16") else None
             roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                    "frac": round(ach / peak, 4), "traffic": None,
+                    "frac": round(ach / peak, 4), "traffic": traffic,
+                    "traffic_note": "HBM bytes/launch, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (profiles/r01_pmc); "
+                                    "algorithmic bytes/launch %.3g" % (
+                                        2 * args.batch * (lay.rows_per_group if lay.pack is not None else args.classes * L)
+                                        * (arch.transformer_width + 4 * arch.transformer_width * 2)
+                                        + 2 * 4 * arch.transformer_width ** 2),
                     "kernel": "gemm_nt_kernel<bf16,bf16,f16,EPI_DQGELU> (text c_proj input-grad GEMM fused with "
                               "QuickGELU'(h), M=text rows, N=4W, K=W)",
                     "avg_launch_ms": round(avg_ms, 4), "launches": cnt.value,

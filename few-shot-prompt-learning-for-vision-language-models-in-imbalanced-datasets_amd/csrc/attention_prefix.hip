@@ -155,13 +155,13 @@ __global__ __launch_bounds__(256) void attn_prefix_fwd_mfma(int G, int P, int R,
     const s16x4 bp = pack4<T>(ep[0], ep[1], ep[2], ep[3]);
     const s16x4 bo = pack4<T>(eo[0], eo[1], eo[2], eo[3]);
     const float inv = 1.0f / ps;
-    T* orow = out + (gR + cur.t0 + r16) * ldo + h * 64 + 4 * g4;
+    f32x4 o[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      f32x4 o = mfma16_t<T>(tr_read(sVp, 4 * g4, 16 * t, lane), bp, (f32x4){0.f, 0.f, 0.f, 0.f});
-      o = mfma16_t<T>(tr_read(sVo, 4 * g4, 16 * t, lane), bo, o);
-      if (qok) store4<T>(orow + 16 * t, o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
+      o[t] = mfma16_t<T>(tr_read(sVp, 4 * g4, 16 * t, lane), bp, (f32x4){0.f, 0.f, 0.f, 0.f});
+      o[t] = mfma16_t<T>(tr_read(sVo, 4 * g4, 16 * t, lane), bo, o[t]);
     }
+    store_tile64<T>(out + (gR + cur.t0 + r16) * ldo + h * 64, o, inv, qok);
     if (lse && g4 == 0 && qok) lse[(gR + cur.t0 + r16) * H + h] = mx + __logf(ps);
   };
   // Batches of tiles: all their loads issued up front (unconditional, clamped), then the
@@ -324,29 +324,32 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int P, int R,
     const s16x4 bTp = pack_bf16x4(dS2p[0], dS2p[1], dS2p[2], dS2p[3]);  // B[k=j][n=i]
     const s16x4 bTo = pack_bf16x4(dS2o[0], dS2o[1], dS2o[2], dS2o[3]);
     lds_fence();
-    TG* orow = dqkv + (gR + cur.t0 + r16) * lddq + h * 64 + 4 * g4;
+    // one output (16 rows x 64) at a time, so only one 16-register tile is live for the
+    // widened store
+    TG* orow = dqkv + (gR + cur.t0 + r16) * lddq + h * 64;
+    f32x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      acc[t] = mfma16_bf16(tr_read(tKp, 4 * g4, 16 * t, lane), bTp, z);
+      acc[t] = mfma16_bf16(tr_read(tKo, 4 * g4, 16 * t, lane), bTo, acc[t]);
+    }
+    store_tile64<TG>(orow, acc, kScale, qok);  // dQ
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const s16x4 aQ = tr_read(tQ, 4 * g4, 16 * t, lane);
+      dkp[t] = mfma16_bf16(aQ, bSp, dkp[t]);
+      acc[t] = mfma16_bf16(aQ, bSo, z);
+      if (own_is_prefix) dkp[t] += acc[t];  // the prefix tile's keys are the prefix rows themselves
+    }
+    if (!own_is_prefix) store_tile64<TG>(orow + W, acc, kScale, qok);  // dK (wave-uniform branch)
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const s16x4 aD = tr_read(tD, 4 * g4, 16 * t, lane);
-      const s16x4 aQ = tr_read(tQ, 4 * g4, 16 * t, lane);
       dvp[t] = mfma16_bf16(aD, bPp, dvp[t]);
-      dkp[t] = mfma16_bf16(aQ, bSp, dkp[t]);
-      f32x4 dq = mfma16_bf16(tr_read(tKp, 4 * g4, 16 * t, lane), bTp, z);
-      dq = mfma16_bf16(tr_read(tKo, 4 * g4, 16 * t, lane), bTo, dq);
-      const f32x4 dvo = mfma16_bf16(aD, bPo, z);
-      const f32x4 dko = mfma16_bf16(aQ, bSo, z);
-      if (own_is_prefix) {  // the prefix tile's keys are the prefix rows themselves
-        dvp[t] += dvo;
-        dkp[t] += dko;
-      }
-      if (qok) {
-        store4<TG>(orow + 16 * t, dq[0] * kScale, dq[1] * kScale, dq[2] * kScale, dq[3] * kScale);
-        if (!own_is_prefix) {
-          store4<TG>(orow + W + 16 * t, dko[0] * kScale, dko[1] * kScale, dko[2] * kScale, dko[3] * kScale);
-          store4<TG>(orow + 2 * W + 16 * t, dvo[0], dvo[1], dvo[2], dvo[3]);
-        }
-      }
+      acc[t] = mfma16_bf16(aD, bPo, z);
+      if (own_is_prefix) dvp[t] += acc[t];
     }
+    if (!own_is_prefix) store_tile64<TG>(orow + 2 * W, acc, 1.0f, qok);  // dV
   };
   for (int u = u_begin; u < u_end; u += kBwdBatch) {
     TileRowsB rr[kBwdBatch];

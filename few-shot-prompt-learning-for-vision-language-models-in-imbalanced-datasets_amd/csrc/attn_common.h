@@ -97,4 +97,45 @@ __device__ __forceinline__ s16x4 pack4(float a, float b, float c, float d) {
   return __builtin_bit_cast(s16x4, v);
 }
 
+// Store a 16-row x 64-column (one head) tile held in the MFMA accumulator layout -- lane
+// (r16, g4) holds row r16, columns 16t + 4g4 .. +3 in o[t] -- as 16-bit values. The packed
+// values go through a lane/slot butterfly (v_permlane32_swap: lane bit 5 <-> slot bit 0, then
+// v_permlane16_swap: lane bit 4 <-> slot bit 0) that leaves lane g4 holding columns
+// 8g4 .. 8g4+7 and 32+8g4 .. +7, so a row leaves as two 16-B stores per lane (each store
+// instruction: 16 rows x 64 contiguous bytes) instead of four 8-B ones. Every lane of the
+// wave must execute it (the swaps cross lanes); `ok` masks only the stores.
+template <typename T>
+__device__ __forceinline__ void store_tile64(T* rowp, const f32x4 (&o)[4], float scale, bool ok) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  uint32_t d[4][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const u32x2 u = __builtin_bit_cast(u32x2, pack4<T>(o[t][0] * scale, o[t][1] * scale, o[t][2] * scale,
+                                                       o[t][3] * scale));
+    d[t][0] = u[0];
+    d[t][1] = u[1];
+  }
+#pragma unroll
+  for (int s = 0; s < 4; s += 2)
+#pragma unroll
+    for (int dw = 0; dw < 2; ++dw) {
+      const auto r = __builtin_amdgcn_permlane32_swap(d[s][dw], d[s + 1][dw], false, false);
+      d[s][dw] = r[0];
+      d[s + 1][dw] = r[1];
+    }
+#pragma unroll
+  for (int s = 0; s < 4; s += 2)
+#pragma unroll
+    for (int dw = 0; dw < 2; ++dw) {
+      const auto r = __builtin_amdgcn_permlane16_swap(d[s][dw], d[s + 1][dw], false, false);
+      d[s][dw] = r[0];
+      d[s + 1][dw] = r[1];
+    }
+  if (ok) {
+    const int g4 = (threadIdx.x & 63) >> 4;
+    *reinterpret_cast<u32x4*>(rowp + 8 * g4) = (u32x4){d[0][0], d[0][1], d[1][0], d[1][1]};
+    *reinterpret_cast<u32x4*>(rowp + 32 + 8 * g4) = (u32x4){d[2][0], d[2][1], d[3][0], d[3][1]};
+  }
+}
+
 }  // namespace clipk
