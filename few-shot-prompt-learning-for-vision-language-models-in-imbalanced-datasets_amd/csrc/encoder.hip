@@ -10,6 +10,7 @@
 #include <array>
 #include <cstring>
 #include <new>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -76,11 +77,25 @@ struct ProfScope {
     if (_rc != CLIPK_OK) return _rc; \
   } while (0)
 
+// sk / skb: split-K workspace (vision: small M); nullptr = one launch over the tile grid
 static int gemm(int in, int out, int epi, int M, int N, int K, const void* A, const void* B,
                 const float* bias, const float* res, void* o, void* o2, const void* aux, int auxdt,
-                hipStream_t st, int prof_cls) {
+                hipStream_t st, int prof_cls, void* sk = nullptr, size_t skb = 0) {
   ProfScope ps(prof_cls, st, 2.0 * M * N * K);
+  if (sk && epi != CLIPK_EPI_DQGELU)
+    return clipk_gemm_splitk(in, out, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, 0, sk, skb, st);
   return clipk_gemm(in, out, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, aux, auxdt, N, st);
+}
+
+// split-K workspace for the block GEMMs of a vision forward at `rows` rows (0 when none splits)
+static size_t vit_splitk_bytes(int act, int rows, int D) {
+  const int shapes[4][2] = {{3 * D, D}, {D, D}, {4 * D, D}, {D, 4 * D}};  // (N, K)
+  size_t best = 0;
+  for (const auto& nk : shapes) {
+    const size_t b = clipk_gemm_splitk_ws_bytes(rows, nk[0], clipk_gemm_auto_splits(act, rows, nk[0], nk[1]));
+    best = b > best ? b : best;
+  }
+  return best;
 }
 
 // ---------------------------------------------------------------- text layout
@@ -210,25 +225,25 @@ static int attn_bwd(const clipk_encoder* e, const SeqShape& sh, const void* qkv,
 static int block_fwd(const clipk_encoder* e, const std::array<const void*, 16>& w, const SeqShape& sh,
                      const float* X, float* Xm, float* Xo, void* xn, void* qkv, void* o,
                      float* lse, void* h, void* g, float* m1, float* r1, float* m2, float* r2,
-                     hipStream_t st, bool text) {
+                     hipStream_t st, bool text, void* sk = nullptr, size_t skb = 0) {
   const int pg = text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE;
   const int W = e->W, rows = sh.rows, act = e->act;
   TRY(clipk_layernorm_fwd(act, rows, W, X, W, nullptr, (const float*)w[0], (const float*)w[1], xn, W,
                           m1, r1, st));
   TRY(gemm(act, act, CLIPK_EPI_BIAS, rows, 3 * W, W, xn, w[2], (const float*)w[3], nullptr, qkv,
-           nullptr, nullptr, 0, st, pg));
+           nullptr, nullptr, 0, st, pg, sk, skb));
   {
     ProfScope ps(text ? CLIPK_PROF_ATTN : CLIPK_PROF_NONE, st, 0.0);
     TRY(attn_fwd(e, sh, qkv, o, lse, st));
   }
   TRY(gemm(act, CLIPK_F32, CLIPK_EPI_BIAS_RES, rows, W, W, o, w[4], (const float*)w[5], X, Xm,
-           nullptr, nullptr, 0, st, pg));
+           nullptr, nullptr, 0, st, pg, sk, skb));
   TRY(clipk_layernorm_fwd(act, rows, W, Xm, W, nullptr, (const float*)w[6], (const float*)w[7], xn, W,
                           m2, r2, st));
   TRY(gemm(act, act, CLIPK_EPI_BIAS_QGELU, rows, 4 * W, W, xn, w[8], (const float*)w[9], nullptr, g,
-           h, nullptr, 0, st, text ? CLIPK_PROF_GEMM_FC : CLIPK_PROF_NONE));
+           h, nullptr, 0, st, text ? CLIPK_PROF_GEMM_FC : CLIPK_PROF_NONE, sk, skb));
   TRY(gemm(act, CLIPK_F32, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo,
-           nullptr, nullptr, 0, st, pg));
+           nullptr, nullptr, 0, st, pg, sk, skb));
   return CLIPK_OK;
 }
 
@@ -463,7 +478,8 @@ namespace clipk {
 struct VitBufs {
   void *patches, *xn, *qkv, *o, *g, *cls;
   float *pout, *x0, *x1, *xm;
-  size_t bytes;
+  void* sk;  // split-K partials (small batches)
+  size_t sk_bytes, bytes;
 };
 static VitBufs vit_layout(const clipk_encoder* e, int B, void* ws) {
   VitBufs v;
@@ -480,6 +496,12 @@ static VitBufs vit_layout(const clipk_encoder* e, int B, void* ws) {
   v.o = c.take(rows * D * a);
   v.g = c.take(rows * 4 * D * a);
   v.cls = c.take((size_t)B * D * a);
+  // split-K for the small-M ViT GEMMs measured even with the 128x128 tile grid at B = 8
+  // (1.19 vs 1.15 ms per step: the slice GEMMs are short and the finish passes cost what
+  // the extra CUs gain), so the workspace is only carved when CLIPK_VIT_SPLITK is set
+  static const bool use_sk = getenv("CLIPK_VIT_SPLITK") != nullptr;
+  v.sk_bytes = use_sk ? vit_splitk_bytes(e->act, (int)rows, (int)D) : 0;
+  v.sk = v.sk_bytes ? c.take(v.sk_bytes) : nullptr;
   v.bytes = c.off;
   return v;
 }
@@ -501,14 +523,16 @@ extern "C" int clipk_vit_forward(const clipk_encoder* e, int B, const float* img
   // head: 0 ln_pre_w 1 ln_pre_b 2 ln_post_w 3 ln_post_b 4 projT[E,D] 5 conv_w[D,Kp] 6 cls 7 pos
   TRY(clipk_im2col(act, B, e->res, e->patch, e->Kp, img, v.patches, st));
   TRY(gemm(act, CLIPK_F32, CLIPK_EPI_NONE, np, D, e->Kp, v.patches, e->head[5], nullptr, nullptr,
-           v.pout, nullptr, nullptr, 0, st, CLIPK_PROF_NONE));
+           v.pout, nullptr, nullptr, 0, st, CLIPK_PROF_NONE,
+           clipk_gemm_splitk_ws_bytes(np, D, clipk_gemm_auto_splits(act, np, D, e->Kp)) <= v.sk_bytes ? v.sk : nullptr,
+           v.sk_bytes));
   TRY(clipk_vit_embed_ln(B, L, D, v.pout, (const float*)e->head[6], (const float*)e->head[7],
                          (const float*)e->head[0], (const float*)e->head[1], v.x0, st));
   float* cur = v.x0;
   float* nxt = v.x1;
   for (int l = 0; l < e->layers; ++l) {
     TRY(block_fwd(e, e->lw[l], SeqShape::plain(B, L, 0), cur, v.xm, nxt, v.xn, v.qkv, v.o, nullptr, nullptr, v.g,
-                  nullptr, nullptr, nullptr, nullptr, st, false));
+                  nullptr, nullptr, nullptr, nullptr, st, false, v.sk, v.sk_bytes));
     float* t = cur; cur = nxt; nxt = t;
   }
   // ln_post on the CLS rows (row stride L*D), then @ proj

@@ -38,6 +38,8 @@ struct GemmArgs {
   void* out; int ldo; void* out2;
   const void* aux; int ldaux;
   unsigned long long* stamp;  // diagnostic (CLIPK_GEMM_STAMP): per block/tile s_memrealtime marks
+  int ksplit;                 // split-K slices (non-persistent only); slice s writes out + s*split_stride
+  long long split_stride;     // elements of TO between slices' fp32 partial outputs
 };
 constexpr int STAMP_TILES = 8, STAMP_BLOCKS = 2048;
 
@@ -114,9 +116,12 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
 
   // ---- XCD-aware bijective tile split: XCD group x owns tiles [t_beg, t_end) (row-panel
   // major, so the tiles sharing an A panel run on one XCD and re-read it from its L2).
+  // Split-K (non-persistent only): units are slice-major, so neighbouring units are
+  // neighbouring tiles over the same K range (shared panels in L2).
   const int ntn = g.N / BN;
   const int ntm = (g.M + BM - 1) / BM;
-  const int nwg = ntm * ntn;
+  const int ntiles = ntm * ntn;
+  const int nwg = ntiles * (PERSIST ? 1 : g.ksplit);
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int t_beg = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
@@ -124,9 +129,14 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
   const int t_step = PERSIST ? (int)(gridDim.x >> 3) : 1;
   int tile = t_beg + (bid >> 3);
   if (tile >= t_end) return;  // block-uniform
+  const int ks = PERSIST ? 0 : tile / ntiles;
+  if (!PERSIST) tile -= ks * ntiles;
 
   const size_t esz = sizeof(T);
-  const int nk = (int)((size_t)g.K * esz / ROWB);
+  const int nk_all = (int)((size_t)g.K * esz / ROWB);
+  const int kt0 = PERSIST ? 0 : ks * nk_all / g.ksplit;
+  const int nk = PERSIST ? nk_all : (ks + 1) * nk_all / g.ksplit - kt0;
+  TO* const outb = (TO*)g.out + (PERSIST ? 0 : (size_t)ks * g.split_stride);
   // source-side swizzle of 16-B chunk c in row r: 128-B rows c ^ ((r >> 1) & 7), 64-B rows
   // c ^ ((r >> 2) & 3) -- either way 16 consecutive rows read at one chunk hit 16 distinct
   // 16-B slots of the 256-B bank row
@@ -141,13 +151,13 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
       const int c = (lane % CPR) ^ swz(row);  // source-side swizzle
       int ga = tm0 + row;
       ga = ga < g.M ? ga : g.M - 1;
-      srcA[i] = g.A + ((size_t)ga * g.lda) * esz + c * 16;
+      srcA[i] = g.A + ((size_t)ga * g.lda) * esz + c * 16 + (size_t)kt0 * ROWB;
     }
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
       const int row = (w * IB + i) * RPI + lane / CPR;
       const int c = (lane % CPR) ^ swz(row);
-      srcB[i] = g.B + ((size_t)(tn0 + row) * g.ldb) * esz + c * 16;
+      srcB[i] = g.B + ((size_t)(tn0 + row) * g.ldb) * esz + c * 16 + (size_t)kt0 * ROWB;
     }
   };
   auto stage = [&](int s, int kt) {
@@ -295,20 +305,20 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
           raw_f32<float, CW>(ext[q], r);
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] += r[c];
-          store_run<TO, CW>((TO*)g.out + (size_t)m * g.ldo + ncol, v);
+          store_run<TO, CW>(outb + (size_t)m * g.ldo + ncol, v);
         } else if constexpr (EPI == CLIPK_EPI_BIAS_QGELU) {
           if (g.out2) store_run<TO, CW>((TO*)g.out2 + (size_t)m * g.ldo + ncol, v);
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] = quick_gelu(v[c]);
-          store_run<TO, CW>((TO*)g.out + (size_t)m * g.ldo + ncol, v);
+          store_run<TO, CW>(outb + (size_t)m * g.ldo + ncol, v);
         } else if constexpr (EPI == CLIPK_EPI_DQGELU) {
           float h[CW];
           raw_f32<TX, CW>(ext[q], h);
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] *= quick_gelu_grad(h[c]);
-          store_run<TO, CW>((TO*)g.out + (size_t)m * g.ldo + ncol, v);
+          store_run<TO, CW>(outb + (size_t)m * g.ldo + ncol, v);
         } else {
-          store_run<TO, CW>((TO*)g.out + (size_t)m * g.ldo + ncol, v);
+          store_run<TO, CW>(outb + (size_t)m * g.ldo + ncol, v);
         }
       }
     }
@@ -494,7 +504,7 @@ extern "C" int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, in
   if (epi == CLIPK_EPI_BIAS_RES && (!res || ldr < N || ldr % 4)) return CLIPK_EINVAL;
   if (epi == CLIPK_EPI_DQGELU && (!aux || ldaux < N || ldaux % 4)) return CLIPK_EINVAL;
   GemmArgs g{(const char*)A, (const char*)B, M, N, K, lda, ldb, bias, res, ldr, out, ldo, out2, aux,
-             ldaux, nullptr};
+             ldaux, nullptr, 1, 0};
   hipStream_t st = (hipStream_t)stream;
   switch (in_dtype) {
     case CLIPK_F16: return dispatch_out<f16>(out_dtype, epi, aux_dtype, g, st);
@@ -502,6 +512,118 @@ extern "C" int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, in
     case CLIPK_F32: return dispatch_out<float>(out_dtype, epi, aux_dtype, g, st);
     default: return CLIPK_EDTYPE;
   }
+}
+
+namespace clipk {
+// Split-K finish: out = epi(sum_s part[s] + bias [+ res]) in a fixed slice order
+// (deterministic), 4 columns per thread.
+template <typename TO, int EPI>
+__global__ __launch_bounds__(256) void splitk_finish_kernel(int S, int M, int N, const float* __restrict__ part,
+                                                            const float* __restrict__ bias,
+                                                            const float* __restrict__ res, int ldr,
+                                                            TO* __restrict__ out, int ldo, TO* __restrict__ out2) {
+  const int n4 = N >> 2;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)M * n4) return;
+  const int m = (int)(i / n4), c = (int)(i % n4) * 4;
+  f32x4 v = *reinterpret_cast<const f32x4*>(part + (size_t)m * N + c);
+  for (int s = 1; s < S; ++s) v += *reinterpret_cast<const f32x4*>(part + ((size_t)s * M + m) * N + c);
+  if constexpr (EPI != CLIPK_EPI_NONE) v += *reinterpret_cast<const f32x4*>(bias + c);
+  if constexpr (EPI == CLIPK_EPI_BIAS_RES) v += *reinterpret_cast<const f32x4*>(res + (size_t)m * ldr + c);
+  if constexpr (EPI == CLIPK_EPI_BIAS_QGELU) {
+    if (out2) store4<TO>(out2 + (size_t)m * ldo + c, v[0], v[1], v[2], v[3]);
+    v = (f32x4){quick_gelu(v[0]), quick_gelu(v[1]), quick_gelu(v[2]), quick_gelu(v[3])};
+  }
+  store4<TO>(out + (size_t)m * ldo + c, v[0], v[1], v[2], v[3]);
+}
+
+// Slices for a GEMM whose 128x128 tile grid would leave most CUs idle (small M): enough
+// slices to give ~2 blocks per CU, each slice >= 4 K steps, at most 8.
+static int auto_splits(int M, int N, int K, int esz) {
+  if (M <= 0 || N % GEMM_NMIN) return 1;
+  const int tiles = ((M + 127) / 128) * (N / 128);
+  const int nk = K * esz / GEMM_ROWB;
+  int s = (2 * num_cus() + tiles - 1) / tiles;
+  s = s > 8 ? 8 : s;
+  s = s > nk / 4 ? nk / 4 : s;
+  return s < 1 ? 1 : s;
+}
+}  // namespace clipk
+
+extern "C" int clipk_gemm_auto_splits(int in_dtype, int M, int N, int K) {
+  return auto_splits(M, N, K, in_dtype == CLIPK_F32 ? 4 : 2);
+}
+
+extern "C" size_t clipk_gemm_splitk_ws_bytes(int M, int N, int splits) {
+  if (M <= 0 || N <= 0 || splits <= 1) return 0;
+  return (size_t)splits * M * N * sizeof(float);
+}
+
+template <typename TO, int EPI>
+static int splitk_finish(int S, const GemmArgs& g, const float* part, hipStream_t st) {
+  const long n = (long)g.M * (g.N / 4);
+  hipLaunchKernelGGL((splitk_finish_kernel<TO, EPI>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, S, g.M,
+                     g.N, part, g.bias, g.res, g.ldr, (TO*)g.out, g.ldo, (TO*)g.out2);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_gemm_splitk(int in_dtype, int out_dtype, int epi, int M, int N, int K,
+                                 const void* A, int lda, const void* B, int ldb,
+                                 const float* bias, const float* res, int ldr,
+                                 void* out, int ldo, void* out2, int splits, void* ws, size_t ws_bytes,
+                                 void* stream) {
+  const int esz = in_dtype == CLIPK_F32 ? 4 : 2;
+  if (splits <= 0) splits = auto_splits(M, N, K, esz);
+  if (splits <= 1 || M <= 0)
+    return clipk_gemm(in_dtype, out_dtype, epi, M, N, K, A, lda, B, ldb, bias, res, ldr, out, ldo, out2,
+                      nullptr, 0, 0, stream);
+  if (!A || !B || !out || !ws) return CLIPK_EINVAL;
+  if (N <= 0 || K <= 0 || N % GEMM_NMIN != 0 || (K * esz) % GEMM_ROWB != 0) return CLIPK_ESHAPE;
+  if (lda < K || ldb < K || (lda * esz) % 16 || (ldb * esz) % 16 || ldo < N || ldo % 4) return CLIPK_ESHAPE;
+  if (splits > K * esz / GEMM_ROWB) return CLIPK_ESHAPE;
+  if (epi == CLIPK_EPI_DQGELU) return CLIPK_EINVAL;
+  if ((epi == CLIPK_EPI_BIAS || epi == CLIPK_EPI_BIAS_RES || epi == CLIPK_EPI_BIAS_QGELU) && !bias)
+    return CLIPK_EINVAL;
+  if (epi == CLIPK_EPI_BIAS_RES && (!res || ldr < N || ldr % 4 || out_dtype != CLIPK_F32)) return CLIPK_EINVAL;
+  if (ws_bytes < clipk_gemm_splitk_ws_bytes(M, N, splits)) return CLIPK_EWORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  // slices: EPI_NONE fp32 partials [splits][M][N] (128x128 tiles, one block per tile and slice)
+  GemmArgs p{(const char*)A, (const char*)B, M, N, K, lda, ldb, nullptr, nullptr, 0, ws, N, nullptr, nullptr, 0,
+             gemm_stamp_buf(), splits, (long long)M * N};
+  const int nwg = ((M + 127) / 128) * (N / 128) * splits;
+  switch (in_dtype) {
+    case CLIPK_F16:
+      hipLaunchKernelGGL((gemm_nt_kernel<f16, float, float, CLIPK_EPI_NONE, 128, 128, 2, 2, false>), dim3(nwg),
+                         dim3(256), 0, st, p);
+      break;
+    case CLIPK_BF16:
+      hipLaunchKernelGGL((gemm_nt_kernel<bf16, float, float, CLIPK_EPI_NONE, 128, 128, 2, 2, false>), dim3(nwg),
+                         dim3(256), 0, st, p);
+      break;
+    case CLIPK_F32:
+      hipLaunchKernelGGL((gemm_nt_kernel<float, float, float, CLIPK_EPI_NONE, 128, 128, 2, 2, false>), dim3(nwg),
+                         dim3(256), 0, st, p);
+      break;
+    default: return CLIPK_EDTYPE;
+  }
+  CLIPK_CHECK_LAUNCH();
+  GemmArgs g{(const char*)A, (const char*)B, M, N, K, lda, ldb, bias, res, ldr, out, ldo, out2, nullptr, 0,
+             nullptr, 1, 0};
+  const float* part = (const float*)ws;
+#define CLIPK_FIN(EPIV)                                                           \
+  switch (out_dtype) {                                                            \
+    case CLIPK_F32: return splitk_finish<float, EPIV>(splits, g, part, st);      \
+    case CLIPK_F16: return splitk_finish<f16, EPIV>(splits, g, part, st);        \
+    case CLIPK_BF16: return splitk_finish<bf16, EPIV>(splits, g, part, st);      \
+    default: return CLIPK_EDTYPE;                                                 \
+  }
+  if (epi == CLIPK_EPI_NONE) { CLIPK_FIN(CLIPK_EPI_NONE) }
+  if (epi == CLIPK_EPI_BIAS) { CLIPK_FIN(CLIPK_EPI_BIAS) }
+  if (epi == CLIPK_EPI_BIAS_QGELU) { CLIPK_FIN(CLIPK_EPI_BIAS_QGELU) }
+  if (epi == CLIPK_EPI_BIAS_RES) return splitk_finish<float, CLIPK_EPI_BIAS_RES>(splits, g, part, st);
+#undef CLIPK_FIN
+  return CLIPK_EINVAL;
 }
 
 // Diagnostic: copy the per-block stamps of the last launch (CLIPK_GEMM_STAMP set) to host

@@ -59,6 +59,25 @@ def gemm(a, b, epi=N.EPI_NONE, out_dtype=torch.float32, bias=None, res=None, aux
     return (out, out2) if want_out2 else out
 
 
+def gemm_splitk(a, b, epi=N.EPI_NONE, out_dtype=torch.float32, bias=None, res=None, want_out2=False,
+                splits=0):
+    """Split-K form of gemm (fp32 partials in a workspace, deterministic slice-order sum);
+    splits <= 0 picks the library's choice for the shape."""
+    _need(a, "A")
+    _need(b, "B", a.dtype)
+    M, K = a.shape
+    Nn = b.shape[0]
+    if splits <= 0:
+        splits = N.load().clipk_gemm_auto_splits(DT[a.dtype], M, Nn, K)
+    out = torch.empty(M, Nn, device=a.device, dtype=out_dtype)
+    out2 = torch.empty_like(out) if want_out2 else None
+    ws = torch.empty(max(N.load().clipk_gemm_splitk_ws_bytes(M, Nn, splits), 1), dtype=torch.uint8,
+                     device=a.device)
+    N.call("clipk_gemm_splitk", DT[a.dtype], DT[out_dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias),
+           _p(res), Nn, _p(out), Nn, _p(out2), splits, _p(ws), ws.numel(), _stream())
+    return (out, out2) if want_out2 else out
+
+
 def layernorm(x, w, b, out_dtype=torch.float32, rows=None, stats=False):
     """LayerNorm over the last dim of fp32 x [R, W] (optionally on gathered rows)."""
     _need(x, "x", torch.float32)

@@ -72,6 +72,20 @@ int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, int K,
                void* out, int ldo, void* out2, const void* aux, int aux_dtype, int ldaux,
                void* stream);
 
+/* Split-K form of clipk_gemm for small M (the ViT at training batch sizes, whose 128x128
+ * tile grid would leave most CUs idle): the K range is cut into `splits` slices whose fp32
+ * partials go to the caller's workspace ws ([splits][M][N] fp32), then one elementwise pass
+ * sums them in slice order (deterministic) and applies the epilogue. Same arguments and
+ * epilogues as clipk_gemm except EPI_DQGELU; splits <= 0 picks clipk_gemm_auto_splits;
+ * one slice is plain clipk_gemm (ws unused). */
+int clipk_gemm_auto_splits(int in_dtype, int M, int N, int K);
+size_t clipk_gemm_splitk_ws_bytes(int M, int N, int splits);
+int clipk_gemm_splitk(int in_dtype, int out_dtype, int epi, int M, int N, int K,
+                      const void* A, int lda, const void* B, int ldb,
+                      const float* bias, const float* res, int ldr,
+                      void* out, int ldo, void* out2, int splits, void* ws, size_t ws_bytes,
+                      void* stream);
+
 /* Benchmark knob: force the 16-bit GEMM tile configuration (0: 128x128, 1: 256x256,
  * 2: 256x128, 3: 256x256 non-persistent, 4: 256x128 / 5: 128x256 two blocks per CU;
  * -1 = automatic by shape). Not needed for normal use. */

@@ -229,6 +229,32 @@ def test_gemm_large_m_every_config(dev, cfg, Nn, K):
         lib.clipk_gemm_set_config(-1)
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,Nn,K,splits", [(1576, 768, 3072, 0), (1576, 2304, 768, 0), (300, 256, 512, 3)])
+def test_gemm_splitk(dev, dtype, M, Nn, K, splits):
+    """Split-K (ViT at small batch) vs torch fp32, every epilogue; slice-order sum is
+    deterministic (bitwise-equal reruns)."""
+    g = torch.Generator(device="cpu").manual_seed(M + Nn + K)
+    A = torch.randn(M, K, generator=g).to(dev).to(dtype)
+    B = (torch.randn(Nn, K, generator=g) / math.sqrt(K)).to(dev).to(dtype)
+    bias = torch.randn(Nn, generator=g).to(dev)
+    res = torch.randn(M, Nn, generator=g).to(dev)
+    if splits == 0:
+        assert N.load().clipk_gemm_auto_splits(ops.DT[dtype], M, Nn, K) > 1
+    ref = A.float() @ B.float().t()
+    o1 = ops.gemm_splitk(A, B, N.EPI_NONE, torch.float32, splits=splits)
+    close(o1, ref, dtype, "splitk none")
+    assert torch.equal(o1, ops.gemm_splitk(A, B, N.EPI_NONE, torch.float32, splits=splits))
+    close(ops.gemm_splitk(A, B, N.EPI_BIAS_RES, torch.float32, bias=bias, res=res, splits=splits),
+          ref + bias + res, dtype, "splitk res")
+    odt = dtype if dtype != torch.float32 else torch.float32
+    gq, hq = ops.gemm_splitk(A, B, N.EPI_BIAS_QGELU, odt, bias=bias, want_out2=True, splits=splits)
+    hr = ref + bias
+    close(hq, hr, dtype, "splitk qgelu.h")
+    close(gq, hr * torch.sigmoid(1.702 * hr), dtype, "splitk qgelu.g")
+    close(ops.gemm_splitk(A, B, N.EPI_BIAS, odt, bias=bias, splits=splits), hr, dtype, "splitk bias")
+
+
 def prefix_case(G, C, P, H, max_q, seed):
     """Random shared-prefix packing: per-class q_len in [1, max_q], group stride R, and the
     host-side attention tiles (whole classes packed into <= 16-row windows)."""
