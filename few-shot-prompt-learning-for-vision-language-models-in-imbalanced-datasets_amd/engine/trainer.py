@@ -26,10 +26,11 @@ from ..clip.model import build_model
 from .metrics import Classification
 
 
-def load_clip(cfg, prec, device):
+def load_clip(cfg, prec, device, text_grad=True):
     """Replacement for load_clip_to_cpu (coop.py:165-184): a local state dict from
     MODEL.WEIGHTS_PATH (torch.load weights_only=True / .npz / safetensors), otherwise
-    the seeded synthetic CLIP of MODEL.BACKBONE.NAME (no network on this path)."""
+    the seeded synthetic CLIP of MODEL.BACKBONE.NAME (no network on this path).
+    text_grad=False packs no backward weights (forward-only text encoder, e.g. zero-shot)."""
     path = cfg.MODEL.get("WEIGHTS_PATH", "")
     if path:
         if path.endswith(".npz"):
@@ -45,7 +46,7 @@ def load_clip(cfg, prec, device):
         sd = {k: v for k, v in sd.items() if k not in ("input_resolution", "context_length", "vocab_size")}
     else:
         sd = synth.make_state_dict(cfg.MODEL.BACKBONE.NAME, seed=0)
-    return build_model(sd, prec=prec, device=device)
+    return build_model(sd, prec=prec, device=device, text_grad=text_grad)
 
 
 class TrainerX:

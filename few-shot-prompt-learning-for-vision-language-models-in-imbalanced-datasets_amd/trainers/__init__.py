@@ -1,2 +1,2 @@
-"""CoOp / CoCoOp trainers (registered in fsp_amd.engine.TRAINER_REGISTRY)."""
-from . import coop, cocoop  # noqa: F401
+"""CoOp / CoCoOp / ZeroshotCLIP trainers (registered in fsp_amd.engine.TRAINER_REGISTRY)."""
+from . import coop, cocoop, zsclip  # noqa: F401

@@ -212,3 +212,50 @@ def test_shared_prefix_tables_reconstruct_prompts(position, n_ctx, P_expect):
     # CSC contexts and over-long class suffixes fall back to the plain layout
     assert shared_prefix_tables(src, cpos, eot, n_ctx, csc=True) is None
     assert shared_prefix_tables(src, cpos, [e + 20 for e in eot], n_ctx, csc=False) is None
+
+
+def test_checkpoint_layout_and_resume(tmp_path):
+    """Dassl checkpoint format (torchtools.py:27-157, trainer.py:118-145): OUTPUT_DIR/<name>/
+    model.pth.tar-<epoch> with keys state_dict/epoch/optimizer/scheduler/val_result plus a
+    `checkpoint` pointer file; resume restores weights, scheduler and the start epoch."""
+    import torch
+    import torch.nn as nn
+    from fsp_amd.engine.config import get_cfg_default
+    from fsp_amd.engine.optim import build_optimizer, build_lr_scheduler
+    from fsp_amd.engine.trainer import TrainerX
+
+    class Learner(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.ctx = nn.Parameter(torch.zeros(4, 8))
+            self.register_buffer("token_prefix", torch.ones(3, 1, 8))
+
+    class Dummy(TrainerX):
+        def build_model(self):
+            self.model = Learner()
+            self.optim = build_optimizer(self.model, self.cfg.OPTIM)
+            self.sched = build_lr_scheduler(self.optim, self.cfg.OPTIM)
+            self.register_model("prompt_learner", self.model, self.optim, self.sched)
+
+    cfg = get_cfg_default()
+    cfg.OUTPUT_DIR = str(tmp_path)
+    cfg.OPTIM.MAX_EPOCH = 5
+    t = Dummy(cfg)
+    with torch.no_grad():
+        t.model.ctx.copy_(torch.arange(32.0).reshape(4, 8))
+    t.update_lr()
+    t.update_lr()
+    lr = t.get_current_lr()
+    t.save_model(2, str(tmp_path), val_result=0.5)
+    d = tmp_path / "prompt_learner"
+    assert (d / "checkpoint").read_text().strip() == "model.pth.tar-3"
+    ck = torch.load(d / "model.pth.tar-3", map_location="cpu", weights_only=True)
+    assert set(ck) == {"state_dict", "epoch", "optimizer", "scheduler", "val_result"}
+    assert ck["epoch"] == 3 and ck["val_result"] == 0.5
+    assert set(ck["state_dict"]) == {"ctx", "token_prefix"}
+    t2 = Dummy(cfg)
+    assert t2.resume_model_if_exist(str(tmp_path)) == 3
+    assert torch.equal(t2.model.ctx, t.model.ctx)
+    assert t2.get_current_lr() == lr
+    with pytest.raises(KeyError):
+        t2.register_model("prompt_learner", t2.model, None, None)

@@ -161,3 +161,51 @@ def test_bench_scale_fp16_matches_fp32(dev):
     assert abs(o16["loss"] - o32["loss"]) <= 0.05
     for k in [k for k in o32 if k.startswith("grad_")]:
         assert cos_err(o16[k].reshape(1, -1), o32[k].reshape(1, -1)) <= 2e-3, k
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+@pytest.mark.parametrize("ensemble", [False, True])
+def test_zeroshot_clip_vs_oracle(dev, prec, ensemble):
+    """ZeroshotCLIP / ZeroshotCLIP2 (zsclip.py:32-99) through the registry, vs the CPU oracle
+    (encode_image / encode_text pinned by the golden vectors): logits = exp(logit_scale) *
+    cos(image, class prompt feature); ZeroshotCLIP2 averages normalised template features.
+    Templates limited to ones the fallback tokenizer covers (no BPE vocab on the GPU box)."""
+    import torch
+    from oracle import clip_oracle as O
+    from fsp_amd.clip import synth
+    from fsp_amd.clip.tokenizer import tokenize
+    from fsp_amd.engine.config import get_cfg_default
+    from fsp_amd.engine.registry import TRAINER_REGISTRY
+    from fsp_amd.data.synthetic import SyntheticDataManager
+    from fsp_amd.trainers import zsclip
+    arch, n_cls, B = "ViT-B/32", 12, 3
+    a = synth.ARCHS[arch]
+    cfg = get_cfg_default()
+    cfg.MODEL.BACKBONE.NAME = arch
+    cfg.INPUT.SIZE = (a.image_resolution, a.image_resolution)
+    cfg.DATASET.NAME = "ImageNet"
+    cfg.TRAINER.COOP.PREC = prec
+    cfg.TRAINER.NAME = "ZeroshotCLIP2" if ensemble else "ZeroshotCLIP"
+    dm = SyntheticDataManager(n_cls, a.image_resolution, B, n_batches=1, device=str(dev))
+    cls = TRAINER_REGISTRY.get(cfg.TRAINER.NAME)
+    templates = ["a photo of a {}.", "X X X X {}."] if ensemble else ["a photo of a {}."]
+    if ensemble:
+        cls = type("ZS2Probe", (cls,), {"templates": templates})
+    tr = cls(cfg, dm=dm)
+    img = torch.from_numpy(synth.make_images(B, a.image_resolution, seed=1)).to(dev)
+    with torch.no_grad():
+        logits = tr.model_inference(img).cpu().numpy()
+    p = O.as_torch_sd(synth.make_state_dict(arch, seed=0))
+    names = synth.synthetic_classnames(n_cls)
+    feats = 0
+    for t in templates:
+        tok = torch.from_numpy(tokenize([t.format(n) for n in names]).astype(np.int64))
+        with torch.no_grad():
+            f = O.encode_text(p, O.token_embed(p, tok), tok)
+        feats = feats + O.normalize(f)
+    feats = O.normalize(feats / len(templates))
+    with torch.no_grad():
+        imf = O.normalize(O.encode_image(p, torch.from_numpy(synth.make_images(B, a.image_resolution, seed=1))))
+    ref = (float(np.exp(float(p["logit_scale"]))) * imf @ feats.t()).numpy()
+    tol = 1e-3 if prec == "fp32" else 5e-4 * 100.0
+    assert float(np.abs(logits - ref).max()) <= tol
