@@ -91,6 +91,15 @@ int clipk_gemm_splitk(int in_dtype, int out_dtype, int epi, int M, int N, int K,
  * -1 = automatic by shape). Not needed for normal use. */
 int clipk_gemm_set_config(int cfg);
 
+/* Image preprocessing (Dassl/torchvision Resize+CenterCrop / RandomResizedCrop+flip,
+ * ToTensor, Normalize; transforms.py:206-354): Pillow-exact bicubic resampling of a crop
+ * window of each uint8 HWC image (src: packed images), from host-built fixed-point tables
+ * (fsp_amd/data/preprocess.py documents desc/tables); out fp32 [B,3,S,S] normalised with
+ * mean/std, or the uint8 pixels when out_uint8. tmp: sum over images of rows*S*3 bytes. */
+int clipk_image_resample(int B, int S, int rows_max, const void* src, const long long* desc,
+                         const int* tables, void* tmp, const float* mean, const float* stdv,
+                         int out_uint8, void* out, void* stream);
+
 /* Diagnostic: per-block / per-tile s_memrealtime marks of the last GEMM launch, recorded
  * only when the process runs with CLIPK_GEMM_STAMP set (synchronises the device). */
 int clipk_gemm_stamps(void* host, size_t bytes);
