@@ -37,6 +37,8 @@ SIGNATURES = {
     "clipk_gemm_stamps": (_I, [_P, _S]),
     "clipk_layernorm_fwd": (_I, [_I, _I, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P]),
     "clipk_layernorm_bwd": (_I, [_I, _I, _I, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P]),
+    "clipk_layernorm_fwd_x": (_I, [_I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P]),
+    "clipk_layernorm_bwd_x": (_I, [_I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P]),
     "clipk_attention_fwd": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P]),
     "clipk_attention_bwd": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _I, _P, _P, _I, _P]),
     "clipk_im2col": (_I, [_I, _I, _I, _I, _I, _P, _P, _P]),

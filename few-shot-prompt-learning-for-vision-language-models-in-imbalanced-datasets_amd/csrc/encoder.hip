@@ -27,6 +27,14 @@ namespace clipk {
 static inline size_t esize(int dt) { return dt == CLIPK_F32 ? 4 : 2; }
 static inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
+// Residual stream dtype of the TEXT encoder: the 16-bit activation dtype under PREC
+// fp16/bf16 (CLIP's own fp16 semantics: the whole residual path in half precision, LN
+// statistics in fp32), fp32 under PREC fp32. CLIPK_TEXT_RES32 forces fp32 (A/B knob).
+static int res_dtype(const clipk_encoder* e) {
+  static const bool force32 = getenv("CLIPK_TEXT_RES32") != nullptr;
+  return (e->act == CLIPK_F32 || force32) ? CLIPK_F32 : e->act;
+}
+
 struct Carver {
   char* base;
   size_t off = 0;
@@ -79,7 +87,7 @@ struct ProfScope {
 
 // sk / skb: split-K workspace (vision: small M); nullptr = one launch over the tile grid
 static int gemm(int in, int out, int epi, int M, int N, int K, const void* A, const void* B,
-                const float* bias, const float* res, void* o, void* o2, const void* aux, int auxdt,
+                const float* bias, const void* res, void* o, void* o2, const void* aux, int auxdt,
                 hipStream_t st, int prof_cls, void* sk = nullptr, size_t skb = 0) {
   ProfScope ps(prof_cls, st, 2.0 * M * N * K);
   if (sk && epi != CLIPK_EPI_DQGELU)
@@ -101,9 +109,11 @@ static size_t vit_splitk_bytes(int act, int rows, int D) {
 // ---------------------------------------------------------------- text layout
 struct TextBufs {
   // saved (per layer)
-  std::vector<float*> X, Xm, mean1, rstd1, mean2, rstd2, lse;
+  // X / Xm: residual stream (layer inputs / post-attention), of the encoder's residual dtype
+  std::vector<void*> X, Xm;
+  std::vector<float*> mean1, rstd1, mean2, rstd2, lse;
   std::vector<void*> qkv, o, h;
-  float* Xf = nullptr;  // final layer output (== X[layers])
+  void* Xf = nullptr;  // final layer output (== X[layers])
   float *meanf = nullptr, *rstdf = nullptr;
   // forward temporaries
   void *xn = nullptr, *g = nullptr, *lnf = nullptr;
@@ -113,7 +123,7 @@ struct TextBufs {
 // save=1: per-layer activations live in `saved`; save=0: buffers are reused across layers
 static TextBufs text_layout(const clipk_encoder* e, size_t rows, int nout, void* saved, void* ws, bool save) {
   TextBufs t;
-  const size_t W = e->W, H = e->heads, a = esize(e->act);
+  const size_t W = e->W, H = e->heads, a = esize(e->act), xs = esize(res_dtype(e));
   const int nl = e->layers;
   Carver sv(saved), wk(ws);
   Carver& S = save ? sv : wk;
@@ -121,9 +131,9 @@ static TextBufs text_layout(const clipk_encoder* e, size_t rows, int nout, void*
   t.mean2.resize(nl); t.rstd2.resize(nl); t.lse.resize(nl); t.qkv.resize(nl); t.o.resize(nl);
   t.h.resize(nl);
   if (save) {
-    for (int l = 0; l <= nl; ++l) t.X[l] = (float*)S.take(rows * W * 4);
+    for (int l = 0; l <= nl; ++l) t.X[l] = S.take(rows * W * xs);
     for (int l = 0; l < nl; ++l) {
-      t.Xm[l] = (float*)S.take(rows * W * 4);
+      t.Xm[l] = S.take(rows * W * xs);
       t.mean1[l] = (float*)S.take(rows * 4); t.rstd1[l] = (float*)S.take(rows * 4);
       t.mean2[l] = (float*)S.take(rows * 4); t.rstd2[l] = (float*)S.take(rows * 4);
       t.lse[l] = (float*)S.take(rows * H * 4);
@@ -134,9 +144,9 @@ static TextBufs text_layout(const clipk_encoder* e, size_t rows, int nout, void*
     t.meanf = (float*)S.take((size_t)nout * 4);
     t.rstdf = (float*)S.take((size_t)nout * 4);
   } else {
-    float* x0 = (float*)wk.take(rows * W * 4);
-    float* x1 = (float*)wk.take(rows * W * 4);
-    float* xm = (float*)wk.take(rows * W * 4);
+    void* x0 = wk.take(rows * W * xs);
+    void* x1 = wk.take(rows * W * xs);
+    void* xm = wk.take(rows * W * xs);
     void* q = wk.take(rows * 3 * W * a);
     void* o = wk.take(rows * W * a);
     for (int l = 0; l <= nl; ++l) t.X[l] = (l & 1) ? x1 : x0;
@@ -222,27 +232,28 @@ static int attn_bwd(const clipk_encoder* e, const SeqShape& sh, const void* qkv,
 }
 
 // one residual block forward (shared by text and vision)
+// X, Xm, Xo: residual stream of dtype rd (fp32, or the 16-bit act dtype for the text encoder)
 static int block_fwd(const clipk_encoder* e, const std::array<const void*, 16>& w, const SeqShape& sh,
-                     const float* X, float* Xm, float* Xo, void* xn, void* qkv, void* o,
+                     int rd, const void* X, void* Xm, void* Xo, void* xn, void* qkv, void* o,
                      float* lse, void* h, void* g, float* m1, float* r1, float* m2, float* r2,
                      hipStream_t st, bool text, void* sk = nullptr, size_t skb = 0) {
   const int pg = text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE;
   const int W = e->W, rows = sh.rows, act = e->act;
-  TRY(clipk_layernorm_fwd(act, rows, W, X, W, nullptr, (const float*)w[0], (const float*)w[1], xn, W,
-                          m1, r1, st));
+  TRY(clipk_layernorm_fwd_x(rd, act, rows, W, X, W, nullptr, (const float*)w[0], (const float*)w[1], xn, W,
+                            m1, r1, st));
   TRY(gemm(act, act, CLIPK_EPI_BIAS, rows, 3 * W, W, xn, w[2], (const float*)w[3], nullptr, qkv,
            nullptr, nullptr, 0, st, pg, sk, skb));
   {
     ProfScope ps(text ? CLIPK_PROF_ATTN : CLIPK_PROF_NONE, st, 0.0);
     TRY(attn_fwd(e, sh, qkv, o, lse, st));
   }
-  TRY(gemm(act, CLIPK_F32, CLIPK_EPI_BIAS_RES, rows, W, W, o, w[4], (const float*)w[5], X, Xm,
+  TRY(gemm(act, rd, CLIPK_EPI_BIAS_RES, rows, W, W, o, w[4], (const float*)w[5], X, Xm,
            nullptr, nullptr, 0, st, pg, sk, skb));
-  TRY(clipk_layernorm_fwd(act, rows, W, Xm, W, nullptr, (const float*)w[6], (const float*)w[7], xn, W,
-                          m2, r2, st));
+  TRY(clipk_layernorm_fwd_x(rd, act, rows, W, Xm, W, nullptr, (const float*)w[6], (const float*)w[7], xn, W,
+                            m2, r2, st));
   TRY(gemm(act, act, CLIPK_EPI_BIAS_QGELU, rows, 4 * W, W, xn, w[8], (const float*)w[9], nullptr, g,
            h, nullptr, 0, st, text ? CLIPK_PROF_GEMM_FC : CLIPK_PROF_NONE, sk, skb));
-  TRY(gemm(act, CLIPK_F32, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo,
+  TRY(gemm(act, rd, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo,
            nullptr, nullptr, 0, st, pg, sk, skb));
   return CLIPK_OK;
 }
@@ -323,24 +334,29 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
   const bool save = saved != nullptr;
   TextBufs t = text_layout(e, sh.rows, sh.nout, saved, ws, save);
   if (ws_bytes < t.ws_bytes || (save && saved_bytes < t.saved_bytes)) return CLIPK_EWORKSPACE;
-  const int W = e->W, rows = sh.rows;
-  // layer-0 input: copy x0 into X[0] when saving (X[0] is needed for LN1 backward)
-  const float* cur = x0;
-  if (save) {
-    if (hipMemcpyAsync(t.X[0], x0, (size_t)rows * W * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
-      return (int)hipGetLastError();
+  const int W = e->W, rows = sh.rows, rd = res_dtype(e);
+  // layer-0 input: x0 (fp32) into X[0] (the residual dtype) when saving (LN1 backward reads
+  // it) or when the residual stream is 16-bit
+  const void* cur = x0;
+  if (save || rd != CLIPK_F32) {
+    if (rd == CLIPK_F32) {
+      if (hipMemcpyAsync(t.X[0], x0, (size_t)rows * W * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return (int)hipGetLastError();
+    } else {
+      TRY(clipk_cast(rd, (long)rows * W, x0, t.X[0], st));
+    }
     cur = t.X[0];
   }
   for (int l = 0; l < e->layers; ++l) {
-    float* Xo = t.X[l + 1];
+    void* Xo = t.X[l + 1];
     if (!save && Xo == cur) Xo = t.X[l];  // ping-pong (cur may be the caller's x0)
-    TRY(block_fwd(e, e->lw[l], sh, cur, t.Xm[l], Xo, t.xn, t.qkv[l], t.o[l], t.lse[l],
+    TRY(block_fwd(e, e->lw[l], sh, rd, cur, t.Xm[l], Xo, t.xn, t.qkv[l], t.o[l], t.lse[l],
                   save ? t.h[l] : nullptr, t.g, t.mean1[l], t.rstd1[l], t.mean2[l], t.rstd2[l], st, true));
     cur = Xo;
   }
   // ln_final on the EOT rows only (exact: LayerNorm is per row), then @ text_projection
-  TRY(clipk_layernorm_fwd(e->act, sh.nout, W, cur, W, eot_rows, (const float*)e->head[0],
-                          (const float*)e->head[1], t.lnf, W, t.meanf, t.rstdf, st));
+  TRY(clipk_layernorm_fwd_x(rd, e->act, sh.nout, W, cur, W, eot_rows, (const float*)e->head[0],
+                            (const float*)e->head[1], t.lnf, W, t.meanf, t.rstdf, st));
   TRY(gemm(e->act, CLIPK_F32, CLIPK_EPI_NONE, sh.nout, e->E, W, t.lnf, e->head[2], nullptr, nullptr, txt,
            nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
   return CLIPK_OK;
@@ -361,7 +377,8 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
   if (hipMemsetAsync(dX, 0, (size_t)rows * W * 4, st) != hipSuccess) return (int)hipGetLastError();
   if (hipMemsetAsync(b.dX_lp, 0, (size_t)rows * W * esize(gd), st) != hipSuccess)
     return (int)hipGetLastError();
-  TRY(clipk_layernorm_bwd(CLIPK_F32, nout, W, b.dlnf, W, t.Xf, W, eot_rows, (const float*)e->head[0], t.meanf,
+  const int rd = res_dtype(e);
+  TRY(clipk_layernorm_bwd_x(rd, CLIPK_F32, nout, W, b.dlnf, W, t.Xf, W, eot_rows, (const float*)e->head[0], t.meanf,
                           t.rstdf, nullptr, W, dX, b.dX_lp, gd, eot_rows, W, st));
   for (int l = e->layers - 1; l >= 0; --l) {
     const auto& w = e->lw[l];
@@ -372,7 +389,7 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
              t.h[l], act, st, CLIPK_PROF_GEMM_DGELU));
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, 4 * W, b.dh, w[14], nullptr, nullptr, b.dxn, nullptr,
              nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
-    TRY(clipk_layernorm_bwd(gd, rows, W, b.dxn, W, t.Xm[l], W, nullptr, (const float*)w[6], t.mean2[l],
+    TRY(clipk_layernorm_bwd_x(rd, gd, rows, W, b.dxn, W, t.Xm[l], W, nullptr, (const float*)w[6], t.mean2[l],
                             t.rstd2[l], dX, W, dX, b.dX_lp, gd, nullptr, W, st));
     // attention: do = dXm . Wout ; dqkv ; dxn1 = dqkv . Win
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, W, b.dX_lp, w[13], nullptr, nullptr, b.do_, nullptr,
@@ -383,7 +400,7 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
     }
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, 3 * W, b.dqkv, w[12], nullptr, nullptr, b.dxn,
              nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
-    TRY(clipk_layernorm_bwd(gd, rows, W, b.dxn, W, t.X[l], W, nullptr, (const float*)w[0], t.mean1[l],
+    TRY(clipk_layernorm_bwd_x(rd, gd, rows, W, b.dxn, W, t.X[l], W, nullptr, (const float*)w[0], t.mean1[l],
                             t.rstd1[l], dX, W, dX, l > 0 ? b.dX_lp : nullptr, gd, nullptr, W, st));
   }
   return CLIPK_OK;
@@ -531,7 +548,7 @@ extern "C" int clipk_vit_forward(const clipk_encoder* e, int B, const float* img
   float* cur = v.x0;
   float* nxt = v.x1;
   for (int l = 0; l < e->layers; ++l) {
-    TRY(block_fwd(e, e->lw[l], SeqShape::plain(B, L, 0), cur, v.xm, nxt, v.xn, v.qkv, v.o, nullptr, nullptr, v.g,
+    TRY(block_fwd(e, e->lw[l], SeqShape::plain(B, L, 0), CLIPK_F32, cur, v.xm, nxt, v.xn, v.qkv, v.o, nullptr, nullptr, v.g,
                   nullptr, nullptr, nullptr, nullptr, st, false, v.sk, v.sk_bytes));
     float* t = cur; cur = nxt; nxt = t;
   }

@@ -34,7 +34,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 struct GemmArgs {
   const char* A; const char* B;
   int M, N, K, lda, ldb;            // lda/ldb in elements
-  const float* bias; const float* res; int ldr;
+  const float* bias; const void* res; int ldr;  // res: TX (fp32, or the 16-bit out dtype)
   void* out; int ldo; void* out2;
   const void* aux; int ldaux;
   unsigned long long* stamp;  // diagnostic (CLIPK_GEMM_STAMP): per block/tile s_memrealtime marks
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
     const int er = lane / LPR, ec = lane % LPR;
     const int ncol = nbase + CW * ec;
     // residual / aux operands of group i+1 are loaded while group i is transposed and stored
-    constexpr int XNB = CW * (EPI == CLIPK_EPI_BIAS_RES ? 4 : (int)sizeof(TX));
+    constexpr int XNB = CW * (int)sizeof(TX);
     typedef Raw<XNB> XR;
     XR ext_nxt[NQ];
     auto load_ext = [&](int i, XR* dst) {
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
           int mc = mg + RPQ * q + er;
           mc = mc < g.M ? mc : g.M - 1;
           if constexpr (EPI == CLIPK_EPI_BIAS_RES)
-            ld_raw<XNB>(g.res + (size_t)mc * g.ldr + ncol, dst[q]);
+            ld_raw<XNB>((const TX*)g.res + (size_t)mc * g.ldr + ncol, dst[q]);
           else
             ld_raw<XNB>((const TX*)g.aux + (size_t)mc * g.ldaux + ncol, dst[q]);
         }
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
         }
         if constexpr (EPI == CLIPK_EPI_BIAS_RES) {
           float r[CW];
-          raw_f32<float, CW>(ext[q], r);
+          raw_f32<TX, CW>(ext[q], r);
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] += r[c];
           store_run<TO, CW>(outb + (size_t)m * g.ldo + ncol, v);
@@ -456,8 +456,12 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
 template <typename T>
 static int dispatch_out(int out_dtype, int epi, int aux_dtype, const GemmArgs& g, hipStream_t st) {
   if (epi == CLIPK_EPI_BIAS_RES) {
-    if (out_dtype != CLIPK_F32) return CLIPK_EDTYPE;
-    return launch_gemm<T, float, float, CLIPK_EPI_BIAS_RES>(g, st);
+    // residual stream in fp32, or (16-bit text residual) in the operand dtype for both res and out
+    if (out_dtype == CLIPK_F32) return launch_gemm<T, float, float, CLIPK_EPI_BIAS_RES>(g, st);
+    if constexpr (sizeof(T) == 2) {
+      if (out_dtype == DT<T>::id) return launch_gemm<T, T, T, CLIPK_EPI_BIAS_RES>(g, st);
+    }
+    return CLIPK_EDTYPE;
   }
   if (epi == CLIPK_EPI_DQGELU) {
     // backward: out in the grad dtype (== T), aux = forward pre-activation
@@ -490,7 +494,7 @@ using namespace clipk;
 
 extern "C" int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, int K,
                           const void* A, int lda, const void* B, int ldb,
-                          const float* bias, const float* res, int ldr,
+                          const float* bias, const void* res, int ldr,
                           void* out, int ldo, void* out2, const void* aux, int aux_dtype,
                           int ldaux, void* stream) {
   if (!A || !B || !out) return CLIPK_EINVAL;
@@ -563,14 +567,14 @@ template <typename TO, int EPI>
 static int splitk_finish(int S, const GemmArgs& g, const float* part, hipStream_t st) {
   const long n = (long)g.M * (g.N / 4);
   hipLaunchKernelGGL((splitk_finish_kernel<TO, EPI>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, S, g.M,
-                     g.N, part, g.bias, g.res, g.ldr, (TO*)g.out, g.ldo, (TO*)g.out2);
+                     g.N, part, g.bias, (const float*)g.res, g.ldr, (TO*)g.out, g.ldo, (TO*)g.out2);
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
 }
 
 extern "C" int clipk_gemm_splitk(int in_dtype, int out_dtype, int epi, int M, int N, int K,
                                  const void* A, int lda, const void* B, int ldb,
-                                 const float* bias, const float* res, int ldr,
+                                 const float* bias, const void* res, int ldr,
                                  void* out, int ldo, void* out2, int splits, void* ws, size_t ws_bytes,
                                  void* stream) {
   const int esz = in_dtype == CLIPK_F32 ? 4 : 2;
@@ -610,7 +614,7 @@ extern "C" int clipk_gemm_splitk(int in_dtype, int out_dtype, int epi, int M, in
   CLIPK_CHECK_LAUNCH();
   GemmArgs g{(const char*)A, (const char*)B, M, N, K, lda, ldb, bias, res, ldr, out, ldo, out2, nullptr, 0,
              nullptr, 1, 0};
-  const float* part = (const float*)ws;
+  const float* part = (const float*)ws;  // the finish pass reads an fp32 residual (checked above)
 #define CLIPK_FIN(EPIV)                                                           \
   switch (out_dtype) {                                                            \
     case CLIPK_F32: return splitk_finish<float, EPIV>(splits, g, part, st);      \

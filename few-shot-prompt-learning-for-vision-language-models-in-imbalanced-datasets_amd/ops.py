@@ -50,7 +50,7 @@ def gemm(a, b, epi=N.EPI_NONE, out_dtype=torch.float32, bias=None, res=None, aux
     if bias is not None:
         _need(bias, "bias", torch.float32)
     if res is not None:
-        _need(res, "res", torch.float32)
+        _need(res, "res", torch.float32 if out.dtype == torch.float32 else out.dtype)
     if aux is not None:
         _need(aux, "aux")
     N.call("clipk_gemm", DT[a.dtype], DT[out.dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias),
@@ -79,8 +79,8 @@ def gemm_splitk(a, b, epi=N.EPI_NONE, out_dtype=torch.float32, bias=None, res=No
 
 
 def layernorm(x, w, b, out_dtype=torch.float32, rows=None, stats=False):
-    """LayerNorm over the last dim of fp32 x [R, W] (optionally on gathered rows)."""
-    _need(x, "x", torch.float32)
+    """LayerNorm over the last dim of x [R, W] (fp32 or 16-bit; optionally on gathered rows)."""
+    _need(x, "x")
     R, W = x.shape
     n = R if rows is None else rows.numel()
     out = torch.empty(n, W, device=x.device, dtype=out_dtype)
@@ -88,8 +88,8 @@ def layernorm(x, w, b, out_dtype=torch.float32, rows=None, stats=False):
     rstd = torch.empty(n, device=x.device) if stats else None
     if rows is not None:
         _need(rows, "rows", torch.int32)
-    N.call("clipk_layernorm_fwd", DT[out_dtype], n, W, _p(x), W, _p(rows), _p(w), _p(b), _p(out), W,
-           _p(mean), _p(rstd), _stream())
+    N.call("clipk_layernorm_fwd_x", DT[x.dtype], DT[out_dtype], n, W, _p(x), W, _p(rows), _p(w), _p(b), _p(out),
+           W, _p(mean), _p(rstd), _stream())
     return (out, mean, rstd) if stats else out
 
 
@@ -98,8 +98,9 @@ def layernorm_bwd(dy, x, w, mean, rstd, dres=None, lp_dtype=None):
     R, W = dy.shape
     dx = torch.empty(R, W, device=dy.device, dtype=torch.float32)
     lp = torch.empty(R, W, device=dy.device, dtype=lp_dtype) if lp_dtype is not None else None
-    N.call("clipk_layernorm_bwd", DT[dy.dtype], R, W, _p(dy), W, _p(x), W, None, _p(w), _p(mean), _p(rstd),
-           _p(dres), W, _p(dx), _p(lp), DT[lp_dtype] if lp_dtype is not None else 0, None, W, _stream())
+    _need(x, "x")
+    N.call("clipk_layernorm_bwd_x", DT[x.dtype], DT[dy.dtype], R, W, _p(dy), W, _p(x), W, None, _p(w), _p(mean),
+           _p(rstd), _p(dres), W, _p(dx), _p(lp), DT[lp_dtype] if lp_dtype is not None else 0, None, W, _stream())
     return (dx, lp) if lp is not None else dx
 
 

@@ -53,7 +53,8 @@ enum {
 /* GEMM epilogues:  acc = A[M,K] . B[N,K]^T  (fp32 accumulate)                         */
 enum {
   CLIPK_EPI_BIAS = 0,       /* out(out_dtype) = acc + bias                                */
-  CLIPK_EPI_BIAS_RES = 1,   /* out(f32)       = acc + bias + res(f32)                     */
+  CLIPK_EPI_BIAS_RES = 1,   /* out = acc + bias + res; out and res both f32, or both the
+                               16-bit in_dtype (16-bit residual stream)                  */
   CLIPK_EPI_BIAS_QGELU = 2, /* out = quickgelu(acc + bias); out2 (optional) = acc + bias */
   CLIPK_EPI_DQGELU = 3,     /* out = acc * quickgelu'(aux)                                */
   CLIPK_EPI_NONE = 4        /* out = acc                                                  */
@@ -68,7 +69,7 @@ int clipk_device_arch_ok(void); /* 1 if device 0 is gfx950 */
  * multiples of 8 elements; A/B of in_dtype; bias/res fp32; aux of aux_dtype. */
 int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, int K,
                const void* A, int lda, const void* B, int ldb,
-               const float* bias, const float* res, int ldr,
+               const float* bias, const void* res, int ldr,
                void* out, int ldo, void* out2, const void* aux, int aux_dtype, int ldaux,
                void* stream);
 
@@ -82,7 +83,7 @@ int clipk_gemm_auto_splits(int in_dtype, int M, int N, int K);
 size_t clipk_gemm_splitk_ws_bytes(int M, int N, int splits);
 int clipk_gemm_splitk(int in_dtype, int out_dtype, int epi, int M, int N, int K,
                       const void* A, int lda, const void* B, int ldb,
-                      const float* bias, const float* res, int ldr,
+                      const float* bias, const void* res, int ldr,
                       void* out, int ldo, void* out2, int splits, void* ws, size_t ws_bytes,
                       void* stream);
 
@@ -109,6 +110,10 @@ int clipk_gemm_stamps(void* host, size_t bytes);
 int clipk_layernorm_fwd(int out_dtype, int rows, int width, const float* x, int ldx,
                         const int* in_rows, const float* gamma, const float* beta,
                         void* out, int ldo, float* mean, float* rstd, void* stream);
+/* same with x of x_dtype (fp32 or 16-bit: the 16-bit text residual stream) */
+int clipk_layernorm_fwd_x(int x_dtype, int out_dtype, int rows, int width, const void* x, int ldx,
+                          const int* in_rows, const float* gamma, const float* beta,
+                          void* out, int ldo, float* mean, float* rstd, void* stream);
 
 /* dx = LN-input-grad(dy; x, gamma, mean, rstd) (+ dres). dy of dy_dtype; x row = x_rows ? x_rows[r] : r;
  * outputs written at row out_rows ? out_rows[r] : r of dx (f32) and dx_lp (lp_dtype, optional). */
@@ -116,6 +121,12 @@ int clipk_layernorm_bwd(int dy_dtype, int rows, int width, const void* dy, int l
                         const int* x_rows, const float* gamma, const float* mean, const float* rstd,
                         const float* dres, int lddres, float* dx, void* dx_lp, int lp_dtype,
                         const int* out_rows, int ldo, void* stream);
+/* same with x of x_dtype */
+int clipk_layernorm_bwd_x(int x_dtype, int dy_dtype, int rows, int width, const void* dy, int lddy,
+                          const void* x, int ldx, const int* x_rows, const float* gamma,
+                          const float* mean, const float* rstd, const float* dres, int lddres,
+                          float* dx, void* dx_lp, int lp_dtype, const int* out_rows, int ldo,
+                          void* stream);
 
 /* Multi-head self-attention core on packed qkv rows [(s*L+t), 3*heads*64] (head dim 64):
  * out[(s*L+t), h*64+d]; lse[(s*L+t)*heads + h] (optional) = logsumexp of scaled scores. */

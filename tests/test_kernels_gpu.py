@@ -83,6 +83,38 @@ def test_layernorm_fwd_bwd(dev, W, dtype):
     close(og, F.layer_norm(x[rows.long()], (W,), w, b, 1e-5), torch.float32, "ln gather")
 
 
+@pytest.mark.parametrize("xdt", [torch.float16, torch.bfloat16])
+def test_layernorm_16bit_residual(dev, xdt):
+    """16-bit residual stream (PREC fp16/bf16 text encoder): LN fwd/bwd read x in the
+    activation dtype, statistics in fp32; vs torch fp32 on the same rounded x."""
+    W = 512
+    g = torch.Generator().manual_seed(11)
+    x = (torch.randn(41, W, generator=g) * 3 + 1).to(dev).to(xdt)
+    w = (1 + 0.1 * torch.randn(W, generator=g)).to(dev)
+    b = (0.1 * torch.randn(W, generator=g)).to(dev)
+    out, mean, rstd = ops.layernorm(x, w, b, xdt, stats=True)
+    xr = x.float().clone().requires_grad_(True)
+    ref = F.layer_norm(xr, (W,), w, b, 1e-5)
+    close(out, ref, xdt, "ln16 fwd")
+    dy = torch.randn(41, W, generator=g).to(dev).to(torch.bfloat16)
+    ref.backward(dy.float())
+    dx = ops.layernorm_bwd(dy, x, w, mean, rstd)
+    close(dx, xr.grad, torch.float32, "ln16 bwd")  # same rounded inputs, fp32 math
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_gemm_bias_res_16bit(dev, dtype):
+    """BIAS_RES with a 16-bit residual stream: out (dtype) = A.B^T + bias + res (dtype)."""
+    for M in (300, 40000):
+        g = torch.Generator().manual_seed(M)
+        A = torch.randn(M, 512, generator=g).to(dev).to(dtype)
+        B = (torch.randn(512, 512, generator=g) / math.sqrt(512)).to(dev).to(dtype)
+        bias = torch.randn(512, generator=g).to(dev)
+        res = torch.randn(M, 512, generator=g).to(dev).to(dtype)
+        ref = A.float() @ B.float().t() + bias + res.float()
+        close(ops.gemm(A, B, N.EPI_BIAS_RES, dtype, bias=bias, res=res), ref, dtype, f"res16 M{M}")
+
+
 def attn_ref(qkv, nseq, L, H, causal):
     W = H * 64
     q, k, v = qkv.float().view(nseq, L, 3, H, 64).permute(2, 0, 3, 1, 4)
