@@ -513,11 +513,10 @@ static VitBufs vit_layout(const clipk_encoder* e, int B, void* ws) {
   v.o = c.take(rows * D * a);
   v.g = c.take(rows * 4 * D * a);
   v.cls = c.take((size_t)B * D * a);
-  // split-K for the small-M ViT GEMMs measured even with the 128x128 tile grid at B = 8
-  // (1.19 vs 1.15 ms per step: the slice GEMMs are short and the finish passes cost what
-  // the extra CUs gain), so the workspace is only carved when CLIPK_VIT_SPLITK is set
-  static const bool use_sk = getenv("CLIPK_VIT_SPLITK") != nullptr;
-  v.sk_bytes = use_sk ? vit_splitk_bytes(e->act, (int)rows, (int)D) : 0;
+  // split-K (clipk_gemm_auto_splits) for the ViT GEMMs whose tile grid covers under half
+  // of the CUs at small batch (the N = D projections); CLIPK_VIT_NOSPLITK turns it off
+  static const bool no_sk = getenv("CLIPK_VIT_NOSPLITK") != nullptr;
+  v.sk_bytes = no_sk ? 0 : vit_splitk_bytes(e->act, (int)rows, (int)D);
   v.sk = v.sk_bytes ? c.take(v.sk_bytes) : nullptr;
   v.bytes = c.off;
   return v;

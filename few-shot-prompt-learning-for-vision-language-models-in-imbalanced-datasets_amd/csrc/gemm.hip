@@ -541,11 +541,14 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(int S, int M, int N,
   store4<TO>(out + (size_t)m * ldo + c, v[0], v[1], v[2], v[3]);
 }
 
-// Slices for a GEMM whose 128x128 tile grid would leave most CUs idle (small M): enough
-// slices to give ~2 blocks per CU, each slice >= 4 K steps, at most 8.
+// Slices for a GEMM whose 128x128 tile grid would leave most CUs idle (small M): only when
+// the grid covers under half of the CUs (the ViT's N = 768 projections at B = 8: 78 tiles;
+// grids of 234-312 tiles measured no better split), enough slices for ~2 blocks per CU,
+// each slice >= 4 K steps, at most 8.
 static int auto_splits(int M, int N, int K, int esz) {
   if (M <= 0 || N % GEMM_NMIN) return 1;
   const int tiles = ((M + 127) / 128) * (N / 128);
+  if (2 * tiles >= num_cus()) return 1;
   const int nk = K * esz / GEMM_ROWB;
   int s = (2 * num_cus() + tiles - 1) / tiles;
   s = s > 8 ? 8 : s;

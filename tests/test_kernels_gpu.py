@@ -262,7 +262,8 @@ def test_gemm_large_m_every_config(dev, cfg, Nn, K):
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("M,Nn,K,splits", [(1576, 768, 3072, 0), (1576, 2304, 768, 0), (300, 256, 512, 3)])
+@pytest.mark.parametrize("M,Nn,K,splits", [(1576, 768, 3072, 0), (1576, 768, 768, 0), (1576, 2304, 768, 2),
+                                           (300, 256, 512, 3)])
 def test_gemm_splitk(dev, dtype, M, Nn, K, splits):
     """Split-K (ViT at small batch) vs torch fp32, every epilogue; slice-order sum is
     deterministic (bitwise-equal reruns)."""
