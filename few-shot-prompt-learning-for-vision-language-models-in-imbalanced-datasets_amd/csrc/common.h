@@ -120,13 +120,17 @@ __device__ __forceinline__ float group_max(float v) {
 
 // QuickGELU (PromptSRC/clip/model.py:162-164): x * sigmoid(1.702 x), and its derivative.
 // v_exp_f32 + v_rcp_f32 (1 ulp) instead of an IEEE division: these run per output element
-// in the GEMM epilogues, where a full-precision divide costed ~10 VALU instructions.
-__device__ __forceinline__ float quick_gelu(float x) {
-  return x * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * x));
+// in the GEMM epilogues, where a full-precision divide costed ~10 VALU instructions. The
+// exponent is formed with ONE multiply (-1.702 * log2 e folded) straight into v_exp_f32
+// (exp2): __expf(-1.702f * x) emitted two v_mul_f32 per element.
+constexpr float kQgeluExp2 = -2.4554669595930157f;  // -1.702 * log2(e)
+__device__ __forceinline__ float qgelu_sigmoid(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(kQgeluExp2 * x));
 }
+__device__ __forceinline__ float quick_gelu(float x) { return x * qgelu_sigmoid(x); }
 __device__ __forceinline__ float quick_gelu_grad(float x) {
-  const float s = __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * x));
-  return s + 1.702f * x * s * (1.0f - s);
+  const float s = qgelu_sigmoid(x);
+  return s * fmaf(1.702f * x, 1.0f - s, 1.0f);  // s + 1.702 x s (1 - s)
 }
 
 }  // namespace clipk

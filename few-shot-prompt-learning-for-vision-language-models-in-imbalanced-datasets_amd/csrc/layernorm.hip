@@ -1,64 +1,93 @@
 // LayerNorm forward / input-grad backward as wavefront row reductions (HBM-bound).
 // Reference: PromptSRC/clip/model.py:153-159 (fp32 upcast, eps 1e-5, affine).
-// One wave per row, 4-element vector loads, the row kept in registers (width <= 1024 ->
-// <= 4 vectors per lane), two-pass mean/variance from registers (no E[x^2]-E[x]^2
-// cancellation). The input row (the residual stream) is fp32 or, for the 16-bit text
-// residual stream, the activation dtype (statistics always in fp32). Optional row gather (in_rows) for ln_final on EOT rows and ln_post on
+// One wave per row, the row kept in registers (width <= 1024), two-pass mean/variance from
+// registers (no E[x^2]-E[x]^2 cancellation); 8 consecutive elements per lane (16-B accesses
+// of 16-bit rows) when the width is a multiple of 512, else 4. The input row (the residual
+// stream) is fp32 or, for the 16-bit text residual stream, the activation dtype (statistics
+// always in fp32). Optional row gather (in_rows) for ln_final on EOT rows and ln_post on
 // CLS rows, optional scatter (out_rows) on the backward.
 #include "common.h"
 
 namespace clipk {
 
-constexpr int LN_MAXV = 4;  // float4 per lane -> width <= 1024
+constexpr int LN_MAXV = 4;  // 4-element vectors per lane -> width <= 1024
 
-template <typename TI, typename TO>
+// VW consecutive elements per lane per chunk: 8 (16-B loads of 16-bit rows, 2x16-B of fp32)
+// when width is a multiple of 512, else 4; NC chunks cover width <= 1024.
+template <typename T, int VW>
+__device__ __forceinline__ void ldv(const T* p, float* o) {
+  if constexpr (VW == 4) {
+    load4<T>(p, o);
+  } else if constexpr (sizeof(T) == 2) {
+    load16_f32<T>(p, o);
+  } else {
+    load16_f32<T>(p, o);
+    load16_f32<T>(p + 4, o + 4);
+  }
+}
+template <typename T, int VW>
+__device__ __forceinline__ void stv(T* p, const float* v) {
+  if constexpr (VW == 4) {
+    store4<T>(p, v[0], v[1], v[2], v[3]);
+  } else if constexpr (sizeof(T) == 2) {
+    store16_f32<T>(p, v);
+  } else {
+    store16_f32<T>(p, v);
+    store16_f32<T>(p + 4, v + 4);
+  }
+}
+
+template <typename TI, typename TO, int VW>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int width, const TI* __restrict__ x,
                                                      int ldx, const int* __restrict__ in_rows,
                                                      const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, TO* __restrict__ out,
                                                      int ldo, float* __restrict__ mean,
                                                      float* __restrict__ rstd) {
+  constexpr int NC = 1024 / (64 * VW);
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= rows) return;
   const int xr = in_rows ? in_rows[r] : r;
   const TI* xp = x + (size_t)xr * ldx;
-  const int nv = width >> 2;  // 4-element vector count
-  f32x4 v[LN_MAXV];
+  const int nv = width / VW;  // vectors per row
+  float v[NC][VW];
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int c = lane + i * 64;
     if (c < nv) {
-      float t4[4];
-      load4<TI>(xp + c * 4, t4);
-      v[i] = (f32x4){t4[0], t4[1], t4[2], t4[3]};
-      s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+      ldv<TI, VW>(xp + c * VW, v[i]);
+#pragma unroll
+      for (int k = 0; k < VW; ++k) s += v[i][k];
     } else {
-      v[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < VW; ++k) v[i][k] = 0.f;
     }
   }
   const float inv_w = 1.0f / (float)width;
   const float mu = wave_sum(s) * inv_w;
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int c = lane + i * 64;
     if (c < nv) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) { const float d = v[i][k] - mu; q += d * d; }
+      for (int k = 0; k < VW; ++k) { const float d = v[i][k] - mu; q += d * d; }
     }
   }
   const float rs = rsqrtf(wave_sum(q) * inv_w + 1e-5f);
   TO* op = out + (size_t)r * ldo;
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int c = lane + i * 64;
     if (c < nv) {
-      const f32x4 gg = reinterpret_cast<const f32x4*>(gamma)[c];
-      const f32x4 bb = reinterpret_cast<const f32x4*>(beta)[c];
-      store4<TO>(op + c * 4, (v[i][0] - mu) * rs * gg[0] + bb[0], (v[i][1] - mu) * rs * gg[1] + bb[1],
-                 (v[i][2] - mu) * rs * gg[2] + bb[2], (v[i][3] - mu) * rs * gg[3] + bb[3]);
+      float gg[VW], bb[VW], o[VW];
+      ldv<float, VW>(gamma + c * VW, gg);
+      ldv<float, VW>(beta + c * VW, bb);
+#pragma unroll
+      for (int k = 0; k < VW; ++k) o[k] = (v[i][k] - mu) * rs * gg[k] + bb[k];
+      stv<TO, VW>(op + c * VW, o);
     }
   }
   if (lane == 0) {
@@ -68,7 +97,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int width, const 
 }
 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)) + dres,   g = dy * gamma
-template <typename TL, typename TD, typename TX>
+template <typename TL, typename TD, typename TX, int VW>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int width, const TD* __restrict__ dy,
                                                      int lddy, const TX* __restrict__ x, int ldx,
                                                      const int* __restrict__ x_rows,
@@ -78,6 +107,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int width, const 
                                                      const float* __restrict__ dres, int lddres,
                                                      float* __restrict__ dx, TL* __restrict__ dx_lp,
                                                      const int* __restrict__ out_rows, int ldo) {
+  constexpr int NC = 1024 / (64 * VW);
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= rows) return;
@@ -86,22 +116,19 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int width, const 
   const float mu = mean[r], rs = rstd[r];
   const TX* xp = x + (size_t)xr * ldx;
   const TD* dp = dy + (size_t)r * lddy;
-  const int nv = width >> 2;
-  f32x4 gv[LN_MAXV], xh[LN_MAXV];
+  const int nv = width / VW;
+  float gv[NC][VW], xh[NC][VW];
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int c = lane + i * 64;
     if (c < nv) {
-      float xva[4];
-      load4<TX>(xp + c * 4, xva);
-      const f32x4 xv = {xva[0], xva[1], xva[2], xva[3]};
-      float dva[4];
-      load4<TD>(dp + c * 4, dva);
-      const f32x4 dv = {dva[0], dva[1], dva[2], dva[3]};
-      const f32x4 gg = reinterpret_cast<const f32x4*>(gamma)[c];
+      float xv[VW], dv[VW], gg[VW];
+      ldv<TX, VW>(xp + c * VW, xv);
+      ldv<TD, VW>(dp + c * VW, dv);
+      ldv<float, VW>(gamma + c * VW, gg);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < VW; ++k) {
         xh[i][k] = (xv[k] - mu) * rs;
         gv[i][k] = dv[k] * gg[k];
         s1 += gv[i][k];
@@ -115,18 +142,20 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int width, const 
   float* op = dx + (size_t)orow * ldo;
   const float* rp = dres ? dres + (size_t)orow * lddres : nullptr;
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int c = lane + i * 64;
     if (c < nv) {
-      f32x4 o;
+      float o[VW];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) o[k] = rs * (gv[i][k] - m1 - xh[i][k] * m2);
+      for (int k = 0; k < VW; ++k) o[k] = rs * (gv[i][k] - m1 - xh[i][k] * m2);
       if (rp) {
-        const f32x4 rv = reinterpret_cast<const f32x4*>(rp)[c];
-        o += rv;
+        float rv[VW];
+        ldv<float, VW>(rp + c * VW, rv);
+#pragma unroll
+        for (int k = 0; k < VW; ++k) o[k] += rv[k];
       }
-      reinterpret_cast<f32x4*>(op)[c] = o;
-      if (dx_lp) store4<TL>(dx_lp + (size_t)orow * ldo + c * 4, o[0], o[1], o[2], o[3]);
+      stv<float, VW>(op + c * VW, o);
+      if (dx_lp) stv<TL, VW>(dx_lp + (size_t)orow * ldo + c * VW, o);
     }
   }
 }
@@ -140,21 +169,21 @@ static int ln_fwd_launch(int out_dtype, int rows, int width, const TI* x, int ld
                          const float* gamma, const float* beta, void* out, int ldo, float* mean, float* rstd,
                          hipStream_t st) {
   dim3 grid((rows + 3) / 4), block(256);
+  const bool v8 = width % 512 == 0 && ldx % 8 == 0 && ldo % 8 == 0;
+#define CLIPK_LNF(TOUT)                                                                                       \
+  if (v8)                                                                                                     \
+    hipLaunchKernelGGL((ln_fwd_kernel<TI, TOUT, 8>), grid, block, 0, st, rows, width, x, ldx, in_rows, gamma, \
+                       beta, (TOUT*)out, ldo, mean, rstd);                                                    \
+  else                                                                                                        \
+    hipLaunchKernelGGL((ln_fwd_kernel<TI, TOUT, 4>), grid, block, 0, st, rows, width, x, ldx, in_rows, gamma, \
+                       beta, (TOUT*)out, ldo, mean, rstd);
   switch (out_dtype) {
-    case CLIPK_F32:
-      hipLaunchKernelGGL((ln_fwd_kernel<TI, float>), grid, block, 0, st, rows, width, x, ldx, in_rows, gamma, beta,
-                         (float*)out, ldo, mean, rstd);
-      break;
-    case CLIPK_F16:
-      hipLaunchKernelGGL((ln_fwd_kernel<TI, f16>), grid, block, 0, st, rows, width, x, ldx, in_rows, gamma, beta,
-                         (f16*)out, ldo, mean, rstd);
-      break;
-    case CLIPK_BF16:
-      hipLaunchKernelGGL((ln_fwd_kernel<TI, bf16>), grid, block, 0, st, rows, width, x, ldx, in_rows, gamma, beta,
-                         (bf16*)out, ldo, mean, rstd);
-      break;
+    case CLIPK_F32: CLIPK_LNF(float) break;
+    case CLIPK_F16: CLIPK_LNF(f16) break;
+    case CLIPK_BF16: CLIPK_LNF(bf16) break;
     default: return CLIPK_EDTYPE;
   }
+#undef CLIPK_LNF
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
 }
@@ -196,18 +225,24 @@ static int ln_bwd_launch(int rows, int width, const void* dy, int lddy, const TX
                          const int* out_rows, int ldo, hipStream_t st) {
   dim3 grid((rows + 3) / 4), block(256);
   const TD* d = (const TD*)dy;
+  const bool v8 = width % 512 == 0 && ldx % 8 == 0 && ldo % 8 == 0 && lddy % 8 == 0 && (!dres || lddres % 8 == 0);
+#define CLIPK_LNB(TLP)                                                                                        \
+  if (v8)                                                                                                     \
+    hipLaunchKernelGGL((ln_bwd_kernel<TLP, TD, TX, 8>), grid, block, 0, st, rows, width, d, lddy, x, ldx,      \
+                       x_rows, gamma, mean, rstd, dres, lddres, dx, (TLP*)dx_lp, out_rows, ldo);              \
+  else                                                                                                        \
+    hipLaunchKernelGGL((ln_bwd_kernel<TLP, TD, TX, 4>), grid, block, 0, st, rows, width, d, lddy, x, ldx,      \
+                       x_rows, gamma, mean, rstd, dres, lddres, dx, (TLP*)dx_lp, out_rows, ldo);
   if (!dx_lp || lp_dtype == CLIPK_F32) {
-    hipLaunchKernelGGL((ln_bwd_kernel<float, TD, TX>), grid, block, 0, st, rows, width, d, lddy, x, ldx,
-                       x_rows, gamma, mean, rstd, dres, lddres, dx, (float*)dx_lp, out_rows, ldo);
+    CLIPK_LNB(float)
   } else if (lp_dtype == CLIPK_BF16) {
-    hipLaunchKernelGGL((ln_bwd_kernel<bf16, TD, TX>), grid, block, 0, st, rows, width, d, lddy, x, ldx,
-                       x_rows, gamma, mean, rstd, dres, lddres, dx, (bf16*)dx_lp, out_rows, ldo);
+    CLIPK_LNB(bf16)
   } else if (lp_dtype == CLIPK_F16) {
-    hipLaunchKernelGGL((ln_bwd_kernel<f16, TD, TX>), grid, block, 0, st, rows, width, d, lddy, x, ldx,
-                       x_rows, gamma, mean, rstd, dres, lddres, dx, (f16*)dx_lp, out_rows, ldo);
+    CLIPK_LNB(f16)
   } else {
     return CLIPK_EDTYPE;
   }
+#undef CLIPK_LNB
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
 }
