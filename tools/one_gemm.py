@@ -7,7 +7,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fsp_amd import ops, _native as N  # noqa: E402
 
-M, W = 88000, 512
+M, W = int(os.environ.get("KB_M", 47160)), 512
 f16, bf = torch.float16, torch.bfloat16
 dev = torch.device("cuda")
 name = sys.argv[1] if len(sys.argv) > 1 else "dgelu"
