@@ -10,7 +10,7 @@ import ctypes
 import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("CLIPK_LIB", os.path.join(_PKG, "libclipk.so"))  # override: A/B builds
+LIB_PATH = os.environ.get("CLIPK_LIB") or os.path.join(_PKG, "libclipk.so")  # override: A/B builds
 
 F32, F16, BF16 = 0, 1, 2
 EPI_BIAS, EPI_BIAS_RES, EPI_BIAS_QGELU, EPI_DQGELU, EPI_NONE = 0, 1, 2, 3, 4

@@ -25,6 +25,9 @@
 
 namespace clipk {
 
+#ifndef CLIPK_XBUD256
+#define CLIPK_XBUD256 8
+#endif
 constexpr int GEMM_ROWB = 128;  // bytes per staged row (BK = 64 halfs / 32 floats)
 constexpr int GEMM_NMIN = 128;  // N granularity accepted by the C-ABI
 constexpr int EPI_SCRATCH = 16 * 64 * 4;  // per-wave epilogue transpose tile [16][64] fp32
@@ -40,6 +43,7 @@ struct GemmArgs {
   unsigned long long* stamp;  // diagnostic (CLIPK_GEMM_STAMP): per block/tile s_memrealtime marks
   int ksplit;                 // split-K slices (non-persistent only); slice s writes out + s*split_stride
   long long split_stride;     // elements of TO between slices' fp32 partial outputs
+  int skew;                   // persistent kernels: ~us of start delay for every other CU of an XCD
 };
 constexpr int STAMP_TILES = 8, STAMP_BLOCKS = 2048;
 
@@ -94,6 +98,37 @@ __device__ __forceinline__ void store_run(TO* p, const float* v) {
   else store4<TO>(p, v[0], v[1], v[2], v[3]);
 }
 
+// Epilogue stores go through a buffer resource spanning the tile's valid rows: a lane whose
+// row is past M stores out of range and the hardware drops it, so no lane branches around
+// its store. (A branch there made the compiler's vmcnt bookkeeping merge a stored / not
+// stored path at every row group and wait vmcnt(0) -- for every earlier store -- in each.)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, long long bytes) {
+  const unsigned n = bytes <= 0 ? 0u : bytes >= 0x7fffffffLL ? 0x7fffffffu : (unsigned)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)n, 0x00020000);
+}
+// 16 bytes of TO (16 / sizeof(TO) fp32 values converted) at byte offset off
+template <typename TO>
+__device__ __forceinline__ void buf_store16(__amdgpu_buffer_rsrc_t r, int off, const float* v) {
+  u32x4 d;
+  if constexpr (sizeof(TO) == 4) {
+    d = __builtin_bit_cast(u32x4, (f32x4){v[0], v[1], v[2], v[3]});
+  } else {
+    typedef TO t8 __attribute__((ext_vector_type(8)));
+    t8 h;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) h[c] = (TO)v[c];
+    d = __builtin_bit_cast(u32x4, h);
+  }
+  __builtin_amdgcn_raw_buffer_store_b128(d, r, off, 0, 0);
+}
+
+// Start skew (knob CLIPK_GEMM_SKEW, ~us): every other CU of each XCD starts late, so that the
+// persistent blocks' store-heavy epilogues stop landing on HBM all at once.
+__device__ __forceinline__ void skew_start(int us, int bid) {
+  if (us > 0 && ((bid >> 3) & 1))
+    for (int i = 0; i < us; ++i) __builtin_amdgcn_s_sleep(32);  // 64 x 32 cycles each
+}
+
 // Block tile BM x BN, WM x WN waves (each (BM/WM) x (BN/WN) = TM x TN 16x16 sub-tiles),
 // 2-stage LDS ring, one barrier per 128-byte K step. PERSIST: the grid is sized to the
 // CU count and each block walks an XCD-contiguous run of tiles; the last K step of a tile
@@ -129,6 +164,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
   const int t_step = PERSIST ? (int)(gridDim.x >> 3) : 1;
   int tile = t_beg + (bid >> 3);
   if (tile >= t_end) return;  // block-uniform
+  if constexpr (PERSIST) skew_start(g.skew, bid);
   const int ks = PERSIST ? 0 : tile / ntiles;
   if (!PERSIST) tile -= ks * ntiles;
 
@@ -204,10 +240,15 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
     constexpr int LPR = 64 / CW, RPQ = 64 / LPR, NQ = 16 / RPQ;
     const int er = lane / LPR, ec = lane % LPR;
     const int ncol = nbase + CW * ec;
-    // residual / aux operands of group i+1 are loaded while group i is transposed and stored
+    // residual / aux operands run XD groups ahead of the group being stored (a register ring
+    // of <= 32 VGPRs): aux h comes from HBM, and one group of lookahead left every group
+    // waiting out a full load latency (dgelu epilogue 8.8 us per 256x256 tile)
     constexpr int XNB = CW * (int)sizeof(TX);
     typedef Raw<XNB> XR;
-    XR ext_nxt[NQ];
+    constexpr int XREG = NQ * XNB / 4;
+    constexpr int XBUD = BM == 192 ? 32 : CLIPK_XBUD256;  // ring VGPRs (256-row tiles: little to spare)
+    constexpr int XD = XBUD / XREG < 1 ? 1 : (XBUD / XREG > TM ? TM : XBUD / XREG);
+    XR extq[XD][NQ];
     auto load_ext = [&](int i, XR* dst) {
       if constexpr (HAS_EXT) {
         const int mg = m0 + wm * (BM / WM) + i * 16;
@@ -233,7 +274,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
         set_tile(next);
         stage(cur ^ 1, 0);  // next tile's first stage flies during this tile's epilogue
       }
-      if (last) load_ext(0, ext_nxt);
+      if (last) load_ext(0, extq[0]);
       const char* As = smem + cur * STAGE + (wm * (BM / WM) + fr) * ROWB;
       const char* Bs = smem + cur * STAGE + OPA + (wn * (BN / WN) + fr) * ROWB;
 #pragma unroll
@@ -273,13 +314,20 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
       }
     }
     float* scr = reinterpret_cast<float*>(smem + 2 * STAGE + w * EPI_SCRATCH);
+    const long long rows_ok = (long long)(g.M - m0 < BM ? g.M - m0 : BM);
+    const __amdgpu_buffer_rsrc_t ro = tile_rsrc(outb + (size_t)m0 * g.ldo, rows_ok * g.ldo * (long long)sizeof(TO));
+    __amdgpu_buffer_rsrc_t ro2 = ro;
+    if constexpr (EPI == CLIPK_EPI_BIAS_QGELU)
+      ro2 = tile_rsrc(g.out2 ? (const TO*)g.out2 + (size_t)m0 * g.ldo : nullptr,
+                      g.out2 ? rows_ok * g.ldo * (long long)sizeof(TO) : 0);
+#pragma unroll
+    for (int d = 1; d < XD; ++d) load_ext(d, extq[d]);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int mg = m0 + wm * (BM / WM) + i * 16;  // first row of this 16-row group
       XR ext[NQ];
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) ext[q] = ext_nxt[q];
-      if (i + 1 < TM) load_ext(i + 1, ext_nxt);
+      for (int q = 0; q < NQ; ++q) ext[q] = extq[i % XD][q];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous group's read-back done
 #pragma unroll
       for (int j = 0; j < TN; ++j)
@@ -295,7 +343,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
           const f32x4 t = *reinterpret_cast<const f32x4*>(scr + rr * 64 + ((((CW / 4) * ec + c) ^ rr) << 2));
           v[4 * c] = t[0]; v[4 * c + 1] = t[1]; v[4 * c + 2] = t[2]; v[4 * c + 3] = t[3];
         }
-        if (m >= g.M) continue;
+        const int off = ((m - m0) * g.ldo + ncol) * (int)sizeof(TO);  // rows >= M: out of range, dropped
         if constexpr (HAS_BIAS) {
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] += bia[c];
@@ -305,22 +353,19 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
           raw_f32<TX, CW>(ext[q], r);
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] += r[c];
-          store_run<TO, CW>(outb + (size_t)m * g.ldo + ncol, v);
         } else if constexpr (EPI == CLIPK_EPI_BIAS_QGELU) {
-          if (g.out2) store_run<TO, CW>((TO*)g.out2 + (size_t)m * g.ldo + ncol, v);
+          buf_store16<TO>(ro2, off, v);  // no-op when out2 is null (zero-sized resource)
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] = quick_gelu(v[c]);
-          store_run<TO, CW>(outb + (size_t)m * g.ldo + ncol, v);
         } else if constexpr (EPI == CLIPK_EPI_DQGELU) {
           float h[CW];
           raw_f32<TX, CW>(ext[q], h);
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] *= quick_gelu_grad(h[c]);
-          store_run<TO, CW>(outb + (size_t)m * g.ldo + ncol, v);
-        } else {
-          store_run<TO, CW>(outb + (size_t)m * g.ldo + ncol, v);
         }
+        buf_store16<TO>(ro, off, v);
       }
+      if (i + XD < TM) load_ext(i + XD, extq[i % XD]);  // this group's slot is free again
     }
     if (stp && ti < STAMP_TILES) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -337,6 +382,273 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+}
+
+// ---- 8-phase ping-pong schedule (cfg 7) ---------------------------------------------------
+// 256x256 tile, 8 waves as two groups of four (wave row wm = 0 / 1, each wave 128x64 as in
+// gemm_nt_kernel), BK = 64 halfs (128-B staged rows). One K-tile is staged as four 16-KiB
+// half-tiles: A0 / A1 = the first / second 64 rows of each group's 128-row band, B0 / B1 =
+// the first / second 32 columns of each wave's 64-column band, so that every phase reads
+// whole half-tiles and a half-tile can be restaged as soon as its readers are done:
+//   phase 1: read B0, A0    MFMA quadrant (A0,B0)    stage A1 of K-tile s+1
+//   phase 2: read B1        MFMA quadrant (A0,B1)    stage A0 of K-tile s+2
+//   phase 3: read A1        MFMA quadrant (A1,B1)    stage B0 of K-tile s+2
+//   phase 4: (registers)    MFMA quadrant (A1,B0)    stage B1 of K-tile s+2; vmcnt(6)
+// A phase is {ds_reads, one half-tile of global_load_lds (2 per thread), lgkmcnt(0)} ->
+// barrier -> 16 MFMAs -> barrier. Group 1 runs one barrier behind group 0, so on each SIMD
+// one group's MFMA cluster overlaps the other group's LDS reads and load issue, and the
+// counted vmcnt keeps three half-tiles (48 KiB) in flight across barriers: never drained in
+// the loop. The K-tile stream runs on across the block's output tiles, so the next tile's
+// first K-tiles land during the epilogue (both groups run it together: one extra barrier
+// each side re-aligns and then re-staggers them).
+// Hazards (barrier pairing: group 0's phase-p first barrier is group 1's phase-(p-1) second):
+// RAW -- every wave's vmcnt for a K-tile precedes a barrier that each reader passes before
+// its first read (the wait is in phase 4, the reads from the next phase 1 on); WAR -- a
+// half-tile is restaged >= 1 phase after the phase that read it, whose reads every wave has
+// retired (lgkmcnt(0)) before that phase's first barrier.
+#define G8_BAR()                       \
+  do {                                 \
+    __builtin_amdgcn_sched_barrier(0); \
+    __builtin_amdgcn_s_barrier();      \
+    __builtin_amdgcn_sched_barrier(0); \
+  } while (0)
+
+template <typename T, typename TO, typename TX, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
+  constexpr int BM = 256, BN = 256, ROWB = 128, HALF = 128 * ROWB, BUF = 4 * HALF;
+  __shared__ CLIPK_LDS_ALIGN char smem[2 * BUF + 8 * EPI_SCRATCH];  // one array (see header)
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  const int ntn = g.N / BN, ntm = (g.M + BM - 1) / BM, ntiles = ntm * ntn;
+  const int bid = blockIdx.x, xcd = bid & 7, q = ntiles >> 3, r = ntiles & 7;
+  const int t_beg = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  const int t_end = t_beg + (xcd < r ? q + 1 : q);
+  const int t_step = (int)(gridDim.x >> 3);
+  const int tfirst = t_beg + (bid >> 3);
+  if (tfirst >= t_end) return;  // block-uniform, before any barrier
+  skew_start(g.skew, bid);
+  const int nk = (int)((size_t)g.K * sizeof(T) / ROWB);
+  const int total = ((t_end - tfirst + t_step - 1) / t_step) * nk;  // K-tiles this block streams
+
+  // staging geometry: thread (w, lane) fills slot srow (+64 in round 1) at 16-B chunk lane&7
+  // of its 128-B row; the chunk is swizzled on the source side (slot bits 1..3)
+  const int srow = w * 8 + (lane >> 3);
+  const int pc = ((lane & 7) ^ ((srow >> 1) & 7)) * 16;
+  const int bcol = (srow >> 5) * 64 + (srow & 31);  // B: tile column of slot srow (half 0, round 0)
+  auto kpos = [&](int s, int& tm0, int& tn0, int& kt) {
+    const int tl = s / nk;
+    kt = s - tl * nk;
+    const int tile = tfirst + tl * t_step;
+    tm0 = (tile / ntn) * BM;
+    tn0 = (tile % ntn) * BN;
+  };
+  auto stageA = [&](int s, int tm0, int kt, int hh) {  // A rows i*128 + hh*64 + srow
+    char* dst = smem + (s & 1) * BUF + hh * HALF + w * 1024;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int row = tm0 + i * 128 + hh * 64 + srow;
+      row = row < g.M ? row : g.M - 1;
+      glds16(g.A + ((size_t)row * g.lda + (size_t)kt * (ROWB / sizeof(T))) * sizeof(T) + pc, dst + i * 8192);
+    }
+  };
+  auto stageB = [&](int s, int tn0, int kt, int hh) {  // B cols (2i + w/4)*64 + hh*32 + srow%32
+    char* dst = smem + (s & 1) * BUF + (2 + hh) * HALF + w * 1024;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int col = tn0 + i * 128 + hh * 32 + bcol;
+      glds16(g.B + ((size_t)col * g.ldb + (size_t)kt * (ROWB / sizeof(T))) * sizeof(T) + pc, dst + i * 8192);
+    }
+  };
+
+  const int fr = lane & 15, fq = lane >> 4, sw = (fr >> 1) & 7;
+  auto rdA = [&](const char* base, u32x4 (&a)[4][2]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        a[i][kk] = *reinterpret_cast<const u32x4*>(base + (wm * 64 + i * 16 + fr) * ROWB + (((kk * 4 + fq) ^ sw) << 4));
+  };
+  auto rdB = [&](const char* base, u32x4 (&b)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        b[j][kk] = *reinterpret_cast<const u32x4*>(base + (wn * 32 + j * 16 + fr) * ROWB + (((kk * 4 + fq) ^ sw) << 4));
+  };
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#define G8_MMA(A_, B_, HA, HB)                                                                        \
+  do {                                                                                                \
+    __builtin_amdgcn_s_setprio(1);                                                                    \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                     \
+    _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                     \
+    _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                                  \
+      acc[(HA) * 4 + i][(HB) * 2 + j] = mma<T>(B_[j][kk], A_[i][kk], acc[(HA) * 4 + i][(HB) * 2 + j]); \
+    __builtin_amdgcn_s_setprio(0);                                                                    \
+  } while (0)
+
+  // ---- epilogue of one output tile (per-wave LDS transpose, as gemm_nt_kernel) ----
+  constexpr bool HAS_BIAS = EPI == CLIPK_EPI_BIAS || EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_BIAS_QGELU;
+  constexpr bool HAS_EXT = EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU;
+  constexpr int CW = sizeof(TO) == 2 ? 8 : 4;
+  constexpr int LPR = 64 / CW, RPQ = 64 / LPR, NQ = 16 / RPQ;
+  constexpr int XNB = CW * (int)sizeof(TX);
+  typedef Raw<XNB> XR;
+  const int er = lane / LPR, ec = lane % LPR;
+  float* scr = reinterpret_cast<float*>(smem + 2 * BUF + w * EPI_SCRATCH);
+  auto epilogue = [&](int m0, int n0) {
+    const int ncol = n0 + wn * 64 + CW * ec;
+    XR ext_nxt[NQ];
+    auto load_ext = [&](int i, XR* dst) {
+      if constexpr (HAS_EXT) {
+        const int mg = m0 + wm * 128 + i * 16;
+#pragma unroll
+        for (int q2 = 0; q2 < NQ; ++q2) {
+          int mc = mg + RPQ * q2 + er;
+          mc = mc < g.M ? mc : g.M - 1;
+          if constexpr (EPI == CLIPK_EPI_BIAS_RES)
+            ld_raw<XNB>((const TX*)g.res + (size_t)mc * g.ldr + ncol, dst[q2]);
+          else
+            ld_raw<XNB>((const TX*)g.aux + (size_t)mc * g.ldaux + ncol, dst[q2]);
+        }
+      }
+    };
+    load_ext(0, ext_nxt);
+    const long long rows_ok = (long long)(g.M - m0 < BM ? g.M - m0 : BM);
+    const __amdgpu_buffer_rsrc_t ro = tile_rsrc((const TO*)g.out + (size_t)m0 * g.ldo,
+                                                rows_ok * g.ldo * (long long)sizeof(TO));
+    __amdgpu_buffer_rsrc_t ro2 = ro;
+    if constexpr (EPI == CLIPK_EPI_BIAS_QGELU)
+      ro2 = tile_rsrc(g.out2 ? (const TO*)g.out2 + (size_t)m0 * g.ldo : nullptr,
+                      g.out2 ? rows_ok * g.ldo * (long long)sizeof(TO) : 0);
+    float bia[CW];
+#pragma unroll
+    for (int c = 0; c < CW; ++c) bia[c] = 0.f;
+    if constexpr (HAS_BIAS) {
+#pragma unroll
+      for (int c = 0; c < CW; c += 4) {
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(g.bias + ncol + c);
+        bia[c] = b4[0]; bia[c + 1] = b4[1]; bia[c + 2] = b4[2]; bia[c + 3] = b4[3];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int mg = m0 + wm * 128 + i * 16;
+      XR ext[NQ];
+#pragma unroll
+      for (int q2 = 0; q2 < NQ; ++q2) ext[q2] = ext_nxt[q2];
+      if (i + 1 < 8) load_ext(i + 1, ext_nxt);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<f32x4*>(scr + fr * 64 + (((4 * j + fq) ^ fr) << 2)) = acc[i][j];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int q2 = 0; q2 < NQ; ++q2) {
+        const int rr = RPQ * q2 + er;
+        const int m = mg + rr;
+        float v[CW];
+#pragma unroll
+        for (int c = 0; c < CW / 4; ++c) {
+          const f32x4 t = *reinterpret_cast<const f32x4*>(scr + rr * 64 + ((((CW / 4) * ec + c) ^ rr) << 2));
+          v[4 * c] = t[0]; v[4 * c + 1] = t[1]; v[4 * c + 2] = t[2]; v[4 * c + 3] = t[3];
+        }
+        const int off = ((m - m0) * g.ldo + ncol) * (int)sizeof(TO);  // rows >= M: dropped
+        if constexpr (HAS_BIAS) {
+#pragma unroll
+          for (int c = 0; c < CW; ++c) v[c] += bia[c];
+        }
+        if constexpr (EPI == CLIPK_EPI_BIAS_RES) {
+          float rv[CW];
+          raw_f32<TX, CW>(ext[q2], rv);
+#pragma unroll
+          for (int c = 0; c < CW; ++c) v[c] += rv[c];
+        } else if constexpr (EPI == CLIPK_EPI_BIAS_QGELU) {
+          buf_store16<TO>(ro2, off, v);
+#pragma unroll
+          for (int c = 0; c < CW; ++c) v[c] = quick_gelu(v[c]);
+        } else if constexpr (EPI == CLIPK_EPI_DQGELU) {
+          float h[CW];
+          raw_f32<TX, CW>(ext[q2], h);
+#pragma unroll
+          for (int c = 0; c < CW; ++c) v[c] *= quick_gelu_grad(h[c]);
+        }
+        buf_store16<TO>(ro, off, v);
+      }
+    }
+  };
+
+  // ---- prologue: K-tile 0 whole, K-tile 1 but its A1 (staged by K-tile 0's phase 1) ----
+  int c_m0, c_n0, c_kt;  // the K-tile being computed
+  kpos(0, c_m0, c_n0, c_kt);
+  stageA(0, c_m0, c_kt, 0); stageB(0, c_n0, c_kt, 0); stageB(0, c_n0, c_kt, 1); stageA(0, c_m0, c_kt, 1);
+  if (total > 1) {
+    int m1, n1, k1;
+    kpos(1, m1, n1, k1);
+    stageA(1, m1, k1, 0); stageB(1, n1, k1, 0); stageB(1, n1, k1, 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  G8_BAR();
+  if (wm) G8_BAR();  // group 1 runs one barrier behind
+
+  u32x4 a0[4][2], a1[4][2], b0[2][2], b1[2][2];
+  for (int s = 0; s < total; ++s) {
+    const char* buf = smem + (s & 1) * BUF;
+    const bool n1 = s + 1 < total, n2 = s + 2 < total;
+    int m1 = 0, nn1 = 0, k1 = 0, m2 = 0, nn2 = 0, k2 = 0;
+    if (n1) kpos(s + 1, m1, nn1, k1);
+    if (n2) kpos(s + 2, m2, nn2, k2);
+    // phase 1
+    rdB(buf + 2 * HALF, b0);
+    rdA(buf, a0);
+    if (n1) stageA(s + 1, m1, k1, 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    G8_BAR();
+    G8_MMA(a0, b0, 0, 0);
+    G8_BAR();
+    // phase 2
+    rdB(buf + 3 * HALF, b1);
+    if (n2) stageA(s + 2, m2, k2, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    G8_BAR();
+    G8_MMA(a0, b1, 0, 1);
+    G8_BAR();
+    // phase 3
+    rdA(buf + HALF, a1);
+    if (n2) stageB(s + 2, nn2, k2, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    G8_BAR();
+    G8_MMA(a1, b1, 1, 1);
+    G8_BAR();
+    // phase 4: K-tile s+1 must have landed before the next phase 1 reads it
+    if (n2) {
+      stageB(s + 2, nn2, k2, 1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    G8_BAR();
+    G8_MMA(a1, b0, 1, 0);
+    G8_BAR();
+    if (c_kt == nk - 1) {
+      if (!wm) G8_BAR();  // wait for group 1's last MFMA cluster: both groups store together
+      epilogue(c_m0, c_n0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (wm) G8_BAR();  // re-stagger
+    }
+    c_m0 = m1; c_n0 = nn1; c_kt = k1;
+  }
+  if (!wm) G8_BAR();  // balance group 1's extra barrier
+#undef G8_MMA
 }
 
 // Tile configurations: 0 = 128x128 (4 waves, 64 KiB LDS, 2 blocks/CU),
@@ -357,7 +669,8 @@ static int pick_cfg(int M, int N, int esz) {
   }
   if (esz == 4) return 0;  // fp32 parity path: one configuration
   if (g_force_cfg >= 0) {
-    if ((g_force_cfg == 1 || g_force_cfg == 3 || g_force_cfg == 5 || g_force_cfg == 6) && N % 256 == 0)
+    if ((g_force_cfg == 1 || g_force_cfg == 3 || g_force_cfg == 5 || g_force_cfg == 6 || g_force_cfg == 7) &&
+        N % 256 == 0)
       return g_force_cfg;
     if (g_force_cfg == 2 || g_force_cfg == 4) return g_force_cfg;
     return 0;
@@ -385,6 +698,7 @@ static unsigned long long* gemm_stamp_buf() {
   return g_stamp;
 }
 
+static int g_skew = -1;
 static int g_num_cus = 0;
 static int num_cus() {
   if (!g_num_cus) {
@@ -402,11 +716,22 @@ template <typename T, typename TO, typename TX, int EPI>
 static int launch_gemm(const GemmArgs& g, hipStream_t st) {
   const int cfg = pick_cfg(g.M, g.N, (int)sizeof(T));
   const_cast<GemmArgs&>(g).stamp = gemm_stamp_buf();
+  if (g_skew < 0) {
+    const char* e = getenv("CLIPK_GEMM_SKEW");
+    g_skew = e ? atoi(e) : 0;
+  }
+  const_cast<GemmArgs&>(g).skew = g_skew;
   if constexpr (sizeof(T) == 4) {
     const int nwg = ((g.M + 127) / 128) * (g.N / 128);
     hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 128, 2, 2, false>), dim3(nwg), dim3(256), 0, st, g);
   } else {
-    if (cfg == 1 || cfg == 3) {
+    if (cfg == 7) {
+      // 8-phase ping-pong, persistent: at most one block per CU, grid a multiple of 8 (XCD groups)
+      const int nwg = ((g.M + 255) / 256) * (g.N / 256);
+      const int cus = num_cus();
+      const int grid = nwg < cus ? ((nwg + 7) / 8) * 8 : (cus / 8) * 8;
+      hipLaunchKernelGGL((gemm8_kernel<T, TO, TX, EPI>), dim3(grid), dim3(512), 0, st, g);
+    } else if (cfg == 1 || cfg == 3) {
       const int nwg = ((g.M + 255) / 256) * (g.N / 256);
       const int cus = num_cus();
       if (cfg == 1 && nwg > 2 * cus) {
@@ -647,7 +972,7 @@ extern "C" int clipk_gemm_stamps(void* host, size_t bytes) {
 
 // Benchmark knob: force a tile configuration (-1 = automatic choice).
 extern "C" int clipk_gemm_set_config(int cfg) {
-  if (cfg < -1 || cfg > 6) return CLIPK_EINVAL;
+  if (cfg < -1 || cfg > 7) return CLIPK_EINVAL;
   g_force_cfg = cfg;
   return CLIPK_OK;
 }

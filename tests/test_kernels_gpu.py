@@ -229,7 +229,7 @@ def test_meta_net_and_sgd(dev):
     close(p, pr.detach(), torch.float32, "sgd")
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("Nn,K", [(2048, 512), (512, 2048)])
 def test_gemm_large_m_every_config(dev, cfg, Nn, K):
     """Bench-scale M (persistent / ring paths engage when tiles > 2x CUs) vs torch fp32."""
@@ -261,8 +261,35 @@ def test_gemm_large_m_every_config(dev, cfg, Nn, K):
         lib.clipk_gemm_set_config(-1)
 
 
+@pytest.mark.parametrize("M,Nn,K", [(1, 256, 64), (255, 512, 128), (1000, 256, 192), (3000, 768, 64),
+                                     (9000, 1536, 512)])
+def test_gemm_8phase_edges(dev, M, Nn, K):
+    """cfg 7 (8-phase ping-pong): single-K-tile streams, partial row tiles, grids smaller than
+    the CU count, odd K-tile counts; fp32 / 16-bit outputs, 16-bit residual."""
+    lib = N.load()
+    g = torch.Generator(device="cpu").manual_seed(M + Nn + K)
+    A = torch.randn(M, K, generator=g).to(dev).to(torch.float16)
+    B = (torch.randn(Nn, K, generator=g) / math.sqrt(K)).to(dev).to(torch.float16)
+    bias = torch.randn(Nn, generator=g).to(dev)
+    res = torch.randn(M, Nn, generator=g).to(dev).to(torch.float16)
+    ref = A.float() @ B.float().t()
+    try:
+        N.check(lib.clipk_gemm_set_config(7), "set_config")
+        close(ops.gemm(A, B, N.EPI_NONE, torch.float32), ref, torch.float16, "8ph none")
+        close(ops.gemm(A, B, N.EPI_BIAS_RES, torch.float16, bias=bias, res=res), ref + bias + res.float(),
+              torch.float16, "8ph res16")
+        gq, hq = ops.gemm(A, B, N.EPI_BIAS_QGELU, torch.float16, bias=bias, want_out2=True)
+        hr = ref + bias
+        close(hq, hr, torch.float16, "8ph qgelu.h")
+        close(gq, hr * torch.sigmoid(1.702 * hr), torch.float16, "8ph qgelu.g")
+        close(ops.gemm(A, B, N.EPI_BIAS_QGELU, torch.float16, bias=bias), hr * torch.sigmoid(1.702 * hr),
+              torch.float16, "8ph qgelu no h")
+    finally:
+        lib.clipk_gemm_set_config(-1)
+
+
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("M,Nn,K,splits", [(1576, 768, 3072, 0), (1576, 768, 768, 0), (1576, 2304, 768, 2),
+@pytest.mark.parametrize("M,Nn,K,splits",[(1576, 768, 3072, 0), (1576, 768, 768, 0), (1576, 2304, 768, 2),
                                            (300, 256, 512, 3)])
 def test_gemm_splitk(dev, dtype, M, Nn, K, splits):
     """Split-K (ViT at small batch) vs torch fp32, every epilogue; slice-order sum is

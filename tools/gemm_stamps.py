@@ -50,6 +50,11 @@ def main():
     run("plain f16  N2048 K512", lambda: ops.gemm(a, b, N.EPI_NONE, torch.float16))
     run("plain f32  N2048 K512", lambda: ops.gemm(a, b, N.EPI_NONE, torch.float32))
     run("qgelu+h    N2048 K512", lambda: ops.gemm(a, b, N.EPI_BIAS_QGELU, torch.float16, bias=bias, want_out2=True))
+    bb, ab = rnd(2048, 512, dt=torch.bfloat16), rnd(M, 512, dt=torch.bfloat16)
+    aux = rnd(M, 2048)
+    run("dgelu bf16 N2048 K512", lambda: ops.gemm(ab, bb, N.EPI_DQGELU, torch.bfloat16, aux=aux))
+    af, bfc = rnd(M, 2048, dt=torch.bfloat16), rnd(512, 2048, dt=torch.bfloat16)
+    run("fcbwd bf16 N512 K2048 ", lambda: ops.gemm(af, bfc, N.EPI_NONE, torch.float32))
     a4, b4 = rnd(M, 2048), rnd(2048, 2048)
     run("plain f16  N2048 K2048", lambda: ops.gemm(a4, b4, N.EPI_NONE, torch.float16))
 
