@@ -25,6 +25,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "CoCoOp ViT-B/16 16-shot train-step images/sec at 1/2/4/8 GPUs; eval images/sec"
 PEAK = {"fp16": 2500.0, "bf16": 2500.0, "amp": 2500.0, "fp32": 157.3}  # dense TFLOP/s (MI355X guide)
+HBM_PEAK_GBS = 8000.0  # HBM3E, MI355X_MICROARCH.md
 
 
 def flops(arch, n_cls, L):
@@ -176,17 +177,29 @@ def main():
             peak = PEAK[args.prec if args.prec != "fp16" else "bf16"]  # dgelu GEMM runs on bf16 operands
             traffic = pmc_traffic(ROOF_KERNEL) if (args.arch, args.classes, args.batch, args.prec) == \
                 ("ViT-B/16", 1000, 8, "fp16") else None
-            roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                    "frac": round(ach / peak, 4), "traffic": traffic,
-                    "traffic_note": "HBM bytes/launch, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (profiles/r01_pmc); "
-                                    "algorithmic bytes/launch %.3g" % (
-                                        2 * args.batch * (lay.rows_per_group if lay.pack is not None else args.classes * L)
-                                        * (arch.transformer_width + 4 * arch.transformer_width * 2)
-                                        + 2 * 4 * arch.transformer_width ** 2),
+            # algorithmic bytes per launch: A [M,W] + aux h [M,4W] read, out [M,4W] written (16-bit),
+            # weight [4W,W] read once
+            rows = args.batch * (lay.rows_per_group if lay.pack is not None else args.classes * L)
+            W = arch.transformer_width
+            esz = 4 if args.prec == "fp32" else 2
+            abytes = esz * (rows * (W + 4 * W * 2) + 4 * W * W)
+            # the binding roofline: the longer of FLOPs at the MFMA peak and bytes at the HBM peak
+            hbm_bound = abytes / (HBM_PEAK_GBS * 1e9) > fl / (peak * 1e12)
+            if hbm_bound:
+                achb = abytes / (avg_ms * 1e-3) / 1e9
+                roof = {"bound": "hbm", "achieved": round(achb, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achb / HBM_PEAK_GBS, 4)}
+            else:
+                roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+                        "frac": round(ach / peak, 4)}
+            roof.update({"traffic": traffic, "algorithmic_bytes": abytes, "mfma_tflops": round(ach, 2),
+                    "mfma_frac": round(ach / peak, 4),
+                    "traffic_note": "traffic = HBM bytes/launch, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
+                                    "(profiles/r01_pmc)",
                     "kernel": "gemm_nt_kernel<bf16,bf16,f16,EPI_DQGELU> (text c_proj input-grad GEMM fused with "
                               "QuickGELU'(h), M=text rows, N=4W, K=W)",
                     "avg_launch_ms": round(avg_ms, 4), "launches": cnt.value,
-                    "flops_per_launch": fl}
+                    "flops_per_launch": fl})
     tmax = dist.max_over_ranks(t)
 
     # eval images/sec (forward only, reference test batch 100)
