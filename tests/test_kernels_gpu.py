@@ -229,7 +229,7 @@ def test_meta_net_and_sgd(dev):
     close(p, pr.detach(), torch.float32, "sgd")
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("Nn,K", [(2048, 512), (512, 2048)])
 def test_gemm_large_m_every_config(dev, cfg, Nn, K):
     """Bench-scale M (persistent / ring paths engage when tiles > 2x CUs) vs torch fp32."""
@@ -263,9 +263,11 @@ def test_gemm_large_m_every_config(dev, cfg, Nn, K):
 
 @pytest.mark.parametrize("M,Nn,K", [(1, 256, 64), (255, 512, 128), (1000, 256, 192), (3000, 768, 64),
                                      (9000, 1536, 512)])
-def test_gemm_8phase_edges(dev, M, Nn, K):
-    """cfg 7 (8-phase ping-pong): single-K-tile streams, partial row tiles, grids smaller than
-    the CU count, odd K-tile counts; fp32 / 16-bit outputs, 16-bit residual."""
+@pytest.mark.parametrize("cfg", [7, 8, 9])
+def test_gemm_stream_edges(dev, cfg, M, Nn, K):
+    """Persistent K-step-stream kernels -- cfg 7 (8-phase ping-pong), 8 / 9 (deep-A ring, 256 /
+    192 rows): single-K-tile streams, partial row tiles, grids smaller than the CU count, odd
+    K-tile counts; fp32 / 16-bit outputs, 16-bit residual."""
     lib = N.load()
     g = torch.Generator(device="cpu").manual_seed(M + Nn + K)
     A = torch.randn(M, K, generator=g).to(dev).to(torch.float16)
@@ -274,7 +276,7 @@ def test_gemm_8phase_edges(dev, M, Nn, K):
     res = torch.randn(M, Nn, generator=g).to(dev).to(torch.float16)
     ref = A.float() @ B.float().t()
     try:
-        N.check(lib.clipk_gemm_set_config(7), "set_config")
+        N.check(lib.clipk_gemm_set_config(cfg), "set_config")
         close(ops.gemm(A, B, N.EPI_NONE, torch.float32), ref, torch.float16, "8ph none")
         close(ops.gemm(A, B, N.EPI_BIAS_RES, torch.float16, bias=bias, res=res), ref + bias + res.float(),
               torch.float16, "8ph res16")
