@@ -75,3 +75,31 @@ def base_new_accuracy(preds, labels, n_base):
     acc_n = 100.0 * np.mean(preds[~base] == labels[~base]) if (~base).any() else 0.0
     hm = 2 * acc_b * acc_n / (acc_b + acc_n) if acc_b + acc_n > 0 else 0.0
     return acc_b, acc_n, hm
+
+
+class LossSummary(dict):
+    """The trainers' per-step loss summary (reference: ``{"loss": loss.item()}``,
+    PromptSRC/trainers/coop.py:461 / cocoop.py:333) holding detached device scalars and converting them
+    on access, so a training step does not stall the host on the GPU every batch; values
+    read through ``[]`` / ``items()`` / ``repr`` are the same Python floats."""
+
+    def __setitem__(self, k, v):
+        super().__setitem__(k, v.detach() if torch.is_tensor(v) else v)
+
+    def __getitem__(self, k):
+        v = super().__getitem__(k)
+        return v.item() if torch.is_tensor(v) else v
+
+    def get(self, k, default=None):
+        return self[k] if k in self else default
+
+    def items(self):
+        return [(k, self[k]) for k in self.keys()]
+
+    def values(self):
+        return [self[k] for k in self.keys()]
+
+    def __repr__(self):
+        return repr(dict(self.items()))
+
+    __str__ = __repr__

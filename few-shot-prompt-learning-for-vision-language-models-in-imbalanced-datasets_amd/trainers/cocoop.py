@@ -19,6 +19,7 @@ import torch.nn as nn
 from ..engine.registry import TRAINER_REGISTRY
 from ..engine.trainer import TrainerX, load_clip
 from ..engine.optim import build_optimizer, build_lr_scheduler
+from ..engine.metrics import LossSummary
 from ..clip.model import TextEncodeFn
 from ._fns import PromptAssembleFn, CosineLogitsFn, MetaNetFn
 from .losses import CrossEntropyLoss, MultiClassFocalLoss, focal_alpha
@@ -154,7 +155,8 @@ class CoCoOp(TrainerX):
         loss.backward()
         self.allreduce_grads(self.model.prompt_learner)
         self.optim.step()
-        loss_summary = {"loss": loss.item()}
+        loss_summary = LossSummary()
+        loss_summary["loss"] = loss
         if (self.batch_idx + 1) == self.num_batches:
             self.update_lr()
         return loss_summary

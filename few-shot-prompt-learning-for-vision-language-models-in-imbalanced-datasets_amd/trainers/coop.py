@@ -18,7 +18,7 @@ import torch.nn as nn
 from ..engine.registry import TRAINER_REGISTRY
 from ..engine.trainer import TrainerX, load_clip
 from ..engine.optim import build_optimizer, build_lr_scheduler
-from ..engine.metrics import compute_accuracy
+from ..engine.metrics import compute_accuracy, LossSummary
 from ..clip.model import TextEncodeFn
 from ._fns import PromptAssembleFn, CosineLogitsFn
 from .losses import CrossEntropyLoss, MultiClassFocalLoss, LogitsNTXentLoss, focal_alpha
@@ -168,12 +168,13 @@ class CoOp(TrainerX):
         loss.backward()
         self.allreduce_grads(self.model.prompt_learner)
         self.optim.step()
-        loss_summary = {"loss": loss.item()}
+        loss_summary = LossSummary()
+        loss_summary["loss"] = loss
         if lbl is not None and x2 is None and self.model.loss_type == "ce":
             # coop.py:464-469: acc from a second forward AFTER the step
             with torch.no_grad():
                 logits_eval = self.model(x1, lbl=None, img2=None)
-                loss_summary["acc"] = compute_accuracy(logits_eval, lbl)[0].item()
+                loss_summary["acc"] = compute_accuracy(logits_eval, lbl)[0]
         if (self.batch_idx + 1) == self.num_batches:
             self.update_lr()
         return loss_summary
