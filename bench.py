@@ -38,7 +38,7 @@ def flops(arch, n_cls, L):
     return f_img, f_txt, b_txt
 
 
-ROOF_KERNEL = "gemm_nt_kernelIDF16bDF16bDF16_Li3ELi256ELi256"  # EPI_DQGELU bf16 persistent 256x256
+ROOF_KERNEL = "gemm_nt_kernelIDF16_DF16_DF16_Li3ELi256ELi256"  # EPI_DQGELU fp16 persistent 256x256
 PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc", "traffic.json")
 
 
@@ -174,7 +174,7 @@ def main():
             avg_ms = tot.value / cnt.value
             fl = work.value / cnt.value
             ach = fl / (avg_ms * 1e-3) / 1e12
-            peak = PEAK[args.prec if args.prec != "fp16" else "bf16"]  # dgelu GEMM runs on bf16 operands
+            peak = PEAK[args.prec]  # dgelu GEMM operands: the gradient dtype (fp16 under PREC fp16)
             traffic = pmc_traffic(ROOF_KERNEL) if (args.arch, args.classes, args.batch, args.prec) == \
                 ("ViT-B/16", 1000, 8, "fp16") else None
             # algorithmic bytes per launch: A [M,W] + aux h [M,4W] read, out [M,4W] written (16-bit),
@@ -196,7 +196,7 @@ def main():
                     "mfma_frac": round(ach / peak, 4),
                     "traffic_note": "traffic = HBM bytes/launch, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
                                     "(profiles/r01_pmc)",
-                    "kernel": "gemm_nt_kernel<bf16,bf16,f16,EPI_DQGELU> (text c_proj input-grad GEMM fused with "
+                    "kernel": "gemm_nt_kernel<f16,f16,f16,EPI_DQGELU> (text c_proj input-grad GEMM fused with "
                               "QuickGELU'(h), M=text rows, N=4W, K=W)",
                     "avg_launch_ms": round(avg_ms, 4), "launches": cnt.value,
                     "flops_per_launch": fl})

@@ -39,6 +39,7 @@ SIGNATURES = {
     "clipk_layernorm_bwd": (_I, [_I, _I, _I, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P]),
     "clipk_layernorm_fwd_x": (_I, [_I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P]),
     "clipk_layernorm_bwd_x": (_I, [_I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P]),
+    "clipk_layernorm_bwd_x2": (_I, [_I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P, _I, _P, _I, _P]),
     "clipk_attention_fwd": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P]),
     "clipk_attention_bwd": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _I, _P, _P, _I, _P]),
     "clipk_im2col": (_I, [_I, _I, _I, _I, _I, _P, _P, _P]),

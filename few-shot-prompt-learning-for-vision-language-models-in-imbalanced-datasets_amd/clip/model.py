@@ -29,10 +29,24 @@ from .synth import ClipArch
 
 PREC_DTYPES = {
     "fp32": (torch.float32, torch.float32),
-    "fp16": (torch.float16, torch.bfloat16),
+    "fp16": (torch.float16, torch.float16),
     "amp": (torch.float16, torch.bfloat16),
     "bf16": (torch.bfloat16, torch.bfloat16),
 }
+
+
+
+def prec_dtypes(prec):
+    """(activation dtype, text-backward gradient dtype) of a PREC. PREC fp16 backpropagates in
+    fp16 as the reference's fp16 model does (PromptSRC/trainers/cocoop.py:277-280: the CLIP
+    weights stay half unless PREC is fp32/amp, so autograd runs in half); CLIPK_GRAD_BF16=1
+    switches its gradients to bf16 (more range, less precision)."""
+    import os
+    act, grad = PREC_DTYPES[prec]
+    if prec == "fp16" and os.environ.get("CLIPK_GRAD_BF16", "0") not in ("", "0"):
+        grad = torch.bfloat16
+    return act, grad
+
 
 _LAYER_KEYS = ["ln_1.weight", "ln_1.bias", "attn.in_proj_weight", "attn.in_proj_bias",
                "attn.out_proj.weight", "attn.out_proj.bias", "ln_2.weight", "ln_2.bias",
@@ -101,7 +115,7 @@ class TextEncoderCore(_Encoder):
     """Packed text transformer + ln_final + projection; native fwd / input-grad bwd."""
 
     def __init__(self, sd, arch: ClipArch, prec: str, device, with_grad: bool = True):
-        act, grad = PREC_DTYPES[prec]
+        act, grad = prec_dtypes(prec)
         self.arch, self.prec, self.device = arch, prec, torch.device(device)
         self.act, self.grad = act, grad
         W, nl = arch.transformer_width, arch.transformer_layers

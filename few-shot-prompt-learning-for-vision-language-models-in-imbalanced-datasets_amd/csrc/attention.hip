@@ -303,7 +303,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma16(int nseq, int L, int H, i
                                                        const TG* __restrict__ dout, int lddo,
                                                        const float* __restrict__ lse,
                                                        TG* __restrict__ dqkv, int lddq) {
-  static_assert(__is_same(TG, bf16), "MFMA attention backward computes in bf16");
+  static_assert(sizeof(T) == 2 && sizeof(TG) == 2, "MFMA attention backward: 16-bit operands, math in TG");
   __shared__ CLIPK_LDS_ALIGN short tiles[4][3][16 * TRS];  // per wave: Q, K, dO (bf16)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
@@ -333,11 +333,11 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma16(int nseq, int L, int H, i
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
     const int c = 8 * g4 + 32 * kk;
-    const s16x8 qb = to_bf16x8<T>(q[kk]), kb = to_bf16x8<T>(k[kk]);
+    const s16x8 qb = to_g8<T, TG>(q[kk]), kb = to_g8<T, TG>(k[kk]);
     *reinterpret_cast<s16x8*>(tQ + r16 * TRS + c) = qb;
     *reinterpret_cast<s16x8*>(tK + r16 * TRS + c) = kb;
     *reinterpret_cast<s16x8*>(tD + r16 * TRS + c) = d[kk];
-    v[kk] = to_bf16x8<T>(v[kk]);
+    v[kk] = to_g8<T, TG>(v[kk]);
     q[kk] = qb;
     k[kk] = kb;
   }
@@ -345,10 +345,10 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma16(int nseq, int L, int H, i
   f32x4 s1 = {0, 0, 0, 0}, s2 = {0, 0, 0, 0}, p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0};
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
-    s1 = mfma32_bf16(q[kk], k[kk], s1);  // S  [i=4g4+r][j=r16]
-    s2 = mfma32_bf16(k[kk], q[kk], s2);  // S^T[j=4g4+r][i=r16]
-    p1 = mfma32_bf16(d[kk], v[kk], p1);  // dP [i][j]
-    p2 = mfma32_bf16(v[kk], d[kk], p2);  // dP^T
+    s1 = mfma32_t<TG>(q[kk], k[kk], s1);  // S  [i=4g4+r][j=r16]
+    s2 = mfma32_t<TG>(k[kk], q[kk], s2);  // S^T[j=4g4+r][i=r16]
+    p1 = mfma32_t<TG>(d[kk], v[kk], p1);  // dP [i][j]
+    p2 = mfma32_t<TG>(v[kk], d[kk], p2);  // dP^T
   }
   // ---- layout 2 (i = r16, j = 4g4+r): P, D_i, dS
   const float* lse_h = lse + h;
@@ -376,9 +376,9 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma16(int nseq, int L, int H, i
     P1[r] = ok ? __expf(s1[r] * kScale - li) : 0.f;
     dS1[r] = P1[r] * (p1[r] - Di);
   }
-  const s16x4 aP = pack_bf16x4(P1[0], P1[1], P1[2], P1[3]);     // A[m=j][k=i] = P[i][j]
-  const s16x4 aS = pack_bf16x4(dS1[0], dS1[1], dS1[2], dS1[3]); // A[m=j][k=i] = dS[i][j]
-  const s16x4 aT = pack_bf16x4(dS2[0], dS2[1], dS2[2], dS2[3]); // A[m=i][k=j] = dS[i][j]
+  const s16x4 aP = pack4<TG>(P1[0], P1[1], P1[2], P1[3]);     // A[m=j][k=i] = P[i][j]
+  const s16x4 aS = pack4<TG>(dS1[0], dS1[1], dS1[2], dS1[3]); // A[m=j][k=i] = dS[i][j]
+  const s16x4 aT = pack4<TG>(dS2[0], dS2[1], dS2[2], dS2[3]); // A[m=i][k=j] = dS[i][j]
   // the tiles are wave-private: LDS ops of one wave complete in order; this wait also
   // fences the compiler (no __syncthreads: waves of a partial block exit early above)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -386,9 +386,9 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma16(int nseq, int L, int H, i
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const f32x4 z = {0, 0, 0, 0};
-    const f32x4 dv = mfma16_bf16(aP, tr_read(tD, 4 * g4, 16 * t, lane), z);  // [j][d]
-    const f32x4 dk = mfma16_bf16(aS, tr_read(tQ, 4 * g4, 16 * t, lane), z);  // [j][d]
-    const f32x4 dq = mfma16_bf16(aT, tr_read(tK, 4 * g4, 16 * t, lane), z);  // [i][d]
+    const f32x4 dv = mfma16_t<TG>(aP, tr_read(tD, 4 * g4, 16 * t, lane), z);  // [j][d]
+    const f32x4 dk = mfma16_t<TG>(aS, tr_read(tQ, 4 * g4, 16 * t, lane), z);  // [j][d]
+    const f32x4 dq = mfma16_t<TG>(aT, tr_read(tK, 4 * g4, 16 * t, lane), z);  // [i][d]
     const int col = 16 * t + r16;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -544,7 +544,7 @@ static int launch_bwd(int nseq, int L, int H, int causal, const void* qkv, int l
                       const void* ofwd, int ldof, const void* dout, int lddo, const float* lse,
                       void* dqkv, int lddq, hipStream_t st) {
   const int pairs = nseq * H;
-  if constexpr (__is_same(TG, bf16)) {
+  if constexpr (sizeof(TG) == 2 && sizeof(T) == 2) {
     if (L <= 16) {
       hipLaunchKernelGGL((attn_bwd_mfma16<T, TG>), dim3((pairs + 3) / 4), dim3(256), 0, st, nseq, L, H,
                          causal, (const T*)qkv, ldq, (const TG*)dout, lddo, lse, (TG*)dqkv, lddq);

@@ -178,7 +178,7 @@ __global__ __launch_bounds__(256) void attn_prefix_fwd_mfma(int G, int P, int R,
   }
 }
 
-// ------------------------------------------------------------------ backward, MFMA (bf16 math)
+// ------------------------------------------------------------------ backward, MFMA (math in the grad dtype)
 // Per tile, with the two 16-key tiles (prefix, own) handled like attn_bwd_mfma16: S / dP in
 // both accumulator layouts, D_i = rowsum(P o dP) over both key tiles in registers; then the
 // transposed products (operands swapped) dV^T = dO^T P, dK^T = Q^T dS, dQ^T = K^T dS^T so
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int P, int R,
                                                             int lddo, const float* __restrict__ lse,
                                                             TG* __restrict__ dqkv, int lddq,
                                                             float* __restrict__ part) {
-  static_assert(__is_same(TG, bf16), "MFMA attention backward computes in bf16");
+  static_assert(sizeof(T) == 2 && sizeof(TG) == 2, "MFMA attention backward: 16-bit operands, math in TG");
   __shared__ CLIPK_LDS_ALIGN short sm[4][4][16 * TRS];  // per wave: K_pre, K_own, Q, dO
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
@@ -246,8 +246,8 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int P, int R,
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
     const int c = 8 * g4 + 32 * kk;
-    kp[kk] = to_bf16x8<T>(ld_row16(pp + W + c, pok));
-    vp[kk] = to_bf16x8<T>(ld_row16(pp + 2 * W + c, pok));
+    kp[kk] = to_g8<T, TG>(ld_row16(pp + W + c, pok));
+    vp[kk] = to_g8<T, TG>(ld_row16(pp + 2 * W + c, pok));
     *reinterpret_cast<s16x8*>(tKp + r16 * TRS + c) = kp[kk];
   }
   f32x4 dkp[4], dvp[4];
@@ -262,9 +262,9 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int P, int R,
     s16x8 q[2], ko[2], vo[2];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      q[kk] = to_bf16x8<T>(cur.q[kk]);
-      ko[kk] = to_bf16x8<T>(cur.k[kk]);
-      vo[kk] = to_bf16x8<T>(cur.v[kk]);
+      q[kk] = to_g8<T, TG>(cur.q[kk]);
+      ko[kk] = to_g8<T, TG>(cur.k[kk]);
+      vo[kk] = to_g8<T, TG>(cur.v[kk]);
     }
     const s16x8* d = cur.d;
     lds_fence();  // previous tile's transposed reads are done
@@ -279,14 +279,14 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int P, int R,
     f32x4 s1p = z, s2p = z, p1p = z, p2p = z, s1o = z, s2o = z, p1o = z, p2o = z;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      s1p = mfma32_bf16(q[kk], kp[kk], s1p);   // S  [i=4g4+r][j=r16]
-      s2p = mfma32_bf16(kp[kk], q[kk], s2p);   // S^T[j=4g4+r][i=r16]
-      p1p = mfma32_bf16(d[kk], vp[kk], p1p);   // dP [i][j]
-      p2p = mfma32_bf16(vp[kk], d[kk], p2p);   // dP^T
-      s1o = mfma32_bf16(q[kk], ko[kk], s1o);
-      s2o = mfma32_bf16(ko[kk], q[kk], s2o);
-      p1o = mfma32_bf16(d[kk], vo[kk], p1o);
-      p2o = mfma32_bf16(vo[kk], d[kk], p2o);
+      s1p = mfma32_t<TG>(q[kk], kp[kk], s1p);   // S  [i=4g4+r][j=r16]
+      s2p = mfma32_t<TG>(kp[kk], q[kk], s2p);   // S^T[j=4g4+r][i=r16]
+      p1p = mfma32_t<TG>(d[kk], vp[kk], p1p);   // dP [i][j]
+      p2p = mfma32_t<TG>(vp[kk], d[kk], p2p);   // dP^T
+      s1o = mfma32_t<TG>(q[kk], ko[kk], s1o);
+      s2o = mfma32_t<TG>(ko[kk], q[kk], s2o);
+      p1o = mfma32_t<TG>(d[kk], vo[kk], p1o);
+      p2o = mfma32_t<TG>(vo[kk], d[kk], p2o);
     }
     // layout 2: i = r16, j = 4g4+r  (rows past the tile are clamped copies: masked, not zeroed)
     float P2p[4], P2o[4], Dsum = 0.f;
@@ -317,12 +317,12 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int P, int R,
       dS1p[r] = P1p[r] * (p1p[r] - Di);
       dS1o[r] = P1o[r] * (p1o[r] - Di);
     }
-    const s16x4 bPp = pack_bf16x4(P1p[0], P1p[1], P1p[2], P1p[3]);      // B[k=i][n=j]
-    const s16x4 bSp = pack_bf16x4(dS1p[0], dS1p[1], dS1p[2], dS1p[3]);
-    const s16x4 bPo = pack_bf16x4(P1o[0], P1o[1], P1o[2], P1o[3]);
-    const s16x4 bSo = pack_bf16x4(dS1o[0], dS1o[1], dS1o[2], dS1o[3]);
-    const s16x4 bTp = pack_bf16x4(dS2p[0], dS2p[1], dS2p[2], dS2p[3]);  // B[k=j][n=i]
-    const s16x4 bTo = pack_bf16x4(dS2o[0], dS2o[1], dS2o[2], dS2o[3]);
+    const s16x4 bPp = pack4<TG>(P1p[0], P1p[1], P1p[2], P1p[3]);      // B[k=i][n=j]
+    const s16x4 bSp = pack4<TG>(dS1p[0], dS1p[1], dS1p[2], dS1p[3]);
+    const s16x4 bPo = pack4<TG>(P1o[0], P1o[1], P1o[2], P1o[3]);
+    const s16x4 bSo = pack4<TG>(dS1o[0], dS1o[1], dS1o[2], dS1o[3]);
+    const s16x4 bTp = pack4<TG>(dS2p[0], dS2p[1], dS2p[2], dS2p[3]);  // B[k=j][n=i]
+    const s16x4 bTo = pack4<TG>(dS2o[0], dS2o[1], dS2o[2], dS2o[3]);
     lds_fence();
     // one output (16 rows x 64) at a time, so only one 16-register tile is live for the
     // widened store
@@ -330,23 +330,23 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int P, int R,
     f32x4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      acc[t] = mfma16_bf16(tr_read(tKp, 4 * g4, 16 * t, lane), bTp, z);
-      acc[t] = mfma16_bf16(tr_read(tKo, 4 * g4, 16 * t, lane), bTo, acc[t]);
+      acc[t] = mfma16_t<TG>(tr_read(tKp, 4 * g4, 16 * t, lane), bTp, z);
+      acc[t] = mfma16_t<TG>(tr_read(tKo, 4 * g4, 16 * t, lane), bTo, acc[t]);
     }
     store_tile64<TG>(orow, acc, kScale, qok);  // dQ
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const s16x4 aQ = tr_read(tQ, 4 * g4, 16 * t, lane);
-      dkp[t] = mfma16_bf16(aQ, bSp, dkp[t]);
-      acc[t] = mfma16_bf16(aQ, bSo, z);
+      dkp[t] = mfma16_t<TG>(aQ, bSp, dkp[t]);
+      acc[t] = mfma16_t<TG>(aQ, bSo, z);
       if (own_is_prefix) dkp[t] += acc[t];  // the prefix tile's keys are the prefix rows themselves
     }
     if (!own_is_prefix) store_tile64<TG>(orow + W, acc, kScale, qok);  // dK (wave-uniform branch)
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const s16x4 aD = tr_read(tD, 4 * g4, 16 * t, lane);
-      dvp[t] = mfma16_bf16(aD, bPp, dvp[t]);
-      acc[t] = mfma16_bf16(aD, bPo, z);
+      dvp[t] = mfma16_t<TG>(aD, bPp, dvp[t]);
+      acc[t] = mfma16_t<TG>(aD, bPo, z);
       if (own_is_prefix) dvp[t] += acc[t];
     }
     if (!own_is_prefix) store_tile64<TG>(orow + 2 * W, acc, 1.0f, qok);  // dV
@@ -673,7 +673,7 @@ template <typename T, typename TG>
 static int prefix_bwd(int G, int P, int R, int ntiles, const int* tiles, const int* row_first, int H,
                       const void* qkv, int ldq, const void* ofwd, int ldof, const void* dout, int lddo,
                       const float* lse, void* dqkv, int lddq, float* part, hipStream_t st) {
-  constexpr bool mfma = __is_same(TG, bf16) && sizeof(T) == 2;
+  constexpr bool mfma = sizeof(TG) == 2 && sizeof(T) == 2;
   const int uc = mfma ? bwd_chunk() : kValuChunk;
   const int nchunk = n_chunks(ntiles, uc);
   const long waves = (long)G * nchunk * H;

@@ -57,6 +57,22 @@ __device__ __forceinline__ s16x8 to_bf16x8(s16x8 v) {
   }
 }
 
+// convert 8 elements of T (raw 16 B) to the math type TG (the backward's grad dtype)
+template <typename T, typename TG>
+__device__ __forceinline__ s16x8 to_g8(s16x8 v) {
+  if constexpr (__is_same(T, TG)) {
+    return v;
+  } else if constexpr (__is_same(TG, bf16)) {
+    return to_bf16x8<T>(v);
+  } else {
+    bf16x8 b = __builtin_bit_cast(bf16x8, v);
+    f16x8 h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = (f16)(float)b[i];
+    return __builtin_bit_cast(s16x8, h);
+  }
+}
+
 __device__ __forceinline__ f32x4 mfma32_bf16(s16x8 a, s16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }

@@ -362,6 +362,22 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
   return CLIPK_OK;
 }
 
+// Residual-gradient stream of the text backward: fp32, or the grad dtype when that is fp16
+// (default; the reference's fp16 model keeps its residual gradients in half). The 16-bit
+// stream is updated in place by each LayerNorm backward and is also the next GEMM's A
+// operand, so the fp32 copy's 4 B/element read + write per LayerNorm disappear (LayerNorm
+// backward 53 -> ~30 us per launch). CLIPK_TEXT_DRES16=0 keeps fp32, =1 also uses the
+// stream for bf16 gradients.
+static bool text_dres16(const clipk_encoder* e) {
+  static int v = -2;
+  if (v == -2) {
+    const char* s = getenv("CLIPK_TEXT_DRES16");
+    v = s ? atoi(s) : -1;
+  }
+  if (e->grad == CLIPK_F32 || v == 0) return false;
+  return v > 0 || e->grad == CLIPK_F16;
+}
+
 static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const int* eot_rows,
                               const float* dtxt, const void* saved, size_t saved_bytes, float* dx0,
                               void* ws, size_t ws_bytes, hipStream_t st) {
@@ -374,12 +390,22 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
   TRY(clipk_cast(gd, (long)nout * e->E, dtxt, b.dtg, st));
   TRY(gemm(gd, CLIPK_F32, CLIPK_EPI_NONE, nout, W, e->E, b.dtg, e->head[3], nullptr, nullptr, b.dlnf,
            nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
-  if (hipMemsetAsync(dX, 0, (size_t)rows * W * 4, st) != hipSuccess) return (int)hipGetLastError();
+  const bool r16 = text_dres16(e);
+  if (!r16 && hipMemsetAsync(dX, 0, (size_t)rows * W * 4, st) != hipSuccess) return (int)hipGetLastError();
   if (hipMemsetAsync(b.dX_lp, 0, (size_t)rows * W * esize(gd), st) != hipSuccess)
     return (int)hipGetLastError();
   const int rd = res_dtype(e);
-  TRY(clipk_layernorm_bwd_x(rd, CLIPK_F32, nout, W, b.dlnf, W, t.Xf, W, eot_rows, (const float*)e->head[0], t.meanf,
-                          t.rstdf, nullptr, W, dX, b.dX_lp, gd, eot_rows, W, st));
+  TRY(clipk_layernorm_bwd_x2(rd, CLIPK_F32, nout, W, b.dlnf, W, t.Xf, W, eot_rows, (const float*)e->head[0], t.meanf,
+                           t.rstdf, nullptr, CLIPK_F32, W, r16 ? nullptr : dX, b.dX_lp, gd, eot_rows, W, st));
+  // residual-gradient update of one LayerNorm backward: dres (fp32 dX or the 16-bit dX_lp,
+  // in place) + LN'(dxn); last: the encoder input's gradient, always fp32 into dX
+  auto ln_bwd = [&](const void* x, const float* gamma, const float* mean, const float* rstd, bool last) {
+    if (!r16)
+      return clipk_layernorm_bwd_x(rd, gd, rows, W, b.dxn, W, x, W, nullptr, gamma, mean, rstd, dX, W, dX,
+                                   last ? nullptr : b.dX_lp, gd, nullptr, W, st);
+    return clipk_layernorm_bwd_x2(rd, gd, rows, W, b.dxn, W, x, W, nullptr, gamma, mean, rstd, b.dX_lp, gd, W,
+                                  last ? dX : nullptr, b.dX_lp, gd, nullptr, W, st);
+  };
   for (int l = e->layers - 1; l >= 0; --l) {
     const auto& w = e->lw[l];
     if (!w[12] || !w[13] || !w[14] || !w[15]) return CLIPK_EINVAL;
@@ -389,8 +415,7 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
              t.h[l], act, st, CLIPK_PROF_GEMM_DGELU));
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, 4 * W, b.dh, w[14], nullptr, nullptr, b.dxn, nullptr,
              nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
-    TRY(clipk_layernorm_bwd_x(rd, gd, rows, W, b.dxn, W, t.Xm[l], W, nullptr, (const float*)w[6], t.mean2[l],
-                            t.rstd2[l], dX, W, dX, b.dX_lp, gd, nullptr, W, st));
+    TRY(ln_bwd(t.Xm[l], (const float*)w[6], t.mean2[l], t.rstd2[l], false));
     // attention: do = dXm . Wout ; dqkv ; dxn1 = dqkv . Win
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, W, b.dX_lp, w[13], nullptr, nullptr, b.do_, nullptr,
              nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
@@ -400,8 +425,7 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
     }
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, 3 * W, b.dqkv, w[12], nullptr, nullptr, b.dxn,
              nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
-    TRY(clipk_layernorm_bwd_x(rd, gd, rows, W, b.dxn, W, t.X[l], W, nullptr, (const float*)w[0], t.mean1[l],
-                            t.rstd1[l], dX, W, dX, l > 0 ? b.dX_lp : nullptr, gd, nullptr, W, st));
+    TRY(ln_bwd(t.X[l], (const float*)w[0], t.mean1[l], t.rstd1[l], l == 0));
   }
   return CLIPK_OK;
 }

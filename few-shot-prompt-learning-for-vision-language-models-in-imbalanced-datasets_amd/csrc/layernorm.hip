@@ -6,6 +6,8 @@
 // stream) is fp32 or, for the 16-bit text residual stream, the activation dtype (statistics
 // always in fp32). Optional row gather (in_rows) for ln_final on EOT rows and ln_post on
 // CLS rows, optional scatter (out_rows) on the backward.
+#include <type_traits>
+
 #include "common.h"
 
 namespace clipk {
@@ -97,15 +99,18 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int width, const 
 }
 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)) + dres,   g = dy * gamma
-template <typename TL, typename TD, typename TX, int VW>
+// RL: the incoming residual gradient dres is in the low-precision dtype TL (a 16-bit residual-
+// gradient stream, updated in place: dres == dx_lp is allowed, each lane reads its chunk
+// before writing it); dx (fp32) may then be null.
+template <typename TL, typename TD, typename TX, int VW, bool RL = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int width, const TD* __restrict__ dy,
                                                      int lddy, const TX* __restrict__ x, int ldx,
                                                      const int* __restrict__ x_rows,
                                                      const float* __restrict__ gamma,
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ rstd,
-                                                     const float* __restrict__ dres, int lddres,
-                                                     float* __restrict__ dx, TL* __restrict__ dx_lp,
+                                                     const void* dres_v, int lddres,
+                                                     float* __restrict__ dx, TL* dx_lp,
                                                      const int* __restrict__ out_rows, int ldo) {
   constexpr int NC = 1024 / (64 * VW);
   const int lane = threadIdx.x & 63;
@@ -139,8 +144,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int width, const 
   const float inv_w = 1.0f / (float)width;
   const float m1 = wave_sum(s1) * inv_w;
   const float m2 = wave_sum(s2) * inv_w;
-  float* op = dx + (size_t)orow * ldo;
-  const float* rp = dres ? dres + (size_t)orow * lddres : nullptr;
+  typedef typename std::conditional<RL, TL, float>::type TR;
+  const TR* rp = dres_v ? (const TR*)dres_v + (size_t)orow * lddres : nullptr;
 #pragma unroll
   for (int i = 0; i < NC; ++i) {
     const int c = lane + i * 64;
@@ -150,11 +155,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int width, const 
       for (int k = 0; k < VW; ++k) o[k] = rs * (gv[i][k] - m1 - xh[i][k] * m2);
       if (rp) {
         float rv[VW];
-        ldv<float, VW>(rp + c * VW, rv);
+        ldv<TR, VW>(rp + c * VW, rv);
 #pragma unroll
         for (int k = 0; k < VW; ++k) o[k] += rv[k];
       }
-      stv<float, VW>(op + c * VW, o);
+      if (dx) stv<float, VW>(dx + (size_t)orow * ldo + c * VW, o);
       if (dx_lp) stv<TL, VW>(dx_lp + (size_t)orow * ldo + c * VW, o);
     }
   }
@@ -221,24 +226,25 @@ extern "C" int clipk_layernorm_fwd(int out_dtype, int rows, int width, const flo
 template <typename TD, typename TX>
 static int ln_bwd_launch(int rows, int width, const void* dy, int lddy, const TX* x, int ldx,
                          const int* x_rows, const float* gamma, const float* mean, const float* rstd,
-                         const float* dres, int lddres, float* dx, void* dx_lp, int lp_dtype,
+                         const void* dres, bool dres_lp, int lddres, float* dx, void* dx_lp, int lp_dtype,
                          const int* out_rows, int ldo, hipStream_t st) {
   dim3 grid((rows + 3) / 4), block(256);
   const TD* d = (const TD*)dy;
   const bool v8 = width % 512 == 0 && ldx % 8 == 0 && ldo % 8 == 0 && lddy % 8 == 0 && (!dres || lddres % 8 == 0);
-#define CLIPK_LNB(TLP)                                                                                        \
-  if (v8)                                                                                                     \
-    hipLaunchKernelGGL((ln_bwd_kernel<TLP, TD, TX, 8>), grid, block, 0, st, rows, width, d, lddy, x, ldx,      \
-                       x_rows, gamma, mean, rstd, dres, lddres, dx, (TLP*)dx_lp, out_rows, ldo);              \
-  else                                                                                                        \
-    hipLaunchKernelGGL((ln_bwd_kernel<TLP, TD, TX, 4>), grid, block, 0, st, rows, width, d, lddy, x, ldx,      \
+#define CLIPK_LNB(TLP, RLV)                                                                                     \
+  if (v8)                                                                                                       \
+    hipLaunchKernelGGL((ln_bwd_kernel<TLP, TD, TX, 8, RLV>), grid, block, 0, st, rows, width, d, lddy, x, ldx,   \
+                       x_rows, gamma, mean, rstd, dres, lddres, dx, (TLP*)dx_lp, out_rows, ldo);                \
+  else                                                                                                          \
+    hipLaunchKernelGGL((ln_bwd_kernel<TLP, TD, TX, 4, RLV>), grid, block, 0, st, rows, width, d, lddy, x, ldx,   \
                        x_rows, gamma, mean, rstd, dres, lddres, dx, (TLP*)dx_lp, out_rows, ldo);
   if (!dx_lp || lp_dtype == CLIPK_F32) {
-    CLIPK_LNB(float)
+    if (dres_lp) return CLIPK_EDTYPE;
+    CLIPK_LNB(float, false)
   } else if (lp_dtype == CLIPK_BF16) {
-    CLIPK_LNB(bf16)
+    if (dres_lp) { CLIPK_LNB(bf16, true) } else { CLIPK_LNB(bf16, false) }
   } else if (lp_dtype == CLIPK_F16) {
-    CLIPK_LNB(f16)
+    if (dres_lp) { CLIPK_LNB(f16, true) } else { CLIPK_LNB(f16, false) }
   } else {
     return CLIPK_EDTYPE;
   }
@@ -250,18 +256,46 @@ static int ln_bwd_launch(int rows, int width, const void* dy, int lddy, const TX
 template <typename TX>
 static int ln_bwd_dy(int dy_dtype, int rows, int width, const void* dy, int lddy, const TX* x, int ldx,
                      const int* x_rows, const float* gamma, const float* mean, const float* rstd,
-                     const float* dres, int lddres, float* dx, void* dx_lp, int lp_dtype,
+                     const void* dres, bool dres_lp, int lddres, float* dx, void* dx_lp, int lp_dtype,
                      const int* out_rows, int ldo, hipStream_t st) {
   switch (dy_dtype) {
     case CLIPK_F32:
-      return ln_bwd_launch<float, TX>(rows, width, dy, lddy, x, ldx, x_rows, gamma, mean, rstd, dres, lddres,
-                                      dx, dx_lp, lp_dtype, out_rows, ldo, st);
+      return ln_bwd_launch<float, TX>(rows, width, dy, lddy, x, ldx, x_rows, gamma, mean, rstd, dres, dres_lp,
+                                      lddres, dx, dx_lp, lp_dtype, out_rows, ldo, st);
     case CLIPK_BF16:
-      return ln_bwd_launch<bf16, TX>(rows, width, dy, lddy, x, ldx, x_rows, gamma, mean, rstd, dres, lddres,
-                                     dx, dx_lp, lp_dtype, out_rows, ldo, st);
+      return ln_bwd_launch<bf16, TX>(rows, width, dy, lddy, x, ldx, x_rows, gamma, mean, rstd, dres, dres_lp,
+                                     lddres, dx, dx_lp, lp_dtype, out_rows, ldo, st);
     case CLIPK_F16:
-      return ln_bwd_launch<f16, TX>(rows, width, dy, lddy, x, ldx, x_rows, gamma, mean, rstd, dres, lddres,
-                                    dx, dx_lp, lp_dtype, out_rows, ldo, st);
+      return ln_bwd_launch<f16, TX>(rows, width, dy, lddy, x, ldx, x_rows, gamma, mean, rstd, dres, dres_lp,
+                                    lddres, dx, dx_lp, lp_dtype, out_rows, ldo, st);
+    default:
+      return CLIPK_EDTYPE;
+  }
+}
+
+extern "C" int clipk_layernorm_bwd_x2(int x_dtype, int dy_dtype, int rows, int width, const void* dy, int lddy,
+                                      const void* x, int ldx, const int* x_rows, const float* gamma,
+                                      const float* mean, const float* rstd, const void* dres, int dres_dtype,
+                                      int lddres, float* dx, void* dx_lp, int lp_dtype,
+                                      const int* out_rows, int ldo, void* stream) {
+  const bool dres_lp = dres && dres_dtype != CLIPK_F32;
+  if (dres_lp && (!dx_lp || dres_dtype != lp_dtype || lp_dtype == CLIPK_F32)) return CLIPK_EDTYPE;
+  if (!dy || !x || !gamma || !mean || !rstd || (!dx && !dx_lp)) return CLIPK_EINVAL;
+  if (rows < 0 || width <= 0 || width % 4 || width > 256 * LN_MAXV || ldx < width || ldo < width ||
+      lddy < width || (dres && lddres < width))
+    return CLIPK_ESHAPE;
+  if (rows == 0) return CLIPK_OK;
+  hipStream_t st = (hipStream_t)stream;
+  switch (x_dtype) {
+    case CLIPK_F32:
+      return ln_bwd_dy<float>(dy_dtype, rows, width, dy, lddy, (const float*)x, ldx, x_rows, gamma, mean, rstd,
+                              dres, dres_lp, lddres, dx, dx_lp, lp_dtype, out_rows, ldo, st);
+    case CLIPK_F16:
+      return ln_bwd_dy<f16>(dy_dtype, rows, width, dy, lddy, (const f16*)x, ldx, x_rows, gamma, mean, rstd, dres,
+                            dres_lp, lddres, dx, dx_lp, lp_dtype, out_rows, ldo, st);
+    case CLIPK_BF16:
+      return ln_bwd_dy<bf16>(dy_dtype, rows, width, dy, lddy, (const bf16*)x, ldx, x_rows, gamma, mean, rstd,
+                             dres, dres_lp, lddres, dx, dx_lp, lp_dtype, out_rows, ldo, st);
     default:
       return CLIPK_EDTYPE;
   }
@@ -272,25 +306,9 @@ extern "C" int clipk_layernorm_bwd_x(int x_dtype, int dy_dtype, int rows, int wi
                                      const float* mean, const float* rstd, const float* dres,
                                      int lddres, float* dx, void* dx_lp, int lp_dtype,
                                      const int* out_rows, int ldo, void* stream) {
-  if (!dy || !x || !gamma || !mean || !rstd || !dx) return CLIPK_EINVAL;
-  if (rows < 0 || width <= 0 || width % 4 || width > 256 * LN_MAXV || ldx < width || ldo < width ||
-      lddy < width || (dres && lddres < width))
-    return CLIPK_ESHAPE;
-  if (rows == 0) return CLIPK_OK;
-  hipStream_t st = (hipStream_t)stream;
-  switch (x_dtype) {
-    case CLIPK_F32:
-      return ln_bwd_dy<float>(dy_dtype, rows, width, dy, lddy, (const float*)x, ldx, x_rows, gamma, mean, rstd,
-                              dres, lddres, dx, dx_lp, lp_dtype, out_rows, ldo, st);
-    case CLIPK_F16:
-      return ln_bwd_dy<f16>(dy_dtype, rows, width, dy, lddy, (const f16*)x, ldx, x_rows, gamma, mean, rstd, dres,
-                            lddres, dx, dx_lp, lp_dtype, out_rows, ldo, st);
-    case CLIPK_BF16:
-      return ln_bwd_dy<bf16>(dy_dtype, rows, width, dy, lddy, (const bf16*)x, ldx, x_rows, gamma, mean, rstd,
-                             dres, lddres, dx, dx_lp, lp_dtype, out_rows, ldo, st);
-    default:
-      return CLIPK_EDTYPE;
-  }
+  if (!dx) return CLIPK_EINVAL;
+  return clipk_layernorm_bwd_x2(x_dtype, dy_dtype, rows, width, dy, lddy, x, ldx, x_rows, gamma, mean, rstd, dres,
+                                CLIPK_F32, lddres, dx, dx_lp, lp_dtype, out_rows, ldo, stream);
 }
 
 extern "C" int clipk_layernorm_bwd(int dy_dtype, int rows, int width, const void* dy, int lddy,

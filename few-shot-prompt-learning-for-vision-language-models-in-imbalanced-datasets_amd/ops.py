@@ -104,6 +104,18 @@ def layernorm_bwd(dy, x, w, mean, rstd, dres=None, lp_dtype=None):
     return (dx, lp) if lp is not None else dx
 
 
+def layernorm_bwd_lp_(dy, x, w, mean, rstd, dres_lp, dx=None):
+    """16-bit residual-gradient stream: dres_lp <- LN-input-grad(dy) + dres_lp, in place (the
+    dtype of dres_lp); also into fp32 dx when given. Returns dres_lp."""
+    _need(dy, "dy")
+    _need(x, "x")
+    _need(dres_lp, "dres_lp")
+    R, W = dy.shape
+    N.call("clipk_layernorm_bwd_x2", DT[x.dtype], DT[dy.dtype], R, W, _p(dy), W, _p(x), W, None, _p(w), _p(mean),
+           _p(rstd), _p(dres_lp), DT[dres_lp.dtype], W, _p(dx), _p(dres_lp), DT[dres_lp.dtype], None, W, _stream())
+    return dres_lp
+
+
 def attention(qkv, nseq, L, heads, causal, lse=False):
     _need(qkv, "qkv")
     W = heads * 64

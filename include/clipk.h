@@ -127,6 +127,14 @@ int clipk_layernorm_bwd_x(int x_dtype, int dy_dtype, int rows, int width, const 
                           const float* mean, const float* rstd, const float* dres, int lddres,
                           float* dx, void* dx_lp, int lp_dtype, const int* out_rows, int ldo,
                           void* stream);
+/* same with the residual gradient dres of dres_dtype: fp32, or lp_dtype (a 16-bit residual-
+ * gradient stream; dres may then alias dx_lp, updated in place). dx (fp32) may be NULL when
+ * dx_lp is given. */
+int clipk_layernorm_bwd_x2(int x_dtype, int dy_dtype, int rows, int width, const void* dy, int lddy,
+                           const void* x, int ldx, const int* x_rows, const float* gamma,
+                           const float* mean, const float* rstd, const void* dres, int dres_dtype,
+                           int lddres, float* dx, void* dx_lp, int lp_dtype, const int* out_rows,
+                           int ldo, void* stream);
 
 /* Multi-head self-attention core on packed qkv rows [(s*L+t), 3*heads*64] (head dim 64):
  * out[(s*L+t), h*64+d]; lse[(s*L+t)*heads + h] (optional) = logsumexp of scaled scores. */

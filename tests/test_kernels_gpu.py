@@ -102,6 +102,28 @@ def test_layernorm_16bit_residual(dev, xdt):
     close(dx, xr.grad, torch.float32, "ln16 bwd")  # same rounded inputs, fp32 math
 
 
+def test_layernorm_bwd_16bit_residual_grad(dev):
+    """16-bit residual-gradient stream (CLIPK_TEXT_DRES16): dres (bf16) updated in place with
+    LN'(dy), and the optional fp32 copy; vs torch fp32 on the same rounded inputs."""
+    W = 512
+    g = torch.Generator().manual_seed(12)
+    x = (torch.randn(45, W, generator=g) * 2).to(dev).to(torch.float16)
+    w = (1 + 0.1 * torch.randn(W, generator=g)).to(dev)
+    b = torch.zeros(W, device=dev)
+    _, mean, rstd = ops.layernorm(x, w, b, torch.float16, stats=True)
+    xr = x.float().clone().requires_grad_(True)
+    ref = F.layer_norm(xr, (W,), w, b, 1e-5)
+    dy = torch.randn(45, W, generator=g).to(dev).to(torch.bfloat16)
+    ref.backward(dy.float())
+    dres = torch.randn(45, W, generator=g).to(dev).to(torch.bfloat16)
+    want = xr.grad + dres.float()
+    dx = torch.empty(45, W, device=dev)
+    got = ops.layernorm_bwd_lp_(dy, x, w, mean, rstd, dres, dx=dx)
+    assert got.data_ptr() == dres.data_ptr()
+    close(got, want, torch.bfloat16, "ln bwd dres16")
+    close(dx, want, torch.float16, "ln bwd dres16 fp32 copy")
+
+
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 def test_gemm_bias_res_16bit(dev, dtype):
     """BIAS_RES with a 16-bit residual stream: out (dtype) = A.B^T + bias + res (dtype)."""
@@ -138,7 +160,8 @@ def test_attention_fwd(dev, dtype, nseq, L, H, causal):
     close(lse, rl, torch.float16 if dtype != torch.float32 else dtype, "attn lse")
 
 
-@pytest.mark.parametrize("dtype,gdtype", [(torch.float16, torch.bfloat16), (torch.float32, torch.float32)])
+@pytest.mark.parametrize("dtype,gdtype", [(torch.float16, torch.bfloat16), (torch.float16, torch.float16),
+                                         (torch.float32, torch.float32)])
 @pytest.mark.parametrize("nseq,L,H", [(6, 11, 8), (3, 23, 2), (2, 64, 2), (4, 5, 2)])
 def test_attention_bwd(dev, dtype, gdtype, nseq, L, H):
     g = torch.Generator().manual_seed(L + 100 * H)
@@ -354,7 +377,7 @@ def attn_prefix_ref(qkv, G, C, P, R, off, qlen, H):
 
 
 @pytest.mark.parametrize("dtype,gdtype", [(torch.float16, torch.bfloat16), (torch.bfloat16, torch.bfloat16),
-                                          (torch.float32, torch.float32)])
+                                          (torch.float16, torch.float16), (torch.float32, torch.float32)])
 @pytest.mark.parametrize("G,C,P,H,max_q", [(2, 37, 5, 8, 6), (1, 19, 16, 2, 7), (3, 16, 2, 4, 16), (2, 3, 9, 2, 1),
                                            (2, 53, 5, 2, 3), (1, 40, 3, 2, 9)])
 def test_attention_prefix_fwd_bwd(dev, dtype, gdtype, G, C, P, H, max_q):
