@@ -41,6 +41,9 @@ static int fwd_chunk() { static int c = chunk_env("CLIPK_PREFIX_FWD_CHUNK", 8); 
 static int bwd_chunk() { static int c = chunk_env("CLIPK_PREFIX_BWD_CHUNK", 16); return c; }
 static int fwd_batch() { static int c = chunk_env("CLIPK_PREFIX_FWD_BATCH", 1); return c; }
 static int bwd_batch() { static int c = chunk_env("CLIPK_PREFIX_BWD_BATCH", 2); return c; }
+// Waves per block (4 or 8; env CLIPK_PREFIX_WPB). Waves are head-fastest, so 8 waves (H = 8)
+// put all heads of a row range in one block: one CU reads whole qkv rows.
+static int prefix_wpb() { static int c = chunk_env("CLIPK_PREFIX_WPB", 4) >= 8 ? 8 : 4; return c; }
 static inline int n_chunks(int ntiles, int uc) { return (ntiles + 1 + uc - 1) / uc; }
 
 // The chunk's tile table in one VGPR (lane i holds tiles[2*(u_begin-1) + i]), read back
@@ -73,17 +76,17 @@ struct TileRows {
   int t0, n, pre, first;  // first: this lane's row's class start, tile-relative
 };
 
-template <typename T, int kFwdBatch>
-__global__ __launch_bounds__(256) void attn_prefix_fwd_mfma(int G, int P, int R, int ntiles,
+template <typename T, int kFwdBatch, int WPB = 4>
+__global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_mfma(int G, int P, int R, int ntiles,
                                                             const int* __restrict__ tiles,
                                                             const int* __restrict__ row_first, int H,
                                                             int nchunk, int uc, const T* __restrict__ qkv,
                                                             int ldq, T* __restrict__ out, int ldo,
                                                             float* __restrict__ lse) {
-  __shared__ CLIPK_LDS_ALIGN short sm[4][2][16 * TRS];  // per wave: prefix V, own V
+  __shared__ CLIPK_LDS_ALIGN short sm[WPB][2][16 * TRS];  // per wave: prefix V, own V
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
-  const int wid = blockIdx.x * 4 + w;
+  const int wid = blockIdx.x * WPB + w;
   if (wid >= G * nchunk * H) return;  // wave-uniform; no block barriers below
   const int h = wid % H, k = (wid / H) % nchunk, g = wid / (H * nchunk);
   const int W = H * 64;
@@ -189,8 +192,8 @@ struct TileRowsB {
   int t0, n, pre, first2, first1[4];  // class starts (tile-relative) of rows r16 and 4g4+r
 };
 
-template <typename T, typename TG, int kBwdBatch>
-__global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int P, int R, int ntiles,
+template <typename T, typename TG, int kBwdBatch, int WPB = 4>
+__global__ __launch_bounds__(WPB * 64) void attn_prefix_bwd_mfma(int G, int P, int R, int ntiles,
                                                             const int* __restrict__ tiles,
                                                             const int* __restrict__ row_first, int H,
                                                             int nchunk, int uc, const T* __restrict__ qkv,
@@ -199,10 +202,10 @@ __global__ __launch_bounds__(256) void attn_prefix_bwd_mfma(int G, int P, int R,
                                                             TG* __restrict__ dqkv, int lddq,
                                                             float* __restrict__ part) {
   static_assert(sizeof(T) == 2 && sizeof(TG) == 2, "MFMA attention backward: 16-bit operands, math in TG");
-  __shared__ CLIPK_LDS_ALIGN short sm[4][4][16 * TRS];  // per wave: K_pre, K_own, Q, dO
+  __shared__ CLIPK_LDS_ALIGN short sm[WPB][4][16 * TRS];  // per wave: K_pre, K_own, Q, dO
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
-  const int wid = blockIdx.x * 4 + w;
+  const int wid = blockIdx.x * WPB + w;
   if (wid >= G * nchunk * H) return;  // wave-uniform
   const int h = wid % H, k = (wid / H) % nchunk, g = wid / (H * nchunk);
   const int W = H * 64;
@@ -652,13 +655,20 @@ static int prefix_fwd(int G, int P, int R, int ntiles, const int* tiles, const i
     const int nchunk = n_chunks(ntiles, uc);
     const long waves = (long)G * nchunk * H;
     const int b = fwd_batch();
+    const int wpb = prefix_wpb();
     auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3((waves + 3) / 4), dim3(256), 0, st, G, P, R, ntiles, tiles, row_first, H,
-                         nchunk, uc, (const T*)qkv, ldq, (T*)out, ldo, lse);
+      hipLaunchKernelGGL(kern, dim3((waves + wpb - 1) / wpb), dim3(64 * wpb), 0, st, G, P, R, ntiles, tiles,
+                         row_first, H, nchunk, uc, (const T*)qkv, ldq, (T*)out, ldo, lse);
     };
-    if (b == 1) go(attn_prefix_fwd_mfma<T, 1>);
-    else if (b == 2) go(attn_prefix_fwd_mfma<T, 2>);
-    else go(attn_prefix_fwd_mfma<T, 4>);
+    if (wpb == 8) {
+      if (b == 1) go(attn_prefix_fwd_mfma<T, 1, 8>);
+      else if (b == 2) go(attn_prefix_fwd_mfma<T, 2, 8>);
+      else go(attn_prefix_fwd_mfma<T, 4, 8>);
+    } else {
+      if (b == 1) go(attn_prefix_fwd_mfma<T, 1>);
+      else if (b == 2) go(attn_prefix_fwd_mfma<T, 2>);
+      else go(attn_prefix_fwd_mfma<T, 4>);
+    }
   } else {
     const int nchunk = n_chunks(ntiles, kValuChunk);
     const long waves = (long)G * nchunk * H;
@@ -678,12 +688,19 @@ static int prefix_bwd(int G, int P, int R, int ntiles, const int* tiles, const i
   const int nchunk = n_chunks(ntiles, uc);
   const long waves = (long)G * nchunk * H;
   if constexpr (mfma) {
+    const int wpb = prefix_wpb();
     auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3((waves + 3) / 4), dim3(256), 0, st, G, P, R, ntiles, tiles, row_first, H,
-                         nchunk, uc, (const T*)qkv, ldq, (const TG*)dout, lddo, lse, (TG*)dqkv, lddq, part);
+      hipLaunchKernelGGL(kern, dim3((waves + wpb - 1) / wpb), dim3(64 * wpb), 0, st, G, P, R, ntiles, tiles,
+                         row_first, H, nchunk, uc, (const T*)qkv, ldq, (const TG*)dout, lddo, lse, (TG*)dqkv,
+                         lddq, part);
     };
-    if (bwd_batch() == 1) go(attn_prefix_bwd_mfma<T, TG, 1>);
-    else go(attn_prefix_bwd_mfma<T, TG, 2>);
+    if (wpb == 8) {
+      if (bwd_batch() == 1) go(attn_prefix_bwd_mfma<T, TG, 1, 8>);
+      else go(attn_prefix_bwd_mfma<T, TG, 2, 8>);
+    } else {
+      if (bwd_batch() == 1) go(attn_prefix_bwd_mfma<T, TG, 1>);
+      else go(attn_prefix_bwd_mfma<T, TG, 2>);
+    }
   } else {
     hipLaunchKernelGGL((attn_prefix_bwd_valu<T, TG>), dim3(waves), dim3(64), 0, st, G, P, R, ntiles, tiles,
                        row_first, H, nchunk, (const T*)qkv, ldq, (const T*)ofwd, ldof, (const TG*)dout, lddo,

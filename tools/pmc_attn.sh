@@ -1,17 +1,27 @@
 #!/bin/bash
-# PMC passes for the shared-prefix attention kernels. Usage (GPU box, repo root): tools/pmc_attn.sh <outdir>
+# SQ stall split and L2 behaviour of the shared-prefix attention kernels at the bench shape
+# (tools/kbench.py KB_ONLY=prefix), one counter group per rocprofv3 --pmc pass.
 set -e
 R=$(pwd)
-OUT=$R/${1:-gpurun_out/pmc_attn}
+OUT=$R/gpurun_out/pmc_attn
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-run() {
-  local name=$1; shift
-  timeout -k 10 200 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o p -- python3 $R/tools/one_attn.py 3 > $OUT/$name.log 2>&1
-}
-run sq SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE
-run inst SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT
-run act SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_WAIT_INST_LDS
-run fetch FETCH_SIZE
-run write WRITE_SIZE
-echo pmc done
+export KB_ONLY=prefix
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq -o p -- python3 $R/tools/kbench.py > $OUT/sq.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/tcc -o p -- python3 $R/tools/kbench.py > $OUT/tcc.log 2>&1 || true
+python3 - <<'PY'
+import csv, glob, collections
+for grp in ("sq", "tcc"):
+    for kern in ("attn_prefix_fwd", "attn_prefix_bwd"):
+        agg = collections.defaultdict(list)
+        for f in glob.glob(f"/root/repo/gpurun_out/pmc_attn/{grp}/**/*counter_collection.csv", recursive=True):
+            for r in csv.DictReader(open(f)):
+                if kern in r["Kernel_Name"]:
+                    agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        m = {k: sum(v) / len(v) for k, v in agg.items()}
+        print(grp, kern, {k: f"{v:.4g}" for k, v in sorted(m.items())})
+        if grp == "sq" and m:
+            wc = m.get("SQ_WAVE_CYCLES", 1)
+            print("   wait_any %.3f wait_inst %.3f active %.3f" % (m.get("SQ_WAIT_ANY", 0) / wc,
+                  m.get("SQ_WAIT_INST_ANY", 0) / wc, m.get("SQ_ACTIVE_INST_ANY", 0) / wc))
+PY
