@@ -53,13 +53,17 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int width, const 
   const int xr = in_rows ? in_rows[r] : r;
   const TI* xp = x + (size_t)xr * ldx;
   const int nv = width / VW;  // vectors per row
-  float v[NC][VW];
+  float v[NC][VW], gg[NC][VW], bb[NC][VW];
   float s = 0.f;
+  // gamma / beta are issued with x: loaded after the two reductions they were one more
+  // dependent round trip per row
 #pragma unroll
   for (int i = 0; i < NC; ++i) {
     const int c = lane + i * 64;
     if (c < nv) {
       ldv<TI, VW>(xp + c * VW, v[i]);
+      ldv<float, VW>(gamma + c * VW, gg[i]);
+      ldv<float, VW>(beta + c * VW, bb[i]);
 #pragma unroll
       for (int k = 0; k < VW; ++k) s += v[i][k];
     } else {
@@ -84,11 +88,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int width, const 
   for (int i = 0; i < NC; ++i) {
     const int c = lane + i * 64;
     if (c < nv) {
-      float gg[VW], bb[VW], o[VW];
-      ldv<float, VW>(gamma + c * VW, gg);
-      ldv<float, VW>(beta + c * VW, bb);
+      float o[VW];
 #pragma unroll
-      for (int k = 0; k < VW; ++k) o[k] = (v[i][k] - mu) * rs * gg[k] + bb[k];
+      for (int k = 0; k < VW; ++k) o[k] = (v[i][k] - mu) * rs * gg[i][k] + bb[i][k];
       stv<TO, VW>(op + c * VW, o);
     }
   }
@@ -122,8 +124,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int width, const 
   const TX* xp = x + (size_t)xr * ldx;
   const TD* dp = dy + (size_t)r * lddy;
   const int nv = width / VW;
-  float gv[NC][VW], xh[NC][VW];
+  float gv[NC][VW], xh[NC][VW], rv[NC][VW];
   float s1 = 0.f, s2 = 0.f;
+  typedef typename std::conditional<RL, TL, float>::type TR;
+  const TR* rp = dres_v ? (const TR*)dres_v + (size_t)orow * lddres : nullptr;
 #pragma unroll
   for (int i = 0; i < NC; ++i) {
     const int c = lane + i * 64;
@@ -132,6 +136,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int width, const 
       ldv<TX, VW>(xp + c * VW, xv);
       ldv<TD, VW>(dp + c * VW, dv);
       ldv<float, VW>(gamma + c * VW, gg);
+      // the residual gradient is issued with the other operands (not after the reductions)
+      if (rp) ldv<TR, VW>(rp + c * VW, rv[i]);
 #pragma unroll
       for (int k = 0; k < VW; ++k) {
         xh[i][k] = (xv[k] - mu) * rs;
@@ -144,8 +150,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int width, const 
   const float inv_w = 1.0f / (float)width;
   const float m1 = wave_sum(s1) * inv_w;
   const float m2 = wave_sum(s2) * inv_w;
-  typedef typename std::conditional<RL, TL, float>::type TR;
-  const TR* rp = dres_v ? (const TR*)dres_v + (size_t)orow * lddres : nullptr;
 #pragma unroll
   for (int i = 0; i < NC; ++i) {
     const int c = lane + i * 64;
@@ -154,10 +158,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int width, const 
 #pragma unroll
       for (int k = 0; k < VW; ++k) o[k] = rs * (gv[i][k] - m1 - xh[i][k] * m2);
       if (rp) {
-        float rv[VW];
-        ldv<TR, VW>(rp + c * VW, rv);
 #pragma unroll
-        for (int k = 0; k < VW; ++k) o[k] += rv[k];
+        for (int k = 0; k < VW; ++k) o[k] += rv[i][k];
       }
       if (dx) stv<float, VW>(dx + (size_t)orow * ldo + c * VW, o);
       if (dx_lp) stv<TL, VW>(dx_lp + (size_t)orow * ldo + c * VW, o);
