@@ -922,6 +922,16 @@ static unsigned long long* gemm_stamp_buf() {
   return g_stamp;
 }
 
+// Persistent launch above this many tiles (knob CLIPK_GEMM_PERSIST_MIN, default 2 x CUs)
+static int persist_min(int cus) {
+  static int v = -2;
+  if (v == -2) {
+    const char* e = getenv("CLIPK_GEMM_PERSIST_MIN");
+    v = e ? atoi(e) : -1;
+  }
+  return v >= 0 ? v : 2 * cus;
+}
+
 static int g_skew = -1;
 static int g_num_cus = 0;
 static int num_cus() {
@@ -978,7 +988,7 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
     } else if (cfg == 6) {
       const int nwg = ((g.M + 191) / 192) * (g.N / 256);
       const int cus = num_cus();
-      if (nwg > 2 * cus)
+      if (nwg > persist_min(cus))
         hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 192, 256, 2, 4, true>), dim3((cus / 8) * 8), dim3(512), 0, st, g);
       else
         hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 192, 256, 2, 4, false>), dim3(nwg), dim3(512), 0, st, g);
