@@ -37,10 +37,11 @@ PREC_DTYPES = {
 
 
 def prec_dtypes(prec):
-    """(activation dtype, text-backward gradient dtype) of a PREC. PREC fp16 backpropagates in
-    fp16 as the reference's fp16 model does (PromptSRC/trainers/cocoop.py:277-280: the CLIP
-    weights stay half unless PREC is fp32/amp, so autograd runs in half); CLIPK_GRAD_BF16=1
-    switches its gradients to bf16 (more range, less precision)."""
+    """(activation dtype, text-backward gradient dtype) of a PREC. The reference's PREC fp16
+    actually runs fp32 (convert_weights is disabled, PromptSRC/clip/model.py:699),
+    so the build's 16-bit modes are judged against the fp32 oracle (tests/test_parity_gpu.py).
+    PREC fp16 backpropagates in fp16: against the oracle its input gradients measure
+    1-cos <= 5e-5, bf16 gradients 1.5e-3. CLIPK_GRAD_BF16=1 switches to bf16 (more range)."""
     import os
     act, grad = PREC_DTYPES[prec]
     if prec == "fp16" and os.environ.get("CLIPK_GRAD_BF16", "0") not in ("", "0"):
