@@ -1119,7 +1119,7 @@ static int auto_splits(int M, int N, int K, int esz) {
   const int tiles = ((M + 127) / 128) * (N / 128);
   if (2 * tiles >= num_cus()) return 1;
   const int nk = K * esz / GEMM_ROWB;
-  int s = (2 * num_cus() + tiles - 1) / tiles;
+  int s = (2 * num_cus()) / tiles;  // slices x tiles within one round of 2 blocks per CU
   s = s > 8 ? 8 : s;
   s = s > nk / 4 ? nk / 4 : s;
   return s < 1 ? 1 : s;
