@@ -129,13 +129,27 @@ __device__ __forceinline__ void skew_start(int us, int bid) {
     for (int i = 0; i < us; ++i) __builtin_amdgcn_s_sleep(32);  // 64 x 32 cycles each
 }
 
+// Raw barrier pinned in program order: glds may stay in flight across it (a __syncthreads()
+// would make the compiler drain them with vmcnt(0)).
+#define G8_BAR()                       \
+  do {                                 \
+    __builtin_amdgcn_sched_barrier(0); \
+    __builtin_amdgcn_s_barrier();      \
+    __builtin_amdgcn_sched_barrier(0); \
+  } while (0)
+
 // Block tile BM x BN, WM x WN waves (each (BM/WM) x (BN/WN) = TM x TN 16x16 sub-tiles),
 // 2-stage LDS ring, one barrier per 128-byte K step. PERSIST: the grid is sized to the
 // CU count and each block walks an XCD-contiguous run of tiles; the last K step of a tile
 // prefetches the first stage of the next tile, so that load overlaps the epilogue.
+// DEPTH > 2 (non-persistent only): a DEPTH-slot LDS ring with DEPTH-1 stages in flight, a
+// counted vmcnt and a raw barrier per K step -- for the latency-bound small-M GEMMs (the ViT's
+// 1,576-row projections: one tile per CU, where a 2-slot ring waits out a load latency every
+// 64-deep K step).
 template <typename T, typename TO, typename TX, int EPI, int BM, int BN, int WM, int WN, bool PERSIST,
-          int ROWB = GEMM_ROWB>
-__global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
+          int ROWB = GEMM_ROWB, int DEPTH = 2>
+__global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
+  static_assert(DEPTH == 2 || !PERSIST, "deep ring: non-persistent launches only");
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int OPA = BM * ROWB, OPB = BN * ROWB, STAGE = OPA + OPB;
@@ -145,7 +159,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
   constexpr int IA = BM / RPI / NW, IB = BN / RPI / NW;  // glds per wave per stage
   static_assert(ROWB == 128 || (ROWB == 64 && sizeof(T) == 2), "staged row is 128 B (or 64 B for 16-bit)");
   static_assert(IA >= 1 && IB >= 1 && BM % (RPI * NW) == 0 && BN % (RPI * NW) == 0, "tile/wave mismatch");
-  __shared__ CLIPK_LDS_ALIGN char smem[2 * STAGE + NW * EPI_SCRATCH];  // one array (see header)
+  __shared__ CLIPK_LDS_ALIGN char smem[DEPTH * STAGE + NW * EPI_SCRATCH];  // one array (see header)
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
@@ -213,9 +227,26 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
   constexpr bool HAS_EXT = EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU;
 
   set_tile(tile);
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  constexpr int PER = IA + IB;  // glds per wave per stage
+  // deep ring: wait until stage kt+1 has landed while `younger` later stages stay in flight
+  auto ring_wait = [&](int younger) {
+    if constexpr (DEPTH > 2) {
+      if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  };
+  static_assert(DEPTH <= 4, "ring_wait covers up to two younger stages");
+  if constexpr (DEPTH == 2) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else {
+    for (int d = 0; d < DEPTH - 1; ++d)
+      if (d < nk) stage(d, d);
+    ring_wait(min(DEPTH - 2, nk - 1));
+    G8_BAR();
+  }
   int it = 0;  // global K-step counter (LDS buffer = it & 1)
   int ti = 0;  // tiles done by this block (diagnostic stamps)
   unsigned long long* stp = (g.stamp && threadIdx.x == 0 && bid < STAMP_BLOCKS)
@@ -266,13 +297,17 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
     if (stp && ti < STAMP_TILES) stp[2 + 3 * ti] = __builtin_amdgcn_s_memrealtime();
     // group 0's operands are loaded at the top of the last K step (its MFMAs hide them)
     for (int kt = 0; kt < nk; ++kt, ++it) {
-      const int cur = it & 1;
+      const int cur = DEPTH == 2 ? (it & 1) : it % DEPTH;
       const bool last = kt + 1 == nk;
-      if (!last) {
-        stage(cur ^ 1, kt + 1);
-      } else if (has_next) {
-        set_tile(next);
-        stage(cur ^ 1, 0);  // next tile's first stage flies during this tile's epilogue
+      if constexpr (DEPTH == 2) {
+        if (!last) {
+          stage(cur ^ 1, kt + 1);
+        } else if (has_next) {
+          set_tile(next);
+          stage(cur ^ 1, 0);  // next tile's first stage flies during this tile's epilogue
+        }
+      } else {
+        if (kt + DEPTH - 1 < nk) stage((kt + DEPTH - 1) % DEPTH, kt + DEPTH - 1);  // slot read at kt-1
       }
       if (last) load_ext(0, extq[0]);
       const char* As = smem + cur * STAGE + (wm * (BM / WM) + fr) * ROWB;
@@ -291,8 +326,13 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
           for (int j = 0; j < TN; ++j) acc[i][j] = mma<T>(b[j], a[i], acc[i][j]);
       }
       if (!last) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        if constexpr (DEPTH == 2) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+        } else {
+          ring_wait(min(DEPTH - 2, nk - 2 - kt));  // stages kt+2 .. issued after kt+1
+          G8_BAR();
+        }
       }
     }
 
@@ -313,7 +353,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
         bia[c] = b4[0]; bia[c + 1] = b4[1]; bia[c + 2] = b4[2]; bia[c + 3] = b4[3];
       }
     }
-    float* scr = reinterpret_cast<float*>(smem + 2 * STAGE + w * EPI_SCRATCH);
+    float* scr = reinterpret_cast<float*>(smem + DEPTH * STAGE + w * EPI_SCRATCH);
     const long long rows_ok = (long long)(g.M - m0 < BM ? g.M - m0 : BM);
     const __amdgpu_buffer_rsrc_t ro = tile_rsrc(outb + (size_t)m0 * g.ldo, rows_ok * g.ldo * (long long)sizeof(TO));
     __amdgpu_buffer_rsrc_t ro2 = ro;
@@ -384,14 +424,6 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_nt_kernel(GemmArgs g) {
   }
 }
 
-// Raw barrier pinned in program order: glds may stay in flight across it (a __syncthreads()
-// would make the compiler drain them with vmcnt(0)).
-#define G8_BAR()                       \
-  do {                                 \
-    __builtin_amdgcn_sched_barrier(0); \
-    __builtin_amdgcn_s_barrier();      \
-    __builtin_amdgcn_sched_barrier(0); \
-  } while (0)
 
 // ---- deep-A ring (cfg 8 / 9) ------------------------------------------------------------
 // The K loop of gemm_nt_kernel waits every step for the stage issued at its top: A comes
@@ -932,6 +964,17 @@ static int persist_min(int cus) {
   return v >= 0 ? v : 2 * cus;
 }
 
+// 4-slot ring for 128x128 grids of at most one tile per CU (knob CLIPK_GEMM_DEEP=1; measured
+// equal to the 2-slot ring on the ViT's 1,576-row GEMMs, so off by default)
+static bool deep_small() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLIPK_GEMM_DEEP");
+    v = e ? atoi(e) : 0;
+  }
+  return v != 0;
+}
+
 static int g_skew = -1;
 static int g_num_cus = 0;
 static int num_cus() {
@@ -1014,7 +1057,11 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
       hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 128, 4, 2, false>), dim3(nwg), dim3(512), 0, st, g);
     } else {
       const int nwg = ((g.M + 127) / 128) * (g.N / 128);
-      hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 128, 2, 2, false>), dim3(nwg), dim3(256), 0, st, g);
+      if (nwg <= num_cus() && deep_small())  // one tile per CU: 4-slot ring (144 KiB LDS), knob
+        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 4>), dim3(nwg),
+                           dim3(256), 0, st, g);
+      else
+        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 128, 2, 2, false>), dim3(nwg), dim3(256), 0, st, g);
     }
   }
   CLIPK_CHECK_LAUNCH();
@@ -1113,7 +1160,7 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(int S, int M, int N,
 // Slices for a GEMM whose 128x128 tile grid would leave most CUs idle (small M): only when
 // the grid covers under half of the CUs (the ViT's N = 768 projections at B = 8: 78 tiles;
 // grids of 234-312 tiles measured no better split), enough slices for ~2 blocks per CU,
-// each slice >= 4 K steps, at most 8.
+// each slice >= 8 K steps, at most 8 slices.
 static int auto_splits(int M, int N, int K, int esz) {
   if (M <= 0 || N % GEMM_NMIN) return 1;
   const int tiles = ((M + 127) / 128) * (N / 128);
@@ -1121,7 +1168,8 @@ static int auto_splits(int M, int N, int K, int esz) {
   const int nk = K * esz / GEMM_ROWB;
   int s = (2 * num_cus()) / tiles;  // slices x tiles within one round of 2 blocks per CU
   s = s > 8 ? 8 : s;
-  s = s > nk / 4 ? nk / 4 : s;
+  s = s > nk / 8 ? nk / 8 : s;  // >= 8 K steps per slice: the ViT's K = 768 c_proj measured
+                                // 11.6 us unsplit vs 17.4 us in 3 slices + finish
   return s < 1 ? 1 : s;
 }
 }  // namespace clipk

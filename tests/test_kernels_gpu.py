@@ -314,7 +314,7 @@ def test_gemm_stream_edges(dev, cfg, M, Nn, K):
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("M,Nn,K,splits",[(1576, 768, 3072, 0), (1576, 768, 768, 0), (1576, 2304, 768, 2),
+@pytest.mark.parametrize("M,Nn,K,splits",[(1576, 768, 3072, 0), (1576, 768, 768, 3), (1576, 2304, 768, 2),
                                            (300, 256, 512, 3)])
 def test_gemm_splitk(dev, dtype, M, Nn, K, splits):
     """Split-K (ViT at small batch) vs torch fp32, every epilogue; slice-order sum is
@@ -326,6 +326,8 @@ def test_gemm_splitk(dev, dtype, M, Nn, K, splits):
     res = torch.randn(M, Nn, generator=g).to(dev)
     if splits == 0:
         assert N.load().clipk_gemm_auto_splits(ops.DT[dtype], M, Nn, K) > 1
+    # 16-bit K = 768 (12 K steps) stays unsplit: slices need >= 8 K steps
+    assert N.load().clipk_gemm_auto_splits(ops.DT[torch.float16], 1576, 768, 768) == 1
     ref = A.float() @ B.float().t()
     o1 = ops.gemm_splitk(A, B, N.EPI_NONE, torch.float32, splits=splits)
     close(o1, ref, dtype, "splitk none")
