@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("CLIPK_LIB") or os.path.join(_PKG, "libclipk.so")  # o
 
 F32, F16, BF16 = 0, 1, 2
 EPI_BIAS, EPI_BIAS_RES, EPI_BIAS_QGELU, EPI_DQGELU, EPI_NONE = 0, 1, 2, 3, 4
+A_QGELU = 0x100  # OR-ed into epi: the GEMM consumes quickgelu(A) (include/clipk.h)
 PROF_NONE, PROF_GEMM_FC, PROF_GEMM_ALL, PROF_ATTN, PROF_LN, PROF_GEMM_DGELU = 0, 1, 2, 3, 4, 5
 
 _P = ctypes.c_void_p

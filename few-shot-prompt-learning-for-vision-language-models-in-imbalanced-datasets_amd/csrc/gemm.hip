@@ -146,10 +146,15 @@ __device__ __forceinline__ void skew_start(int us, int bid) {
 // counted vmcnt and a raw barrier per K step -- for the latency-bound small-M GEMMs (the ViT's
 // 1,576-row projections: one tile per CU, where a 2-slot ring waits out a load latency every
 // 64-deep K step).
+// AG (CLIPK_A_QGELU, non-persistent 2-slot only): A is a pre-activation h; each thread loads
+// its A chunks of the next stage into registers at the top of a K step (where the glds would
+// have been issued), and after the step's MFMAs writes quickgelu(h) to the same lane-linear
+// LDS slots the glds would have filled.
 template <typename T, typename TO, typename TX, int EPI, int BM, int BN, int WM, int WN, bool PERSIST,
-          int ROWB = GEMM_ROWB, int DEPTH = 2>
+          int ROWB = GEMM_ROWB, int DEPTH = 2, bool AG = false>
 __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
   static_assert(DEPTH == 2 || !PERSIST, "deep ring: non-persistent launches only");
+  static_assert(!AG || (!PERSIST && DEPTH == 2 && sizeof(T) == 2 && ROWB == 128), "A-operand QuickGELU path");
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int OPA = BM * ROWB, OPB = BN * ROWB, STAGE = OPA + OPB;
@@ -210,13 +215,32 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       srcB[i] = g.B + ((size_t)(tn0 + row) * g.ldb) * esz + c * 16 + (size_t)kt0 * ROWB;
     }
   };
+  u32x4 ra[AG ? IA : 1];  // AG: the next stage's A chunks in flight
   auto stage = [&](int s, int kt) {
     char* base = smem + s * STAGE;
     const size_t koff = (size_t)kt * ROWB;
+    if constexpr (AG) {
 #pragma unroll
-    for (int i = 0; i < IA; ++i) glds16(srcA[i] + koff, base + (w * IA + i) * 1024);
+      for (int i = 0; i < IA; ++i) ra[i] = *reinterpret_cast<const u32x4*>(srcA[i] + koff);
+    } else {
+#pragma unroll
+      for (int i = 0; i < IA; ++i) glds16(srcA[i] + koff, base + (w * IA + i) * 1024);
+    }
 #pragma unroll
     for (int i = 0; i < IB; ++i) glds16(srcB[i] + koff, base + OPA + (w * IB + i) * 1024);
+  };
+  auto write_a = [&](int s) {  // AG: quickgelu of the loaded chunks into stage s
+    if constexpr (AG) {
+      typedef T t8 __attribute__((ext_vector_type(8)));
+      char* base = smem + s * STAGE;
+#pragma unroll
+      for (int i = 0; i < IA; ++i) {
+        t8 hv = __builtin_bit_cast(t8, ra[i]);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) hv[c] = (T)quick_gelu((float)hv[c]);
+        *reinterpret_cast<u32x4*>(base + (w * IA + i) * 1024 + lane * 16) = __builtin_bit_cast(u32x4, hv);
+      }
+    }
   };
 
   const int wm = w / WN, wn = w % WN;
@@ -239,6 +263,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
   static_assert(DEPTH <= 4, "ring_wait covers up to two younger stages");
   if constexpr (DEPTH == 2) {
     stage(0, 0);
+    write_a(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   } else {
@@ -327,6 +352,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       }
       if (!last) {
         if constexpr (DEPTH == 2) {
+          write_a(cur ^ 1);  // AG: slot cur^1 was last read in step kt-1 (before its barrier)
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __syncthreads();
         } else {
@@ -1068,17 +1094,48 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
   return CLIPK_OK;
 }
 
+// CLIPK_A_QGELU launches: non-persistent 2-slot kernels of the tile the shape would get
+template <typename T, typename TO, typename TX, int EPI>
+static int launch_gemm_ag(const GemmArgs& g, hipStream_t st) {
+  const int cfg = pick_cfg(g.M, g.N, (int)sizeof(T));
+  if (cfg == 6) {
+    const int nwg = ((g.M + 191) / 192) * (g.N / 256);
+    hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 192, 256, 2, 4, false, GEMM_ROWB, 2, true>), dim3(nwg),
+                       dim3(512), 0, st, g);
+  } else if (g.N % 256 == 0 && g.M >= 4096) {
+    const int nwg = ((g.M + 255) / 256) * (g.N / 256);
+    hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 256, 2, 4, false, GEMM_ROWB, 2, true>), dim3(nwg),
+                       dim3(512), 0, st, g);
+  } else {
+    const int nwg = ((g.M + 127) / 128) * (g.N / 128);
+    hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 2, true>), dim3(nwg),
+                       dim3(256), 0, st, g);
+  }
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
 // dtype dispatch: (in, out, epi[, aux])
 template <typename T>
-static int dispatch_out(int out_dtype, int epi, int aux_dtype, const GemmArgs& g, hipStream_t st) {
+static int dispatch_out(int out_dtype, int epi, int aux_dtype, const GemmArgs& g, hipStream_t st,
+                        bool ag = false) {
   if (epi == CLIPK_EPI_BIAS_RES) {
     // residual stream in fp32, or (16-bit text residual) in the operand dtype for both res and out
+    if constexpr (sizeof(T) == 2) {
+      if (ag) {
+        if (out_dtype == CLIPK_F32) return launch_gemm_ag<T, float, float, CLIPK_EPI_BIAS_RES>(g, st);
+        if (out_dtype == DT<T>::id) return launch_gemm_ag<T, T, T, CLIPK_EPI_BIAS_RES>(g, st);
+        return CLIPK_EDTYPE;
+      }
+    }
+    if (ag) return CLIPK_EINVAL;
     if (out_dtype == CLIPK_F32) return launch_gemm<T, float, float, CLIPK_EPI_BIAS_RES>(g, st);
     if constexpr (sizeof(T) == 2) {
       if (out_dtype == DT<T>::id) return launch_gemm<T, T, T, CLIPK_EPI_BIAS_RES>(g, st);
     }
     return CLIPK_EDTYPE;
   }
+  if (ag) return CLIPK_EINVAL;  // the A-operand QuickGELU is wired for the residual epilogue
   if (epi == CLIPK_EPI_DQGELU) {
     // backward: out in the grad dtype (== T), aux = forward pre-activation
     if (out_dtype != DT<T>::id) return CLIPK_EDTYPE;
@@ -1114,6 +1171,9 @@ extern "C" int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, in
                           void* out, int ldo, void* out2, const void* aux, int aux_dtype,
                           int ldaux, void* stream) {
   if (!A || !B || !out) return CLIPK_EINVAL;
+  const bool ag = (epi & CLIPK_A_QGELU) != 0;
+  epi &= ~CLIPK_A_QGELU;
+  if (ag && (in_dtype == CLIPK_F32 || epi != CLIPK_EPI_BIAS_RES)) return CLIPK_EINVAL;
   if (M <= 0) return M == 0 ? CLIPK_OK : CLIPK_ESHAPE;
   const int esz = in_dtype == CLIPK_F32 ? 4 : 2;
   if (N <= 0 || K <= 0 || N % GEMM_NMIN != 0 || (K * esz) % GEMM_ROWB != 0) return CLIPK_ESHAPE;
@@ -1127,8 +1187,8 @@ extern "C" int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, in
              ldaux, nullptr, 1, 0};
   hipStream_t st = (hipStream_t)stream;
   switch (in_dtype) {
-    case CLIPK_F16: return dispatch_out<f16>(out_dtype, epi, aux_dtype, g, st);
-    case CLIPK_BF16: return dispatch_out<bf16>(out_dtype, epi, aux_dtype, g, st);
+    case CLIPK_F16: return dispatch_out<f16>(out_dtype, epi, aux_dtype, g, st, ag);
+    case CLIPK_BF16: return dispatch_out<bf16>(out_dtype, epi, aux_dtype, g, st, ag);
     case CLIPK_F32: return dispatch_out<float>(out_dtype, epi, aux_dtype, g, st);
     default: return CLIPK_EDTYPE;
   }

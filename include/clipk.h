@@ -59,6 +59,10 @@ enum {
   CLIPK_EPI_DQGELU = 3,     /* out = acc * quickgelu'(aux)                                */
   CLIPK_EPI_NONE = 4        /* out = acc                                                  */
 };
+/* Operand flag OR-ed into epi: A is a pre-activation h and the GEMM consumes quickgelu(h)
+ * (applied to each 16-B chunk of A as it is staged into LDS), so the producer of h need
+ * not also write quickgelu(h) (the text c_proj forward). 16-bit in_dtype only. */
+enum { CLIPK_A_QGELU = 0x100 };
 
 const char* clipk_version(void);
 const char* clipk_strerror(int status);

@@ -125,6 +125,28 @@ def test_layernorm_bwd_16bit_residual_grad(dev):
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("M,Nn,K", [(40000, 512, 2048), (300, 256, 512), (8192, 2048, 512), (1, 128, 64)])
+def test_gemm_a_qgelu(dev, dtype, M, Nn, K):
+    """CLIPK_A_QGELU: out = quickgelu(A) . B^T + bias + res, QuickGELU applied to the 16-bit A
+    chunks while they are staged (the text c_proj forward reading c_fc's pre-activation);
+    vs torch on the same 16-bit rounding of quickgelu(A)."""
+    g = torch.Generator().manual_seed(M + K)
+    h = (torch.randn(M, K, generator=g) * 2).to(dev).to(dtype)
+    B = (torch.randn(Nn, K, generator=g) / math.sqrt(K)).to(dev).to(dtype)
+    bias = torch.randn(Nn, generator=g).to(dev)
+    res = torch.randn(M, Nn, generator=g).to(dev).to(dtype)
+    hf = h.float()
+    a = (hf * torch.sigmoid(1.702 * hf)).to(dtype).float()
+    ref = a @ B.float().t() + bias + res.float()
+    close(ops.gemm(h, B, N.EPI_BIAS_RES | N.A_QGELU, dtype, bias=bias, res=res), ref, dtype, f"a_qgelu M{M}")
+    resf = res.float()
+    close(ops.gemm(h, B, N.EPI_BIAS_RES | N.A_QGELU, torch.float32, bias=bias, res=resf),
+          a @ B.float().t() + bias + resf, dtype, f"a_qgelu f32 M{M}")
+    with pytest.raises(N.ClipkError):
+        ops.gemm(h, B, N.EPI_NONE | N.A_QGELU, torch.float32)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 def test_gemm_bias_res_16bit(dev, dtype):
     """BIAS_RES with a 16-bit residual stream: out (dtype) = A.B^T + bias + res (dtype)."""
     for M in (300, 40000):
