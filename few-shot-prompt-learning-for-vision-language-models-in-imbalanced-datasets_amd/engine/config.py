@@ -111,7 +111,8 @@ def get_cfg_default() -> CfgNode:
                   "MAX_EPOCH": 10, "WARMUP_EPOCH": -1, "WARMUP_TYPE": "linear",
                   "WARMUP_CONS_LR": 1e-5, "WARMUP_MIN_LR": 1e-5, "WARMUP_RECOUNT": True},
         "TRAIN": {"PRINT_FREQ": 10, "CHECKPOINT_FREQ": 0},
-        "TEST": {"EVALUATOR": "Classification", "FINAL_MODEL": "last_step", "NO_TEST": False},
+        "TEST": {"EVALUATOR": "Classification", "FINAL_MODEL": "last_step", "NO_TEST": False,
+                 "SPLIT": "test"},
         "TRAINER": {
             "NAME": "",
             # PromptSRC/train.py:101-108
@@ -122,5 +123,7 @@ def get_cfg_default() -> CfgNode:
         },
         # MI355X-native knobs (not in the reference): prompt truncation to the EOT and the
         # max rows per text-encoder launch chunk (memory bound for large B*C).
-        "NATIVE": {"TRUNCATE_PROMPTS": True, "SHARED_PREFIX": True, "MAX_TEXT_ROWS": 2_000_000},
+        # CLASS_SHARD: CoOp under torchrun encodes C / world classes per rank.
+        "NATIVE": {"TRUNCATE_PROMPTS": True, "SHARED_PREFIX": True, "MAX_TEXT_ROWS": 2_000_000,
+                   "CLASS_SHARD": True},
     })

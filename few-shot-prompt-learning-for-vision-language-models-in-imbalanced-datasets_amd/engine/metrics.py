@@ -24,8 +24,10 @@ def compute_accuracy(output, target, topk=(1,)):
 
 
 def macro_f1(y_true, y_pred):
-    """sklearn f1_score(average='macro') over the labels present in y_true or y_pred."""
-    labels = np.unique(np.concatenate([y_true, y_pred]))
+    """sklearn f1_score(average='macro', labels=np.unique(y_true)), as Dassl's evaluator
+    calls it (evaluator.py:71-76): classes only predicted, never present in y_true, are not
+    averaged in."""
+    labels = np.unique(y_true)
     f1s = []
     for c in labels:
         tp = np.sum((y_pred == c) & (y_true == c))
@@ -55,8 +57,13 @@ class Classification:
     def evaluate(self):
         if not self._pred:
             return {"accuracy": 0.0, "error": 100.0, "macro_f1": 0.0}
-        p = torch.cat(self._pred).cpu().numpy()
-        g = torch.cat(self._gt).cpu().numpy()
+        return self.evaluate_arrays(torch.cat(self._gt).cpu().numpy(), torch.cat(self._pred).cpu().numpy())
+
+    def evaluate_arrays(self, g, p):
+        """evaluator.py:67-125 on host arrays (labels g, predictions p)."""
+        g, p = np.asarray(g), np.asarray(p)
+        if len(g) == 0:
+            return {"accuracy": 0.0, "error": 100.0, "macro_f1": 0.0}
         correct = int((p == g).sum())
         acc = 100.0 * correct / len(g)
         res = {"accuracy": acc, "error": 100.0 - acc, "macro_f1": 100.0 * macro_f1(g, p)}

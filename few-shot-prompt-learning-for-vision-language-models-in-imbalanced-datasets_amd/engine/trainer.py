@@ -1,18 +1,25 @@
 """Trainer contract of Dassl's TrainerX (Dassl.pytorch/dassl/engine/trainer.py:77-303,
 306-503, 596-650) for the CoOp/CoCoOp path: register_model / get_model_names /
-update_lr / set_model_mode / save_model / resume / train / run_epoch / test /
-model_inference, with the same checkpoint layout
-(OUTPUT_DIR/<name>/model.pth.tar-<epoch> + ``checkpoint`` pointer, dict keys
-state_dict/epoch/optimizer/scheduler/val_result; torchtools.py:27-157).
+update_lr / set_model_mode / save_model / resume_model_if_exist / load_model / train /
+run_epoch / test / model_inference / parse_batch_test / get_current_lr, with the same
+checkpoint layout (engine/checkpoint.py; torchtools.py:27-157) and the same ``test``
+return contract (trainer.py:446-486: ``(y_true, y_pred)`` with ``return_pred``, else the
+first metric).
 
-Multi-GPU: one process per GPU (torchrun); the learnable prompt gradients are
-all-reduced over RCCL in ``allreduce_grads`` (fsp_amd.dist), replacing the reference's
-nn.DataParallel wrap (coop.py:435-436, cocoop.py:308-311).
+Multi-GPU: one process per GPU (torchrun) instead of the reference's nn.DataParallel wrap
+(coop.py:435-436, cocoop.py:308-311):
+* the trainable prompt parameters are broadcast from rank 0 after ``build_model``, so
+  every rank starts from the same ctx / Meta-Net whatever its seed;
+* training batches come from a rank-aware loader (data/manager.py: every rank walks the
+  same global sampler stream and takes its slice of each global batch), and the prompt
+  gradients are all-reduced in ``allreduce_grads`` -- weighted by each rank's share of the
+  global batch, so the update equals the single-process one on the union batch;
+* ``test`` runs each rank on its shard of the test set and gathers (label, prediction)
+  pairs, so every rank reports the metrics of the whole set.
 """
 from __future__ import annotations
 
 import datetime
-import os
 import os.path as osp
 import time
 from collections import OrderedDict
@@ -23,29 +30,19 @@ import torch
 from .. import dist
 from ..clip import synth
 from ..clip.model import build_model
+from ..clip.weights import load_state_dict
+from . import checkpoint as ckpt
 from .metrics import Classification
 
 
 def load_clip(cfg, prec, device, text_grad=True):
-    """Replacement for load_clip_to_cpu (coop.py:165-184): a local state dict from
-    MODEL.WEIGHTS_PATH (torch.load weights_only=True / .npz / safetensors), otherwise
-    the seeded synthetic CLIP of MODEL.BACKBONE.NAME (no network on this path).
-    text_grad=False packs no backward weights (forward-only text encoder, e.g. zero-shot)."""
+    """Replacement for load_clip_to_cpu (coop.py:165-184): the CLIP weights file at
+    MODEL.WEIGHTS_PATH (OpenAI TorchScript archive, torch.save state dict, .npz or
+    .safetensors; clip/weights.py), otherwise the seeded synthetic CLIP of
+    MODEL.BACKBONE.NAME (no network on this path). text_grad=False packs no backward
+    weights (forward-only text encoder, e.g. zero-shot)."""
     path = cfg.MODEL.get("WEIGHTS_PATH", "")
-    if path:
-        if path.endswith(".npz"):
-            with np.load(path, allow_pickle=False) as z:
-                sd = {k: z[k] for k in z.files}
-        elif path.endswith(".safetensors"):
-            from safetensors.torch import load_file
-            sd = load_file(path)
-        else:
-            sd = torch.load(path, map_location="cpu", weights_only=True)
-            if "state_dict" in sd:
-                sd = sd["state_dict"]
-        sd = {k: v for k, v in sd.items() if k not in ("input_resolution", "context_length", "vocab_size")}
-    else:
-        sd = synth.make_state_dict(cfg.MODEL.BACKBONE.NAME, seed=0)
+    sd = load_state_dict(path) if path else synth.make_state_dict(cfg.MODEL.BACKBONE.NAME, seed=0)
     return build_model(sd, prec=prec, device=device, text_grad=text_grad)
 
 
@@ -54,6 +51,7 @@ class TrainerX:
         self._models = OrderedDict()
         self._optims = OrderedDict()
         self._scheds = OrderedDict()
+        self._writer = None
         self.cfg = cfg
         self.dm = dm
         self.device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
@@ -65,6 +63,7 @@ class TrainerX:
         self.num_batches = 1
         self.check_cfg(cfg)
         self.build_model()
+        self.sync_trainable()
         self.evaluator = Classification(cfg, getattr(getattr(dm, "dataset", None), "lab2cname", None))
         self.best_result = -np.inf
 
@@ -80,7 +79,7 @@ class TrainerX:
 
     def register_model(self, name="model", model=None, optim=None, sched=None):
         if name in self._models:
-            raise KeyError("Cannot assign model with the same name")
+            raise KeyError("Found duplicate model names")
         self._models[name] = model
         self._optims[name] = optim
         self._scheds[name] = sched
@@ -104,11 +103,38 @@ class TrainerX:
 
     def set_model_mode(self, mode="train", names=None):
         for n in self.get_model_names(names):
-            self._models[n].train() if mode == "train" else self._models[n].eval()
-        self.model.train() if mode == "train" else self.model.eval()
+            if mode == "train":
+                self._models[n].train()
+            elif mode in ("test", "eval"):
+                self._models[n].eval()
+            else:
+                raise KeyError(mode)
+        model = getattr(self, "model", None)
+        if model is not None:
+            model.train() if mode == "train" else model.eval()
+
+    # ---- multi-GPU --------------------------------------------------------------------
+    def trainable_params(self):
+        return [p for n in self.get_model_names() for p in self._models[n].parameters() if p.requires_grad]
+
+    def sync_trainable(self):
+        """Broadcast the trainable parameters from rank 0 (no-op single-process)."""
+        if dist.is_dist() and dist.world_size() > 1:
+            dist.broadcast_params(self.trainable_params(), src=0)
 
     def allreduce_grads(self, module):
         dist.allreduce_grads([p for p in module.parameters() if p.requires_grad])
+
+    @staticmethod
+    def batch_weight(batch, n_local):
+        """Scale for this rank's loss before backward, so that the averaged all-reduce
+        gives the gradient of the mean loss over the global batch: n_local * world /
+        n_global (1 when every rank holds an equal share)."""
+        n_global = batch.get("n_global") if isinstance(batch, dict) else None
+        w = dist.world_size()
+        if not n_global or w == 1:
+            return 1.0
+        return float(n_local) * w / float(n_global)
 
     def model_inference(self, x):
         return self.model(x)
@@ -119,48 +145,39 @@ class TrainerX:
     # ---- checkpoints ----------------------------------------------------------------
     @staticmethod
     def load_checkpoint(path):
-        return torch.load(path, map_location="cpu", weights_only=True)
+        return ckpt.load_checkpoint(path)
 
     @staticmethod
     def load_pretrained_weights(module, path):
-        ckpt = torch.load(path, map_location="cpu", weights_only=True)
-        sd = ckpt.get("state_dict", ckpt)
-        module.load_state_dict(sd, strict=False)
+        """Dassl load_pretrained_weights (torchtools.py:267-314): matching keys and shapes."""
+        ck = ckpt.load_checkpoint(path)
+        sd = ck.get("state_dict", ck)
+        own = module.state_dict()
+        keep = {k[7:] if k.startswith("module.") else k: v for k, v in sd.items()}
+        keep = {k: v for k, v in keep.items() if k in own and own[k].shape == v.shape}
+        module.load_state_dict(keep, strict=False)
 
     def save_model(self, epoch, directory, is_best=False, val_result=None, model_name=""):
         if dist.rank() != 0:
             return
         for name in self.get_model_names():
-            sd = {k: v.detach().cpu() for k, v in self._models[name].state_dict().items()}
+            sd = OrderedDict((k, v.detach().cpu()) for k, v in self._models[name].state_dict().items())
             optim = self._optims[name].state_dict() if self._optims[name] is not None else None
             sched = self._scheds[name].state_dict() if self._scheds[name] is not None else None
-            d = osp.join(directory, name)
-            os.makedirs(d, exist_ok=True)
-            fname = model_name or f"model.pth.tar-{epoch + 1}"
-            torch.save({"state_dict": sd, "epoch": epoch + 1, "optimizer": optim, "scheduler": sched,
-                        "val_result": val_result}, osp.join(d, fname))
-            with open(osp.join(d, "checkpoint"), "w") as f:
-                f.write(f"{fname}\n")
-            if is_best:
-                torch.save({"state_dict": sd, "epoch": epoch + 1, "optimizer": optim, "scheduler": sched,
-                            "val_result": val_result}, osp.join(d, "model-best.pth.tar"))
+            ckpt.save_checkpoint({"state_dict": sd, "epoch": epoch + 1, "optimizer": optim, "scheduler": sched,
+                                  "val_result": val_result}, osp.join(directory, name), is_best=is_best,
+                                 model_name=model_name)
 
     def resume_model_if_exist(self, directory):
+        names = self.get_model_names()
+        if any(not osp.exists(osp.join(directory, n)) for n in names):
+            print("No checkpoint found, train from scratch")
+            return 0
+        print(f"Found checkpoint at {directory} (will resume training)")
         start = 0
-        for name in self.get_model_names():
-            d = osp.join(directory, name)
-            ptr = osp.join(d, "checkpoint")
-            if not osp.exists(ptr):
-                return 0
-            with open(ptr) as f:
-                fname = f.readline().strip()
-            ckpt = self.load_checkpoint(osp.join(d, fname))
-            self._models[name].load_state_dict(ckpt["state_dict"])
-            if ckpt.get("optimizer") and self._optims[name] is not None:
-                self._optims[name].load_state_dict(ckpt["optimizer"])
-            if ckpt.get("scheduler") and self._scheds[name] is not None:
-                self._scheds[name].load_state_dict(ckpt["scheduler"])
-            start = ckpt["epoch"]
+        for name in names:
+            start = ckpt.resume_from_checkpoint(osp.join(directory, name), self._models[name],
+                                                self._optims[name], self._scheds[name])
         return start
 
     # ---- loops ----------------------------------------------------------------------
@@ -170,13 +187,21 @@ class TrainerX:
         t0 = time.time()
         for self.epoch in range(self.start_epoch, self.max_epoch):
             self.run_epoch()
-            self.save_model(self.epoch, self.output_dir)
+            self.after_epoch()
         if not self.cfg.TEST.NO_TEST:
             self.test()
         print(f"Elapsed: {datetime.timedelta(seconds=round(time.time() - t0))}")
 
+    def after_epoch(self):
+        """trainer.py:422-443: checkpoint at CHECKPOINT_FREQ and at the last epoch."""
+        last = (self.epoch + 1) == self.max_epoch
+        freq = self.cfg.TRAIN.get("CHECKPOINT_FREQ", 0)
+        if last or (freq > 0 and (self.epoch + 1) % freq == 0):
+            self.save_model(self.epoch, self.output_dir)
+
     def run_epoch(self):
         self.set_model_mode("train")
+        dist.sync_rng_from(0)  # one global sampler stream on every rank (data/manager.py)
         loader = self.dm.train_loader_x
         self.num_batches = len(loader)
         for self.batch_idx, batch in enumerate(loader):
@@ -186,13 +211,33 @@ class TrainerX:
                       f"{self.num_batches}] {summary} lr {self.get_current_lr():.4e}")
 
     @torch.no_grad()
-    def test(self, split="test", return_pred=False):
+    def test(self, split=None, return_pred=False):
+        """trainer.py:446-486. Each rank evaluates its shard of the split (the loader is
+        rank-aware); labels and predictions are gathered so every rank evaluates the union.
+        Returns (y_true, y_pred) numpy arrays with ``return_pred``, else the first metric."""
         self.set_model_mode("eval")
         self.evaluator.reset()
-        loader = self.dm.test_loader if split == "test" else self.dm.val_loader
+        if split is None:
+            split = self.cfg.TEST.get("SPLIT", "test")
+        val = getattr(self.dm, "val_loader", None)
+        if split == "val" and val is not None:
+            loader = val
+        else:
+            split = "test"
+            loader = self.dm.test_loader
+        print(f"Evaluate on the *{split}* set")
+        preds, labels = [], []
         for batch in loader:
             x, y = self.parse_batch_test(batch)
             out = self.model_inference(x)
-            self.evaluator.process(out, y)
-        results = self.evaluator.evaluate()
-        return (results, self.evaluator.preds()) if return_pred else results
+            preds.append(out.argmax(1).to(torch.int64))
+            labels.append(y.to(torch.int64))
+        dev = self.device
+        p = torch.cat(preds) if preds else torch.zeros(0, dtype=torch.int64, device=dev)
+        y = torch.cat(labels) if labels else torch.zeros(0, dtype=torch.int64, device=dev)
+        p, y = dist.all_gather_varlen(p), dist.all_gather_varlen(y)
+        y_true, y_pred = y.cpu().numpy(), p.cpu().numpy()
+        results = self.evaluator.evaluate_arrays(y_true, y_pred)
+        if return_pred:
+            return y_true, y_pred
+        return list(results.values())[0]

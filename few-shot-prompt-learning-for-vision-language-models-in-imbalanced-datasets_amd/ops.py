@@ -217,7 +217,15 @@ def cosine_logits_bwd(imf, txt, inv_t, inv_i, dlogits, scale, per_image):
 
 
 def ce_loss(logits, labels, alpha=None, gamma=2.0, focal=False, grad=True):
+    _need(logits, "logits", torch.float32)
+    _need(labels, "labels", torch.int64)
     B, C = logits.shape
+    if labels.shape != (B,):
+        raise N.ClipkError(f"labels must be [{B}], got {tuple(labels.shape)}")
+    if alpha is not None:
+        _need(alpha, "alpha", torch.float32)
+        if alpha.numel() < C:
+            raise N.ClipkError(f"alpha must hold {C} class weights, got {alpha.numel()}")
     row = torch.empty(B, device=logits.device)
     dl = torch.empty_like(logits) if grad else None
     N.call("clipk_ce_loss", B, C, _p(logits), _p(labels), _p(alpha), float(gamma), int(focal),

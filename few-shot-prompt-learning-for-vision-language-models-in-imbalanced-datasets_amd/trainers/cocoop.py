@@ -23,7 +23,7 @@ from ..engine.metrics import LossSummary
 from ..clip.model import TextEncodeFn
 from ._fns import PromptAssembleFn, CosineLogitsFn, MetaNetFn
 from .losses import CrossEntropyLoss, MultiClassFocalLoss, focal_alpha
-from .prompt_base import init_prompts
+from .prompt_base import init_prompts, grads_finite
 from .coop import TextEncoder  # noqa: F401  (same API-compatible text encoder)
 
 
@@ -149,12 +149,15 @@ class CoCoOp(TrainerX):
         self.register_model("prompt_learner", self.model.prompt_learner, self.optim, self.sched)
 
     def forward_backward(self, batch):
+        """cocoop.py:313-338 (multi-GPU weighting and the amp skip test as CoOp's)."""
         image, label = self.parse_batch_train(batch)
         loss = self.model(image, label)
         self.optim.zero_grad()
-        loss.backward()
+        w = self.batch_weight(batch, image.shape[0])
+        (loss * w if w != 1.0 else loss).backward()
         self.allreduce_grads(self.model.prompt_learner)
-        self.optim.step()
+        if self.cfg.TRAINER.COCOOP.PREC != "amp" or grads_finite(self.model.prompt_learner):
+            self.optim.step()
         loss_summary = LossSummary()
         loss_summary["loss"] = loss
         if (self.batch_idx + 1) == self.num_batches:

@@ -15,6 +15,7 @@ import os.path as osp
 import torch
 import torch.nn as nn
 
+from .. import dist
 from ..engine.registry import TRAINER_REGISTRY
 from ..engine.trainer import TrainerX, load_clip
 from ..engine.optim import build_optimizer, build_lr_scheduler
@@ -22,7 +23,7 @@ from ..engine.metrics import compute_accuracy, LossSummary
 from ..clip.model import TextEncodeFn
 from ._fns import PromptAssembleFn, CosineLogitsFn
 from .losses import CrossEntropyLoss, MultiClassFocalLoss, LogitsNTXentLoss, focal_alpha
-from .prompt_base import init_prompts, TextShape
+from .prompt_base import init_prompts, TextShape, grads_finite
 
 
 class TextEncoder(nn.Module):
@@ -48,7 +49,7 @@ class PromptLearner(nn.Module):
     """coop.py:207-296. forward() returns prompts [C,77,W] for API compatibility; the
     trainer's fast path uses ``assemble()`` (fused slot splice, no [C,77,W] concat)."""
 
-    def __init__(self, cfg, classnames, clip_model):
+    def __init__(self, cfg, classnames, clip_model, class_range=None):
         super().__init__()
         c = cfg.TRAINER.COOP
         clip_imsize = clip_model.visual.input_resolution
@@ -62,13 +63,16 @@ class PromptLearner(nn.Module):
         shared = cfg.get("NATIVE", {}).get("SHARED_PREFIX", True)
         ctx_vectors, self.prompt_prefix = init_prompts(
             self, classnames, clip_model, c.N_CTX, c.CTX_INIT, c.CLASS_TOKEN_POSITION,
-            bool(c.CSC) and not c.CTX_INIT, truncate, shared)
+            bool(c.CSC) and not c.CTX_INIT, truncate, shared, class_range)
         self.ctx = nn.Parameter(ctx_vectors)
         self.class_token_position = c.CLASS_TOKEN_POSITION
 
     def assemble(self):
-        """[C*L, W] fp32 text-encoder input (prompts + positional embedding), grad -> ctx."""
-        return PromptAssembleFn.apply(self.ctx, None, self.layout)
+        """Text-encoder input rows (prompts + positional embedding) of the classes this
+        process encodes (all of them unless class-sharded), grad -> ctx."""
+        lo, hi = self.class_range
+        ctx = self.ctx[lo:hi] if (self.ctx.dim() == 3 and (lo, hi) != (0, self.n_cls)) else self.ctx
+        return PromptAssembleFn.apply(ctx, None, self.layout)
 
     def forward(self):
         ctx = self.ctx
@@ -92,10 +96,22 @@ class PromptLearner(nn.Module):
 
 
 class CustomCLIP(nn.Module):
-    def __init__(self, cfg, classnames, clip_model):
+    """coop.py:302-390. ``class_counts`` (per-rank class counts, rank order) turns on
+    class-sharded text encoding: this process encodes only its classes and the [C, E] text
+    features are all-gathered (dist.AllGatherRows: in backward the text-feature gradient
+    is reduce-scattered back to the class owners). In eval mode without autograd the text
+    features are computed once and reused until ctx changes (the reference re-encodes all
+    C prompts on every test batch, coop.py:356-363)."""
+
+    def __init__(self, cfg, classnames, clip_model, class_counts=None):
         super().__init__()
         self.cfg = cfg
-        self.prompt_learner = PromptLearner(cfg, classnames, clip_model)
+        self.class_counts = class_counts
+        class_range = None
+        if class_counts is not None:
+            lo = sum(class_counts[:dist.rank()])
+            class_range = (lo, lo + class_counts[dist.rank()])
+        self.prompt_learner = PromptLearner(cfg, classnames, clip_model, class_range)
         self.tokenized_prompts = self.prompt_learner.tokenized_prompts
         self.image_encoder = clip_model.visual
         self.text_encoder = TextEncoder(clip_model)
@@ -120,11 +136,29 @@ class CustomCLIP(nn.Module):
     def text_features(self):
         pl = self.prompt_learner
         x0 = pl.assemble()
-        return TextEncodeFn.apply(x0, self.text_core, pl.layout.shape(1))
+        txt = TextEncodeFn.apply(x0, self.text_core, pl.layout.shape(1))
+        if self.class_counts is not None:
+            txt = dist.AllGatherRows.apply(txt, self.class_counts)
+        return txt
+
+    def _cached_text_features(self):
+        ctx = self.prompt_learner.ctx
+        key = (ctx.data_ptr(), ctx._version, getattr(ctx, "_clipk_gen", 0))
+        cache = getattr(self, "_txt_cache", None)
+        if cache is None or cache[0] != key:
+            cache = self._txt_cache = (key, self.text_features())
+        return cache[1]
+
+    def train(self, mode=True):
+        self._txt_cache = None
+        return super().train(mode)
 
     def forward_once(self, image):
         imf = self.image_encoder(image)
-        txt = self.text_features()
+        if not self.training and not torch.is_grad_enabled():
+            txt = self._cached_text_features()
+        else:
+            txt = self.text_features()
         return CosineLogitsFn.apply(imf, txt, self.logit_scale_value, 0, self.prompt_learner.n_cls)
 
     def forward(self, img1, lbl=None, img2=None):
@@ -151,7 +185,11 @@ class CoOp(TrainerX):
         classnames = self.dm.dataset.classnames
         clip_model = load_clip(cfg, cfg.TRAINER.COOP.PREC, self.device)
         print("Building custom CLIP w. logit-simclr or CE")
-        self.model = CustomCLIP(cfg, classnames, clip_model)
+        counts = None
+        if dist.world_size() > 1 and cfg.get("NATIVE", {}).get("CLASS_SHARD", True):
+            w = dist.world_size()
+            counts = [hi - lo for lo, hi in (dist.shard_range(len(classnames), r, w) for r in range(w))]
+        self.model = CustomCLIP(cfg, classnames, clip_model, class_counts=counts)
         for name, param in self.model.named_parameters():
             if "prompt_learner" not in name:
                 param.requires_grad = False
@@ -162,12 +200,18 @@ class CoOp(TrainerX):
         self.register_model("prompt_learner", self.model.prompt_learner, self.optim, self.sched)
 
     def forward_backward(self, batch):
+        """coop.py:438-474. Multi-GPU: the loss is scaled by this rank's share of the global
+        batch before backward and the prompt gradients all-reduced (TrainerX). PREC amp: the
+        step is skipped when a gradient is not finite, as GradScaler.step does (the bf16
+        backward needs no loss scaling)."""
         x1, lbl, x2 = self.parse_batch_train(batch)
         loss = self.model(x1, lbl, x2)
         self.optim.zero_grad()
-        loss.backward()
+        w = self.batch_weight(batch, x1.shape[0])
+        (loss * w if w != 1.0 else loss).backward()
         self.allreduce_grads(self.model.prompt_learner)
-        self.optim.step()
+        if self.cfg.TRAINER.COOP.PREC != "amp" or grads_finite(self.model.prompt_learner):
+            self.optim.step()
         loss_summary = LossSummary()
         loss_summary["loss"] = loss
         if lbl is not None and x2 is None and self.model.loss_type == "ce":

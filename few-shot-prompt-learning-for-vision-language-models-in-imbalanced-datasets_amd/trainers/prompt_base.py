@@ -17,6 +17,14 @@ from ..clip.tokenizer import tokenize, default_tokenizer
 from ._fns import prompt_layout
 
 
+def grads_finite(module) -> bool:
+    """GradScaler.step's skip test (inf / nan in any gradient); one host sync."""
+    gs = [p.grad for p in module.parameters() if p.grad is not None]
+    if not gs:
+        return True
+    return bool(torch.stack([torch.isfinite(g).all() for g in gs]).all().item())
+
+
 class TextShape:
     """Row structure of one text-encoder call, as the native encoder takes it.
 
@@ -148,8 +156,12 @@ class PromptLayout:
 
 
 def init_prompts(module: nn.Module, classnames, clip_model, n_ctx, ctx_init, position, csc,
-                 truncate: bool, shared_prefix: bool = True):
-    """Common __init__ body; returns (ctx_vectors, prompt_prefix)."""
+                 truncate: bool, shared_prefix: bool = True, class_range=None):
+    """Common __init__ body; returns (ctx_vectors, prompt_prefix).
+
+    class_range (lo, hi): the native layout covers only classes [lo, hi) -- this rank's
+    shard under class-sharded text encoding (CoOp); the checkpointed buffers
+    (token_prefix / token_suffix) and ``n_cls`` still cover every class."""
     n_cls = len(classnames)
     W = clip_model.arch.transformer_width
     dev = clip_model.positional_embedding.device
@@ -182,9 +194,11 @@ def init_prompts(module: nn.Module, classnames, clip_model, n_ctx, ctx_init, pos
     emb[:, 1:1 + n_ctx] = 0.0
     eot = tokenized.argmax(dim=-1).numpy()
     src, cpos, L = prompt_layout(n_cls, n_ctx, name_lens, position, eot, truncate)
-    module.layout = PromptLayout(n_cls, n_ctx, src, cpos, L, eot, emb.to(dev).contiguous(),
-                                 clip_model.positional_embedding.detach(), csc=csc,
-                                 shared_prefix=shared_prefix and truncate)
+    lo, hi = (0, n_cls) if class_range is None else class_range
+    module.class_range = (lo, hi)
+    module.layout = PromptLayout(hi - lo, n_ctx, src[lo:hi], cpos[lo:hi], L, eot[lo:hi],
+                                 emb[lo:hi].to(dev).contiguous(), clip_model.positional_embedding.detach(),
+                                 csc=csc, shared_prefix=shared_prefix and truncate)
     module.n_cls, module.n_ctx = n_cls, n_ctx
     module.tokenized_prompts = tokenized
     module.name_lens = name_lens

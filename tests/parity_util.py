@@ -80,6 +80,7 @@ def run_native(meta, arrays, prec, cocoop=False, dev="cuda", truncate=True, shar
     for n, p in model.named_parameters():
         if "prompt_learner" not in n:
             p.requires_grad_(False)
+    out["ctx0"] = pl.ctx.detach().cpu().numpy().copy()
     B = meta["batch"]
     img = torch.from_numpy(synth.make_images(B, a.image_resolution, seed=1)).to(dev)
     img2 = torch.from_numpy(synth.make_images(B, a.image_resolution, seed=5)).to(dev)

@@ -153,7 +153,14 @@ def test_metrics_match_sklearn():
     from fsp_amd.engine.metrics import macro_f1, compute_accuracy, base_new_accuracy
     rs = np.random.RandomState(0)
     y, p = rs.randint(0, 7, 200), rs.randint(0, 7, 200)
-    assert abs(macro_f1(y, p) - f1_score(y, p, average="macro")) < 1e-12
+    assert abs(macro_f1(y, p) - f1_score(y, p, average="macro", labels=np.unique(y))) < 1e-12
+    # Dassl's evaluator averages over the labels present in y_true only (evaluator.py:71-76):
+    # a class that is only ever predicted must not add an F1 of 0
+    y2, p2 = rs.randint(0, 5, 100), rs.randint(0, 7, 100)
+    assert set(p2) - set(y2)
+    ref = f1_score(y2, p2, average="macro", labels=np.unique(y2))
+    assert abs(macro_f1(y2, p2) - ref) < 1e-12
+    assert macro_f1(y2, p2) != f1_score(y2, p2, average="macro")
     logits = torch.from_numpy(rs.randn(10, 5))
     lab = torch.from_numpy(rs.randint(0, 5, 10))
     acc = compute_accuracy(logits, lab)[0].item()
@@ -212,6 +219,122 @@ def test_shared_prefix_tables_reconstruct_prompts(position, n_ctx, P_expect):
     # CSC contexts and over-long class suffixes fall back to the plain layout
     assert shared_prefix_tables(src, cpos, eot, n_ctx, csc=True) is None
     assert shared_prefix_tables(src, cpos, [e + 20 for e in eot], n_ctx, csc=False) is None
+
+
+class _CpuLogits(torch.nn.Module):
+    """Test double for a CustomCLIP on CPU: logits = image.flatten(1) @ proj."""
+
+    def __init__(self, proj):
+        super().__init__()
+        self.proj = proj
+
+    def forward(self, x):
+        return x.reshape(x.shape[0], -1) @ self.proj
+
+
+def _dummy_trainer(tmp_path, test_batches=None, n_ctx=4, W=8, C=3):
+    import torch.nn as nn
+    from fsp_amd.engine.config import get_cfg_default
+    from fsp_amd.engine.optim import build_optimizer, build_lr_scheduler
+    from fsp_amd.engine.trainer import TrainerX
+
+    class Learner(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.ctx = nn.Parameter(torch.zeros(n_ctx, W))
+            self.register_buffer("token_prefix", torch.ones(C, 1, W))
+            self.register_buffer("token_suffix", torch.ones(C, 72, W))
+
+    class Dummy(TrainerX):
+        def build_model(self):
+            self.learner = Learner()
+            self.model = _CpuLogits(torch.from_numpy(np.random.RandomState(0).randn(12, C).astype(np.float32)))
+            self.optim = build_optimizer(self.learner, self.cfg.OPTIM)
+            self.sched = build_lr_scheduler(self.optim, self.cfg.OPTIM)
+            self.register_model("prompt_learner", self.learner, self.optim, self.sched)
+
+    cfg = get_cfg_default()
+    cfg.OUTPUT_DIR = str(tmp_path)
+    cfg.OPTIM.MAX_EPOCH = 2
+    cfg.OPTIM.WARMUP_EPOCH = 1
+    cfg.OPTIM.WARMUP_TYPE = "constant"
+
+    class DM:
+        test_loader = test_batches or []
+        val_loader = None
+    return Dummy(cfg, dm=DM())
+
+
+def test_trainer_test_contract(tmp_path):
+    """TrainerX.test follows Dassl (trainer.py:446-486): (y_true, y_pred) numpy arrays with
+    return_pred (PromptSRC/train.py:328,356 unpack it), otherwise the first metric (accuracy)
+    as a float; the split defaults to cfg.TEST.SPLIT."""
+    from sklearn.metrics import f1_score
+    rs = np.random.RandomState(3)
+    batches = [{"img": torch.from_numpy(rs.randn(5, 3, 2, 2).astype(np.float32)),
+                "label": torch.from_numpy(rs.randint(0, 3, 5))} for _ in range(3)]
+    t = _dummy_trainer(tmp_path, batches)
+    y_true, y_pred = t.test(return_pred=True)
+    assert isinstance(y_true, np.ndarray) and isinstance(y_pred, np.ndarray)
+    ref_pred = np.concatenate([t.model(b["img"]).argmax(1).numpy() for b in batches])
+    np.testing.assert_array_equal(y_true, np.concatenate([b["label"].numpy() for b in batches]))
+    np.testing.assert_array_equal(y_pred, ref_pred)
+    acc = t.test()
+    assert isinstance(acc, float) and abs(acc - 100.0 * np.mean(y_true == y_pred)) < 1e-9
+    res = t.evaluator.evaluate_arrays(y_true, y_pred)
+    assert list(res)[:3] == ["accuracy", "error", "macro_f1"]
+    assert abs(res["macro_f1"] - 100 * f1_score(y_true, y_pred, average="macro", labels=np.unique(y_true))) < 1e-9
+    assert t.cfg.TEST.SPLIT == "test"
+
+
+def test_reference_checkpoint_resume(tmp_path):
+    """A checkpoint written by the REFERENCE's own save_model / save_checkpoint
+    (tests/golden/make_golden_trainer.py: Dassl TrainerBase.save_model after 2 epochs of
+    CoOp, scheduler = ConstantWarmupScheduler whose state pickles its CosineAnnealingLR
+    successor) resumes here: weights, SGD momentum state and the epoch / LR position."""
+    import shutil
+    from parity_util import load_fixture
+    meta, ref = load_fixture("trainer_coop")
+    src = os.path.join(ROOT, "tests", "golden", "ref_ckpt_coop")
+    shutil.copytree(src, tmp_path / "out")
+    t = _dummy_trainer(tmp_path, n_ctx=4, W=128, C=5)
+    start = t.resume_model_if_exist(str(tmp_path / "out"))
+    assert start == meta["epochs"] == 2
+    np.testing.assert_array_equal(t.learner.ctx.detach().numpy(), ref["ctx_final"])
+    assert abs(t.get_current_lr() - ref["lr_after_epoch"][-1]) < 1e-15
+    st = t.optim.state[t.learner.ctx]
+    assert st["momentum_buffer"].shape == (4, 128)
+    g = t.optim.param_groups[0]
+    assert g["momentum"] == 0.9 and g["weight_decay"] == 5e-4 and g["dampening"] == 0
+
+
+def test_checkpoint_shapes_match_reference(tmp_path):
+    """Our checkpoints have the reference's shape: the optimizer state loads into
+    torch.optim.SGD (same param-group keys), the scheduler state has the keys of Dassl's
+    ConstantWarmupScheduler (a CosineAnnealingLR successor advanced past warmup; the
+    wrapper's count saturates at WARMUP_EPOCH), and the file reads back here."""
+    from fsp_amd.engine import checkpoint as C
+    ref = C.load_checkpoint(os.path.join(ROOT, "tests", "golden", "ref_ckpt_coop", "prompt_learner",
+                                         "model.pth.tar-2"))
+    t = _dummy_trainer(tmp_path, n_ctx=4, W=128, C=5)
+    t.learner.ctx.grad = torch.ones_like(t.learner.ctx)
+    t.update_lr()
+    t.update_lr()
+    t.save_model(1, str(tmp_path / "ours"))
+    ours = C.load_checkpoint(str(tmp_path / "ours" / "prompt_learner" / "model.pth.tar-2"))
+    assert set(ours) == set(ref)
+    assert set(ours["state_dict"]) == set(ref["state_dict"])
+    assert set(ours["optimizer"]["param_groups"][0]) == set(ref["optimizer"]["param_groups"][0])
+    assert set(ours["scheduler"]) == set(ref["scheduler"])
+    assert ours["scheduler"]["last_epoch"] == ref["scheduler"]["last_epoch"] == 1
+    assert ours["scheduler"]["successor"]["last_epoch"] == ref["scheduler"]["successor"]["last_epoch"] == 1
+    assert ours["scheduler"]["_last_lr"] == ref["scheduler"]["_last_lr"]
+    p = torch.nn.Parameter(torch.zeros(4, 128))
+    sgd = torch.optim.SGD([p], lr=0.1, momentum=0.9)
+    sgd.load_state_dict(ours["optimizer"])  # what the reference's resume does
+    t2 = _dummy_trainer(tmp_path, n_ctx=4, W=128, C=5)
+    assert t2.resume_model_if_exist(str(tmp_path / "ours")) == 2
+    assert t2.get_current_lr() == t.get_current_lr()
 
 
 def test_checkpoint_layout_and_resume(tmp_path):

@@ -5,11 +5,17 @@ Tolerances (stated here):
 * PREC "fp32" (f32-input MFMA, fp32 everything): |d logit| <= 1e-3 absolute (the
   north-star figure), features / loss / ctx-after-step rel err <= 1e-4, gradients
   rel err <= 1e-3 (prompt truncation to L_eff only reorders fp32 sums).
-* PREC "fp16" (fp16 forward GEMM operands, bf16 backward operands, fp32 accumulate):
+* PREC "fp16" (fp16 forward GEMM operands and 16-bit residual stream, fp16 backward
+  operands, fp32 accumulate / LayerNorm statistics / softmax):
   1 - cos(feature) <= 5e-4, |d logit| <= 5e-4 * logit_scale (= the cosine bound at
   scale 100), |d loss| <= 0.05 (the same logit bound through a CE/focal loss, whose
   Lipschitz constant w.r.t. the max-norm of the logits is <= 2 * alpha_max here),
   gradient 1 - cos <= 2e-3.
+* PREC "bf16" (bf16 forward and backward operands, bf16 residual stream): the SURVEY
+  §8(c) bf16 gate 1 - cos(feature) <= 5e-3, |d logit| <= 5e-3 * 100, |d loss| <= 0.5,
+  gradient 1 - cos <= 1e-2.
+* PREC "amp" (fp16 forward as PREC fp16, bf16 backward operands): the fp16 forward gates,
+  the bf16 gradient gate.
 Every case runs twice: on the shared-prefix packed row layout (default; the prompt's
 SOT + context rows encoded once per image / class set, rows past each EOT dropped) and
 on the plain [B*C, L] layout (NATIVE.SHARED_PREFIX False); both against the same vectors.
@@ -32,6 +38,10 @@ TINY_COCOOP = ["cocoop_tiny_ctxinit_ce", "cocoop_tiny_focal"]
 FULL_COOP = ["coop_vitb32_c10", "coop_vitb16_c6_focal", "coop_vitl14_c4"]
 FULL_COCOOP = ["cocoop_vitb16_c4", "cocoop_vitl14_336_c3"]
 
+
+PRECS = ["fp32", "fp16", "bf16", "amp"]
+# 16-bit gates: (feature 1-cos [logit bound = it x 100], |d loss|, gradient 1-cos)
+TOL16 = {"fp16": (5e-4, 0.05, 2e-3), "bf16": (5e-3, 0.5, 1e-2), "amp": (5e-4, 0.05, 1e-2)}
 
 SHOULD_PACK = {"coop_tiny_end_csc0_ce", "coop_tiny_middle_csc0_ce", "coop_tiny_end_focal", "coop_tiny_end_simclr",
                "coop_tiny_ctxinit_ce", "coop_tinyp8_end_ce", "cocoop_tiny_ctxinit_ce", "cocoop_tiny_focal",
@@ -62,52 +72,62 @@ def _check(name, cocoop, prec, dev, layout="packed"):
         if "text_features" in ref:
             assert rel_err(out["text_features"], ref["text_features"]) <= 1e-4
     else:
+        fwd_cos, loss_tol, grad_cos = TOL16[prec]
         report["imf_cos"] = cos_err(out["image_features"], ref["image_features"])
         report["logit_abs"] = float(np.abs(out["logits"] - ref["logits"]).max())
         report["loss_abs"] = abs(out["loss"] - float(ref["loss"]))
         for g in grads:
             report[g] = cos_err(out[g].reshape(1, -1), ref[g].reshape(1, -1))
-        print(name, prec, report)
-        assert report["imf_cos"] <= 5e-4
-        assert report["logit_abs"] <= 5e-4 * 100.0
-        assert report["loss_abs"] <= 0.05
-        for g in grads:
-            assert report[g] <= 2e-3, (g, report[g])
         if "text_features" in ref:
-            assert cos_err(out["text_features"], ref["text_features"]) <= 5e-4
+            report["txt_cos"] = cos_err(out["text_features"], ref["text_features"])
+        print(name, prec, layout, report)
+        assert report["imf_cos"] <= fwd_cos
+        assert report["logit_abs"] <= fwd_cos * 100.0
+        assert report["loss_abs"] <= loss_tol
+        for g in grads:
+            assert report[g] <= grad_cos, (g, report[g])
+        if "text_features" in ref:
+            assert report["txt_cos"] <= fwd_cos
 
 
 @pytest.mark.parametrize("layout", ["packed", "plain"])
-@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("name", TINY_COOP)
 def test_coop_tiny(dev, name, prec, layout):
     _check(name, False, prec, dev, layout)
 
 
 @pytest.mark.parametrize("layout", ["packed", "plain"])
-@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("name", TINY_COCOOP)
 def test_cocoop_tiny(dev, name, prec, layout):
     _check(name, True, prec, dev, layout)
 
 
 @pytest.mark.parametrize("layout", ["packed", "plain"])
-@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("name", FULL_COOP)
 def test_coop_full(dev, name, prec, layout):
     _check(name, False, prec, dev, layout)
 
 
 @pytest.mark.parametrize("layout", ["packed", "plain"])
-@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("name", FULL_COCOOP)
 def test_cocoop_full(dev, name, prec, layout):
     _check(name, True, prec, dev, layout)
 
 
-def _cocoop_oracle_logits_grad(arch, n_cls, batch, seed_img=1):
+_ORACLE_CACHE = {}
+
+
+def _cocoop_oracle(arch, n_cls, batch, seed_img=1):
     """CPU oracle (pinned by the golden vectors) for a CoCoOp configuration too large for
-    a committed fixture: logits, CE loss, d ctx."""
+    a committed fixture ("a photo of a" context, CE): logits, loss, d ctx, d meta_net.
+    Cached per configuration (the ViT-B/16 C = 1000 case costs ~5 TFLOP on the host)."""
+    key = (arch, n_cls, batch, seed_img)
+    if key in _ORACLE_CACHE:
+        return _ORACLE_CACHE[key]
     import torch
     from oracle import clip_oracle as O
     from fsp_amd.clip import synth
@@ -126,7 +146,13 @@ def _cocoop_oracle_logits_grad(arch, n_cls, batch, seed_img=1):
     y = torch.from_numpy(synth.make_labels(batch, n_cls, seed=2))
     loss = torch.nn.functional.cross_entropy(logits, y)
     loss.backward()
-    return logits.detach().numpy(), float(loss.detach()), ctx.grad.numpy(), ctx.detach().numpy()
+    out = {"logits": logits.detach().numpy(), "loss": float(loss.detach()), "grad_ctx": ctx.grad.numpy(),
+           "ctx0": ctx.detach().numpy()}
+    for k, v in mp.items():
+        out["grad_" + k] = v.grad.numpy()
+    _ORACLE_CACHE.clear()
+    _ORACLE_CACHE[key] = out
+    return out
 
 
 @pytest.mark.parametrize("prec", ["fp32", "fp16"])
@@ -134,33 +160,48 @@ def _cocoop_oracle_logits_grad(arch, n_cls, batch, seed_img=1):
 def test_cocoop_large_rows_vs_oracle(dev, prec, layout):
     """tiny CLIP, C = 2000 classes x B = 3 images: 66k text rows, so the large-M GEMM
     paths (persistent 256x256) run inside the full model; checked against the oracle."""
-    import torch
     meta = {"arch": "tiny", "n_cls": 2000, "batch": 3, "n_ctx": 4, "ctx_init": "a photo of a", "focal": 0}
-    logits, loss, gctx, ctx0 = _cocoop_oracle_logits_grad("tiny", 2000, 3)
-    out = run_native(meta, {"ctx0": ctx0, "tokenized": None}, prec, cocoop=True, dev=str(dev),
+    ref = _cocoop_oracle("tiny", 2000, 3)
+    out = run_native(meta, {"ctx0": ref["ctx0"], "tokenized": None}, prec, cocoop=True, dev=str(dev),
                      shared=layout == "packed")
     assert out["packed"] == (layout == "packed")
     if prec == "fp32":
-        assert float(np.abs(out["logits"] - logits).max()) <= 1e-3
-        assert rel_err(out["grad_ctx"], gctx) <= 1e-3
+        assert float(np.abs(out["logits"] - ref["logits"]).max()) <= 1e-3
+        assert rel_err(out["grad_ctx"], ref["grad_ctx"]) <= 1e-3
     else:
-        assert float(np.abs(out["logits"] - logits).max()) <= 5e-2
-        assert cos_err(out["grad_ctx"].reshape(1, -1), gctx.reshape(1, -1)) <= 2e-3
+        assert float(np.abs(out["logits"] - ref["logits"]).max()) <= 5e-2
+        assert cos_err(out["grad_ctx"].reshape(1, -1), ref["grad_ctx"].reshape(1, -1)) <= 2e-3
 
 
-def test_bench_scale_fp16_matches_fp32(dev):
-    """The benchmark workload shape (ViT-B/16, C = 1000, n_ctx 4) at B = 2: the fp16 packed
-    path (large-M GEMM configurations, shared-prefix attention) against the fp32 plain
-    path (f32 MFMA, 128x128 tiles, [B*C, L] rows)."""
+@pytest.mark.parametrize("prec", ["fp32", "fp16", "bf16", "amp"])
+def test_headline_shape_vs_oracle(dev, prec):
+    """The benchmark workload's shape (BASELINE config 3: CoCoOp ViT-B/16, C = 1000 classes,
+    n_ctx 4 "a photo of a", shared-prefix packed rows, the 192/256-row GEMM tiles and the
+    W = 512 prefix-attention tiling) at B = 2 images, against the CPU oracle: logits, CE loss,
+    d ctx and d meta_net. Gates as _check (fp32: |d logit| <= 1e-3, grads rel <= 1e-3)."""
     meta = {"arch": "ViT-B/16", "n_cls": 1000, "batch": 2, "n_ctx": 4, "ctx_init": "a photo of a", "focal": 0}
-    o32 = run_native(meta, {"ctx0": None, "tokenized": None}, "fp32", cocoop=True, dev=str(dev), shared=False)
-    o16 = run_native(meta, {"ctx0": None, "tokenized": None}, "fp16", cocoop=True, dev=str(dev))
-    assert o16["packed"] and not o32["packed"]
-    assert np.isfinite(o16["logits"]).all() and np.isfinite(o16["grad_ctx"]).all()
-    assert float(np.abs(o16["logits"] - o32["logits"]).max()) <= 5e-2
-    assert abs(o16["loss"] - o32["loss"]) <= 0.05
-    for k in [k for k in o32 if k.startswith("grad_")]:
-        assert cos_err(o16[k].reshape(1, -1), o32[k].reshape(1, -1)) <= 2e-3, k
+    ref = _cocoop_oracle("ViT-B/16", 1000, 2)
+    out = run_native(meta, {"ctx0": None, "tokenized": None}, prec, cocoop=True, dev=str(dev))
+    assert out["packed"]
+    np.testing.assert_array_equal(out["ctx0"], ref["ctx0"])
+    grads = [k for k in ref if k.startswith("grad_")]
+    report = {"logit_abs": float(np.abs(out["logits"] - ref["logits"]).max()),
+              "loss_abs": abs(out["loss"] - ref["loss"])}
+    if prec == "fp32":
+        report.update({g: rel_err(out[g], ref[g]) for g in grads})
+        print("headline", prec, report)
+        assert report["logit_abs"] <= 1e-3
+        assert report["loss_abs"] <= 1e-4 * max(1.0, abs(ref["loss"]))
+        for g in grads:
+            assert report[g] <= 1e-3, (g, report[g])
+    else:
+        fwd_cos, loss_tol, grad_cos = TOL16[prec]
+        report.update({g: cos_err(out[g].reshape(1, -1), ref[g].reshape(1, -1)) for g in grads})
+        print("headline", prec, report)
+        assert report["logit_abs"] <= fwd_cos * 100.0
+        assert report["loss_abs"] <= loss_tol
+        for g in grads:
+            assert report[g] <= grad_cos, (g, report[g])
 
 
 @pytest.mark.parametrize("prec", ["fp32", "fp16"])
