@@ -7,15 +7,28 @@ on the MI355X-native path (BASELINE.json metric, configs[2]).
 
 A step = one CoCoOp.forward_backward on a resident synthetic batch: ViT-B/16 image
 encode -> Meta-Net -> B*C conditional prompts -> text encoder fwd + input-grad bwd ->
-cosine logits -> CE -> RCCL all-reduce of the prompt grads (N>1) -> fused SGD step ->
-loss.item(). Weak scaling: every rank processes its own B images (value = total images
-over all ranks / max-over-ranks time). Weights are the seeded synthetic CLIP (no network).
+cosine logits -> CE -> RCCL all-reduce of the prompt grads (N>1) -> fused SGD step.
+Weak scaling: every rank processes its own B images (value = total images over all ranks /
+max-over-ranks time). Weights are the seeded synthetic CLIP (no network).
+
+The JSON line also carries (rank 0, N=1 unless noted):
+* ``roofline``: the dominant kernel of the step (by time) with its algorithmic FLOPs / bytes
+  per launch over its average launch time, both from hipEvents recorded around every launch
+  site (clipk_prof_sites_*) during --prof-steps extra steps run right after the timed ones
+  (events inside the timed region would add ~15 % wall time), and its HBM traffic from the
+  committed rocprofv3 PMC passes; ``kernels``: the same for every kernel class of the step
+  (GEMMs: fraction of the MFMA peak; attention / LayerNorm: GB/s and fraction of the HBM peak);
+* ``eval_images_per_sec`` over --eval-images (default 5,000) images, test batch 100;
+* ``fp32``: train / eval images/sec at PREC fp32 (the 1e-3-logit parity path);
+* ``batch1``: train images/sec at 1 image per step (the reference CoCoOp config batch size);
+* ``cpu_baseline``: the oracle (fp32 restatement) on the host cores, with nproc stated.
 """
 from __future__ import annotations
 
 import argparse
+import contextlib
+import io
 import json
-import math
 import os
 import sys
 import time
@@ -26,6 +39,28 @@ sys.path.insert(0, ROOT)
 METRIC = "CoCoOp ViT-B/16 16-shot train-step images/sec at 1/2/4/8 GPUs; eval images/sec"
 PEAK = {"fp16": 2500.0, "bf16": 2500.0, "amp": 2500.0, "fp32": 157.3}  # dense TFLOP/s (MI355X guide)
 HBM_PEAK_GBS = 8000.0  # HBM3E, MI355X_MICROARCH.md
+PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc", "traffic.json")
+
+# kernel classes of the step: launch sites that run the same kernel instantiation (rocprofv3
+# kernel-name key, for the PMC traffic lookup) -- the text GEMMs by role, attention, LN
+KERNELS = {
+    "gemm_dx_n512": (["text.fc_dx", "text.qkv_dx", "text.out_dx"], "EPI_NONE 192x256", "mfma"),
+    "gemm_proj_fwd": (["text.proj_fwd"], "EPI_BIAS_RES A_QGELU", "mfma"),
+    "gemm_dgelu": (["text.proj_dx_dgelu"], "EPI_DQGELU", "mfma"),
+    "gemm_fc_fwd": (["text.fc_fwd"], "EPI_BIAS N=2048", "mfma"),
+    "gemm_qkv_fwd": (["text.qkv_fwd"], "EPI_BIAS N=1536", "mfma"),
+    "gemm_out_fwd": (["text.out_fwd"], "EPI_BIAS_RES N=512", "mfma"),
+    "attn_bwd": (["text.attn_bwd"], "attn_prefix_bwd", "hbm"),
+    "attn_fwd": (["text.attn_fwd"], "attn_prefix_fwd", "hbm"),
+    "ln_bwd": (["text.ln_bwd"], "ln_bwd_kernel", "hbm"),
+    "ln_fwd": (["text.ln_fwd"], "ln_fwd_kernel", "hbm"),
+    "vit": (["vit.patch_embed", "vit.qkv_fwd", "vit.attn_fwd", "vit.out_fwd", "vit.fc_fwd", "vit.proj_fwd",
+             "vit.ln_fwd", "vit.head"], "ViT forward (all sites)", "mfma"),
+}
+ROOF_PMC_KEY = {"gemm_dx_n512": "gemm_nt_kernelIDF16_DF16_fLi4ELi192ELi256",
+                "gemm_dgelu": "gemm_nt_kernelIDF16_DF16_DF16_Li3E",
+                "gemm_proj_fwd": "gemm_nt_kernelIDF16_DF16_DF16_Li1ELi192ELi256ELi2ELi4ELb0ELi128ELi2ELb1E",
+                "attn_bwd": "attn_prefix_bwd_mfma"}
 
 
 def flops(arch, n_cls, L):
@@ -38,20 +73,16 @@ def flops(arch, n_cls, L):
     return f_img, f_txt, b_txt
 
 
-ROOF_KERNEL = "gemm_nt_kernelIDF16_DF16_DF16_Li3ELi256ELi256"  # EPI_DQGELU fp16 persistent 256x256
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc", "traffic.json")
-
-
 def pmc_traffic(kernel_key):
-    """HBM bytes per launch of the roofline kernel from the committed PMC passes of this
-    workload (tools/pmc_bench.sh: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of
-    bench.py; FETCH_SIZE doubled per the gfx950 note, MI355X_MICROARCH.md HBM). None if absent."""
+    """HBM bytes per launch of a kernel from the committed PMC passes of this workload
+    (tools/pmc_bench.sh: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of bench.py;
+    FETCH_SIZE doubled per the gfx950 note, MI355X_MICROARCH.md HBM). None if absent."""
     try:
         with open(PMC_FILE) as f:
             d = json.load(f)
     except OSError:
         return None
-    hits = [v["hbm_bytes"] for k, v in d.items() if kernel_key in k]
+    hits = [v["hbm_bytes"] for k, v in d.items() if kernel_key and kernel_key in k]
     return hits[0] if hits else None
 
 
@@ -76,6 +107,7 @@ def cpu_baseline(arch_name, n_ctx_init, n_cls_full, sample_cls, threads):
     img = torch.from_numpy(synth.make_images(1, a.image_resolution, seed=1))
     y = torch.zeros(1, dtype=torch.long)
     with torch.no_grad():
+        O.encode_image(sd, img)  # warm-up
         t0 = time.perf_counter()
         O.encode_image(sd, img)
         t_img = time.perf_counter() - t0
@@ -87,8 +119,141 @@ def cpu_baseline(arch_name, n_ctx_init, n_cls_full, sample_cls, threads):
     t_text = max(t_all - t_img, 1e-9)
     per_img = t_img + t_text * (n_cls_full / sample_cls)
     return {"value": round(1.0 / per_img, 6), "unit": "images/sec", "cores": threads, "kind": "port",
+            "nproc": os.cpu_count(),
             "sample": f"oracle/clip_oracle.py fp32 CPU, CoCoOp {arch_name} 1 image x {sample_cls} classes "
-                      f"fwd+bwd at 77 tokens ({t_all:.2f}s), text cost scaled linearly to {n_cls_full} classes"}
+                      f"fwd+bwd at 77 tokens ({t_all:.2f}s) on {threads} threads (host nproc {os.cpu_count()}), "
+                      f"text cost scaled linearly to {n_cls_full} classes"}
+
+
+def kernel_table(sites, steps, prec):
+    """Per kernel class: launches, avg ms, algorithmic TF/s and GB/s per launch, fractions."""
+    peak = PEAK[prec]
+    out = {}
+    for name, (members, desc, bound) in KERNELS.items():
+        ms = sum(sites[s][0] for s in members if s in sites)
+        n = sum(sites[s][1] for s in members if s in sites)
+        fl = sum(sites[s][2] for s in members if s in sites)
+        by = sum(sites[s][3] for s in members if s in sites)
+        if not n:
+            continue
+        sec = ms * 1e-3
+        tf = fl / sec / 1e12 if fl else 0.0
+        gbs = by / sec / 1e9
+        out[name] = {"kernel": desc, "launches_per_step": round(n / steps, 2), "ms_per_step": round(ms / steps, 4),
+                     "avg_launch_ms": round(ms / n, 4), "tflops": round(tf, 1), "mfma_frac": round(tf / peak, 4),
+                     "gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4), "bound": bound,
+                     "flops_per_launch": fl / n, "bytes_per_launch": by / n}
+    return out
+
+
+def roofline_of(table, prec):
+    name = max((k for k in table if k != "vit"), key=lambda k: table[k]["ms_per_step"])
+    k = table[name]
+    peak = PEAK[prec]
+    fl, by, avg = k["flops_per_launch"], k["bytes_per_launch"], k["avg_launch_ms"] * 1e-3
+    # the binding roofline: the longer of FLOPs at the MFMA peak and bytes at the HBM peak
+    hbm_bound = fl == 0 or by / (HBM_PEAK_GBS * 1e9) > fl / (peak * 1e12)
+    if hbm_bound:
+        ach = by / avg / 1e9
+        r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(ach / HBM_PEAK_GBS, 4)}
+    else:
+        ach = fl / avg / 1e12
+        r = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4)}
+    r.update({"traffic": pmc_traffic(ROOF_PMC_KEY.get(name)) if prec == "fp16" else None,
+              "kernel_class": name, "kernel": k["kernel"], "avg_launch_ms": k["avg_launch_ms"],
+              "flops_per_launch": fl, "algorithmic_bytes": by,
+              "traffic_note": "HBM bytes/launch, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (profiles/r02_pmc)"})
+    return r
+
+
+def build_trainer(args, prec, batch, dev, rank, n_test=0):
+    from fsp_amd.engine.config import get_cfg_default
+    from fsp_amd.data.synthetic import SyntheticDataManager
+    from fsp_amd.trainers.cocoop import CoCoOp
+    from fsp_amd.clip import synth
+    arch = synth.ARCHS[args.arch]
+    cfg = get_cfg_default()
+    cfg.TRAINER.NAME = "CoCoOp"
+    cfg.MODEL.BACKBONE.NAME = args.arch
+    cfg.INPUT.SIZE = (arch.image_resolution, arch.image_resolution)
+    cfg.TRAINER.COCOOP.N_CTX = 4
+    cfg.TRAINER.COCOOP.CTX_INIT = "a photo of a"
+    cfg.TRAINER.COCOOP.PREC = prec
+    cfg.DATALOADER.TRAIN_X.BATCH_SIZE = batch
+    cfg.DATASET.NUM_SHOTS = 16
+    cfg.OPTIM.MAX_EPOCH = 10
+    cfg.OPTIM.WARMUP_EPOCH = 1
+    cfg.OPTIM.WARMUP_TYPE = "constant"
+    cfg.TEST.NO_TEST = True
+    dm = SyntheticDataManager(args.classes, arch.image_resolution, batch, n_batches=2, test_batch=100,
+                              n_test=n_test, device=dev, rank=rank)
+    with contextlib.redirect_stdout(io.StringIO()):
+        trainer = CoCoOp(cfg, dm=dm)  # broadcasts the prompt parameters (N>1)
+    trainer.num_batches = 10 ** 9  # keep update_lr out of the timed loop (epoch boundary)
+    return trainer, dm
+
+
+def time_train(trainer, dm, steps, warmup, batch=None, prof_steps=0):
+    """Warm-up, then `steps` timed steps (barrier + synchronize both sides, max over ranks);
+    then, when prof_steps > 0, that many more steps with hipEvents around every launch
+    site (kept out of the timed region: ~300 event records per step add ~15 % wall time),
+    returning the per-site table."""
+    import torch
+    from fsp_amd import dist, _native as N
+    batches = dm.train_loader_x
+    if batch is not None:
+        batches = [{"img": b["img"][:batch], "label": b["label"][:batch]} for b in batches]
+
+    def step(i):
+        trainer.batch_idx = i
+        return trainer.forward_backward(batches[i % len(batches)])
+
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = time.perf_counter() - t0
+    table = None
+    if prof_steps > 0:
+        lib = N.load()
+        lib.clipk_prof_sites_enable(1)
+        for i in range(prof_steps):
+            step(i)
+        torch.cuda.synchronize()
+        table = N.prof_sites_read()
+        lib.clipk_prof_sites_enable(0)
+    return dist.max_over_ranks(t), table
+
+
+def time_eval(trainer, dm, n_images):
+    """Forward-only images/sec over n_images (test batch 100; the resident synthetic test
+    batches are cycled)."""
+    import torch
+    from fsp_amd import dist
+    trainer.set_model_mode("eval")
+    tl = dm.test_loader
+    nb = (n_images + 99) // 100
+    with torch.no_grad():
+        trainer.model_inference(tl[0]["img"])
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        n = 0
+        for i in range(nb):
+            x = tl[i % len(tl)]["img"]
+            trainer.model_inference(x)
+            n += x.shape[0]
+        torch.cuda.synchronize()
+        dist.barrier()
+        te = dist.max_over_ranks(time.perf_counter() - t0)
+    trainer.set_model_mode("train")
+    return dist.sum_over_ranks(n) / te, n
 
 
 def main():
@@ -100,17 +265,16 @@ def main():
     ap.add_argument("--classes", type=int, default=1000)
     ap.add_argument("--arch", default="ViT-B/16")
     ap.add_argument("--prec", default="fp16")
-    ap.add_argument("--eval-images", type=int, default=200)
+    ap.add_argument("--eval-images", type=int, default=5000)
     ap.add_argument("--cpu-classes", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-prof", action="store_true")
+    ap.add_argument("--prof-steps", type=int, default=3, help="steps after the timed ones with per-site hipEvents")
+    ap.add_argument("--no-prof", action="store_true", help="no per-site profiling steps")
+    ap.add_argument("--no-extra", action="store_true", help="skip the fp32 / batch-1 lines")
     args = ap.parse_args()
 
     import torch
-    from fsp_amd import dist, _native as N
-    from fsp_amd.engine.config import get_cfg_default
-    from fsp_amd.data.synthetic import SyntheticDataManager
-    from fsp_amd.trainers.cocoop import CoCoOp
+    from fsp_amd import dist
     from fsp_amd.clip import synth
 
     local = dist.init_from_env()
@@ -118,113 +282,23 @@ def main():
     rank = dist.rank()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-
     arch = synth.ARCHS[args.arch]
-    cfg = get_cfg_default()
-    cfg.TRAINER.NAME = "CoCoOp"
-    cfg.MODEL.BACKBONE.NAME = args.arch
-    cfg.INPUT.SIZE = (arch.image_resolution, arch.image_resolution)
-    cfg.TRAINER.COCOOP.N_CTX = 4
-    cfg.TRAINER.COCOOP.CTX_INIT = "a photo of a"
-    cfg.TRAINER.COCOOP.PREC = args.prec
-    cfg.DATALOADER.TRAIN_X.BATCH_SIZE = args.batch
-    cfg.DATASET.NUM_SHOTS = 16
-    cfg.OPTIM.MAX_EPOCH = 10
-    cfg.OPTIM.WARMUP_EPOCH = 1
-    cfg.OPTIM.WARMUP_TYPE = "constant"
-    cfg.TEST.NO_TEST = True
-    dm = SyntheticDataManager(args.classes, arch.image_resolution, args.batch, n_batches=2,
-                              test_batch=100, n_test=args.eval_images, device=dev, rank=rank)
-    import contextlib, io
-    with contextlib.redirect_stdout(io.StringIO()):
-        trainer = CoCoOp(cfg, dm=dm)
-    dist.broadcast_params([p for p in trainer.model.prompt_learner.parameters()])
-    trainer.num_batches = 10 ** 9  # keep update_lr out of the timed loop (epoch boundary)
+
+    trainer, dm = build_trainer(args, args.prec, args.batch, dev, rank, n_test=1000)
     lay = trainer.model.prompt_learner.layout
     L = lay.L
-    batches = dm.train_loader_x
-
-    def step(i):
-        trainer.batch_idx = i
-        return trainer.forward_backward(batches[i % len(batches)])
-
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    dist.barrier()
-    lib = N.load()
-    prof = not args.no_prof
-    if prof:
-        lib.clipk_prof_enable(N.PROF_GEMM_DGELU)
-    torch.cuda.synchronize()
-    dist.barrier()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    torch.cuda.synchronize()
-    dist.barrier()
-    t = time.perf_counter() - t0
-    roof = None
-    if prof:
-        import ctypes
-        tot, cnt, work = ctypes.c_double(), ctypes.c_long(), ctypes.c_double()
-        N.check(lib.clipk_prof_read(ctypes.byref(tot), ctypes.byref(cnt), ctypes.byref(work)), "prof_read")
-        lib.clipk_prof_enable(N.PROF_NONE)
-        if cnt.value:
-            avg_ms = tot.value / cnt.value
-            fl = work.value / cnt.value
-            ach = fl / (avg_ms * 1e-3) / 1e12
-            peak = PEAK[args.prec]  # dgelu GEMM operands: the gradient dtype (fp16 under PREC fp16)
-            traffic = pmc_traffic(ROOF_KERNEL) if (args.arch, args.classes, args.batch, args.prec) == \
-                ("ViT-B/16", 1000, 8, "fp16") else None
-            # algorithmic bytes per launch: A [M,W] + aux h [M,4W] read, out [M,4W] written (16-bit),
-            # weight [4W,W] read once
-            rows = args.batch * (lay.rows_per_group if lay.pack is not None else args.classes * L)
-            W = arch.transformer_width
-            esz = 4 if args.prec == "fp32" else 2
-            abytes = esz * (rows * (W + 4 * W * 2) + 4 * W * W)
-            # the binding roofline: the longer of FLOPs at the MFMA peak and bytes at the HBM peak
-            hbm_bound = abytes / (HBM_PEAK_GBS * 1e9) > fl / (peak * 1e12)
-            if hbm_bound:
-                achb = abytes / (avg_ms * 1e-3) / 1e9
-                roof = {"bound": "hbm", "achieved": round(achb, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(achb / HBM_PEAK_GBS, 4)}
-            else:
-                roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                        "frac": round(ach / peak, 4)}
-            roof.update({"traffic": traffic, "algorithmic_bytes": abytes, "mfma_tflops": round(ach, 2),
-                    "mfma_frac": round(ach / peak, 4),
-                    "traffic_note": "traffic = HBM bytes/launch, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
-                                    "(profiles/r01_pmc)",
-                    "kernel": "gemm_nt_kernel<f16,f16,f16,EPI_DQGELU> (text c_proj input-grad GEMM fused with "
-                              "QuickGELU'(h), M=text rows, N=4W, K=W)",
-                    "avg_launch_ms": round(avg_ms, 4), "launches": cnt.value,
-                    "flops_per_launch": fl})
-    tmax = dist.max_over_ranks(t)
-
-    # eval images/sec (forward only, reference test batch 100)
-    trainer.set_model_mode("eval")
-    with torch.no_grad():
-        for b in dm.test_loader[:1]:
-            trainer.model_inference(b["img"])
-        torch.cuda.synchronize()
-        dist.barrier()
-        te0 = time.perf_counter()
-        n_eval = 0
-        for b in dm.test_loader:
-            trainer.model_inference(b["img"])
-            n_eval += b["img"].shape[0]
-        torch.cuda.synchronize()
-        dist.barrier()
-        te = dist.max_over_ranks(time.perf_counter() - te0)
-    eval_ips = dist.sum_over_ranks(n_eval) / te if n_eval else None
+    n_prof = 0 if args.no_prof else args.prof_steps
+    t, sites = time_train(trainer, dm, args.steps, args.warmup, prof_steps=n_prof)
+    table = kernel_table(sites, n_prof, args.prec) if sites else None
+    roof = roofline_of(table, args.prec) if table else None
+    eval_ips, n_eval = time_eval(trainer, dm, args.eval_images)
 
     f_img, f_txt, b_txt = flops(arch, args.classes, L)
     step_flops = args.batch * (f_img + args.classes * (f_txt + b_txt))
-    value = world * args.batch * args.steps / tmax
+    value = world * args.batch * args.steps / t
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "images/sec", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * tmax / args.steps, 3),
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * t / args.steps, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.prec,
         "data": "synthetic (seeded U[0,1) CLIP-normalised images, random-init CLIP weights)",
         "config": {"workload": f"CoCoOp {args.arch} n_ctx=4 ctx_init='a photo of a', {args.classes} classes, "
@@ -234,15 +308,42 @@ def main():
                    "text_layout": ("shared-prefix packed, %d text rows/image (plain: %d)"
                                    % (lay.rows_per_group, args.classes * L)) if lay.pack is not None
                                   else f"plain [B*C, {L}]"},
-        "eval_images_per_sec": round(eval_ips, 3) if eval_ips else None,
+        "eval_images_per_sec": round(eval_ips, 3),
+        "eval_images": int(dist.sum_over_ranks(n_eval)),
         # reference-equivalent FLOPs (plain [B*C, L_eff] layout) per second, not executed FLOPs
-        "model_tflops_per_gpu": round(step_flops * args.steps / tmax / 1e12, 2),
+        "model_tflops_per_gpu": round(step_flops * args.steps / t / 1e12, 2),
         "roofline": roof,
+        "kernels": ({k: {kk: v[kk] for kk in ("kernel", "launches_per_step", "ms_per_step", "avg_launch_ms",
+                                               "tflops", "mfma_frac", "gbs", "hbm_frac", "bound")}
+                     for k, v in table.items()} if table else None),
     }
+    del trainer, dm
+    torch.cuda.empty_cache()
+    if not args.no_extra:
+        # the reference's batch size for CoCoOp (configs/trainers/CoCoOp/*.yaml: 1 image/step)
+        tr1, dm1 = build_trainer(args, args.prec, 1, dev, rank)
+        t1, _ = time_train(tr1, dm1, 10, 3)
+        out["batch1"] = {"images_per_sec": round(world * 10 / t1, 3), "ms_per_step": round(100 * t1, 3),
+                         "images_per_gpu_per_step": 1}
+        del tr1, dm1
+        torch.cuda.empty_cache()
+        # PREC fp32: f32-input MFMA everywhere, the path that meets |d logit| <= 1e-3
+        tr32, dm32 = build_trainer(args, "fp32", args.batch, dev, rank, n_test=500)
+        t32, _ = time_train(tr32, dm32, 3, 1)
+        e32, n32 = time_eval(tr32, dm32, 500)
+        out["fp32"] = {"images_per_sec": round(world * args.batch * 3 / t32, 3),
+                       "ms_per_step": round(1000 * t32 / 3, 3), "eval_images_per_sec": round(e32, 3),
+                       "eval_images": int(dist.sum_over_ranks(n32))}
+        del tr32, dm32
+        torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             threads = min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(args.arch, "a photo of a", args.classes, args.cpu_classes, threads)
+            cb = cpu_baseline(args.arch, "a photo of a", args.classes, args.cpu_classes, threads)
+            cb8 = cpu_baseline(args.arch, "a photo of a", args.classes, args.cpu_classes, min(8, threads))
+            cb["value_8_threads"] = cb8["value"]
+            cb["sample_8_threads"] = cb8["sample"]
+            out["cpu_baseline"] = cb
         except Exception as e:  # report, never fake
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:

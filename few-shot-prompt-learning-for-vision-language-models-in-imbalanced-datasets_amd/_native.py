@@ -77,7 +77,29 @@ SIGNATURES = {
     "clipk_vit_forward": (_I, [_P, _I, _P, _P, _P, _S, _P]),
     "clipk_prof_enable": (_I, [_I]),
     "clipk_prof_read": (_I, [_P, _P, _P]),
+    "clipk_prof_sites_enable": (_I, [_I]),
+    "clipk_prof_sites_read": (_I, [_I, _P, _P, _P, _P, _P, _P]),
 }
+
+PROF_NAME_LEN = 32
+
+
+def prof_sites_read(max_sites: int = 64):
+    """{site: (total_ms, launches, flops, bytes)} accumulated since the last read / enable."""
+    lib = load()
+    names = ctypes.create_string_buffer(max_sites * PROF_NAME_LEN)
+    ms = (ctypes.c_double * max_sites)()
+    cnt = (ctypes.c_long * max_sites)()
+    fl = (ctypes.c_double * max_sites)()
+    by = (ctypes.c_double * max_sites)()
+    n = ctypes.c_int()
+    check(lib.clipk_prof_sites_read(max_sites, names, ms, cnt, fl, by, ctypes.byref(n)), "clipk_prof_sites_read")
+    out = {}
+    for i in range(n.value):
+        nm = names.raw[i * PROF_NAME_LEN:(i + 1) * PROF_NAME_LEN].split(b"\0", 1)[0].decode()
+        if cnt[i]:
+            out[nm] = (ms[i], cnt[i], fl[i], by[i])
+    return out
 
 _lib = None
 

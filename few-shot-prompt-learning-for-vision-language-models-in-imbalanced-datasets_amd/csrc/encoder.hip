@@ -47,31 +47,53 @@ struct Carver {
 };
 
 // ---------------------------------------------------------------- profiling (bench roofline)
+// Two modes, both hipEvent pairs on the launch stream around each launch:
+//  * kind (clipk_prof_enable): one kernel class, summed (total ms, launches, work);
+//  * sites (clipk_prof_sites_enable): every named launch site of the encoders, with its
+//    algorithmic FLOPs and HBM bytes, aggregated per site by clipk_prof_sites_read.
 struct ProfState {
   int kind = CLIPK_PROF_NONE;
+  bool sites = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
-  std::vector<double> work;
+  std::vector<double> work, bytes;
+  std::vector<int> site;
+  std::vector<const char*> names;  // site table (string literals)
   size_t used = 0;
 };
 static ProfState g_prof;
+
+static int site_index(const char* name) {
+  for (size_t i = 0; i < g_prof.names.size(); ++i)
+    if (std::strcmp(g_prof.names[i], name) == 0) return (int)i;
+  g_prof.names.push_back(name);
+  return (int)g_prof.names.size() - 1;
+}
 
 struct ProfScope {
   bool on = false;
   hipStream_t st;
   size_t idx = 0;
-  ProfScope(int cls, hipStream_t s, double work) : st(s) {
-    if (g_prof.kind == CLIPK_PROF_NONE) return;
-    if (cls == CLIPK_PROF_NONE) return;
-    const bool is_gemm = cls == CLIPK_PROF_GEMM_FC || cls == CLIPK_PROF_GEMM_ALL || cls == CLIPK_PROF_GEMM_DGELU;
-    if (!(g_prof.kind == cls || (g_prof.kind == CLIPK_PROF_GEMM_ALL && is_gemm))) return;
+  ProfScope(int cls, hipStream_t s, double work, const char* site = nullptr, double bytes = 0.0) : st(s) {
+    bool take = false;
+    if (g_prof.sites) {
+      take = site != nullptr;
+    } else if (g_prof.kind != CLIPK_PROF_NONE && cls != CLIPK_PROF_NONE) {
+      const bool is_gemm = cls == CLIPK_PROF_GEMM_FC || cls == CLIPK_PROF_GEMM_ALL || cls == CLIPK_PROF_GEMM_DGELU;
+      take = g_prof.kind == cls || (g_prof.kind == CLIPK_PROF_GEMM_ALL && is_gemm);
+    }
+    if (!take) return;
     if (g_prof.used == g_prof.ev.size()) {
       hipEvent_t a, b;
       if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
       g_prof.ev.push_back({a, b});
       g_prof.work.push_back(0.0);
+      g_prof.bytes.push_back(0.0);
+      g_prof.site.push_back(-1);
     }
     idx = g_prof.used++;
     g_prof.work[idx] = work;
+    g_prof.bytes[idx] = bytes;
+    g_prof.site[idx] = site ? site_index(site) : -1;
     on = hipEventRecord(g_prof.ev[idx].first, st) == hipSuccess;
   }
   ~ProfScope() {
@@ -85,11 +107,23 @@ struct ProfScope {
     if (_rc != CLIPK_OK) return _rc; \
   } while (0)
 
+// Algorithmic HBM bytes of one GEMM: A, B read once, out (+ out2) written, residual / aux
+// read once (epi without the CLIPK_A_QGELU flag).
+static double gemm_bytes(int in, int out, int epi, int M, int N, int K, bool has_o2, int auxdt) {
+  const double a = esize(in), o = esize(out);
+  double b = (double)M * K * a + (double)N * K * a + (double)M * N * o * (has_o2 ? 2 : 1);
+  const int e = epi & ~CLIPK_A_QGELU;
+  if (e == CLIPK_EPI_BIAS_RES) b += (double)M * N * o;
+  if (e == CLIPK_EPI_DQGELU) b += (double)M * N * esize(auxdt);
+  return b;
+}
+
 // sk / skb: split-K workspace (vision: small M); nullptr = one launch over the tile grid
 static int gemm(int in, int out, int epi, int M, int N, int K, const void* A, const void* B,
                 const float* bias, const void* res, void* o, void* o2, const void* aux, int auxdt,
-                hipStream_t st, int prof_cls, void* sk = nullptr, size_t skb = 0) {
-  ProfScope ps(prof_cls, st, 2.0 * M * N * K);
+                hipStream_t st, int prof_cls, void* sk = nullptr, size_t skb = 0, const char* site = nullptr) {
+  ProfScope ps(prof_cls, st, 2.0 * M * N * K, site,
+               site ? gemm_bytes(in, out, epi, M, N, K, o2 != nullptr, auxdt) : 0.0);
   if (sk && epi != CLIPK_EPI_DQGELU)
     return clipk_gemm_splitk(in, out, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, 0, sk, skb, st);
   return clipk_gemm(in, out, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, aux, auxdt, N, st);
@@ -250,18 +284,27 @@ static int block_fwd(const clipk_encoder* e, const std::array<const void*, 16>& 
                      hipStream_t st, bool text, void* sk = nullptr, size_t skb = 0) {
   const int pg = text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE;
   const int W = e->W, rows = sh.rows, act = e->act;
-  TRY(clipk_layernorm_fwd_x(rd, act, rows, W, X, W, nullptr, (const float*)w[0], (const float*)w[1], xn, W,
-                            m1, r1, st));
-  TRY(gemm(act, act, CLIPK_EPI_BIAS, rows, 3 * W, W, xn, w[2], (const float*)w[3], nullptr, qkv,
-           nullptr, nullptr, 0, st, pg, sk, skb));
+  const double lnb = (double)rows * W * (esize(rd) + esize(act)) + (m1 ? 8.0 * rows : 0.0);
   {
-    ProfScope ps(text ? CLIPK_PROF_ATTN : CLIPK_PROF_NONE, st, 0.0);
+    ProfScope ps(CLIPK_PROF_NONE, st, 0.0, text ? "text.ln_fwd" : "vit.ln_fwd", lnb);
+    TRY(clipk_layernorm_fwd_x(rd, act, rows, W, X, W, nullptr, (const float*)w[0], (const float*)w[1], xn, W,
+                              m1, r1, st));
+  }
+  TRY(gemm(act, act, CLIPK_EPI_BIAS, rows, 3 * W, W, xn, w[2], (const float*)w[3], nullptr, qkv,
+           nullptr, nullptr, 0, st, pg, sk, skb, text ? "text.qkv_fwd" : "vit.qkv_fwd"));
+  {
+    // algorithmic: read q|k|v, write o (+ the fp32 log-sum-exp when saved)
+    const double ab = (double)rows * 4 * W * esize(act) + (lse ? 4.0 * rows * e->heads : 0.0);
+    ProfScope ps(text ? CLIPK_PROF_ATTN : CLIPK_PROF_NONE, st, 0.0, text ? "text.attn_fwd" : "vit.attn_fwd", ab);
     TRY(attn_fwd(e, sh, qkv, o, lse, st));
   }
   TRY(gemm(act, rd, CLIPK_EPI_BIAS_RES, rows, W, W, o, w[4], (const float*)w[5], X, Xm,
-           nullptr, nullptr, 0, st, pg, sk, skb));
-  TRY(clipk_layernorm_fwd_x(rd, act, rows, W, Xm, W, nullptr, (const float*)w[6], (const float*)w[7], xn, W,
-                            m2, r2, st));
+           nullptr, nullptr, 0, st, pg, sk, skb, text ? "text.out_fwd" : "vit.out_fwd"));
+  {
+    ProfScope ps(CLIPK_PROF_NONE, st, 0.0, text ? "text.ln_fwd" : "vit.ln_fwd", lnb);
+    TRY(clipk_layernorm_fwd_x(rd, act, rows, W, Xm, W, nullptr, (const float*)w[6], (const float*)w[7], xn, W,
+                              m2, r2, st));
+  }
   if (text && act != CLIPK_F32 && h && a_qgelu_on()) {
     // training: c_fc writes only the pre-activation h (kept for the backward) and c_proj
     // applies QuickGELU to its A operand while staging it, so the g write (rows x 4W x 2 B
@@ -270,15 +313,15 @@ static int block_fwd(const clipk_encoder* e, const std::array<const void*, 16>& 
     // register staging + QuickGELU of h by 3.6 % eval images/s.
     void* hb = h;
     TRY(gemm(act, act, CLIPK_EPI_BIAS, rows, 4 * W, W, xn, w[8], (const float*)w[9], nullptr, hb,
-             nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_FC));
+             nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_FC, nullptr, 0, "text.fc_fwd"));
     TRY(gemm(act, rd, CLIPK_EPI_BIAS_RES | CLIPK_A_QGELU, rows, W, 4 * W, hb, w[10], (const float*)w[11], Xm,
-             Xo, nullptr, nullptr, 0, st, pg));
+             Xo, nullptr, nullptr, 0, st, pg, nullptr, 0, "text.proj_fwd"));
     return CLIPK_OK;
   }
   TRY(gemm(act, act, CLIPK_EPI_BIAS_QGELU, rows, 4 * W, W, xn, w[8], (const float*)w[9], nullptr, g,
-           h, nullptr, 0, st, text ? CLIPK_PROF_GEMM_FC : CLIPK_PROF_NONE, sk, skb));
+           h, nullptr, 0, st, text ? CLIPK_PROF_GEMM_FC : CLIPK_PROF_NONE, sk, skb, text ? "text.fc_fwd" : "vit.fc_fwd"));
   TRY(gemm(act, rd, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo,
-           nullptr, nullptr, 0, st, pg, sk, skb));
+           nullptr, nullptr, 0, st, pg, sk, skb, text ? "text.proj_fwd" : "vit.proj_fwd"));
   return CLIPK_OK;
 }
 
@@ -423,7 +466,11 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
                            t.rstdf, nullptr, CLIPK_F32, W, r16 ? nullptr : dX, b.dX_lp, gd, eot_rows, W, st));
   // residual-gradient update of one LayerNorm backward: dres (fp32 dX or the 16-bit dX_lp,
   // in place) + LN'(dxn); last: the encoder input's gradient, always fp32 into dX
+  // algorithmic LN-backward bytes per row: dy (grad), x (residual dtype), residual gradient
+  // read + written (16-bit stream or fp32), mean / rstd
+  const double lnbb = (double)rows * W * (esize(gd) + esize(rd) + 2.0 * (r16 ? esize(gd) : 4)) + 8.0 * rows;
   auto ln_bwd = [&](const void* x, const float* gamma, const float* mean, const float* rstd, bool last) {
+    ProfScope ps(CLIPK_PROF_NONE, st, 0.0, "text.ln_bwd", lnbb);
     if (!r16)
       return clipk_layernorm_bwd_x(rd, gd, rows, W, b.dxn, W, x, W, nullptr, gamma, mean, rstd, dX, W, dX,
                                    last ? nullptr : b.dX_lp, gd, nullptr, W, st);
@@ -436,19 +483,21 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
     // MLP: dg = dX . Wproj ; dh = dg * qgelu'(h)  (h saved in the act dtype: more precise
     // than saving qgelu'(h), which rounds the saturated region)
     TRY(gemm(gd, gd, CLIPK_EPI_DQGELU, rows, 4 * W, W, b.dX_lp, w[15], nullptr, nullptr, b.dh, nullptr,
-             t.h[l], act, st, CLIPK_PROF_GEMM_DGELU));
+             t.h[l], act, st, CLIPK_PROF_GEMM_DGELU, nullptr, 0, "text.proj_dx_dgelu"));
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, 4 * W, b.dh, w[14], nullptr, nullptr, b.dxn, nullptr,
-             nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
+             nullptr, 0, st, CLIPK_PROF_GEMM_ALL, nullptr, 0, "text.fc_dx"));
     TRY(ln_bwd(t.Xm[l], (const float*)w[6], t.mean2[l], t.rstd2[l], false));
     // attention: do = dXm . Wout ; dqkv ; dxn1 = dqkv . Win
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, W, b.dX_lp, w[13], nullptr, nullptr, b.do_, nullptr,
-             nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
+             nullptr, 0, st, CLIPK_PROF_GEMM_ALL, nullptr, 0, "text.out_dx"));
     {
-      ProfScope ps(CLIPK_PROF_ATTN, st, 0.0);
+      // algorithmic: read q|k|v, o (act), do (grad), lse; write dq|dk|dv (grad)
+      const double ab = (double)rows * W * (4.0 * esize(act) + 4.0 * esize(gd)) + 4.0 * rows * e->heads;
+      ProfScope ps(CLIPK_PROF_ATTN, st, 0.0, "text.attn_bwd", ab);
       TRY(attn_bwd(e, sh, t.qkv[l], t.o[l], b.do_, t.lse[l], b.dqkv, b.part, st));
     }
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, 3 * W, b.dqkv, w[12], nullptr, nullptr, b.dxn,
-             nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
+             nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL, nullptr, 0, "text.qkv_dx"));
     TRY(ln_bwd(t.X[l], (const float*)w[0], t.mean1[l], t.rstd1[l], l == 0));
   }
   return CLIPK_OK;
@@ -589,7 +638,7 @@ extern "C" int clipk_vit_forward(const clipk_encoder* e, int B, const float* img
   TRY(gemm(act, CLIPK_F32, CLIPK_EPI_NONE, np, D, e->Kp, v.patches, e->head[5], nullptr, nullptr,
            v.pout, nullptr, nullptr, 0, st, CLIPK_PROF_NONE,
            clipk_gemm_splitk_ws_bytes(np, D, clipk_gemm_auto_splits(act, np, D, e->Kp)) <= v.sk_bytes ? v.sk : nullptr,
-           v.sk_bytes));
+           v.sk_bytes, "vit.patch_embed"));
   TRY(clipk_vit_embed_ln(B, L, D, v.pout, (const float*)e->head[6], (const float*)e->head[7],
                          (const float*)e->head[0], (const float*)e->head[1], v.x0, st));
   float* cur = v.x0;
@@ -603,12 +652,44 @@ extern "C" int clipk_vit_forward(const clipk_encoder* e, int B, const float* img
   TRY(clipk_layernorm_fwd(act, B, D, cur, L * D, nullptr, (const float*)e->head[2],
                           (const float*)e->head[3], v.cls, D, nullptr, nullptr, st));
   TRY(gemm(act, CLIPK_F32, CLIPK_EPI_NONE, B, e->E, D, v.cls, e->head[4], nullptr, nullptr, feat,
-           nullptr, nullptr, 0, st, CLIPK_PROF_NONE));
+           nullptr, nullptr, 0, st, CLIPK_PROF_NONE, nullptr, 0, "vit.head"));
   return CLIPK_OK;
 }
 
 extern "C" int clipk_prof_enable(int kind) {
   g_prof.kind = kind;
+  g_prof.sites = false;
+  g_prof.used = 0;
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_prof_sites_enable(int on) {
+  g_prof.sites = on != 0;
+  g_prof.kind = CLIPK_PROF_NONE;
+  g_prof.used = 0;
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_prof_sites_read(int max_sites, char* names, double* total_ms, long* count, double* flops,
+                                     double* bytes, int* n_sites) {
+  if (!n_sites || max_sites < 0 || (max_sites > 0 && (!names || !total_ms || !count || !flops || !bytes)))
+    return CLIPK_EINVAL;
+  const int ns = (int)g_prof.names.size();
+  for (int i = 0; i < max_sites && i < ns; ++i) {
+    std::strncpy(names + (size_t)i * CLIPK_PROF_NAME_LEN, g_prof.names[i], CLIPK_PROF_NAME_LEN - 1);
+    names[(size_t)i * CLIPK_PROF_NAME_LEN + CLIPK_PROF_NAME_LEN - 1] = 0;
+    total_ms[i] = 0.0; count[i] = 0; flops[i] = 0.0; bytes[i] = 0.0;
+  }
+  for (size_t i = 0; i < g_prof.used; ++i) {
+    const int s = g_prof.site[i];
+    if (s < 0 || s >= max_sites) continue;
+    float ms = 0.f;
+    if (hipEventSynchronize(g_prof.ev[i].second) != hipSuccess) return (int)hipGetLastError();
+    if (hipEventElapsedTime(&ms, g_prof.ev[i].first, g_prof.ev[i].second) != hipSuccess)
+      return (int)hipGetLastError();
+    total_ms[s] += ms; count[s] += 1; flops[s] += g_prof.work[i]; bytes[s] += g_prof.bytes[i];
+  }
+  *n_sites = ns < max_sites ? ns : max_sites;
   g_prof.used = 0;
   return CLIPK_OK;
 }

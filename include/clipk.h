@@ -300,6 +300,16 @@ enum { CLIPK_PROF_NONE = 0, CLIPK_PROF_GEMM_FC = 1, CLIPK_PROF_GEMM_ALL = 2, CLI
 int clipk_prof_enable(int kind);
 int clipk_prof_read(double* total_ms, long* count, double* flops_or_bytes);
 
+/* Per-launch-site timing (bench.py's per-kernel roofline table): when on, every named launch
+ * site of the encoders ("text.qkv_fwd", "text.attn_bwd", "text.ln_fwd", "vit.fc_fwd", ...) is
+ * bracketed by hipEvents on its launch stream, with its algorithmic FLOPs and HBM bytes.
+ * clipk_prof_sites_read fills up to max_sites rows (names: CLIPK_PROF_NAME_LEN chars each,
+ * NUL-terminated) summed since the last read / enable, sets *n_sites, and resets. */
+enum { CLIPK_PROF_NAME_LEN = 32 };
+int clipk_prof_sites_enable(int on);
+int clipk_prof_sites_read(int max_sites, char* names, double* total_ms, long* count, double* flops,
+                          double* bytes, int* n_sites);
+
 #ifdef __cplusplus
 }
 #endif

@@ -118,3 +118,129 @@ def test_data_parallel_grad_equals_full_batch():
     for r in (0, 1):
         np.testing.assert_allclose(out[r]["ctx"], ctx.grad.numpy(), rtol=1e-4, atol=2e-6)
         np.testing.assert_allclose(out[r]["w1"], mp_["meta_net.linear1.weight"].grad.numpy(), rtol=1e-4, atol=2e-6)
+
+
+def _sampler_shards(rank, world):
+    """Every rank walks the same global sampler stream (RNG synced from rank 0) and takes
+    its slice of each global batch."""
+    from fsp_amd import dist
+    from fsp_amd.data.fewshot import Datum, WeightedClassSampler
+    from fsp_amd.data.manager import ShardedBatchSampler
+    from torch.utils.data import RandomSampler
+    torch.manual_seed(1234 + 7 * rank)  # ranks start out of sync on purpose
+    data = [Datum(impath=f"x{i}", label=i % 4 if i < 14 else 0) for i in range(23)]
+    out = {}
+    for name, smp in (("random", RandomSampler(data)), ("weighted", WeightedClassSampler(data))):
+        dist.sync_rng_from(0)
+        bs = ShardedBatchSampler(smp, batch_size=3, drop_last=False)
+        out[name] = [list(b) for b in bs]
+        out[name + "_len"] = len(bs)
+    return out
+
+
+def test_sharded_batches_union_is_the_global_stream():
+    out = _run(_sampler_shards)
+    from fsp_amd.data.fewshot import Datum, WeightedClassSampler
+    from torch.utils.data import RandomSampler
+    data = [Datum(impath=f"x{i}", label=i % 4 if i < 14 else 0) for i in range(23)]
+    for name, cls in (("random", RandomSampler), ("weighted", WeightedClassSampler)):
+        torch.manual_seed(1234)  # rank 0's state, which every rank adopted
+        if name == "weighted":
+            list(RandomSampler(data))  # rank 0 consumed the random stream first
+        glob = list(iter(cls(data)))
+        batches = [glob[b:b + 6] for b in range(0, len(glob), 6)]
+        assert out[0][name + "_len"] == out[1][name + "_len"] == len(batches)
+        for i, gb in enumerate(batches):
+            k0, k1 = out[0][name][i], out[1][name][i]
+            assert all(n == len(gb) for _, n in k0 + k1)  # n_global rides along
+            got = [j for j, _ in k0] + [j for j, _ in k1]
+            if len(gb) >= 2:
+                assert got == gb
+            else:  # a 1-item last batch: rank 1 repeats it so it still joins the all-reduce
+                assert got == gb + gb
+
+
+def _test_sharded_eval(rank, world):
+    """TrainerX.test on each rank's contiguous shard of the test set (test double model on
+    CPU): every rank returns the labels / predictions / accuracy of the WHOLE set."""
+    import tempfile
+    from fsp_amd import dist
+    from test_host_cpu import _dummy_trainer
+    rs = np.random.RandomState(3)
+    imgs = torch.from_numpy(rs.randn(23, 3, 2, 2).astype(np.float32))
+    lbl = torch.from_numpy(rs.randint(0, 3, 23))
+    lo, hi = dist.shard_range(23)
+    mine = [{"img": imgs[i:min(i + 5, hi)], "label": lbl[i:min(i + 5, hi)]} for i in range(lo, hi, 5)]
+    t = _dummy_trainer(tempfile.mkdtemp(), mine)
+    y_true, y_pred = t.test(return_pred=True)
+    return {"y_true": y_true, "y_pred": y_pred, "acc": t.test()}
+
+
+def test_eval_sharded_over_ranks_matches_single_process(tmp_path):
+    out = _run(_test_sharded_eval)
+    from test_host_cpu import _dummy_trainer
+    rs = np.random.RandomState(3)
+    imgs = torch.from_numpy(rs.randn(23, 3, 2, 2).astype(np.float32))
+    lbl = torch.from_numpy(rs.randint(0, 3, 23))
+    t = _dummy_trainer(tmp_path, [{"img": imgs[i:i + 7], "label": lbl[i:i + 7]} for i in range(0, 23, 7)])
+    y_true, y_pred = t.test(return_pred=True)
+    acc = t.test()
+    for r in (0, 1):
+        np.testing.assert_array_equal(out[r]["y_true"], y_true)
+        np.testing.assert_array_equal(out[r]["y_pred"], y_pred)
+        assert out[r]["acc"] == acc
+
+
+def _coop_sharded_grad(rank, world, n_img=5):
+    """CoOp with class-sharded text encoding + image data parallel, on the oracle's math:
+    rank r encodes classes shard_range(C) only, dist.AllGatherRows forms the [C, E] text
+    features (reduce-scatter of their gradient in backward), each rank scores its own images
+    (uneven 3 / 2 split) with the loss weighted by its batch share, then the averaged
+    all-reduce of d ctx."""
+    from oracle import clip_oracle as O
+    from fsp_amd.clip import synth
+    from fsp_amd import dist
+    from fsp_amd.engine.trainer import TrainerX
+    from parity_util import load_fixture
+    meta, ref = load_fixture("coop_tiny_end_csc0_ce")
+    p = O.as_torch_sd(synth.make_state_dict("tiny", seed=0))
+    tok = torch.from_numpy(ref["tokenized"].astype(np.int64))
+    emb = O.token_embed(p, tok)
+    C = meta["n_cls"]
+    counts = [hi - lo for lo, hi in (dist.shard_range(C, r, world) for r in range(world))]
+    clo, chi = dist.shard_range(C)
+    ctx = torch.nn.Parameter(torch.from_numpy(ref["ctx0"]))
+    a = synth.ARCHS["tiny"]
+    img = torch.from_numpy(synth.make_images(n_img, a.image_resolution, seed=1))
+    y = torch.from_numpy(synth.make_labels(n_img, C, seed=2))
+    ilo, ihi = dist.shard_range(n_img)
+    pr = O.coop_prompts(ctx, emb[clo:chi, :1], emb[clo:chi, 5:], ref["name_lens"][clo:chi], "end")
+    txt = dist.AllGatherRows.apply(O.encode_text(p, pr, tok[clo:chi]), counts)
+    imf = O.normalize(O.encode_image(p, img[ilo:ihi]))
+    logits = p["logit_scale"].exp() * imf @ O.normalize(txt).t()
+    loss = torch.nn.functional.cross_entropy(logits, y[ilo:ihi])
+    w = TrainerX.batch_weight({"n_global": n_img}, ihi - ilo)
+    (loss * w).backward()
+    dist.allreduce_grads([ctx])
+    return {"ctx": ctx.grad.numpy().copy(), "txt": txt.detach().numpy().copy()}
+
+
+def test_coop_class_sharded_grad_equals_full_batch():
+    out = _run(_coop_sharded_grad)
+    from oracle import clip_oracle as O
+    from fsp_amd.clip import synth
+    from parity_util import load_fixture
+    meta, ref = load_fixture("coop_tiny_end_csc0_ce")
+    p = O.as_torch_sd(synth.make_state_dict("tiny", seed=0))
+    tok = torch.from_numpy(ref["tokenized"].astype(np.int64))
+    emb = O.token_embed(p, tok)
+    ctx = torch.nn.Parameter(torch.from_numpy(ref["ctx0"]))
+    a = synth.ARCHS["tiny"]
+    img = torch.from_numpy(synth.make_images(5, a.image_resolution, seed=1))
+    y = torch.from_numpy(synth.make_labels(5, meta["n_cls"], seed=2))
+    logits = O.coop_logits(p, img, ctx, emb[:, :1], emb[:, 5:], tok, ref["name_lens"], "end")
+    torch.nn.functional.cross_entropy(logits, y).backward()
+    txt = O.encode_text(p, O.coop_prompts(ctx.detach(), emb[:, :1], emb[:, 5:], ref["name_lens"], "end"), tok)
+    for r in (0, 1):
+        np.testing.assert_allclose(out[r]["txt"], txt.numpy(), rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(out[r]["ctx"], ctx.grad.numpy(), rtol=1e-4, atol=2e-5)

@@ -1,0 +1,86 @@
+"""The step's text GEMM shapes (CoCoOp ViT-B/16, B = 8, C = 1000, shared-prefix packed:
+M = 47,160 rows) on our kernel vs hipBLASLt (torch.matmul), in one process, with the A
+operand rotated over buffers totalling > 512 MB so that every launch reads A from HBM as
+inside the training step (back-to-back launches on one buffer would re-read it from the
+256 MB Infinity Cache). HIP events, min over rounds of the mean of `iters` launches.
+
+    python tools/gemm_yardstick.py [M]
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fsp_amd import ops, _native as N  # noqa: E402
+
+W = 512
+SHAPES = [  # name, N, K, epi, out dtype, aux/res
+    ("qkv_fwd  N1536 K512  BIAS", 3 * W, W, "bias"),
+    ("out_fwd  N512  K512  BIAS_RES", W, W, "res"),
+    ("fc_fwd   N2048 K512  BIAS", 4 * W, W, "bias"),
+    ("proj_fwd N512  K2048 BIAS_RES|AQGELU", W, 4 * W, "res_ag"),
+    ("dgelu    N2048 K512  DQGELU", 4 * W, W, "dqgelu"),
+    ("fc_dx    N512  K2048 NONE", W, 4 * W, "none"),
+    ("out_dx   N512  K512  NONE", W, W, "none"),
+    ("qkv_dx   N512  K1536 NONE", W, 3 * W, "none"),
+]
+
+
+def timeit(fn, iters=12, warm=3, rounds=3):
+    for i in range(warm):
+        fn(i)
+    torch.cuda.synchronize()
+    best = float("inf")
+    for _ in range(rounds):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for i in range(iters):
+            fn(i)
+        e.record()
+        torch.cuda.synchronize()
+        best = min(best, s.elapsed_time(e) / iters)
+    return best
+
+
+def main():
+    M = int(sys.argv[1]) if len(sys.argv) > 1 else 47160
+    dev = torch.device("cuda")
+    f16 = torch.float16
+    g = torch.Generator(device=dev).manual_seed(0)
+    rnd = lambda *s: (torch.randn(*s, device=dev, generator=g) * 0.5).to(f16)
+    tot_ours = tot_t = 0.0
+    for name, n, k, kind in SHAPES:
+        nbuf = max(2, -(-600_000_000 // (M * k * 2)))
+        As = [rnd(M, k) for _ in range(nbuf)]
+        B = rnd(n, k)
+        bias = torch.randn(n, device=dev)
+        res = rnd(M, n)
+        aux = rnd(M, n)
+        out = torch.empty(M, n, device=dev, dtype=f16)
+        if kind == "none":
+            ours = lambda i: ops.gemm(As[i % nbuf], B, N.EPI_NONE, f16, out=out)
+        elif kind == "bias":
+            ours = lambda i: ops.gemm(As[i % nbuf], B, N.EPI_BIAS, f16, bias=bias, out=out)
+        elif kind == "res":
+            ours = lambda i: ops.gemm(As[i % nbuf], B, N.EPI_BIAS_RES, f16, bias=bias, res=res, out=out)
+        elif kind == "res_ag":
+            ours = lambda i: ops.gemm(As[i % nbuf], B, N.EPI_BIAS_RES | N.A_QGELU, f16, bias=bias, res=res,
+                                      out=out)
+        else:
+            ours = lambda i: ops.gemm(As[i % nbuf], B, N.EPI_DQGELU, f16, aux=aux, out=out)
+        ref = lambda i: torch.matmul(As[i % nbuf], B.t(), out=out)
+        ms_o = timeit(ours)
+        ms_t = timeit(ref)
+        fl = 2.0 * M * n * k
+        tot_ours += ms_o
+        tot_t += ms_t
+        print(f"{name:38s} ours {ms_o*1e3:7.1f} us {fl/ms_o/1e9:7.1f} TF/s | hipBLASLt (plain) {ms_t*1e3:7.1f} us "
+              f"{fl/ms_t/1e9:7.1f} TF/s", flush=True)
+        del As, B, res, aux, out
+        torch.cuda.empty_cache()
+    print(f"sum ours {tot_ours*1e3:.1f} us | hipBLASLt {tot_t*1e3:.1f} us (hipBLASLt without the fused epilogues)")
+
+
+if __name__ == "__main__":
+    main()
