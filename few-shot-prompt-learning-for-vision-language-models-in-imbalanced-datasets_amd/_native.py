@@ -60,6 +60,7 @@ SIGNATURES = {
     "clipk_meta_net_bwd": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "clipk_sgd_step": (_I, [_L, _P, _P, _P, _F, _F, _F, _I, _P]),
     "clipk_cast": (_I, [_I, _L, _P, _P, _P]),
+    "clipk_rows_copy": (_I, [_I, _I, _P, _P, _P, _P, _P]),
     "clipk_encoder_create": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "clipk_encoder_destroy": (None, [_P]),
     "clipk_text_saved_bytes": (_S, [_P, _I, _I]),

@@ -10,10 +10,12 @@ but the encoders run as libclipk.so launch sequences:
   (TextEncoder.forward, trainers/coop.py:195-205) with a native input-grad backward
   (weights frozen: coop.py:419-421), exposed through ``TextEncodeFn``.
 
-Precision (cfg ``PREC``): "fp32" -> fp32 operands on f32-input MFMA (parity mode);
-"fp16"/"amp" -> fp16 forward GEMM operands, bf16 backward operands (range), fp32
-residual stream / LayerNorm / softmax / accumulation everywhere; "bf16" -> bf16 both.
-The reference's own "fp16" runs in fp32 (convert_weights disabled, model.py:699).
+Precision (cfg ``PREC``; PREC_DTYPES): "fp32" -> fp32 operands on f32-input MFMA, fp32
+residual stream (parity mode); "fp16" -> fp16 forward and backward GEMM operands, a 16-bit
+text residual stream and residual-gradient stream; "amp" -> fp16 forward, bf16 backward
+operands; "bf16" -> bf16 both. LayerNorm statistics, softmax and MFMA accumulation are fp32
+in every mode. The reference's own "fp16" runs in fp32 (convert_weights disabled,
+model.py:699), so the 16-bit modes are judged against the fp32 oracle.
 """
 from __future__ import annotations
 

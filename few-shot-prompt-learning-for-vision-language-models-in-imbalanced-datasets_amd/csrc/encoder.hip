@@ -149,8 +149,9 @@ struct TextBufs {
   std::vector<void*> qkv, o, h;
   void* Xf = nullptr;  // final layer output (== X[layers])
   float *meanf = nullptr, *rstdf = nullptr;
-  // forward temporaries
-  void *xn = nullptr, *g = nullptr, *lnf = nullptr;
+  // forward temporaries (oc / xc: the last layer's attention output and residual input
+  // gathered to the EOT rows, text_eot_last)
+  void *xn = nullptr, *g = nullptr, *lnf = nullptr, *oc = nullptr, *xc = nullptr;
   size_t saved_bytes = 0, ws_bytes = 0;
 };
 
@@ -193,6 +194,8 @@ static TextBufs text_layout(const clipk_encoder* e, size_t rows, int nout, void*
   t.xn = wk.take(rows * W * a);
   t.g = wk.take(rows * 4 * W * a);
   t.lnf = wk.take((size_t)nout * W * a);
+  t.oc = wk.take((size_t)nout * W * a);
+  t.xc = wk.take((size_t)nout * W * xs);
   t.saved_bytes = save ? sv.off : 0;
   t.ws_bytes = wk.off;
   return t;
@@ -265,23 +268,10 @@ static int attn_bwd(const clipk_encoder* e, const SeqShape& sh, const void* qkv,
                              lse, dqkv, 3 * W, st);
 }
 
-// one residual block forward (shared by text and vision)
-// X, Xm, Xo: residual stream of dtype rd (fp32, or the 16-bit act dtype for the text encoder)
-// text c_proj consumes quickgelu(h) from its A staging (knob CLIPK_TEXT_AQGELU=0: c_fc writes
-// both h and quickgelu(h) as before)
-static bool a_qgelu_on() {
-  static int v = -1;
-  if (v < 0) {
-    const char* s = getenv("CLIPK_TEXT_AQGELU");
-    v = s ? atoi(s) : 1;
-  }
-  return v != 0;
-}
-
-static int block_fwd(const clipk_encoder* e, const std::array<const void*, 16>& w, const SeqShape& sh,
-                     int rd, const void* X, void* Xm, void* Xo, void* xn, void* qkv, void* o,
-                     float* lse, void* h, void* g, float* m1, float* r1, float* m2, float* r2,
-                     hipStream_t st, bool text, void* sk = nullptr, size_t skb = 0) {
+// Attention half of a residual block: xn = LN1(X); qkv = xn Win^T + b; o = attention(qkv).
+static int block_attn(const clipk_encoder* e, const std::array<const void*, 16>& w, const SeqShape& sh, int rd,
+                      const void* X, void* xn, void* qkv, void* o, float* lse, float* m1, float* r1,
+                      hipStream_t st, bool text, void* sk, size_t skb) {
   const int pg = text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE;
   const int W = e->W, rows = sh.rows, act = e->act;
   const double lnb = (double)rows * W * (esize(rd) + esize(act)) + (m1 ? 8.0 * rows : 0.0);
@@ -298,9 +288,32 @@ static int block_fwd(const clipk_encoder* e, const std::array<const void*, 16>& 
     ProfScope ps(text ? CLIPK_PROF_ATTN : CLIPK_PROF_NONE, st, 0.0, text ? "text.attn_fwd" : "vit.attn_fwd", ab);
     TRY(attn_fwd(e, sh, qkv, o, lse, st));
   }
+  return CLIPK_OK;
+}
+
+// Post-attention half over `rows` rows: Xm = X + o Wout^T + b; xn = LN2(Xm);
+// Xo = Xm + MLP(xn). (The text encoder's last layer runs it on the EOT rows only.)
+// Residual stream X, Xm, Xo of dtype rd (fp32, or the 16-bit act dtype for the text encoder).
+// Text c_proj consumes quickgelu(h) from its A staging (knob CLIPK_TEXT_AQGELU=0: c_fc writes
+// both h and quickgelu(h) as before)
+static bool a_qgelu_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char* s = getenv("CLIPK_TEXT_AQGELU");
+    v = s ? atoi(s) : 1;
+  }
+  return v != 0;
+}
+
+static int block_post(const clipk_encoder* e, const std::array<const void*, 16>& w, int rows, int rd,
+                      const void* X, const void* o, void* Xm, void* Xo, void* xn, void* h, void* g, float* m2,
+                      float* r2, hipStream_t st, bool text, void* sk, size_t skb) {
+  const int pg = text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE;
+  const int W = e->W, act = e->act;
   TRY(gemm(act, rd, CLIPK_EPI_BIAS_RES, rows, W, W, o, w[4], (const float*)w[5], X, Xm,
            nullptr, nullptr, 0, st, pg, sk, skb, text ? "text.out_fwd" : "vit.out_fwd"));
   {
+    const double lnb = (double)rows * W * (esize(rd) + esize(act)) + (m2 ? 8.0 * rows : 0.0);
     ProfScope ps(CLIPK_PROF_NONE, st, 0.0, text ? "text.ln_fwd" : "vit.ln_fwd", lnb);
     TRY(clipk_layernorm_fwd_x(rd, act, rows, W, Xm, W, nullptr, (const float*)w[6], (const float*)w[7], xn, W,
                               m2, r2, st));
@@ -311,10 +324,9 @@ static int block_fwd(const clipk_encoder* e, const std::array<const void*, 16>& 
     // per layer) is gone: +2.7 % train images/s. Forward-only (no h kept) stays on the
     // QuickGELU epilogue: there c_fc writes g alone, and c_proj's glds staging of g beat the
     // register staging + QuickGELU of h by 3.6 % eval images/s.
-    void* hb = h;
-    TRY(gemm(act, act, CLIPK_EPI_BIAS, rows, 4 * W, W, xn, w[8], (const float*)w[9], nullptr, hb,
+    TRY(gemm(act, act, CLIPK_EPI_BIAS, rows, 4 * W, W, xn, w[8], (const float*)w[9], nullptr, h,
              nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_FC, nullptr, 0, "text.fc_fwd"));
-    TRY(gemm(act, rd, CLIPK_EPI_BIAS_RES | CLIPK_A_QGELU, rows, W, 4 * W, hb, w[10], (const float*)w[11], Xm,
+    TRY(gemm(act, rd, CLIPK_EPI_BIAS_RES | CLIPK_A_QGELU, rows, W, 4 * W, h, w[10], (const float*)w[11], Xm,
              Xo, nullptr, nullptr, 0, st, pg, nullptr, 0, "text.proj_fwd"));
     return CLIPK_OK;
   }
@@ -323,6 +335,15 @@ static int block_fwd(const clipk_encoder* e, const std::array<const void*, 16>& 
   TRY(gemm(act, rd, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo,
            nullptr, nullptr, 0, st, pg, sk, skb, text ? "text.proj_fwd" : "vit.proj_fwd"));
   return CLIPK_OK;
+}
+
+// one residual block forward over all rows (shared by text and vision)
+static int block_fwd(const clipk_encoder* e, const std::array<const void*, 16>& w, const SeqShape& sh,
+                     int rd, const void* X, void* Xm, void* Xo, void* xn, void* qkv, void* o,
+                     float* lse, void* h, void* g, float* m1, float* r1, float* m2, float* r2,
+                     hipStream_t st, bool text, void* sk = nullptr, size_t skb = 0) {
+  TRY(block_attn(e, w, sh, rd, X, xn, qkv, o, lse, m1, r1, st, text, sk, skb));
+  return block_post(e, w, sh.rows, rd, X, o, Xm, Xo, xn, h, g, m2, r2, st, text, sk, skb);
 }
 
 }  // namespace clipk
@@ -395,6 +416,21 @@ extern "C" void clipk_encoder_destroy(clipk_encoder* enc) { delete enc; }
 
 namespace clipk {
 
+// The text encoder's output is read at the EOT rows alone (ln_final + projection), so the
+// last layer's out_proj, LN2 and MLP run on those nout rows only (C=1000 packed: 8,000 of
+// 47,160 rows); its attention still covers every row, since the EOT rows attend to their
+// whole prompt. Exact (all row-wise ops); knob CLIPK_TEXT_EOT_LAST=0 runs the full layer.
+// Forward and backward must agree: the saved Xm / h / X[layers] of the last layer then hold
+// nout compact rows.
+static bool text_eot_last(const SeqShape& sh) {
+  static int v = -1;
+  if (v < 0) {
+    const char* s = getenv("CLIPK_TEXT_EOT_LAST");
+    v = s ? atoi(s) : 1;
+  }
+  return v != 0 && sh.nout < sh.rows;
+}
+
 static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const float* x0, const int* eot_rows,
                              float* txt, void* saved, size_t saved_bytes, void* ws, size_t ws_bytes,
                              hipStream_t st) {
@@ -414,15 +450,32 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
     }
     cur = t.X[0];
   }
-  for (int l = 0; l < e->layers; ++l) {
+  const bool eotl = text_eot_last(sh);
+  const int nl = e->layers, nout = sh.nout;
+  for (int l = 0; l < nl; ++l) {
     void* Xo = t.X[l + 1];
     if (!save && Xo == cur) Xo = t.X[l];  // ping-pong (cur may be the caller's x0)
-    TRY(block_fwd(e, e->lw[l], sh, rd, cur, t.Xm[l], Xo, t.xn, t.qkv[l], t.o[l], t.lse[l],
-                  save ? t.h[l] : nullptr, t.g, t.mean1[l], t.rstd1[l], t.mean2[l], t.rstd2[l], st, true));
+    if (eotl && l == nl - 1) {
+      // last layer: attention over all rows (the EOT rows attend to their whole prefix),
+      // then out_proj / LN2 / MLP on the EOT rows alone; Xm, h, Xo hold nout compact rows
+      TRY(block_attn(e, e->lw[l], sh, rd, cur, t.xn, t.qkv[l], t.o[l], t.lse[l], t.mean1[l], t.rstd1[l], st,
+                     true, nullptr, 0));
+      {
+        ProfScope ps(CLIPK_PROF_NONE, st, 0.0, "text.eot_gather",
+                     2.0 * nout * W * (esize(e->act) + esize(rd)));
+        TRY(clipk_rows_copy(W * (int)esize(e->act), nout, t.o[l], eot_rows, t.oc, nullptr, st));
+        TRY(clipk_rows_copy(W * (int)esize(rd), nout, cur, eot_rows, t.xc, nullptr, st));
+      }
+      TRY(block_post(e, e->lw[l], nout, rd, t.xc, t.oc, t.Xm[l], Xo, t.xn, save ? t.h[l] : nullptr, t.g,
+                     t.mean2[l], t.rstd2[l], st, true, nullptr, 0));
+    } else {
+      TRY(block_fwd(e, e->lw[l], sh, rd, cur, t.Xm[l], Xo, t.xn, t.qkv[l], t.o[l], t.lse[l],
+                    save ? t.h[l] : nullptr, t.g, t.mean1[l], t.rstd1[l], t.mean2[l], t.rstd2[l], st, true));
+    }
     cur = Xo;
   }
   // ln_final on the EOT rows only (exact: LayerNorm is per row), then @ text_projection
-  TRY(clipk_layernorm_fwd_x(rd, e->act, sh.nout, W, cur, W, eot_rows, (const float*)e->head[0],
+  TRY(clipk_layernorm_fwd_x(rd, e->act, sh.nout, W, cur, W, eotl ? nullptr : eot_rows, (const float*)e->head[0],
                             (const float*)e->head[1], t.lnf, W, t.meanf, t.rstdf, st));
   TRY(gemm(e->act, CLIPK_F32, CLIPK_EPI_NONE, sh.nout, e->E, W, t.lnf, e->head[2], nullptr, nullptr, txt,
            nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
@@ -458,38 +511,60 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
   TRY(gemm(gd, CLIPK_F32, CLIPK_EPI_NONE, nout, W, e->E, b.dtg, e->head[3], nullptr, nullptr, b.dlnf,
            nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
   const bool r16 = text_dres16(e);
-  if (!r16 && hipMemsetAsync(dX, 0, (size_t)rows * W * 4, st) != hipSuccess) return (int)hipGetLastError();
-  if (hipMemsetAsync(b.dX_lp, 0, (size_t)rows * W * esize(gd), st) != hipSuccess)
-    return (int)hipGetLastError();
+  const bool eotl = text_eot_last(sh);
+  auto zero = [&](void* p, size_t bytes) {
+    return hipMemsetAsync(p, 0, bytes, st) == hipSuccess ? CLIPK_OK : (int)hipGetLastError();
+  };
+  if (!eotl) {
+    // ln_final's gradient lands on the EOT rows of zeroed full-row streams
+    if (!r16) TRY(zero(dX, (size_t)rows * W * 4));
+    TRY(zero(b.dX_lp, (size_t)rows * W * esize(gd)));
+  }
   const int rd = res_dtype(e);
-  TRY(clipk_layernorm_bwd_x2(rd, CLIPK_F32, nout, W, b.dlnf, W, t.Xf, W, eot_rows, (const float*)e->head[0], t.meanf,
-                           t.rstdf, nullptr, CLIPK_F32, W, r16 ? nullptr : dX, b.dX_lp, gd, eot_rows, W, st));
-  // residual-gradient update of one LayerNorm backward: dres (fp32 dX or the 16-bit dX_lp,
-  // in place) + LN'(dxn); last: the encoder input's gradient, always fp32 into dX
+  const int* frows = eotl ? nullptr : eot_rows;  // EOT-last: the last layer's rows are compact
+  TRY(clipk_layernorm_bwd_x2(rd, CLIPK_F32, nout, W, b.dlnf, W, t.Xf, W, frows, (const float*)e->head[0], t.meanf,
+                             t.rstdf, nullptr, CLIPK_F32, W, r16 ? nullptr : dX, b.dX_lp, gd, frows, W, st));
+  // residual-gradient update of one LayerNorm backward over n rows: dres (fp32 dX or the
+  // 16-bit dX_lp, in place) + LN'(dxn); last: the encoder input's gradient, always fp32 into dX
   // algorithmic LN-backward bytes per row: dy (grad), x (residual dtype), residual gradient
   // read + written (16-bit stream or fp32), mean / rstd
-  const double lnbb = (double)rows * W * (esize(gd) + esize(rd) + 2.0 * (r16 ? esize(gd) : 4)) + 8.0 * rows;
-  auto ln_bwd = [&](const void* x, const float* gamma, const float* mean, const float* rstd, bool last) {
+  auto ln_bwd = [&](int n, const void* x, const float* gamma, const float* mean, const float* rstd, bool last) {
+    const double lnbb = (double)n * W * (esize(gd) + esize(rd) + 2.0 * (r16 ? esize(gd) : 4)) + 8.0 * n;
     ProfScope ps(CLIPK_PROF_NONE, st, 0.0, "text.ln_bwd", lnbb);
     if (!r16)
-      return clipk_layernorm_bwd_x(rd, gd, rows, W, b.dxn, W, x, W, nullptr, gamma, mean, rstd, dX, W, dX,
+      return clipk_layernorm_bwd_x(rd, gd, n, W, b.dxn, W, x, W, nullptr, gamma, mean, rstd, dX, W, dX,
                                    last ? nullptr : b.dX_lp, gd, nullptr, W, st);
-    return clipk_layernorm_bwd_x2(rd, gd, rows, W, b.dxn, W, x, W, nullptr, gamma, mean, rstd, b.dX_lp, gd, W,
+    return clipk_layernorm_bwd_x2(rd, gd, n, W, b.dxn, W, x, W, nullptr, gamma, mean, rstd, b.dX_lp, gd, W,
                                   last ? dX : nullptr, b.dX_lp, gd, nullptr, W, st);
   };
   for (int l = e->layers - 1; l >= 0; --l) {
     const auto& w = e->lw[l];
     if (!w[12] || !w[13] || !w[14] || !w[15]) return CLIPK_EINVAL;
+    const bool compact = eotl && l == e->layers - 1;
+    const int n = compact ? nout : rows;  // rows of the post-attention half
     // MLP: dg = dX . Wproj ; dh = dg * qgelu'(h)  (h saved in the act dtype: more precise
     // than saving qgelu'(h), which rounds the saturated region)
-    TRY(gemm(gd, gd, CLIPK_EPI_DQGELU, rows, 4 * W, W, b.dX_lp, w[15], nullptr, nullptr, b.dh, nullptr,
+    TRY(gemm(gd, gd, CLIPK_EPI_DQGELU, n, 4 * W, W, b.dX_lp, w[15], nullptr, nullptr, b.dh, nullptr,
              t.h[l], act, st, CLIPK_PROF_GEMM_DGELU, nullptr, 0, "text.proj_dx_dgelu"));
-    TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, 4 * W, b.dh, w[14], nullptr, nullptr, b.dxn, nullptr,
+    TRY(gemm(gd, gd, CLIPK_EPI_NONE, n, W, 4 * W, b.dh, w[14], nullptr, nullptr, b.dxn, nullptr,
              nullptr, 0, st, CLIPK_PROF_GEMM_ALL, nullptr, 0, "text.fc_dx"));
-    TRY(ln_bwd(t.Xm[l], (const float*)w[6], t.mean2[l], t.rstd2[l], false));
+    TRY(ln_bwd(n, t.Xm[l], (const float*)w[6], t.mean2[l], t.rstd2[l], false));
     // attention: do = dXm . Wout ; dqkv ; dxn1 = dqkv . Win
-    TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, W, b.dX_lp, w[13], nullptr, nullptr, b.do_, nullptr,
-             nullptr, 0, st, CLIPK_PROF_GEMM_ALL, nullptr, 0, "text.out_dx"));
+    TRY(gemm(gd, gd, CLIPK_EPI_NONE, n, W, W, b.dX_lp, w[13], nullptr, nullptr, compact ? b.dh : b.do_,
+             nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL, nullptr, 0, "text.out_dx"));
+    if (compact) {
+      // back to the full row layout: do and the residual gradient (the one LN1's backward
+      // reads: the 16-bit stream, or fp32 dX) scattered to the EOT rows of zeroed buffers
+      const int gb = W * (int)esize(gd), rb = W * (r16 ? (int)esize(gd) : 4);
+      void* res = r16 ? b.dX_lp : (void*)dX;
+      ProfScope ps(CLIPK_PROF_NONE, st, 0.0, "text.eot_scatter",
+                   2.0 * nout * (gb + 2.0 * rb) + (double)rows * (gb + rb));
+      TRY(zero(b.do_, (size_t)rows * gb));
+      TRY(clipk_rows_copy(gb, nout, b.dh, nullptr, b.do_, eot_rows, st));
+      TRY(clipk_rows_copy(rb, nout, res, nullptr, b.dqkv, nullptr, st));
+      TRY(zero(res, (size_t)rows * rb));
+      TRY(clipk_rows_copy(rb, nout, b.dqkv, nullptr, res, eot_rows, st));
+    }
     {
       // algorithmic: read q|k|v, o (act), do (grad), lse; write dq|dk|dv (grad)
       const double ab = (double)rows * W * (4.0 * esize(act) + 4.0 * esize(gd)) + 4.0 * rows * e->heads;
@@ -498,7 +573,7 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
     }
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, 3 * W, b.dqkv, w[12], nullptr, nullptr, b.dxn,
              nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL, nullptr, 0, "text.qkv_dx"));
-    TRY(ln_bwd(t.X[l], (const float*)w[0], t.mean1[l], t.rstd1[l], l == 0));
+    TRY(ln_bwd(rows, t.X[l], (const float*)w[0], t.mean1[l], t.rstd1[l], l == 0));
   }
   return CLIPK_OK;
 }

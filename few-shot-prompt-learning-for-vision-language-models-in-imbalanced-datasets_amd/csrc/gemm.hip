@@ -451,495 +451,9 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
 }
 
 
-// ---- deep-A ring (cfg 8 / 9) ------------------------------------------------------------
-// The K loop of gemm_nt_kernel waits every step for the stage issued at its top: A comes
-// from HBM / Infinity Cache (per-CU ~25-35 GB/s), B from L2, so a 64-KiB stage with one
-// step of lead (1.8 us) is fetch-bound. Here A gets a 3-deep ring (two steps of lead), B a
-// 2-deep one: 3 x BM x 128 B + 2 x 256 x 128 B = 160 KiB (256-row) / 136 KiB (192-row).
-// Step s issues B(s+1) then A(s+2), computes s, then waits vmcnt(IA) -- everything but
-// A(s+2) -- and a raw barrier (the glds stays in flight across it). Persistent: the K-step
-// stream runs across the block's output tiles. The epilogue's per-wave transpose scratch
-// is the B buffer the tile's last step just consumed (after that step's barrier).
-template <typename T, typename TO, typename TX, int EPI, int BM>
-__global__ __launch_bounds__(512, 1) void gemm_deep_kernel(GemmArgs g) {
-  constexpr int BN = 256, ROWB = 128, WM = 2, WN = 4, NW = 8;
-  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;  // TN = 4
-  constexpr int OPA = BM * ROWB, OPB = BN * ROWB;
-  constexpr int RPI = 1024 / ROWB, CPR = ROWB / 16, KK = ROWB / 64;
-  constexpr int IA = BM / RPI / NW, IB = BN / RPI / NW;
-  static_assert(BM % (RPI * NW) == 0 && OPB >= NW * EPI_SCRATCH, "deep ring geometry");
-  __shared__ CLIPK_LDS_ALIGN char smem[3 * OPA + 2 * OPB];  // one array (see header)
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = w / WN, wn = w % WN;
-  const int ntn = g.N / BN, ntm = (g.M + BM - 1) / BM, ntiles = ntm * ntn;
-  const int bid = blockIdx.x, xcd = bid & 7, q = ntiles >> 3, r = ntiles & 7;
-  const int t_beg = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  const int t_end = t_beg + (xcd < r ? q + 1 : q);
-  const int t_step = (int)(gridDim.x >> 3);
-  const int tfirst = t_beg + (bid >> 3);
-  if (tfirst >= t_end) return;  // block-uniform, before any barrier
-  const int nk = (int)((size_t)g.K * sizeof(T) / ROWB);
-  const int total = ((t_end - tfirst + t_step - 1) / t_step) * nk;
-  char* const Abuf = smem;
-  char* const Bbuf = smem + 3 * OPA;
-
-  auto swz = [](int rr) { return (rr >> 1) & 7; };
-  auto kpos = [&](int s, int& tm0, int& tn0, int& kt) {
-    const int tl = s / nk;
-    kt = s - tl * nk;
-    const int tile = tfirst + tl * t_step;
-    tm0 = (tile / ntn) * BM;
-    tn0 = (tile % ntn) * BN;
-  };
-  auto stageA = [&](int s) {
-    int tm0, tn0, kt;
-    kpos(s, tm0, tn0, kt);
-    char* base = Abuf + (s % 3) * OPA;
-#pragma unroll
-    for (int i = 0; i < IA; ++i) {
-      const int row = (w * IA + i) * RPI + lane / CPR;
-      const int c = (lane % CPR) ^ swz(row);
-      int ga = tm0 + row;
-      ga = ga < g.M ? ga : g.M - 1;
-      glds16(g.A + ((size_t)ga * g.lda) * sizeof(T) + c * 16 + (size_t)kt * ROWB, base + (w * IA + i) * 1024);
-    }
-  };
-  auto stageB = [&](int s) {
-    int tm0, tn0, kt;
-    kpos(s, tm0, tn0, kt);
-    char* base = Bbuf + (s & 1) * OPB;
-#pragma unroll
-    for (int i = 0; i < IB; ++i) {
-      const int row = (w * IB + i) * RPI + lane / CPR;
-      const int c = (lane % CPR) ^ swz(row);
-      glds16(g.B + ((size_t)(tn0 + row) * g.ldb) * sizeof(T) + c * 16 + (size_t)kt * ROWB, base + (w * IB + i) * 1024);
-    }
-  };
-  auto vm_wait = [&](bool a_in_flight) {
-    if (a_in_flight) {
-      if constexpr (IA == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  };
-  static_assert(IA == 4 || IA == 3, "vmcnt immediates");
-
-  const int fr = lane & 15, fq = lane >> 4, sw = swz(fr);
-  constexpr bool HAS_BIAS = EPI == CLIPK_EPI_BIAS || EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_BIAS_QGELU;
-  constexpr bool HAS_EXT = EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU;
-  constexpr int CW = sizeof(TO) == 2 ? 8 : 4;
-  constexpr int LPR = 64 / CW, RPQ = 64 / LPR, NQ = 16 / RPQ;
-  constexpr int XNB = CW * (int)sizeof(TX);
-  typedef Raw<XNB> XR;
-  constexpr int XREG = NQ * XNB / 4;
-  constexpr int XBUD = BM == 192 ? 32 : CLIPK_XBUD256;
-  constexpr int XD = XBUD / XREG < 1 ? 1 : (XBUD / XREG > TM ? TM : XBUD / XREG);
-  const int er = lane / LPR, ec = lane % LPR;
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  // prologue: A(0), B(0), A(1); retire the first two
-  stageA(0);
-  stageB(0);
-  if (total > 1) stageA(1);
-  vm_wait(total > 1);
-  G8_BAR();
-
-  int c_m0, c_n0, c_kt;
-  kpos(0, c_m0, c_n0, c_kt);
-  XR extq[XD][NQ];
-  for (int s = 0; s < total; ++s) {
-    const bool lastk = c_kt == nk - 1;
-    const int m0 = c_m0, n0 = c_n0;
-    const int ncol = n0 + wn * 64 + CW * ec;
-    auto load_ext = [&](int i, XR* dst) {
-      if constexpr (HAS_EXT) {
-        const int mg = m0 + wm * (BM / WM) + i * 16;
-#pragma unroll
-        for (int q2 = 0; q2 < NQ; ++q2) {
-          int mc = mg + RPQ * q2 + er;
-          mc = mc < g.M ? mc : g.M - 1;
-          if constexpr (EPI == CLIPK_EPI_BIAS_RES)
-            ld_raw<XNB>((const TX*)g.res + (size_t)mc * g.ldr + ncol, dst[q2]);
-          else
-            ld_raw<XNB>((const TX*)g.aux + (size_t)mc * g.ldaux + ncol, dst[q2]);
-        }
-      }
-    };
-    // group 0's residual / aux first: a load into those registers after the glds made the
-    // compiler drain the glds (vmcnt(0)) once per tile
-    if (lastk) load_ext(0, extq[0]);
-    if (s + 1 < total) stageB(s + 1);
-    if (s + 2 < total) stageA(s + 2);
-    const char* As = Abuf + (s % 3) * OPA + (wm * (BM / WM) + fr) * ROWB;
-    const char* Bs = Bbuf + (s & 1) * OPB + (wn * (BN / WN) + fr) * ROWB;
-#pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-      const int p = ((kk * 4 + fq) ^ sw) * 16;
-      u32x4 a[TM], b[TN];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const u32x4*>(Bs + j * 16 * ROWB + p);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const u32x4*>(As + i * 16 * ROWB + p);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mma<T>(b[j], a[i], acc[i][j]);
-    }
-    vm_wait(s + 2 < total);  // A(s+1), B(s+1) landed; A(s+2) stays in flight
-    G8_BAR();
-    if (s + 1 < total) kpos(s + 1, c_m0, c_n0, c_kt);
-    if (!lastk) continue;
-
-    // ---- epilogue: scratch = the B buffer step s consumed (every wave is past its reads)
-    float* scr = reinterpret_cast<float*>(Bbuf + (s & 1) * OPB + w * EPI_SCRATCH);
-    const long long rows_ok = (long long)(g.M - m0 < BM ? g.M - m0 : BM);
-    const __amdgpu_buffer_rsrc_t ro = tile_rsrc((const TO*)g.out + (size_t)m0 * g.ldo,
-                                                rows_ok * g.ldo * (long long)sizeof(TO));
-    __amdgpu_buffer_rsrc_t ro2 = ro;
-    if constexpr (EPI == CLIPK_EPI_BIAS_QGELU)
-      ro2 = tile_rsrc(g.out2 ? (const TO*)g.out2 + (size_t)m0 * g.ldo : nullptr,
-                      g.out2 ? rows_ok * g.ldo * (long long)sizeof(TO) : 0);
-    float bia[CW];
-#pragma unroll
-    for (int c = 0; c < CW; ++c) bia[c] = 0.f;
-    if constexpr (HAS_BIAS) {
-#pragma unroll
-      for (int c = 0; c < CW; c += 4) {
-        const f32x4 b4 = *reinterpret_cast<const f32x4*>(g.bias + ncol + c);
-        bia[c] = b4[0]; bia[c + 1] = b4[1]; bia[c + 2] = b4[2]; bia[c + 3] = b4[3];
-      }
-    }
-#pragma unroll
-    for (int d = 1; d < XD; ++d) load_ext(d, extq[d]);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int mg = m0 + wm * (BM / WM) + i * 16;
-      XR ext[NQ];
-#pragma unroll
-      for (int q2 = 0; q2 < NQ; ++q2) ext[q2] = extq[i % XD][q2];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        *reinterpret_cast<f32x4*>(scr + fr * 64 + (((4 * j + fq) ^ fr) << 2)) = acc[i][j];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int q2 = 0; q2 < NQ; ++q2) {
-        const int rr = RPQ * q2 + er;
-        const int m = mg + rr;
-        float v[CW];
-#pragma unroll
-        for (int c = 0; c < CW / 4; ++c) {
-          const f32x4 t = *reinterpret_cast<const f32x4*>(scr + rr * 64 + ((((CW / 4) * ec + c) ^ rr) << 2));
-          v[4 * c] = t[0]; v[4 * c + 1] = t[1]; v[4 * c + 2] = t[2]; v[4 * c + 3] = t[3];
-        }
-        const int off = ((m - m0) * g.ldo + ncol) * (int)sizeof(TO);  // rows >= M: dropped
-        if constexpr (HAS_BIAS) {
-#pragma unroll
-          for (int c = 0; c < CW; ++c) v[c] += bia[c];
-        }
-        if constexpr (EPI == CLIPK_EPI_BIAS_RES) {
-          float rv[CW];
-          raw_f32<TX, CW>(ext[q2], rv);
-#pragma unroll
-          for (int c = 0; c < CW; ++c) v[c] += rv[c];
-        } else if constexpr (EPI == CLIPK_EPI_BIAS_QGELU) {
-          buf_store16<TO>(ro2, off, v);
-#pragma unroll
-          for (int c = 0; c < CW; ++c) v[c] = quick_gelu(v[c]);
-        } else if constexpr (EPI == CLIPK_EPI_DQGELU) {
-          float h[CW];
-          raw_f32<TX, CW>(ext[q2], h);
-#pragma unroll
-          for (int c = 0; c < CW; ++c) v[c] *= quick_gelu_grad(h[c]);
-        }
-        buf_store16<TO>(ro, off, v);
-      }
-      if (i + XD < TM) load_ext(i + XD, extq[i % XD]);
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    G8_BAR();  // scratch reads done before step s+1 restages this B buffer
-  }
-}
-
-// ---- 8-phase ping-pong schedule (cfg 7) ---------------------------------------------------
-// 256x256 tile, 8 waves as two groups of four (wave row wm = 0 / 1, each wave 128x64 as in
-// gemm_nt_kernel), BK = 64 halfs (128-B staged rows). One K-tile is staged as four 16-KiB
-// half-tiles: A0 / A1 = the first / second 64 rows of each group's 128-row band, B0 / B1 =
-// the first / second 32 columns of each wave's 64-column band, so that every phase reads
-// whole half-tiles and a half-tile can be restaged as soon as its readers are done:
-//   phase 1: read B0, A0    MFMA quadrant (A0,B0)    stage A1 of K-tile s+1
-//   phase 2: read B1        MFMA quadrant (A0,B1)    stage A0 of K-tile s+2
-//   phase 3: read A1        MFMA quadrant (A1,B1)    stage B0 of K-tile s+2
-//   phase 4: (registers)    MFMA quadrant (A1,B0)    stage B1 of K-tile s+2; vmcnt(6)
-// A phase is {ds_reads, one half-tile of global_load_lds (2 per thread), lgkmcnt(0)} ->
-// barrier -> 16 MFMAs -> barrier. Group 1 runs one barrier behind group 0, so on each SIMD
-// one group's MFMA cluster overlaps the other group's LDS reads and load issue, and the
-// counted vmcnt keeps three half-tiles (48 KiB) in flight across barriers: never drained in
-// the loop. The K-tile stream runs on across the block's output tiles, so the next tile's
-// first K-tiles land during the epilogue (both groups run it together: one extra barrier
-// each side re-aligns and then re-staggers them).
-// Hazards (barrier pairing: group 0's phase-p first barrier is group 1's phase-(p-1) second):
-// RAW -- every wave's vmcnt for a K-tile precedes a barrier that each reader passes before
-// its first read (the wait is in phase 4, the reads from the next phase 1 on); WAR -- a
-// half-tile is restaged >= 1 phase after the phase that read it, whose reads every wave has
-// retired (lgkmcnt(0)) before that phase's first barrier.
-
-template <typename T, typename TO, typename TX, int EPI>
-__global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
-  constexpr int BM = 256, BN = 256, ROWB = 128, HALF = 128 * ROWB, BUF = 4 * HALF;
-  __shared__ CLIPK_LDS_ALIGN char smem[2 * BUF + 8 * EPI_SCRATCH];  // one array (see header)
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = w >> 2, wn = w & 3;
-  const int ntn = g.N / BN, ntm = (g.M + BM - 1) / BM, ntiles = ntm * ntn;
-  const int bid = blockIdx.x, xcd = bid & 7, q = ntiles >> 3, r = ntiles & 7;
-  const int t_beg = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  const int t_end = t_beg + (xcd < r ? q + 1 : q);
-  const int t_step = (int)(gridDim.x >> 3);
-  const int tfirst = t_beg + (bid >> 3);
-  if (tfirst >= t_end) return;  // block-uniform, before any barrier
-  skew_start(g.skew, bid);
-  const int nk = (int)((size_t)g.K * sizeof(T) / ROWB);
-  const int total = ((t_end - tfirst + t_step - 1) / t_step) * nk;  // K-tiles this block streams
-
-  // staging geometry: thread (w, lane) fills slot srow (+64 in round 1) at 16-B chunk lane&7
-  // of its 128-B row; the chunk is swizzled on the source side (slot bits 1..3)
-  const int srow = w * 8 + (lane >> 3);
-  const int pc = ((lane & 7) ^ ((srow >> 1) & 7)) * 16;
-  const int bcol = (srow >> 5) * 64 + (srow & 31);  // B: tile column of slot srow (half 0, round 0)
-  auto kpos = [&](int s, int& tm0, int& tn0, int& kt) {
-    const int tl = s / nk;
-    kt = s - tl * nk;
-    const int tile = tfirst + tl * t_step;
-    tm0 = (tile / ntn) * BM;
-    tn0 = (tile % ntn) * BN;
-  };
-  auto stageA = [&](int s, int tm0, int kt, int hh) {  // A rows i*128 + hh*64 + srow
-    char* dst = smem + (s & 1) * BUF + hh * HALF + w * 1024;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int row = tm0 + i * 128 + hh * 64 + srow;
-      row = row < g.M ? row : g.M - 1;
-      glds16(g.A + ((size_t)row * g.lda + (size_t)kt * (ROWB / sizeof(T))) * sizeof(T) + pc, dst + i * 8192);
-    }
-  };
-  auto stageB = [&](int s, int tn0, int kt, int hh) {  // B cols (2i + w/4)*64 + hh*32 + srow%32
-    char* dst = smem + (s & 1) * BUF + (2 + hh) * HALF + w * 1024;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int col = tn0 + i * 128 + hh * 32 + bcol;
-      glds16(g.B + ((size_t)col * g.ldb + (size_t)kt * (ROWB / sizeof(T))) * sizeof(T) + pc, dst + i * 8192);
-    }
-  };
-
-  const int fr = lane & 15, fq = lane >> 4, sw = (fr >> 1) & 7;
-  auto rdA = [&](const char* base, u32x4 (&a)[4][2]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        a[i][kk] = *reinterpret_cast<const u32x4*>(base + (wm * 64 + i * 16 + fr) * ROWB + (((kk * 4 + fq) ^ sw) << 4));
-  };
-  auto rdB = [&](const char* base, u32x4 (&b)[2][2]) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        b[j][kk] = *reinterpret_cast<const u32x4*>(base + (wn * 32 + j * 16 + fr) * ROWB + (((kk * 4 + fq) ^ sw) << 4));
-  };
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#define G8_MMA(A_, B_, HA, HB)                                                                        \
-  do {                                                                                                \
-    __builtin_amdgcn_s_setprio(1);                                                                    \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                     \
-    _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                     \
-    _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                                  \
-      acc[(HA) * 4 + i][(HB) * 2 + j] = mma<T>(B_[j][kk], A_[i][kk], acc[(HA) * 4 + i][(HB) * 2 + j]); \
-    __builtin_amdgcn_s_setprio(0);                                                                    \
-  } while (0)
-
-  // ---- epilogue of one output tile (per-wave LDS transpose, as gemm_nt_kernel) ----
-  constexpr bool HAS_BIAS = EPI == CLIPK_EPI_BIAS || EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_BIAS_QGELU;
-  constexpr bool HAS_EXT = EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU;
-  constexpr int CW = sizeof(TO) == 2 ? 8 : 4;
-  constexpr int LPR = 64 / CW, RPQ = 64 / LPR, NQ = 16 / RPQ;
-  constexpr int XNB = CW * (int)sizeof(TX);
-  typedef Raw<XNB> XR;
-  const int er = lane / LPR, ec = lane % LPR;
-  float* scr = reinterpret_cast<float*>(smem + 2 * BUF + w * EPI_SCRATCH);
-  auto epilogue = [&](int m0, int n0) {
-    const int ncol = n0 + wn * 64 + CW * ec;
-    XR ext_nxt[NQ];
-    auto load_ext = [&](int i, XR* dst) {
-      if constexpr (HAS_EXT) {
-        const int mg = m0 + wm * 128 + i * 16;
-#pragma unroll
-        for (int q2 = 0; q2 < NQ; ++q2) {
-          int mc = mg + RPQ * q2 + er;
-          mc = mc < g.M ? mc : g.M - 1;
-          if constexpr (EPI == CLIPK_EPI_BIAS_RES)
-            ld_raw<XNB>((const TX*)g.res + (size_t)mc * g.ldr + ncol, dst[q2]);
-          else
-            ld_raw<XNB>((const TX*)g.aux + (size_t)mc * g.ldaux + ncol, dst[q2]);
-        }
-      }
-    };
-    load_ext(0, ext_nxt);
-    const long long rows_ok = (long long)(g.M - m0 < BM ? g.M - m0 : BM);
-    const __amdgpu_buffer_rsrc_t ro = tile_rsrc((const TO*)g.out + (size_t)m0 * g.ldo,
-                                                rows_ok * g.ldo * (long long)sizeof(TO));
-    __amdgpu_buffer_rsrc_t ro2 = ro;
-    if constexpr (EPI == CLIPK_EPI_BIAS_QGELU)
-      ro2 = tile_rsrc(g.out2 ? (const TO*)g.out2 + (size_t)m0 * g.ldo : nullptr,
-                      g.out2 ? rows_ok * g.ldo * (long long)sizeof(TO) : 0);
-    float bia[CW];
-#pragma unroll
-    for (int c = 0; c < CW; ++c) bia[c] = 0.f;
-    if constexpr (HAS_BIAS) {
-#pragma unroll
-      for (int c = 0; c < CW; c += 4) {
-        const f32x4 b4 = *reinterpret_cast<const f32x4*>(g.bias + ncol + c);
-        bia[c] = b4[0]; bia[c + 1] = b4[1]; bia[c + 2] = b4[2]; bia[c + 3] = b4[3];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int mg = m0 + wm * 128 + i * 16;
-      XR ext[NQ];
-#pragma unroll
-      for (int q2 = 0; q2 < NQ; ++q2) ext[q2] = ext_nxt[q2];
-      if (i + 1 < 8) load_ext(i + 1, ext_nxt);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        *reinterpret_cast<f32x4*>(scr + fr * 64 + (((4 * j + fq) ^ fr) << 2)) = acc[i][j];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int q2 = 0; q2 < NQ; ++q2) {
-        const int rr = RPQ * q2 + er;
-        const int m = mg + rr;
-        float v[CW];
-#pragma unroll
-        for (int c = 0; c < CW / 4; ++c) {
-          const f32x4 t = *reinterpret_cast<const f32x4*>(scr + rr * 64 + ((((CW / 4) * ec + c) ^ rr) << 2));
-          v[4 * c] = t[0]; v[4 * c + 1] = t[1]; v[4 * c + 2] = t[2]; v[4 * c + 3] = t[3];
-        }
-        const int off = ((m - m0) * g.ldo + ncol) * (int)sizeof(TO);  // rows >= M: dropped
-        if constexpr (HAS_BIAS) {
-#pragma unroll
-          for (int c = 0; c < CW; ++c) v[c] += bia[c];
-        }
-        if constexpr (EPI == CLIPK_EPI_BIAS_RES) {
-          float rv[CW];
-          raw_f32<TX, CW>(ext[q2], rv);
-#pragma unroll
-          for (int c = 0; c < CW; ++c) v[c] += rv[c];
-        } else if constexpr (EPI == CLIPK_EPI_BIAS_QGELU) {
-          buf_store16<TO>(ro2, off, v);
-#pragma unroll
-          for (int c = 0; c < CW; ++c) v[c] = quick_gelu(v[c]);
-        } else if constexpr (EPI == CLIPK_EPI_DQGELU) {
-          float h[CW];
-          raw_f32<TX, CW>(ext[q2], h);
-#pragma unroll
-          for (int c = 0; c < CW; ++c) v[c] *= quick_gelu_grad(h[c]);
-        }
-        buf_store16<TO>(ro, off, v);
-      }
-    }
-  };
-
-  // ---- prologue: K-tile 0 whole, K-tile 1 but its A1 (staged by K-tile 0's phase 1) ----
-  int c_m0, c_n0, c_kt;  // the K-tile being computed
-  kpos(0, c_m0, c_n0, c_kt);
-  stageA(0, c_m0, c_kt, 0); stageB(0, c_n0, c_kt, 0); stageB(0, c_n0, c_kt, 1); stageA(0, c_m0, c_kt, 1);
-  if (total > 1) {
-    int m1, n1, k1;
-    kpos(1, m1, n1, k1);
-    stageA(1, m1, k1, 0); stageB(1, n1, k1, 0); stageB(1, n1, k1, 1);
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  G8_BAR();
-  if (wm) G8_BAR();  // group 1 runs one barrier behind
-
-  u32x4 a0[4][2], a1[4][2], b0[2][2], b1[2][2];
-  for (int s = 0; s < total; ++s) {
-    const char* buf = smem + (s & 1) * BUF;
-    const bool n1 = s + 1 < total, n2 = s + 2 < total;
-    int m1 = 0, nn1 = 0, k1 = 0, m2 = 0, nn2 = 0, k2 = 0;
-    if (n1) kpos(s + 1, m1, nn1, k1);
-    if (n2) kpos(s + 2, m2, nn2, k2);
-    // phase 1
-    rdB(buf + 2 * HALF, b0);
-    rdA(buf, a0);
-    if (n1) stageA(s + 1, m1, k1, 1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    G8_BAR();
-    G8_MMA(a0, b0, 0, 0);
-    G8_BAR();
-    // phase 2
-    rdB(buf + 3 * HALF, b1);
-    if (n2) stageA(s + 2, m2, k2, 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    G8_BAR();
-    G8_MMA(a0, b1, 0, 1);
-    G8_BAR();
-    // phase 3
-    rdA(buf + HALF, a1);
-    if (n2) stageB(s + 2, nn2, k2, 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    G8_BAR();
-    G8_MMA(a1, b1, 1, 1);
-    G8_BAR();
-    // phase 4: K-tile s+1 must have landed before the next phase 1 reads it
-    if (n2) {
-      stageB(s + 2, nn2, k2, 1);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    G8_BAR();
-    G8_MMA(a1, b0, 1, 0);
-    G8_BAR();
-    if (c_kt == nk - 1) {
-      if (!wm) G8_BAR();  // wait for group 1's last MFMA cluster: both groups store together
-      epilogue(c_m0, c_n0);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      if (wm) G8_BAR();  // re-stagger
-    }
-    c_m0 = m1; c_n0 = nn1; c_kt = k1;
-  }
-  if (!wm) G8_BAR();  // balance group 1's extra barrier
-#undef G8_MMA
-}
-
 // Tile configurations: 0 = 128x128 (4 waves, 64 KiB LDS, 2 blocks/CU),
 // 1 = 256x256 (8 waves, 128 KiB, persistent when the grid exceeds 2 waves of CUs),
 // 2 = 256x128 (8 waves, 96 KiB), 3 = 256x256 non-persistent (benchmark knob),
-// 4 = 256x128 / 5 = 128x256: 4 waves of 128x64, 64-B staged rows (48 KiB + 16 KiB epilogue
-// scratch), two blocks per CU, persistent over 2 x CUs blocks (benchmark knobs: measured
-// 5-25 % slower than 1 on every text shape -- a 32-deep K step halves the MFMA work per
-// barrier, and co-resident blocks did not overlap their epilogues),
 // 6 = 192x256 (8 waves of 96x64, 112 KiB + scratch): 4/3 more row tiles, chosen when it
 // fills the last wave of CUs better than 256-row tiles (N = 512 at 47k rows: 1.45 -> 1.92
 // waves).
@@ -951,10 +465,8 @@ static int pick_cfg(int M, int N, int esz) {
   }
   if (esz == 4) return 0;  // fp32 parity path: one configuration
   if (g_force_cfg >= 0) {
-    if ((g_force_cfg == 1 || g_force_cfg == 3 || g_force_cfg == 5 || g_force_cfg == 6 || g_force_cfg >= 7) &&
-        N % 256 == 0)
-      return g_force_cfg;
-    if (g_force_cfg == 2 || g_force_cfg == 4) return g_force_cfg;
+    if ((g_force_cfg == 1 || g_force_cfg == 3 || g_force_cfg == 6) && N % 256 == 0) return g_force_cfg;
+    if (g_force_cfg == 2) return g_force_cfg;
     return 0;
   }
   if (M >= 4096 && N % 256 == 0) {
@@ -1028,23 +540,7 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
     const int nwg = ((g.M + 127) / 128) * (g.N / 128);
     hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 128, 2, 2, false>), dim3(nwg), dim3(256), 0, st, g);
   } else {
-    if (cfg == 8 || cfg == 9) {
-      // deep-A ring, persistent: at most one block per CU, grid a multiple of 8 (XCD groups)
-      const int bm = cfg == 8 ? 256 : 192;
-      const int nwg = ((g.M + bm - 1) / bm) * (g.N / 256);
-      const int cus = num_cus();
-      const int grid = nwg < cus ? ((nwg + 7) / 8) * 8 : (cus / 8) * 8;
-      if (cfg == 8)
-        hipLaunchKernelGGL((gemm_deep_kernel<T, TO, TX, EPI, 256>), dim3(grid), dim3(512), 0, st, g);
-      else
-        hipLaunchKernelGGL((gemm_deep_kernel<T, TO, TX, EPI, 192>), dim3(grid), dim3(512), 0, st, g);
-    } else if (cfg == 7) {
-      // 8-phase ping-pong, persistent: at most one block per CU, grid a multiple of 8 (XCD groups)
-      const int nwg = ((g.M + 255) / 256) * (g.N / 256);
-      const int cus = num_cus();
-      const int grid = nwg < cus ? ((nwg + 7) / 8) * 8 : (cus / 8) * 8;
-      hipLaunchKernelGGL((gemm8_kernel<T, TO, TX, EPI>), dim3(grid), dim3(512), 0, st, g);
-    } else if (cfg == 1 || cfg == 3) {
+    if (cfg == 1 || cfg == 3) {
       const int nwg = ((g.M + 255) / 256) * (g.N / 256);
       const int cus = num_cus();
       if (cfg == 1 && nwg > 2 * cus) {
@@ -1061,23 +557,6 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
         hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 192, 256, 2, 4, true>), dim3((cus / 8) * 8), dim3(512), 0, st, g);
       else
         hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 192, 256, 2, 4, false>), dim3(nwg), dim3(512), 0, st, g);
-    } else if (cfg == 4 || cfg == 5) {
-      constexpr int R = 64;
-      const int nwg = cfg == 4 ? ((g.M + 255) / 256) * (g.N / 128) : ((g.M + 127) / 128) * (g.N / 256);
-      const int slots = 2 * num_cus();
-      const bool pers = nwg > slots;
-      const int grid = pers ? (slots / 8) * 8 : nwg;
-      if (cfg == 4) {
-        if (pers)
-          hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 128, 2, 2, true, R>), dim3(grid), dim3(256), 0, st, g);
-        else
-          hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 128, 2, 2, false, R>), dim3(grid), dim3(256), 0, st, g);
-      } else {
-        if (pers)
-          hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 256, 1, 4, true, R>), dim3(grid), dim3(256), 0, st, g);
-        else
-          hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 256, 1, 4, false, R>), dim3(grid), dim3(256), 0, st, g);
-      }
     } else if (cfg == 2) {
       const int nwg = ((g.M + 255) / 256) * (g.N / 128);
       hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 128, 4, 2, false>), dim3(nwg), dim3(512), 0, st, g);
@@ -1324,7 +803,7 @@ extern "C" int clipk_gemm_stamps(void* host, size_t bytes) {
 
 // Benchmark knob: force a tile configuration (-1 = automatic choice).
 extern "C" int clipk_gemm_set_config(int cfg) {
-  if (cfg < -1 || cfg > 9) return CLIPK_EINVAL;
+  if (cfg < -1 || cfg > 6 || cfg == 4 || cfg == 5) return CLIPK_EINVAL;
   g_force_cfg = cfg;
   return CLIPK_OK;
 }

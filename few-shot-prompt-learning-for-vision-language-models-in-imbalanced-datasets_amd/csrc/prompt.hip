@@ -395,6 +395,19 @@ __global__ __launch_bounds__(256) void cast_kernel(long n, const float* __restri
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) y[i] = (TO)x[i];
 }
 
+// ---------------------------------------------------------------- row gather / scatter
+// dst row (dst_rows ? dst_rows[i] : i) = src row (src_rows ? src_rows[i] : i), 16 B per thread
+__global__ __launch_bounds__(256) void rows_copy_kernel(int n, int chunks, const uint4* __restrict__ src,
+                                                        const int* __restrict__ src_rows, uint4* __restrict__ dst,
+                                                        const int* __restrict__ dst_rows) {
+  const long total = (long)n * chunks;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int r = (int)(i / chunks), c = (int)(i % chunks);
+    const long sr = src_rows ? src_rows[r] : r, dr = dst_rows ? dst_rows[r] : r;
+    dst[dr * chunks + c] = src[sr * chunks + c];
+  }
+}
+
 static inline int grid_for(long n) {
   long g = (n + 255) / 256;
   return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
@@ -557,6 +570,19 @@ extern "C" int clipk_sgd_step(long n, float* p, const float* g, float* buf, floa
   if (n == 0) return CLIPK_OK;
   hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, buf, lr,
                      momentum, weight_decay, has_buf);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_rows_copy(int row_bytes, int n, const void* src, const int* src_rows, void* dst,
+                               const int* dst_rows, void* stream) {
+  if (!src || !dst) return CLIPK_EINVAL;
+  if (n < 0 || row_bytes <= 0 || row_bytes % 16) return CLIPK_ESHAPE;
+  if (((uintptr_t)src | (uintptr_t)dst) & 15) return CLIPK_ESHAPE;
+  if (n == 0) return CLIPK_OK;
+  const int chunks = row_bytes / 16;
+  hipLaunchKernelGGL(rows_copy_kernel, grid_for((long)n * chunks), 256, 0, (hipStream_t)stream, n, chunks,
+                     (const uint4*)src, src_rows, (uint4*)dst, dst_rows);
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
 }

@@ -91,9 +91,9 @@ int clipk_gemm_splitk(int in_dtype, int out_dtype, int epi, int M, int N, int K,
                       void* out, int ldo, void* out2, int splits, void* ws, size_t ws_bytes,
                       void* stream);
 
-/* Benchmark knob: force the 16-bit GEMM tile configuration (0: 128x128, 1: 256x256,
- * 2: 256x128, 3: 256x256 non-persistent, 4: 256x128 / 5: 128x256 two blocks per CU;
- * -1 = automatic by shape). Not needed for normal use. */
+/* Benchmark knob: force the 16-bit GEMM tile configuration (0: 128x128, 1: 256x256
+ * (persistent above 2 x CUs tiles), 2: 256x128, 3: 256x256 non-persistent, 6: 192x256;
+ * -1 = automatic by shape; other values: CLIPK_EINVAL). Not needed for normal use. */
 int clipk_gemm_set_config(int cfg);
 
 /* Image preprocessing (Dassl/torchvision Resize+CenterCrop / RandomResizedCrop+flip,
@@ -233,6 +233,13 @@ int clipk_meta_net_bwd(int B, int V, int Hd, int Wd, const float* x, const float
 /* p -= lr * (buf = momentum*buf + (g + wd*p)); first step (has_buf==0): buf = g + wd*p. */
 int clipk_sgd_step(long n, float* p, const float* g, float* buf, float lr, float momentum,
                    float weight_decay, int has_buf, void* stream);
+
+/* Row gather / scatter: dst row (dst_rows ? dst_rows[i] : i) = src row (src_rows ? src_rows[i] : i)
+ * for i < n; rows of row_bytes (multiple of 16) bytes, 16-B aligned. The text encoder's last
+ * layer runs on the EOT rows only (the output is read there alone; exact) and moves rows
+ * between the compact and the full layouts with it. */
+int clipk_rows_copy(int row_bytes, int n, const void* src, const int* src_rows, void* dst,
+                    const int* dst_rows, void* stream);
 
 /* Elementwise cast fp32 -> dtype. */
 int clipk_cast(int out_dtype, long n, const float* x, void* y, void* stream);

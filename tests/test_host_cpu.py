@@ -30,6 +30,20 @@ def test_library_exports_every_header_symbol():
     assert "shape" in _native.strerror(-2)
 
 
+def test_gemm_config_knob_range():
+    """The GEMM tile knob accepts the shipped configurations only: the variants measured
+    slower (4 / 5: 64-B rows, 7: 8-phase ping-pong, 8 / 9: deep-A ring) left the build."""
+    from fsp_amd import _native
+    lib = _native.load()
+    try:
+        for cfg in (-1, 0, 1, 2, 3, 6):
+            assert lib.clipk_gemm_set_config(cfg) == 0, cfg
+        for cfg in (-2, 4, 5, 7, 8, 9, 10):
+            assert lib.clipk_gemm_set_config(cfg) == -1, cfg
+    finally:
+        lib.clipk_gemm_set_config(-1)
+
+
 def test_missing_library_fails_loudly(monkeypatch):
     from fsp_amd import _native
     monkeypatch.setattr(_native, "_lib", None)

@@ -274,7 +274,7 @@ def test_meta_net_and_sgd(dev):
     close(p, pr.detach(), torch.float32, "sgd")
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 6])
 @pytest.mark.parametrize("Nn,K", [(2048, 512), (512, 2048)])
 def test_gemm_large_m_every_config(dev, cfg, Nn, K):
     """Bench-scale M (persistent / ring paths engage when tiles > 2x CUs) vs torch fp32."""
@@ -302,35 +302,6 @@ def test_gemm_large_m_every_config(dev, cfg, Nn, K):
         s = torch.sigmoid(1.702 * aux.float())
         close(ops.gemm(Ab, Bb, N.EPI_DQGELU, torch.bfloat16, aux=aux),
               refb * (s + 1.702 * aux.float() * s * (1 - s)), torch.bfloat16, f"cfg{cfg} dqgelu")
-    finally:
-        lib.clipk_gemm_set_config(-1)
-
-
-@pytest.mark.parametrize("M,Nn,K", [(1, 256, 64), (255, 512, 128), (1000, 256, 192), (3000, 768, 64),
-                                     (9000, 1536, 512)])
-@pytest.mark.parametrize("cfg", [7, 8, 9])
-def test_gemm_stream_edges(dev, cfg, M, Nn, K):
-    """Persistent K-step-stream kernels -- cfg 7 (8-phase ping-pong), 8 / 9 (deep-A ring, 256 /
-    192 rows): single-K-tile streams, partial row tiles, grids smaller than the CU count, odd
-    K-tile counts; fp32 / 16-bit outputs, 16-bit residual."""
-    lib = N.load()
-    g = torch.Generator(device="cpu").manual_seed(M + Nn + K)
-    A = torch.randn(M, K, generator=g).to(dev).to(torch.float16)
-    B = (torch.randn(Nn, K, generator=g) / math.sqrt(K)).to(dev).to(torch.float16)
-    bias = torch.randn(Nn, generator=g).to(dev)
-    res = torch.randn(M, Nn, generator=g).to(dev).to(torch.float16)
-    ref = A.float() @ B.float().t()
-    try:
-        N.check(lib.clipk_gemm_set_config(cfg), "set_config")
-        close(ops.gemm(A, B, N.EPI_NONE, torch.float32), ref, torch.float16, "8ph none")
-        close(ops.gemm(A, B, N.EPI_BIAS_RES, torch.float16, bias=bias, res=res), ref + bias + res.float(),
-              torch.float16, "8ph res16")
-        gq, hq = ops.gemm(A, B, N.EPI_BIAS_QGELU, torch.float16, bias=bias, want_out2=True)
-        hr = ref + bias
-        close(hq, hr, torch.float16, "8ph qgelu.h")
-        close(gq, hr * torch.sigmoid(1.702 * hr), torch.float16, "8ph qgelu.g")
-        close(ops.gemm(A, B, N.EPI_BIAS_QGELU, torch.float16, bias=bias), hr * torch.sigmoid(1.702 * hr),
-              torch.float16, "8ph qgelu no h")
     finally:
         lib.clipk_gemm_set_config(-1)
 
