@@ -50,8 +50,8 @@ KERNELS = {
     "gemm_fc_fwd": (["text.fc_fwd"], "EPI_BIAS N=2048", "mfma"),
     "gemm_qkv_fwd": (["text.qkv_fwd"], "EPI_BIAS N=1536", "mfma"),
     "gemm_out_fwd": (["text.out_fwd"], "EPI_BIAS_RES N=512", "mfma"),
-    "attn_bwd": (["text.attn_bwd"], "attn_prefix_bwd", "hbm"),
-    "attn_fwd": (["text.attn_fwd"], "attn_prefix_fwd", "hbm"),
+    "attn_bwd": (["text.attn_bwd"], "attn_prefix_bwd_lds", "hbm"),
+    "attn_fwd": (["text.attn_fwd"], "attn_prefix_fwd_lds", "hbm"),
     "ln_bwd": (["text.ln_bwd"], "ln_bwd_kernel", "hbm"),
     "ln_fwd": (["text.ln_fwd"], "ln_fwd_kernel", "hbm"),
     "vit": (["vit.patch_embed", "vit.qkv_fwd", "vit.attn_fwd", "vit.out_fwd", "vit.fc_fwd", "vit.proj_fwd",
@@ -60,7 +60,7 @@ KERNELS = {
 ROOF_PMC_KEY = {"gemm_dx_n512": "gemm_nt_kernelIDF16_DF16_fLi4ELi192ELi256",
                 "gemm_dgelu": "gemm_nt_kernelIDF16_DF16_DF16_Li3E",
                 "gemm_proj_fwd": "gemm_nt_kernelIDF16_DF16_DF16_Li1ELi192ELi256ELi2ELi4ELb0ELi128ELi2ELb1E",
-                "attn_bwd": "attn_prefix_bwd_mfma"}
+                "attn_bwd": "attn_prefix_bwd_lds"}
 
 
 def flops(arch, n_cls, L):
@@ -236,6 +236,8 @@ def time_eval(trainer, dm, n_images):
     batches are cycled)."""
     import torch
     from fsp_amd import dist
+    if n_images <= 0:  # profiling runs of the train step alone
+        return 0.0, 0
     trainer.set_model_mode("eval")
     tl = dm.test_loader
     nb = (n_images + 99) // 100

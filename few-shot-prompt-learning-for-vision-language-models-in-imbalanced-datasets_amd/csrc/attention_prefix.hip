@@ -37,7 +37,9 @@ static int chunk_env(const char* name, int def) {
   const int v = e ? atoi(e) : def;
   return v >= 1 && v <= 16 ? v : def;
 }
-static int fwd_chunk() { static int c = chunk_env("CLIPK_PREFIX_FWD_CHUNK", 8); return c; }
+static int lds_slots();
+// (the LDS-staged forward measured best at 4 units per wave, the register one at 8)
+static int fwd_chunk() { static int c = chunk_env("CLIPK_PREFIX_FWD_CHUNK", lds_slots() ? 4 : 8); return c; }
 static int bwd_chunk() { static int c = chunk_env("CLIPK_PREFIX_BWD_CHUNK", 16); return c; }
 static int fwd_batch() { static int c = chunk_env("CLIPK_PREFIX_FWD_BATCH", 1); return c; }
 static int bwd_batch() { static int c = chunk_env("CLIPK_PREFIX_BWD_BATCH", 2); return c; }
@@ -45,6 +47,28 @@ static int bwd_batch() { static int c = chunk_env("CLIPK_PREFIX_BWD_BATCH", 2); 
 // put all heads of a row range in one block: one CU reads whole qkv rows.
 static int prefix_wpb() { static int c = chunk_env("CLIPK_PREFIX_WPB", 4) >= 8 ? 8 : 4; return c; }
 static inline int n_chunks(int ntiles, int uc) { return (ntiles + 1 + uc - 1) / uc; }
+// LDS-staged kernels (attn_prefix_*_lds): ring slots per wave (CLIPK_PREFIX_LDS: 0 = the
+// register-operand kernels, 2 or 3) and waves per block (CLIPK_PREFIX_LDS_WPB: 1, 2 or 4).
+// Bench shape (G 8, C 1000, P 5; clean-cache HIP events, tools/attn_sweep.py): backward
+// 98.4 -> 82.4 us (0.50 -> 0.60 of HBM), forward 48.4 -> 43.0 us at 2 slots / 4 waves.
+static int lds_slots() {
+  static int c = -1;
+  if (c < 0) {
+    const char* e = getenv("CLIPK_PREFIX_LDS");
+    c = e ? atoi(e) : 2;
+    if (c != 0 && c != 2 && c != 3) c = 2;
+  }
+  return c;
+}
+static int lds_wpb() {
+  static int c = -1;
+  if (c < 0) {
+    const char* e = getenv("CLIPK_PREFIX_LDS_WPB");
+    c = e ? atoi(e) : 4;
+    if (c != 1 && c != 2 && c != 4) c = 4;
+  }
+  return c;
+}
 
 // The chunk's tile table in one VGPR (lane i holds tiles[2*(u_begin-1) + i]), read back
 // with v_readlane: no dependent scalar-memory round trip inside the tile loop.
@@ -375,6 +399,359 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_bwd_mfma(int G, int P, i
   }
 }
 
+// ------------------------------------------------------------------ LDS-staged MFMA kernels
+// The kernels above load each lane's operand fragment straight into registers: one load
+// instruction covers 16 rows x 64 B (half of each 128-B head slice), and a wave waits out a
+// full load latency per batch of tiles. Here a tile's head slices arrive by global_load_lds
+// (16 B per lane, lane-linear: one instruction = 8 whole 128-B rows) into a per-wave LDS ring
+// of NS slots, NS-1 tiles ahead of the one being computed, so the next tiles' bytes are in
+// flight during this tile's math. Per-row side data (row_first, and the backward's lse) come
+// the same way (4 B per lane), so the loop carries no register loads. The math is that of the
+// register kernels, operand for operand (bitwise-equal results).
+// LDS tile: 16 rows x 128 B; 16-B chunk G of row r sits at slot G ^ ((r >> 1) & 7), so the
+// 16 lanes reading one chunk of rows 0..15 hit 16 distinct slots of the 256-B bank row.
+__device__ __forceinline__ int tsw(int r) { return (r >> 1) & 7; }
+
+__device__ __forceinline__ void glds_b(const void* src, void* lds, int bytes) {
+  if (bytes == 16)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+  else
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
+}
+
+// one head slice (64 x 16-bit) of tile rows t0 .. t0+15 (clamped to n-1) into a 2-KB LDS tile
+template <typename T>
+__device__ __forceinline__ void stage_slice(const T* col, int ld, int row0, int n, char* dst, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int rr = 8 * i + (lane >> 3), c = (lane & 7) ^ tsw(rr);
+    glds_b(col + (size_t)(row0 + min(rr, n - 1)) * ld + 8 * c, dst + i * 1024, 16);
+  }
+}
+// 16-B operand fragment: row r, 16-B chunk G
+__device__ __forceinline__ s16x8 lds_frag(const char* tile, int r, int G) {
+  return *reinterpret_cast<const s16x8*>(tile + r * 128 + ((G ^ tsw(r)) << 4));
+}
+// Transposed operand reads (cf. tr_read) of the four 16-column blocks of a tile, and their
+// completion, in one asm statement. Issued through the ds_read_tr intrinsic, each read gets a
+// vmcnt(0) in front of it from the compiler (it cannot tell the read from the in-flight
+// global_load_lds of the next ring slot), which would drain the prefetch every tile.
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+__device__ __forceinline__ void tr_read4_at(const uint32_t (&a)[4], s16x4 (&r)[4]) {
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %4\n\t"
+      "ds_read_b64_tr_b16 %1, %5\n\t"
+      "ds_read_b64_tr_b16 %2, %6\n\t"
+      "ds_read_b64_tr_b16 %3, %7\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3])
+      : "memory");
+}
+// swizzled 2-KB ring tile, rows rbase..rbase+3 per lane group (rbase = 4 g4)
+__device__ __forceinline__ void tr_read4_sw(const char* tile, int rbase, int lane, s16x4 (&r)[4]) {
+  const int li = lane & 15, row = rbase + (li >> 2);
+  uint32_t a[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int col = 16 * t + 4 * (li & 3);
+    a[t] = lds_off(tile + row * 128 + (((col >> 3) ^ tsw(row)) << 4) + (col & 7) * 2);
+  }
+  tr_read4_at(a, r);
+}
+// padded TRS tile (the prefix K / V staged once per wave)
+__device__ __forceinline__ void tr_read4_pad(const short* tile, int rbase, int lane, s16x4 (&r)[4]) {
+  const int li = lane & 15;
+  uint32_t a[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) a[t] = lds_off(tile + (rbase + (li >> 2)) * TRS + 16 * t + 4 * (li & 3));
+  tr_read4_at(a, r);
+}
+
+template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+template <typename T, int NS, int WPB>
+__global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_lds(int G, int P, int R, int ntiles,
+                                                           const int* __restrict__ tiles,
+                                                           const int* __restrict__ row_first, int H,
+                                                           int nchunk, int uc, const T* __restrict__ qkv,
+                                                           int ldq, T* __restrict__ out, int ldo,
+                                                           float* __restrict__ lse) {
+  constexpr int SLOT = 3 * 2048 + 256;  // q | k | v tiles, row_first of the 16 rows (+ lane copies)
+  constexpr int PER = 7;                // global_load_lds per tile
+  __shared__ CLIPK_LDS_ALIGN char sm[WPB][NS * SLOT + 16 * TRS * 2];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int wid = blockIdx.x * WPB + w;
+  if (wid >= G * nchunk * H) return;  // wave-uniform; no block barriers below
+  const int h = wid % H, k = (wid / H) % nchunk, g = wid / (H * nchunk);
+  const int W = H * 64;
+  char* ring = sm[w];
+  short* sVp = reinterpret_cast<short*>(ring + NS * SLOT);
+  const int gR = g * R;
+  const T* qh = qkv + h * 64;
+  const int u_begin = k * uc, u_end = min((k + 1) * uc, ntiles + 1);
+  const int tab = load_tile_table(tiles, ntiles, u_begin, lane);
+  auto issue = [&](int u, int slot) {
+    int t0, n, pre;
+    tile_info(tab, P, u, u_begin, t0, n, pre);
+    char* b = ring + slot * SLOT;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) stage_slice<T>(qh + j * W, ldq, gR + t0, n, b + j * 2048, lane);
+    glds_b(row_first + t0 + min(r16, n - 1), b + 3 * 2048, 4);
+  };
+  const bool pok = r16 < P;
+  const T* pp = qh + (gR + (pok ? r16 : 0)) * ldq;
+  s16x8 kp[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int c = 8 * g4 + 32 * kk;
+    kp[kk] = ld_row16(pp + W + c, pok);
+    *reinterpret_cast<s16x8*>(sVp + r16 * TRS + c) = ld_row16(pp + 2 * W + c, pok);
+  }
+  const int nu = u_end - u_begin;
+#pragma unroll
+  for (int d = 0; d < NS - 1; ++d)
+    if (d < nu) issue(u_begin + d, d);
+  for (int i = 0; i < nu; ++i) {
+    const int u = u_begin + i;
+    // ring: tile i+NS-1 goes into the slot tile i-1 was read from (its reads retired)
+    lds_fence();
+    if (i + NS - 1 < nu) issue(u + NS - 1, (i + NS - 1) % NS);
+    const int ahead = min(NS - 1, nu - 1 - i);  // tiles issued after tile i
+    if (ahead >= 2) vm_wait<2 * PER>();
+    else if (ahead == 1) vm_wait<PER>();
+    else vm_wait<0>();
+    const char* b = ring + (i % NS) * SLOT;
+    int t0, n, pre;
+    tile_info(tab, P, u, u_begin, t0, n, pre);
+    const int first = u == 0 ? 0 : reinterpret_cast<const int*>(b + 3 * 2048)[r16] - t0;
+    const bool qok = r16 < n;
+    s16x8 q[2], ko[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      q[kk] = lds_frag(b, r16, g4 + 4 * kk);
+      ko[kk] = lds_frag(b + 2048, r16, g4 + 4 * kk);
+    }
+    f32x4 sp = {0.f, 0.f, 0.f, 0.f}, so = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      sp = mfma32_t<T>(kp[kk], q[kk], sp);
+      so = mfma32_t<T>(ko[kk], q[kk], so);
+    }
+    float vp[4], vq[4], mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = 4 * g4 + r;
+      vp[r] = key < pre ? sp[r] * kScale : -INFINITY;
+      vq[r] = (key <= r16 && key >= first) ? so[r] * kScale : -INFINITY;
+      mx = fmaxf(mx, fmaxf(vp[r], vq[r]));
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float ep[4], eo[4], ps = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      ep[r] = __expf(vp[r] - mx);
+      eo[r] = __expf(vq[r] - mx);
+      ps += ep[r] + eo[r];
+    }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    const s16x4 bp = pack4<T>(ep[0], ep[1], ep[2], ep[3]);
+    const s16x4 bo = pack4<T>(eo[0], eo[1], eo[2], eo[3]);
+    const float inv = 1.0f / ps;
+    s16x4 tp[4], to[4];
+    tr_read4_pad(sVp, 4 * g4, lane, tp);
+    tr_read4_sw(b + 2 * 2048, 4 * g4, lane, to);
+    f32x4 o[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      o[t] = mfma16_t<T>(tp[t], bp, (f32x4){0.f, 0.f, 0.f, 0.f});
+      o[t] = mfma16_t<T>(to[t], bo, o[t]);
+    }
+    store_tile64<T>(out + (gR + t0 + r16) * ldo + h * 64, o, inv, qok);
+    if (lse && g4 == 0 && qok) lse[(gR + t0 + r16) * H + h] = mx + __logf(ps);
+  }
+}
+
+template <typename T, int NS, int WPB>
+__global__ __launch_bounds__(WPB * 64) void attn_prefix_bwd_lds(int G, int P, int R, int ntiles,
+                                                           const int* __restrict__ tiles,
+                                                           const int* __restrict__ row_first, int H,
+                                                           int nchunk, int uc, const T* __restrict__ qkv,
+                                                           int ldq, const T* __restrict__ dout, int lddo,
+                                                           const float* __restrict__ lse,
+                                                           T* __restrict__ dqkv, int lddq,
+                                                           float* __restrict__ part) {
+  static_assert(sizeof(T) == 2, "MFMA attention backward: 16-bit operands");
+  constexpr int SLOT = 4 * 2048 + 2 * 256;  // q | k | v | dO tiles, row_first, lse
+  constexpr int PER = 10;
+  __shared__ CLIPK_LDS_ALIGN char sm[WPB][NS * SLOT + 16 * TRS * 2];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int wid = blockIdx.x * WPB + w;
+  if (wid >= G * nchunk * H) return;  // wave-uniform
+  const int h = wid % H, k = (wid / H) % nchunk, g = wid / (H * nchunk);
+  const int W = H * 64;
+  char* ring = sm[w];
+  short* tKp = reinterpret_cast<short*>(ring + NS * SLOT);
+  const int gR = g * R;
+  const T* qh = qkv + h * 64;
+  const int u_begin = k * uc, u_end = min((k + 1) * uc, ntiles + 1);
+  const int tab = load_tile_table(tiles, ntiles, u_begin, lane);
+  auto issue = [&](int u, int slot) {
+    int t0, n, pre;
+    tile_info(tab, P, u, u_begin, t0, n, pre);
+    char* b = ring + slot * SLOT;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) stage_slice<T>(qh + j * W, ldq, gR + t0, n, b + j * 2048, lane);
+    stage_slice<T>(dout + h * 64, lddo, gR + t0, n, b + 3 * 2048, lane);
+    const int rr = t0 + min(r16, n - 1);
+    glds_b(row_first + rr, b + 4 * 2048, 4);
+    glds_b(lse + (size_t)(gR + rr) * H + h, b + 4 * 2048 + 256, 4);
+  };
+  const bool pok = r16 < P;
+  const T* pp = qh + (gR + (pok ? r16 : 0)) * ldq;
+  s16x8 kp[2], vp[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int c = 8 * g4 + 32 * kk;
+    kp[kk] = ld_row16(pp + W + c, pok);
+    vp[kk] = ld_row16(pp + 2 * W + c, pok);
+    *reinterpret_cast<s16x8*>(tKp + r16 * TRS + c) = kp[kk];
+  }
+  f32x4 dkp[4], dvp[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    dkp[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    dvp[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  const int nu = u_end - u_begin;
+#pragma unroll
+  for (int d = 0; d < NS - 1; ++d)
+    if (d < nu) issue(u_begin + d, d);
+  for (int i = 0; i < nu; ++i) {
+    const int u = u_begin + i;
+    lds_fence();
+    if (i + NS - 1 < nu) issue(u + NS - 1, (i + NS - 1) % NS);
+    const int ahead = min(NS - 1, nu - 1 - i);
+    if (ahead >= 2) vm_wait<2 * PER>();
+    else if (ahead == 1) vm_wait<PER>();
+    else vm_wait<0>();
+    const char* b = ring + (i % NS) * SLOT;
+    const char* tQ = b;
+    const char* tKo = b + 2048;
+    const char* tD = b + 3 * 2048;
+    const int* sF = reinterpret_cast<const int*>(b + 4 * 2048);
+    const float* sL = reinterpret_cast<const float*>(b + 4 * 2048 + 256);
+    int t0, n, pre;
+    tile_info(tab, P, u, u_begin, t0, n, pre);
+    const bool own_is_prefix = u == 0;
+    const bool qok = r16 < n;
+    s16x8 q[2], ko[2], vo[2], d[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      q[kk] = lds_frag(tQ, r16, g4 + 4 * kk);
+      ko[kk] = lds_frag(tKo, r16, g4 + 4 * kk);
+      vo[kk] = lds_frag(b + 2 * 2048, r16, g4 + 4 * kk);
+      d[kk] = lds_frag(tD, r16, g4 + 4 * kk);
+    }
+    const float l2 = sL[r16];
+    const int first2 = own_is_prefix ? 0 : sF[r16] - t0;
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    f32x4 s1p = z, s2p = z, p1p = z, p2p = z, s1o = z, s2o = z, p1o = z, p2o = z;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      s1p = mfma32_t<T>(q[kk], kp[kk], s1p);
+      s2p = mfma32_t<T>(kp[kk], q[kk], s2p);
+      p1p = mfma32_t<T>(d[kk], vp[kk], p1p);
+      p2p = mfma32_t<T>(vp[kk], d[kk], p2p);
+      s1o = mfma32_t<T>(q[kk], ko[kk], s1o);
+      s2o = mfma32_t<T>(ko[kk], q[kk], s2o);
+      p1o = mfma32_t<T>(d[kk], vo[kk], p1o);
+      p2o = mfma32_t<T>(vo[kk], d[kk], p2o);
+    }
+    float P2p[4], P2o[4], Dsum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 4 * g4 + r;
+      P2p[r] = (qok && j < pre) ? __expf(s2p[r] * kScale - l2) : 0.f;
+      P2o[r] = (qok && j <= r16 && j >= first2) ? __expf(s2o[r] * kScale - l2) : 0.f;
+      Dsum += P2p[r] * p2p[r] + P2o[r] * p2o[r];
+    }
+    Dsum += __shfl_xor(Dsum, 16, 64);
+    Dsum += __shfl_xor(Dsum, 32, 64);
+    float dS2p[4], dS2o[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      dS2p[r] = P2p[r] * (p2p[r] - Dsum);
+      dS2o[r] = P2o[r] * (p2o[r] - Dsum);
+    }
+    float P1p[4], P1o[4], dS1p[4], dS1o[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i4 = 4 * g4 + r;
+      const bool iok = i4 < n;
+      const float Di = __shfl(Dsum, i4, 64);
+      const float l1 = sL[i4];
+      const int first1 = own_is_prefix ? 0 : sF[i4] - t0;
+      P1p[r] = (iok && r16 < pre) ? __expf(s1p[r] * kScale - l1) : 0.f;
+      P1o[r] = (iok && r16 <= i4 && r16 >= first1) ? __expf(s1o[r] * kScale - l1) : 0.f;
+      dS1p[r] = P1p[r] * (p1p[r] - Di);
+      dS1o[r] = P1o[r] * (p1o[r] - Di);
+    }
+    const s16x4 bPp = pack4<T>(P1p[0], P1p[1], P1p[2], P1p[3]);
+    const s16x4 bSp = pack4<T>(dS1p[0], dS1p[1], dS1p[2], dS1p[3]);
+    const s16x4 bPo = pack4<T>(P1o[0], P1o[1], P1o[2], P1o[3]);
+    const s16x4 bSo = pack4<T>(dS1o[0], dS1o[1], dS1o[2], dS1o[3]);
+    const s16x4 bTp = pack4<T>(dS2p[0], dS2p[1], dS2p[2], dS2p[3]);
+    const s16x4 bTo = pack4<T>(dS2o[0], dS2o[1], dS2o[2], dS2o[3]);
+    T* orow = dqkv + (gR + t0 + r16) * lddq + h * 64;
+    f32x4 acc[4];
+    s16x4 ta[4], tb[4];
+    tr_read4_pad(tKp, 4 * g4, lane, ta);
+    tr_read4_sw(tKo, 4 * g4, lane, tb);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      acc[t] = mfma16_t<T>(ta[t], bTp, z);
+      acc[t] = mfma16_t<T>(tb[t], bTo, acc[t]);
+    }
+    store_tile64<T>(orow, acc, kScale, qok);  // dQ
+    tr_read4_sw(tQ, 4 * g4, lane, ta);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const s16x4 aQ = ta[t];
+      dkp[t] = mfma16_t<T>(aQ, bSp, dkp[t]);
+      acc[t] = mfma16_t<T>(aQ, bSo, z);
+      if (own_is_prefix) dkp[t] += acc[t];
+    }
+    if (!own_is_prefix) store_tile64<T>(orow + W, acc, kScale, qok);  // dK
+    tr_read4_sw(tD, 4 * g4, lane, tb);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const s16x4 aD = tb[t];
+      dvp[t] = mfma16_t<T>(aD, bPp, dvp[t]);
+      acc[t] = mfma16_t<T>(aD, bPo, z);
+      if (own_is_prefix) dvp[t] += acc[t];
+    }
+    if (!own_is_prefix) store_tile64<T>(orow + 2 * W, acc, 1.0f, qok);  // dV
+  }
+  float* pb = part + ((size_t)g * nchunk + k) * 16 * (2 * W);
+  if (r16 < P) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float* dst = pb + (size_t)r16 * 2 * W + h * 64 + 16 * t + 4 * g4;
+      *reinterpret_cast<f32x4*>(dst) = dkp[t] * kScale;
+      *reinterpret_cast<f32x4*>(dst + W) = dvp[t];
+    }
+  }
+}
+
 // ------------------------------------------------------------------ VALU versions (fp32 path)
 // One wave per (group, chunk of kValuChunk units, head); 4 tiles in flight (lane group
 // grp = lane>>4), lane r16 = row of the tile (query for the forward and dQ, key for dK/dV).
@@ -654,6 +1031,21 @@ static int prefix_fwd(int G, int P, int R, int ntiles, const int* tiles, const i
     const int uc = fwd_chunk();
     const int nchunk = n_chunks(ntiles, uc);
     const long waves = (long)G * nchunk * H;
+    if (const int ns = lds_slots()) {
+      const int wpb = lds_wpb();
+      auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3((waves + wpb - 1) / wpb), dim3(64 * wpb), 0, st, G, P, R, ntiles, tiles,
+                           row_first, H, nchunk, uc, (const T*)qkv, ldq, (T*)out, ldo, lse);
+      };
+#define CLIPK_LDS_GO(K, T_, ...)                                                               \
+  if (ns == 2) { if (wpb == 1) go(K<T_, 2, 1 __VA_ARGS__>); else if (wpb == 2) go(K<T_, 2, 2 __VA_ARGS__>); \
+                 else go(K<T_, 2, 4 __VA_ARGS__>); }                                                 \
+  else { if (wpb == 1) go(K<T_, 3, 1 __VA_ARGS__>); else if (wpb == 2) go(K<T_, 3, 2 __VA_ARGS__>);     \
+         else go(K<T_, 3, 4 __VA_ARGS__>); }
+      CLIPK_LDS_GO(attn_prefix_fwd_lds, T)
+      CLIPK_CHECK_LAUNCH();
+      return CLIPK_OK;
+    }
     const int b = fwd_batch();
     const int wpb = prefix_wpb();
     auto go = [&](auto kern) {
@@ -687,6 +1079,23 @@ static int prefix_bwd(int G, int P, int R, int ntiles, const int* tiles, const i
   const int uc = mfma ? bwd_chunk() : kValuChunk;
   const int nchunk = n_chunks(ntiles, uc);
   const long waves = (long)G * nchunk * H;
+  if constexpr (mfma && __is_same(T, TG)) {
+    if (const int ns = lds_slots()) {
+      const int wpb = lds_wpb();
+      auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3((waves + wpb - 1) / wpb), dim3(64 * wpb), 0, st, G, P, R, ntiles, tiles,
+                           row_first, H, nchunk, uc, (const T*)qkv, ldq, (const T*)dout, lddo, lse, (T*)dqkv,
+                           lddq, part);
+      };
+      CLIPK_LDS_GO(attn_prefix_bwd_lds, T)
+      CLIPK_CHECK_LAUNCH();
+      const int W = H * 64;
+      hipLaunchKernelGGL((prefix_kv_reduce<TG>), dim3(G * P, (2 * W + 255) / 256), dim3(256), 0, st, P, R, W,
+                         nchunk, part, (TG*)dqkv, lddq);
+      CLIPK_CHECK_LAUNCH();
+      return CLIPK_OK;
+    }
+  }
   if constexpr (mfma) {
     const int wpb = prefix_wpb();
     auto go = [&](auto kern) {

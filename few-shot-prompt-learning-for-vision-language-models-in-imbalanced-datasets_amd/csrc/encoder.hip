@@ -566,8 +566,10 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
       TRY(clipk_rows_copy(rb, nout, b.dqkv, nullptr, res, eot_rows, st));
     }
     {
-      // algorithmic: read q|k|v, o (act), do (grad), lse; write dq|dk|dv (grad)
-      const double ab = (double)rows * W * (4.0 * esize(act) + 4.0 * esize(gd)) + 4.0 * rows * e->heads;
+      // algorithmic: read q|k|v (act), do (grad), lse; write dq|dk|dv (grad); the fp32 VALU
+      // kernels also read o (the 16-bit MFMA ones recompute D_i = rowsum(P o dP) instead)
+      const double ab = (double)rows * W * ((act == CLIPK_F32 ? 4.0 : 3.0) * esize(act) + 4.0 * esize(gd)) +
+                        4.0 * rows * e->heads;
       ProfScope ps(CLIPK_PROF_ATTN, st, 0.0, "text.attn_bwd", ab);
       TRY(attn_bwd(e, sh, t.qkv[l], t.o[l], b.do_, t.lse[l], b.dqkv, b.part, st));
     }

@@ -3,6 +3,9 @@ the same op (float kernels), through the C-ABI. Tolerances are stated per dtype:
 fp32 kernels (f32-input MFMA / fp32 VALU) 2e-5 relative-to-scale, fp16 1e-2, bf16 3e-2
 (all relative to the reference's max |value|)."""
 import math
+import os
+import subprocess
+import sys
 
 import pytest
 import torch
@@ -391,6 +394,24 @@ def test_attention_prefix_fwd_bwd(dev, dtype, gdtype, G, C, P, H, max_q):
     ref = q32.grad
     for part, sl in (("dq", slice(0, W)), ("dk", slice(W, 2 * W)), ("dv", slice(2 * W, 3 * W))):
         close(dq[:, sl], ref[:, sl], gdtype if dtype != torch.float32 else dtype, f"prefix attn {part}")
+
+
+@pytest.mark.parametrize("knobs", [
+    {"CLIPK_PREFIX_LDS": "0"},
+    {"CLIPK_PREFIX_LDS": "3", "CLIPK_PREFIX_LDS_WPB": "1"},
+    {"CLIPK_PREFIX_LDS": "2", "CLIPK_PREFIX_LDS_WPB": "2", "CLIPK_PREFIX_FWD_CHUNK": "1",
+     "CLIPK_PREFIX_BWD_CHUNK": "3"},
+])
+def test_attention_prefix_kernel_variants(knobs):
+    """The other shared-prefix attention variants -- the register-operand kernels, a 3-slot
+    LDS ring, 1- and 2-wave blocks, 1- and 3-tile chunks -- through the same cases, in a child
+    process (the knobs are read once per process)."""
+    env = dict(os.environ, **knobs)
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", os.path.abspath(__file__),
+                        "-k", "test_attention_prefix_fwd_bwd"], env=env, capture_output=True, text=True, timeout=300,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert "24 passed" in r.stdout, r.stdout[-500:]
 
 
 def test_prompt_rows_and_ctx_grad_rows(dev):
