@@ -61,6 +61,14 @@ SIGNATURES = {
     "clipk_sgd_step": (_I, [_L, _P, _P, _P, _F, _F, _F, _I, _P]),
     "clipk_cast": (_I, [_I, _L, _P, _P, _P]),
     "clipk_rows_copy": (_I, [_I, _I, _P, _P, _P, _P, _P]),
+    "clipk_vit_embed_ln_vpt": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "clipk_rows_inject": (_I, [_I, _I, _I, _I, _P, _P, _P, _I, _P]),
+    "clipk_rows_collect": (_I, [_I, _I, _I, _I, _P, _I, _P, _I, _I, _P, _P, _I, _I, _P]),
+    "clipk_encoder_set_deep_prompts": (_I, [_P, _I, _I, _I, _P, _P, _P]),
+    "clipk_vit_prompted_saved_bytes": (_S, [_P, _I, _I]),
+    "clipk_vit_prompted_ws_bytes": (_S, [_P, _I, _I]),
+    "clipk_vit_forward_prompted": (_I, [_P, _I, _P, _I, _P, _P, _P, _S, _P, _S, _P]),
+    "clipk_vit_backward_prompted": (_I, [_P, _I, _I, _P, _P, _P, _P, _S, _P, _P, _S, _P]),
     "clipk_encoder_create": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "clipk_encoder_destroy": (None, [_P]),
     "clipk_text_saved_bytes": (_S, [_P, _I, _I]),

@@ -5,10 +5,14 @@ Mirrors the pieces of ``PromptSRC/clip/model.py`` that the CoOp/CoCoOp trainers 
 ``positional_embedding``, ``ln_final``, ``text_projection``, ``logit_scale``, ``dtype``),
 but the encoders run as libclipk.so launch sequences:
 
-* ``VisionEncoder``  — VisionTransformer.forward (model.py:401-431), frozen, forward only.
+* ``VisionEncoder``  — VisionTransformer.forward (model.py:401-431), frozen; with
+  ``with_grad`` also the prompted ViT of IVLP / MaPLe / PromptSRC (visual prompt rows after the
+  image tokens + deep prompts, model.py:191-331, 434-485) with its input-grad backward,
+  exposed through ``PromptedVisionFn``.
 * ``TextEncoderCore`` — the text Transformer + ln_final + text_projection
   (TextEncoder.forward, trainers/coop.py:195-205) with a native input-grad backward
-  (weights frozen: coop.py:419-421), exposed through ``TextEncodeFn``.
+  (weights frozen: coop.py:419-421), exposed through ``TextEncodeFn`` (``DeepTextEncodeFn``:
+  with per-layer deep prompts).
 
 Precision (cfg ``PREC``; PREC_DTYPES): "fp32" -> fp32 operands on f32-input MFMA, fp32
 residual stream (parity mode); "fp16" -> fp16 forward and backward GEMM operands, a 16-bit
@@ -151,6 +155,16 @@ class TextEncoderCore(_Encoder):
                 "clipk_encoder_create(text)")
         self.handle = h
 
+    def set_deep(self, deep, rows, n_per, grads=None):
+        """Deep prompts for the next call(s): deep fp32 [n_deep, n_ctx, W] (None clears)."""
+        if deep is None:
+            N.check(N.load().clipk_encoder_set_deep_prompts(self.handle, 0, 0, 0, None, None, None),
+                    "clipk_encoder_set_deep_prompts")
+            return
+        N.check(N.load().clipk_encoder_set_deep_prompts(self.handle, deep.shape[0], deep.shape[1], n_per, ops._p(rows),
+                                                        ops._p(deep), ops._p(grads)),
+                "clipk_encoder_set_deep_prompts")
+
     def forward(self, x0, shape, save):
         """x0 fp32 [shape.rows, W] -> txt fp32 [shape.nout, E] (+ saved arena if save)."""
         lib = N.load()
@@ -214,10 +228,55 @@ class TextEncodeFn(torch.autograd.Function):
         return dx0, None, None
 
 
-class VisionEncoder(nn.Module, _Encoder):
-    """Frozen ViT image encoder on the native path: image [B,3,R,R] fp32 -> [B,E] fp32."""
+def deep_text_rows(shape, n_ctx, device):
+    """Rows the text deep prompts replace (tokens 1..n_ctx of every sequence, model.py:244-252),
+    as the [n_ctx][n_per] table of clipk_rows_inject: packed layout -> prefix rows of each group."""
+    if shape.packed:
+        base, n_per, stride = 1, shape.G, shape.R
+    else:
+        base, n_per, stride = 1, shape.nseq, shape.L
+    p = torch.arange(n_ctx, dtype=torch.int64)[:, None]
+    i = torch.arange(n_per, dtype=torch.int64)[None, :]
+    return (i * stride + base + p).reshape(-1).to(torch.int32).to(device), n_per
 
-    def __init__(self, sd, arch: ClipArch, prec: str, device):
+
+class DeepTextEncodeFn(torch.autograd.Function):
+    """TextEncodeFn with deep prompts (IVLP / MaPLe / PromptSRC text side, model.py:229-256 /
+    287-331): deep fp32 [n_deep, n_ctx, W] replace rows 1..n_ctx before layers 1..n_deep."""
+
+    @staticmethod
+    def forward(ctx, x0, deep, core, shape):
+        rows, n_per = deep_text_rows(shape, deep.shape[1], x0.device)
+        deep = deep.contiguous()
+        core.set_deep(deep, rows, n_per)
+        try:
+            txt, saved = core.forward(x0.contiguous(), shape, save=any(ctx.needs_input_grad[:2]))
+        finally:
+            core.set_deep(None, None, 0)
+        ctx.core, ctx.shape, ctx.saved_arena = core, shape, saved
+        ctx.deep, ctx.rows, ctx.n_per = deep, rows, n_per
+        return txt
+
+    @staticmethod
+    def backward(ctx, dtxt):
+        if ctx.saved_arena is None:
+            raise RuntimeError("text encoder backward without saved activations")
+        ddeep = torch.empty_like(ctx.deep)
+        ctx.core.set_deep(ctx.deep, ctx.rows, ctx.n_per, ddeep)
+        try:
+            dx0 = ctx.core.backward(dtxt, ctx.shape, ctx.saved_arena)
+        finally:
+            ctx.core.set_deep(None, None, 0)
+        ctx.saved_arena = None
+        return dx0, ddeep, None, None
+
+
+class VisionEncoder(nn.Module, _Encoder):
+    """ViT image encoder on the native path: image [B,3,R,R] fp32 -> [B,E] fp32. Frozen
+    weights; ``with_grad`` packs the transposed layer weights for the prompted input-grad
+    backward (forward_prompted / PromptedVisionFn)."""
+
+    def __init__(self, sd, arch: ClipArch, prec: str, device, with_grad: bool = False):
         nn.Module.__init__(self)
         act, _ = PREC_DTYPES[prec]
         self.arch, self.act, self.dev = arch, act, torch.device(device)
@@ -226,6 +285,8 @@ class VisionEncoder(nn.Module, _Encoder):
         D, nl, p = arch.vision_width, arch.vision_layers, arch.vision_patch_size
         f32 = lambda x: _t(x).float().to(self.dev).contiguous()
         A = lambda x: _t(x).float().to(self.dev, act).contiguous()
+        G = lambda x: _t(x).float().t().contiguous().to(self.dev, act) if with_grad else None
+        self.with_grad = with_grad
         table = []
         for i in range(nl):
             pre = f"visual.transformer.resblocks.{i}."
@@ -233,7 +294,9 @@ class VisionEncoder(nn.Module, _Encoder):
             table += [f32(q["ln_1.weight"]), f32(q["ln_1.bias"]), A(q["attn.in_proj_weight"]),
                       f32(q["attn.in_proj_bias"]), A(q["attn.out_proj.weight"]), f32(q["attn.out_proj.bias"]),
                       f32(q["ln_2.weight"]), f32(q["ln_2.bias"]), A(q["mlp.c_fc.weight"]), f32(q["mlp.c_fc.bias"]),
-                      A(q["mlp.c_proj.weight"]), f32(q["mlp.c_proj.bias"]), None, None, None, None]
+                      A(q["mlp.c_proj.weight"]), f32(q["mlp.c_proj.bias"]),
+                      G(q["attn.in_proj_weight"]), G(q["attn.out_proj.weight"]), G(q["mlp.c_fc.weight"]),
+                      G(q["mlp.c_proj.weight"])]
         k = 3 * p * p
         kq = 32 if act == torch.float32 else 64
         self.Kp = (k + kq - 1) // kq * kq
@@ -244,21 +307,87 @@ class VisionEncoder(nn.Module, _Encoder):
                 _t(sd["visual.proj"]).float().t().contiguous().to(self.dev, act),
                 conv.to(self.dev, act).contiguous(), f32(sd["visual.class_embedding"]),
                 f32(sd["visual.positional_embedding"])]
+        # backward of the head: d ln_post(CLS) = dfeat . proj^T  (proj [D, E], B operand [N=D, K=E])
+        self.proj_bwd = _t(sd["visual.proj"]).float().contiguous().to(self.dev, act) if with_grad else None
         self._keep = [t for t in table if t is not None] + head
+        self.width, self.n_tokens = D, (arch.image_resolution // p) ** 2 + 1
         h = ctypes.c_void_p()
         N.check(N.load().clipk_vision_create(D, nl, D // 64, arch.embed_dim, arch.image_resolution, p,
                                              ops.DT[act], _ptrs(table), _ptrs(head), ctypes.byref(h)),
                 "clipk_vision_create")
         self.handle = h
 
-    def forward(self, image):
-        if image.requires_grad:
-            raise RuntimeError("the image encoder is frozen and forward-only (no input grad)")
+    def _check_image(self, image):
         image = image.to(self.dev, torch.float32).contiguous()
-        B = image.shape[0]
         if image.shape[1:] != (3, self.input_resolution, self.input_resolution):
             raise RuntimeError(f"expected [B,3,{self.input_resolution},{self.input_resolution}] images, "
                                f"got {tuple(image.shape)}")
+        return image
+
+    def deep_rows(self, B, n_vpt):
+        """Rows the deep visual prompts replace: the last n_vpt rows of every image
+        (model.py:234-241), as the [n_vpt][B] table of clipk_rows_inject."""
+        Lp = self.n_tokens + n_vpt
+        p = torch.arange(n_vpt, dtype=torch.int64)[:, None]
+        b = torch.arange(B, dtype=torch.int64)[None, :]
+        return (b * Lp + self.n_tokens + p).reshape(-1).to(torch.int32).to(self.dev)
+
+    def set_deep(self, deep, rows, n_per, grads=None):
+        lib = N.load()
+        if deep is None or deep.shape[0] == 0:
+            N.check(lib.clipk_encoder_set_deep_prompts(self.handle, 0, 0, 0, None, None, None),
+                    "clipk_encoder_set_deep_prompts")
+            return
+        N.check(lib.clipk_encoder_set_deep_prompts(self.handle, deep.shape[0], deep.shape[1], n_per, ops._p(rows),
+                                                   ops._p(deep), ops._p(grads)), "clipk_encoder_set_deep_prompts")
+
+    def forward_prompted(self, image, vpt, deep=None, save=False):
+        """image [B,3,R,R], vpt fp32 [n_vpt, D] (n_vpt may be 0), deep fp32 [n_deep, n_vpt, D]
+        -> (feat [B, E] fp32, saved arena or None)."""
+        image = self._check_image(image)
+        B, n_vpt = image.shape[0], vpt.shape[0]
+        lib = N.load()
+        feat = torch.empty(B, self.output_dim, device=self.dev)
+        wsb = lib.clipk_vit_prompted_ws_bytes(self.handle, B, n_vpt)
+        ws = WORKSPACE.get(wsb, self.dev, "vitp")
+        sb = lib.clipk_vit_prompted_saved_bytes(self.handle, B, n_vpt) if save else 0
+        saved = torch.empty(sb, dtype=torch.uint8, device=self.dev) if save else None
+        rows = self.deep_rows(B, n_vpt) if deep is not None and deep.shape[0] else None
+        self.set_deep(deep, rows, B)
+        try:
+            N.check(lib.clipk_vit_forward_prompted(self.handle, B, ops._p(image), n_vpt, ops._p(vpt), ops._p(feat),
+                                                   ops._p(saved), sb, ops._p(ws), ws.numel(), ops._stream()),
+                    "clipk_vit_forward_prompted")
+        finally:
+            self.set_deep(None, None, 0)
+        return feat, saved
+
+    def backward_prompted(self, dfeat, vpt, deep, saved, B):
+        """-> (d vpt [n_vpt, D], d deep [n_deep, n_vpt, D] or None)."""
+        if not self.with_grad:
+            raise RuntimeError("the image encoder was built without backward weights (with_grad=False)")
+        lib = N.load()
+        n_vpt = vpt.shape[0]
+        dvpt = torch.empty_like(vpt)
+        ddeep = torch.empty_like(deep) if deep is not None and deep.shape[0] else None
+        wsb = lib.clipk_vit_prompted_ws_bytes(self.handle, B, n_vpt)
+        ws = WORKSPACE.get(wsb, self.dev, "vitp")
+        rows = self.deep_rows(B, n_vpt) if ddeep is not None else None
+        self.set_deep(deep if ddeep is not None else None, rows, B, ddeep)
+        try:
+            N.check(lib.clipk_vit_backward_prompted(self.handle, B, n_vpt, ops._p(vpt), ops._p(self.proj_bwd),
+                                                    ops._p(dfeat.contiguous()), ops._p(saved), saved.numel(),
+                                                    ops._p(dvpt), ops._p(ws), ws.numel(), ops._stream()),
+                    "clipk_vit_backward_prompted")
+        finally:
+            self.set_deep(None, None, 0)
+        return dvpt, ddeep
+
+    def forward(self, image):
+        if image.requires_grad:
+            raise RuntimeError("the image encoder is frozen and forward-only (no input grad)")
+        image = self._check_image(image)
+        B = image.shape[0]
         lib = N.load()
         feat = torch.empty(B, self.output_dim, device=self.dev)
         wsb = lib.clipk_vit_ws_bytes(self.handle, B)
@@ -271,17 +400,40 @@ class VisionEncoder(nn.Module, _Encoder):
         _Encoder.__del__(self)
 
 
+class PromptedVisionFn(torch.autograd.Function):
+    """(vpt [n_vpt, D], deep [n_deep, n_vpt, D], image) -> image features [B, E] through the
+    prompted ViT; gradients flow to the prompts only (the image and the weights are frozen)."""
+
+    @staticmethod
+    def forward(ctx, vpt, deep, image, enc):
+        vpt = vpt.contiguous()
+        deep = deep.contiguous() if deep is not None else None
+        need = ctx.needs_input_grad[0] or (deep is not None and ctx.needs_input_grad[1])
+        feat, saved = enc.forward_prompted(image, vpt, deep, save=need)
+        ctx.enc, ctx.saved_arena, ctx.B = enc, saved, image.shape[0]
+        ctx.vpt, ctx.deep = vpt, deep
+        return feat
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        if ctx.saved_arena is None:
+            raise RuntimeError("image encoder backward without saved activations")
+        dvpt, ddeep = ctx.enc.backward_prompted(dfeat, ctx.vpt, ctx.deep, ctx.saved_arena, ctx.B)
+        ctx.saved_arena = None
+        return dvpt, ddeep, None, None
+
+
 class CLIP(nn.Module):
     """Container with the attributes the prompt learners read (model.py:488-561)."""
 
-    def __init__(self, sd, prec: str = "fp16", device="cuda", text_grad: bool = True):
+    def __init__(self, sd, prec: str = "fp16", device="cuda", text_grad: bool = True, vision_grad: bool = False):
         super().__init__()
         if prec not in PREC_DTYPES:
             raise AssertionError(f"PREC must be one of {list(PREC_DTYPES)}")
         arch = arch_from_state_dict(sd)
         self.arch, self.prec = arch, prec
         dev = torch.device(device)
-        self.visual = VisionEncoder(sd, arch, prec, dev)
+        self.visual = VisionEncoder(sd, arch, prec, dev, with_grad=vision_grad)
         self.text = TextEncoderCore(sd, arch, prec, dev, with_grad=text_grad)
         W = arch.transformer_width
         self.token_embedding = nn.Embedding(arch.vocab_size, W)
@@ -300,6 +452,8 @@ class CLIP(nn.Module):
         return torch.float32  # host-facing tensors are fp32; kernels pick operand types
 
 
-def build_model(state_dict, prec: str = "fp16", device="cuda", text_grad: bool = True) -> CLIP:
-    """build_model(state_dict) analogue (model.py:662-705) for the native path."""
-    return CLIP(state_dict, prec=prec, device=device, text_grad=text_grad)
+def build_model(state_dict, prec: str = "fp16", device="cuda", text_grad: bool = True,
+                vision_grad: bool = False) -> CLIP:
+    """build_model(state_dict) analogue (model.py:662-705) for the native path; vision_grad
+    packs the ViT's backward weights (trainers whose visual prompts train)."""
+    return CLIP(state_dict, prec=prec, device=device, text_grad=text_grad, vision_grad=vision_grad)

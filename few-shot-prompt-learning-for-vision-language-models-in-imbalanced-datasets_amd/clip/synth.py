@@ -64,6 +64,7 @@ ARCHS = {
     # Small shapes for exhaustive parity (every width a multiple of 128, head dim 64).
     "tiny": ClipArch(128, 32, 2, 128, 16, 77, 49408, 128, 2, 2),
     "tiny-p8": ClipArch(128, 32, 2, 128, 8, 77, 49408, 128, 2, 2),
+    "tiny4": ClipArch(128, 32, 4, 128, 16, 77, 49408, 128, 2, 4),  # deep-prompt depth coverage
 }
 
 

@@ -507,6 +507,317 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(int nseq, int L, int H, int
   if (lse && g4 == 0 && qok) lse[(row0 + qr) * H + h] = m + __logf(l);
 }
 
+// ------------------------------------------------------------------ backward, any L (vision)
+// The ViT's input-grad backward (deep visual prompts, IVLP / MaPLe / PromptSRC: model.py:
+// 191-331, 401-431): L = 50..600 rows per sequence, non-causal (causal supported). Two passes
+// that each recompute P from the saved log-sum-exp, so no atomics and no workspace:
+//   pass KV -- a wave owns a 16-key tile j and sweeps the query tiles i: dK_j += dS^T Q_i,
+//              dV_j += P^T dO_i (accumulators in registers, as the shared-prefix kernel's
+//              prefix keys);
+//   pass Q  -- a wave owns a 16-query tile i and sweeps the key tiles j: dQ_i += dS K_j.
+// D_i = rowsum(dO_i o O_i) from the saved forward output (the row's keys span many tiles).
+template <typename T, typename TG>
+__device__ __forceinline__ float row_D(const TG* dor, const T* orow, bool ok, int g4) {
+  // lane (r16, g4) holds 16 of row r16's 64 columns (8 g4 + 32 kk .. +7); reduce over g4
+  float acc = 0.f;
+  if (ok) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      float a[8], b[8];
+      load16_f32<TG>(dor + 8 * g4 + 32 * kk, a);
+      load16_f32<T>(orow + 8 * g4 + 32 * kk, b);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc = fmaf(a[c], b[c], acc);
+    }
+  }
+  acc += __shfl_xor(acc, 16, 64);
+  acc += __shfl_xor(acc, 32, 64);
+  return acc;
+}
+
+template <typename T, typename TG>
+__global__ __launch_bounds__(256) void attn_bwd_long_kv(int nseq, int L, int H, int causal,
+                                                        const T* __restrict__ qkv, int ldq,
+                                                        const T* __restrict__ o_fwd, int ldof,
+                                                        const TG* __restrict__ dout, int lddo,
+                                                        const float* __restrict__ lse,
+                                                        TG* __restrict__ dqkv, int lddq) {
+  __shared__ CLIPK_LDS_ALIGN short sm[4][2][16 * TRS];  // per wave: Q_i, dO_i (transposed reads)
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int h = blockIdx.y, s = blockIdx.z, W = H * 64;
+  const size_t row0 = (size_t)s * L;
+  const int j0 = blockIdx.x * 64 + w * 16;
+  if (j0 >= L) return;  // wave-uniform; no block barriers below
+  short* tQ = sm[w][0];
+  short* tD = sm[w][1];
+  const int kr = min(j0 + r16, L - 1);
+  const bool kok = j0 + r16 < L;
+  s16x8 kp[2], vp[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const T* kb = qkv + (row0 + kr) * ldq + h * 64 + 8 * g4 + 32 * kk;
+    kp[kk] = to_g8<T, TG>(*reinterpret_cast<const s16x8*>(kb + W));
+    vp[kk] = to_g8<T, TG>(*reinterpret_cast<const s16x8*>(kb + 2 * W));
+  }
+  f32x4 dkp[4], dvp[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    dkp[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    dvp[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  const int nt = (L + 15) / 16;
+  for (int it = causal ? j0 / 16 : 0; it < nt; ++it) {
+    const int i0 = it * 16;
+    const int qr = min(i0 + r16, L - 1);
+    const T* qb = qkv + (row0 + qr) * ldq + h * 64;
+    const TG* db = dout + (row0 + qr) * lddo + h * 64;
+    s16x8 q[2], d[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      q[kk] = to_g8<T, TG>(*reinterpret_cast<const s16x8*>(qb + 8 * g4 + 32 * kk));
+      d[kk] = *reinterpret_cast<const s16x8*>(db + 8 * g4 + 32 * kk);
+    }
+    const float Drow = row_D<T, TG>(db, o_fwd + (row0 + qr) * ldof + h * 64, true, g4);  // row r16
+    float l1[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) l1[r] = lse[(row0 + min(i0 + 4 * g4 + r, L - 1)) * H + h];
+    lds_fence_a();  // the previous tile's transposed reads are done
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      *reinterpret_cast<s16x8*>(tQ + r16 * TRS + 8 * g4 + 32 * kk) = q[kk];
+      *reinterpret_cast<s16x8*>(tD + r16 * TRS + 8 * g4 + 32 * kk) = d[kk];
+    }
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    f32x4 s1 = z, p1 = z;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      s1 = mfma32_t<TG>(q[kk], kp[kk], s1);  // S [i = 4g4+r][j = r16]
+      p1 = mfma32_t<TG>(d[kk], vp[kk], p1);  // dP[i][j]
+    }
+    float P1[4], dS1[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + 4 * g4 + r;
+      const bool ok = i < L && kok && !(causal && j0 + r16 > i);
+      const float Di = __shfl(Drow, 4 * g4 + r, 64);
+      P1[r] = ok ? __expf(s1[r] * kScale - l1[r]) : 0.f;
+      dS1[r] = P1[r] * (p1[r] - Di);
+    }
+    const s16x4 bP = pack4<TG>(P1[0], P1[1], P1[2], P1[3]);
+    const s16x4 bS = pack4<TG>(dS1[0], dS1[1], dS1[2], dS1[3]);
+    lds_fence_a();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      dkp[t] = mfma16_t<TG>(tr_read(tQ, 4 * g4, 16 * t, lane), bS, dkp[t]);
+      dvp[t] = mfma16_t<TG>(tr_read(tD, 4 * g4, 16 * t, lane), bP, dvp[t]);
+    }
+  }
+  TG* orow = dqkv + (row0 + j0 + r16) * lddq + h * 64;
+  store_tile64<TG>(orow + W, dkp, kScale, kok);
+  store_tile64<TG>(orow + 2 * W, dvp, 1.0f, kok);
+}
+
+template <typename T, typename TG>
+__global__ __launch_bounds__(256) void attn_bwd_long_q(int nseq, int L, int H, int causal,
+                                                       const T* __restrict__ qkv, int ldq,
+                                                       const T* __restrict__ o_fwd, int ldof,
+                                                       const TG* __restrict__ dout, int lddo,
+                                                       const float* __restrict__ lse,
+                                                       TG* __restrict__ dqkv, int lddq) {
+  __shared__ CLIPK_LDS_ALIGN short sm[4][16 * TRS];  // per wave: K_j (transposed reads)
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int h = blockIdx.y, s = blockIdx.z, W = H * 64;
+  const size_t row0 = (size_t)s * L;
+  const int i0 = blockIdx.x * 64 + w * 16;
+  if (i0 >= L) return;  // wave-uniform
+  short* tK = sm[w];
+  const int qr = min(i0 + r16, L - 1);
+  const bool qok = i0 + r16 < L;
+  const T* qb = qkv + (row0 + qr) * ldq + h * 64;
+  const TG* db = dout + (row0 + qr) * lddo + h * 64;
+  s16x8 q[2], d[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    q[kk] = to_g8<T, TG>(*reinterpret_cast<const s16x8*>(qb + 8 * g4 + 32 * kk));
+    d[kk] = *reinterpret_cast<const s16x8*>(db + 8 * g4 + 32 * kk);
+  }
+  const float D2 = row_D<T, TG>(db, o_fwd + (row0 + qr) * ldof + h * 64, true, g4);
+  const float l2 = lse[(row0 + qr) * H + h];
+  f32x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int jt_end = causal ? (min(i0 + 15, L - 1)) / 16 + 1 : (L + 15) / 16;
+  for (int jt = 0; jt < jt_end; ++jt) {
+    const int j0 = jt * 16;
+    const int kr = min(j0 + r16, L - 1);
+    const T* kb = qkv + (row0 + kr) * ldq + h * 64;
+    s16x8 k[2], v[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      k[kk] = to_g8<T, TG>(*reinterpret_cast<const s16x8*>(kb + W + 8 * g4 + 32 * kk));
+      v[kk] = to_g8<T, TG>(*reinterpret_cast<const s16x8*>(kb + 2 * W + 8 * g4 + 32 * kk));
+    }
+    lds_fence_a();
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) *reinterpret_cast<s16x8*>(tK + r16 * TRS + 8 * g4 + 32 * kk) = k[kk];
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    f32x4 s2 = z, p2 = z;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      s2 = mfma32_t<TG>(k[kk], q[kk], s2);  // S^T[j = 4g4+r][i = r16]
+      p2 = mfma32_t<TG>(v[kk], d[kk], p2);  // dP^T
+    }
+    float dS2[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = j0 + 4 * g4 + r;
+      const bool ok = qok && j < L && !(causal && j > i0 + r16);
+      const float P2 = ok ? __expf(s2[r] * kScale - l2) : 0.f;
+      dS2[r] = P2 * (p2[r] - D2);
+    }
+    const s16x4 bT = pack4<TG>(dS2[0], dS2[1], dS2[2], dS2[3]);
+    lds_fence_a();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = mfma16_t<TG>(tr_read(tK, 4 * g4, 16 * t, lane), bT, acc[t]);
+  }
+  store_tile64<TG>(dqkv + (row0 + i0 + r16) * lddq + h * 64, acc, kScale, qok);
+}
+
+// VALU form (PREC fp32, and any dtype pair): 64 rows per block (lane = row), the other side
+// streamed through LDS in chunks of 64 rows (row stride 65 floats where lanes read their own
+// row: conflict-free column access).
+template <typename T, typename TG>
+__global__ __launch_bounds__(64) void attn_bwd_long_valu_q(int nseq, int L, int H, int causal,
+                                                           const T* __restrict__ qkv, int ldq,
+                                                           const T* __restrict__ o_fwd, int ldof,
+                                                           const TG* __restrict__ dout, int lddo,
+                                                           const float* __restrict__ lse,
+                                                           TG* __restrict__ dqkv, int lddq) {
+  __shared__ float sK[64 * 64], sV[64 * 64];
+  const int lane = threadIdx.x, h = blockIdx.y, s = blockIdx.z, W = H * 64;
+  const size_t row0 = (size_t)s * L;
+  const int i = blockIdx.x * 64 + lane;
+  const bool qok = i < L;
+  const size_t row = row0 + (qok ? i : L - 1);
+  float q[64], dO[64], acc[64];
+  load_row64<T>(qkv + row * ldq + h * 64, q);
+#pragma unroll
+  for (int d = 0; d < 64; ++d) q[d] *= kScale;
+  load_row64<TG>(dout + row * lddo + h * 64, dO);
+  load_row64<T>(o_fwd + row * ldof + h * 64, acc);
+  const float Di = dot64(dO, acc);
+  const float li = lse[row * H + h];
+#pragma unroll
+  for (int d = 0; d < 64; ++d) acc[d] = 0.f;
+  const int kend = causal ? min(L, (int)blockIdx.x * 64 + 64) : L;
+  for (int k0 = 0; k0 < kend; k0 += 64) {
+    __syncthreads();
+    {
+      const size_t kr = row0 + min(k0 + lane, L - 1);
+#pragma unroll
+      for (int c = 0; c < 64; c += 8) {
+        float t[8];
+        load_cols8<T>(qkv + kr * ldq + W + h * 64 + c, t);
+#pragma unroll
+        for (int d = 0; d < 8; ++d) sK[lane * 64 + c + d] = t[d];
+        load_cols8<T>(qkv + kr * ldq + 2 * W + h * 64 + c, t);
+#pragma unroll
+        for (int d = 0; d < 8; ++d) sV[lane * 64 + c + d] = t[d];
+      }
+    }
+    __syncthreads();
+    const int nj = min(64, kend - k0);
+    for (int jj = 0; jj < nj; ++jj) {
+      const int j = k0 + jj;
+      if (causal && j > i) continue;
+      const float p = __expf(dot64(q, &sK[jj * 64]) - li);
+      const float ds = p * (dot64(dO, &sV[jj * 64]) - Di);
+#pragma unroll
+      for (int d = 0; d < 64; ++d) acc[d] = fmaf(ds, sK[jj * 64 + d], acc[d]);
+    }
+  }
+  if (qok) {
+#pragma unroll
+    for (int d = 0; d < 64; ++d) acc[d] *= kScale;
+    store_row64<TG>(dqkv + row * lddq + h * 64, acc);
+  }
+}
+
+template <typename T, typename TG>
+__global__ __launch_bounds__(64) void attn_bwd_long_valu_kv(int nseq, int L, int H, int causal,
+                                                            const T* __restrict__ qkv, int ldq,
+                                                            const T* __restrict__ o_fwd, int ldof,
+                                                            const TG* __restrict__ dout, int lddo,
+                                                            const float* __restrict__ lse,
+                                                            TG* __restrict__ dqkv, int lddq) {
+  __shared__ float sQ[64 * 64], sO[64 * 64], sVo[64 * 65];
+  __shared__ float sL[64], sD[64];
+  const int lane = threadIdx.x, h = blockIdx.y, s = blockIdx.z, W = H * 64;
+  const size_t row0 = (size_t)s * L;
+  const int j = blockIdx.x * 64 + lane;
+  const bool kok = j < L;
+  const size_t krow = row0 + (kok ? j : L - 1);
+  float k[64], dk[64], dv[64];
+  load_row64<T>(qkv + krow * ldq + W + h * 64, k);
+  load_row64<T>(qkv + krow * ldq + 2 * W + h * 64, dv);
+#pragma unroll
+  for (int d = 0; d < 64; ++d) {
+    sVo[lane * 65 + d] = dv[d];
+    dk[d] = 0.f;
+    dv[d] = 0.f;
+  }
+  (void)sVo[0];
+  const int q_begin = causal ? (int)blockIdx.x * 64 : 0;
+  for (int q0 = q_begin; q0 < L; q0 += 64) {
+    __syncthreads();
+    {
+      // staged in 8-column pieces (k, dk, dv stay live: keep the temporaries small)
+      const size_t qr = row0 + min(q0 + lane, L - 1);
+      float Dsum = 0.f;
+#pragma unroll
+      for (int c = 0; c < 64; c += 8) {
+        float t[8], u[8];
+        load_cols8<T>(qkv + qr * ldq + h * 64 + c, t);
+#pragma unroll
+        for (int d = 0; d < 8; ++d) sQ[lane * 64 + c + d] = t[d] * kScale;
+        load_cols8<TG>(dout + qr * lddo + h * 64 + c, t);
+        load_cols8<T>(o_fwd + qr * ldof + h * 64 + c, u);
+#pragma unroll
+        for (int d = 0; d < 8; ++d) {
+          Dsum = fmaf(t[d], u[d], Dsum);
+          sO[lane * 64 + c + d] = t[d];  // dO rows
+        }
+      }
+      sD[lane] = Dsum;
+      sL[lane] = lse[qr * H + h];
+    }
+    __syncthreads();
+    const int ni = min(64, L - q0);
+    for (int ii = 0; ii < ni; ++ii) {
+      const int i = q0 + ii;
+      if (causal && j > i) continue;
+      const float* qr = &sQ[ii * 64];
+      const float* dor = &sO[ii * 64];
+      const float p = __expf(dot64(qr, k) - sL[ii]);
+      float dp = 0.f;
+#pragma unroll
+      for (int d = 0; d < 64; ++d) dp = fmaf(dor[d], sVo[lane * 65 + d], dp);
+      const float ds = p * (dp - sD[ii]);
+#pragma unroll
+      for (int d = 0; d < 64; ++d) {
+        dv[d] = fmaf(p, dor[d], dv[d]);
+        dk[d] = fmaf(ds, qr[d], dk[d]);
+      }
+    }
+  }
+  if (kok) {
+    store_row64<TG>(dqkv + krow * lddq + W + h * 64, dk);
+    store_row64<TG>(dqkv + krow * lddq + 2 * W + h * 64, dv);
+  }
+}
+
 template <typename T>
 static int launch_fwd(int nseq, int L, int H, int causal, const void* qkv, int ldq, void* out,
                       int ldo, float* lse, hipStream_t st) {
@@ -539,6 +850,17 @@ static int launch_fwd(int nseq, int L, int H, int causal, const void* qkv, int l
   return CLIPK_OK;
 }
 
+// 16 < L <= 64 with 16-bit operands (CoOp n_ctx 16: L_eff 23): the two-pass MFMA kernels
+// instead of the VALU attn_bwd_short (knob CLIPK_ATTN_MFMA_BWD, default on)
+static bool mfma_long_bwd() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLIPK_ATTN_MFMA_BWD");
+    v = e ? atoi(e) : 1;
+  }
+  return v != 0;
+}
+
 template <typename T, typename TG>
 static int launch_bwd(int nseq, int L, int H, int causal, const void* qkv, int ldq,
                       const void* ofwd, int ldof, const void* dout, int lddo, const float* lse,
@@ -551,6 +873,26 @@ static int launch_bwd(int nseq, int L, int H, int causal, const void* qkv, int l
       CLIPK_CHECK_LAUNCH();
       return CLIPK_OK;
     }
+  }
+  if (L > 64 || (sizeof(TG) == 2 && sizeof(T) == 2 && mfma_long_bwd())) {
+    // two passes (dK/dV per key tile, dQ per query tile); MFMA for 16-bit operands
+    if constexpr (sizeof(TG) == 2 && sizeof(T) == 2) {
+      dim3 grid((L + 63) / 64, H, nseq);
+      hipLaunchKernelGGL((attn_bwd_long_kv<T, TG>), grid, dim3(256), 0, st, nseq, L, H, causal, (const T*)qkv, ldq,
+                         (const T*)ofwd, ldof, (const TG*)dout, lddo, lse, (TG*)dqkv, lddq);
+      CLIPK_CHECK_LAUNCH();
+      hipLaunchKernelGGL((attn_bwd_long_q<T, TG>), grid, dim3(256), 0, st, nseq, L, H, causal, (const T*)qkv, ldq,
+                         (const T*)ofwd, ldof, (const TG*)dout, lddo, lse, (TG*)dqkv, lddq);
+    } else {
+      dim3 grid((L + 63) / 64, H, nseq);
+      hipLaunchKernelGGL((attn_bwd_long_valu_kv<T, TG>), grid, dim3(64), 0, st, nseq, L, H, causal,
+                         (const T*)qkv, ldq, (const T*)ofwd, ldof, (const TG*)dout, lddo, lse, (TG*)dqkv, lddq);
+      CLIPK_CHECK_LAUNCH();
+      hipLaunchKernelGGL((attn_bwd_long_valu_q<T, TG>), grid, dim3(64), 0, st, nseq, L, H, causal,
+                         (const T*)qkv, ldq, (const T*)ofwd, ldof, (const TG*)dout, lddo, lse, (TG*)dqkv, lddq);
+    }
+    CLIPK_CHECK_LAUNCH();
+    return CLIPK_OK;
   }
   auto go = [&](auto lp_tag) {
     constexpr int LP = decltype(lp_tag)::value;
@@ -597,7 +939,6 @@ extern "C" int clipk_attention_bwd(int dtype, int grad_dtype, int nseq, int L, i
   if (nseq < 0 || L <= 0 || heads <= 0 || ldqkv < 3 * heads * 64 || lddqkv < 3 * heads * 64 ||
       ldof < heads * 64 || lddo < heads * 64)
     return CLIPK_ESHAPE;
-  if (L > 64) return CLIPK_ESHAPE;
   if (nseq == 0) return CLIPK_OK;
   hipStream_t st = (hipStream_t)stream;
 #define CLIPK_BWD(TT, TGG) \

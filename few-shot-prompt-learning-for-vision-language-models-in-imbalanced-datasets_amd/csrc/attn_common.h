@@ -22,6 +22,16 @@ __device__ __forceinline__ void store_row64(T* p, const float* in) {
   for (int c = 0; c < 64 / V; ++c) store16_f32<T>(p + c * V, in + c * V);
 }
 
+// 8 consecutive columns of a row as fp32 (one 16-B load for 16-bit T, two for fp32)
+template <typename T>
+__device__ __forceinline__ void load_cols8(const T* p, float* out) {
+  constexpr int V = Vec16<T>::N;
+#pragma unroll
+  for (int c = 0; c < 8 / V; ++c) load16_f32<T>(p + c * V, out + c * V);
+}
+
+__device__ __forceinline__ void lds_fence_a() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 __device__ __forceinline__ float dot64(const float* a, const float* b) {
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll

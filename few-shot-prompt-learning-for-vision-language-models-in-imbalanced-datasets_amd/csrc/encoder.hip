@@ -11,8 +11,20 @@
 #include <cstring>
 #include <new>
 #include <cstdlib>
+#include <algorithm>
 
 #include "common.h"
+
+// Deep prompts (IVLP / MaPLe / PromptSRC, model.py:191-331): before layer l in 1..n_deep the
+// rows rows[p * n_per + i] of the residual stream are replaced by prompt row p of
+// prompts[l-1] ([n_deep][n_ctx][W] fp32); the backward sums the gradient of those rows into
+// grads[l-1] and zeroes them (the replaced rows' previous values reach nothing).
+struct DeepPrompts {
+  int n_deep = 0, n_ctx = 0, n_per = 0;
+  const int* rows = nullptr;
+  const float* prompts = nullptr;
+  float* grads = nullptr;
+};
 
 struct clipk_encoder {
   int kind;  // 0 text, 1 vision
@@ -20,6 +32,7 @@ struct clipk_encoder {
   int res, patch, Kp, Limg;
   std::vector<std::array<const void*, 16>> lw;
   std::array<const void*, 8> head;
+  DeepPrompts deep;
 };
 
 namespace clipk {
@@ -156,9 +169,11 @@ struct TextBufs {
 };
 
 // save=1: per-layer activations live in `saved`; save=0: buffers are reused across layers
-static TextBufs text_layout(const clipk_encoder* e, size_t rows, int nout, void* saved, void* ws, bool save) {
+// rd: residual dtype (-1: the text encoder's, res_dtype; the ViT's is fp32)
+static TextBufs text_layout(const clipk_encoder* e, size_t rows, int nout, void* saved, void* ws, bool save,
+                            int rd = -1) {
   TextBufs t;
-  const size_t W = e->W, H = e->heads, a = esize(e->act), xs = esize(res_dtype(e));
+  const size_t W = e->W, H = e->heads, a = esize(e->act), xs = esize(rd < 0 ? res_dtype(e) : rd);
   const int nl = e->layers;
   Carver sv(saved), wk(ws);
   Carver& S = save ? sv : wk;
@@ -431,13 +446,44 @@ static bool text_eot_last(const SeqShape& sh) {
   return v != 0 && sh.nout < sh.rows;
 }
 
+// What differs between the text encoder and the ViT around the shared layer loop: residual
+// dtype, final LayerNorm + projection (text: ln_final / text_projection on the EOT rows,
+// model.py:606-616; ViT: ln_post / proj on the CLS rows, model.py:426-431), launch-site names.
+struct EncIO {
+  int rd;
+  const float *lnf_w, *lnf_b;
+  const void* proj_f;  // [E, W] act dtype (forward B operand)
+  const void* proj_b;  // [W, E] grad dtype (backward B operand)
+  bool text;
+  void* sk = nullptr;  // split-K workspace for the forward GEMMs (ViT: small M)
+  size_t skb = 0;
+};
+static EncIO text_io(const clipk_encoder* e) {
+  EncIO io;
+  io.rd = res_dtype(e);
+  io.lnf_w = (const float*)e->head[0]; io.lnf_b = (const float*)e->head[1];
+  io.proj_f = e->head[2]; io.proj_b = e->head[3];
+  io.text = true;
+  return io;
+}
+#define SITE(n) (io.text ? "text." n : "vit." n)
+
+// deep prompts of layer l (1..n_deep) into the layer's input rows
+static int deep_inject(const clipk_encoder* e, int l, int rd, void* X, hipStream_t st) {
+  const DeepPrompts& d = e->deep;
+  if (l < 1 || l > d.n_deep || !d.prompts) return CLIPK_OK;
+  return clipk_rows_inject(rd, d.n_ctx, d.n_per, e->W, d.prompts + (size_t)(l - 1) * d.n_ctx * e->W, d.rows, X,
+                           e->W, st);
+}
+
 static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const float* x0, const int* eot_rows,
                              float* txt, void* saved, size_t saved_bytes, void* ws, size_t ws_bytes,
-                             hipStream_t st) {
+                             hipStream_t st, const EncIO& io) {
   const bool save = saved != nullptr;
-  TextBufs t = text_layout(e, sh.rows, sh.nout, saved, ws, save);
+  TextBufs t = text_layout(e, sh.rows, sh.nout, saved, ws, save, io.rd);
   if (ws_bytes < t.ws_bytes || (save && saved_bytes < t.saved_bytes)) return CLIPK_EWORKSPACE;
-  const int W = e->W, rows = sh.rows, rd = res_dtype(e);
+  const int W = e->W, rows = sh.rows, rd = io.rd;
+  const int pg = io.text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE;
   // layer-0 input: x0 (fp32) into X[0] (the residual dtype) when saving (LN1 backward reads
   // it) or when the residual stream is 16-bit
   const void* cur = x0;
@@ -455,30 +501,32 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
   for (int l = 0; l < nl; ++l) {
     void* Xo = t.X[l + 1];
     if (!save && Xo == cur) Xo = t.X[l];  // ping-pong (cur may be the caller's x0)
+    if (l >= 1) TRY(deep_inject(e, l, rd, const_cast<void*>(cur), st));  // l >= 1: cur is ours
     if (eotl && l == nl - 1) {
       // last layer: attention over all rows (the EOT rows attend to their whole prefix),
       // then out_proj / LN2 / MLP on the EOT rows alone; Xm, h, Xo hold nout compact rows
       TRY(block_attn(e, e->lw[l], sh, rd, cur, t.xn, t.qkv[l], t.o[l], t.lse[l], t.mean1[l], t.rstd1[l], st,
-                     true, nullptr, 0));
+                     io.text, io.sk, io.skb));
       {
-        ProfScope ps(CLIPK_PROF_NONE, st, 0.0, "text.eot_gather",
+        ProfScope ps(CLIPK_PROF_NONE, st, 0.0, SITE("eot_gather"),
                      2.0 * nout * W * (esize(e->act) + esize(rd)));
         TRY(clipk_rows_copy(W * (int)esize(e->act), nout, t.o[l], eot_rows, t.oc, nullptr, st));
         TRY(clipk_rows_copy(W * (int)esize(rd), nout, cur, eot_rows, t.xc, nullptr, st));
       }
       TRY(block_post(e, e->lw[l], nout, rd, t.xc, t.oc, t.Xm[l], Xo, t.xn, save ? t.h[l] : nullptr, t.g,
-                     t.mean2[l], t.rstd2[l], st, true, nullptr, 0));
+                     t.mean2[l], t.rstd2[l], st, io.text, nullptr, 0));
     } else {
       TRY(block_fwd(e, e->lw[l], sh, rd, cur, t.Xm[l], Xo, t.xn, t.qkv[l], t.o[l], t.lse[l],
-                    save ? t.h[l] : nullptr, t.g, t.mean1[l], t.rstd1[l], t.mean2[l], t.rstd2[l], st, true));
+                    save ? t.h[l] : nullptr, t.g, t.mean1[l], t.rstd1[l], t.mean2[l], t.rstd2[l], st, io.text,
+                    io.sk, io.skb));
     }
     cur = Xo;
   }
-  // ln_final on the EOT rows only (exact: LayerNorm is per row), then @ text_projection
-  TRY(clipk_layernorm_fwd_x(rd, e->act, sh.nout, W, cur, W, eotl ? nullptr : eot_rows, (const float*)e->head[0],
-                            (const float*)e->head[1], t.lnf, W, t.meanf, t.rstdf, st));
-  TRY(gemm(e->act, CLIPK_F32, CLIPK_EPI_NONE, sh.nout, e->E, W, t.lnf, e->head[2], nullptr, nullptr, txt,
-           nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
+  // final LayerNorm on the output rows only (exact: LayerNorm is per row), then @ projection
+  TRY(clipk_layernorm_fwd_x(rd, e->act, sh.nout, W, cur, W, eotl ? nullptr : eot_rows, io.lnf_w, io.lnf_b, t.lnf, W,
+                            t.meanf, t.rstdf, st));
+  TRY(gemm(e->act, CLIPK_F32, CLIPK_EPI_NONE, sh.nout, e->E, W, t.lnf, io.proj_f, nullptr, nullptr, txt,
+           nullptr, nullptr, 0, st, pg, nullptr, 0, SITE("head")));
   return CLIPK_OK;
 }
 
@@ -500,17 +548,19 @@ static bool text_dres16(const clipk_encoder* e) {
 
 static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const int* eot_rows,
                               const float* dtxt, const void* saved, size_t saved_bytes, float* dx0,
-                              void* ws, size_t ws_bytes, hipStream_t st) {
-  TextBufs t = text_layout(e, sh.rows, sh.nout, const_cast<void*>(saved), nullptr, true);
+                              void* ws, size_t ws_bytes, hipStream_t st, const EncIO& io) {
+  TextBufs t = text_layout(e, sh.rows, sh.nout, const_cast<void*>(saved), nullptr, true, io.rd);
   TextBwdBufs b = text_bwd_layout(e, sh.rows, sh.nout, sh.part_bytes(e->heads), ws);
   if (saved_bytes < t.saved_bytes || ws_bytes < b.bytes) return CLIPK_EWORKSPACE;
   const int W = e->W, rows = sh.rows, nout = sh.nout, gd = e->grad, act = e->act;
+  const int pg = io.text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE;
   float* dX = dx0;
-  // d lnf = dtxt . P^T   (txt = lnf @ P, P = text_projection [W,E])
+  // d lnf = dtxt . P^T   (txt = lnf @ P, P = projection [W,E])
   TRY(clipk_cast(gd, (long)nout * e->E, dtxt, b.dtg, st));
-  TRY(gemm(gd, CLIPK_F32, CLIPK_EPI_NONE, nout, W, e->E, b.dtg, e->head[3], nullptr, nullptr, b.dlnf,
-           nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL));
-  const bool r16 = text_dres16(e);
+  TRY(gemm(gd, CLIPK_F32, CLIPK_EPI_NONE, nout, W, e->E, b.dtg, io.proj_b, nullptr, nullptr, b.dlnf,
+           nullptr, nullptr, 0, st, pg));
+  // the ViT's residual stream is fp32: its gradient stays fp32 too
+  const bool r16 = io.rd != CLIPK_F32 && text_dres16(e);
   const bool eotl = text_eot_last(sh);
   auto zero = [&](void* p, size_t bytes) {
     return hipMemsetAsync(p, 0, bytes, st) == hipSuccess ? CLIPK_OK : (int)hipGetLastError();
@@ -520,9 +570,9 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
     if (!r16) TRY(zero(dX, (size_t)rows * W * 4));
     TRY(zero(b.dX_lp, (size_t)rows * W * esize(gd)));
   }
-  const int rd = res_dtype(e);
+  const int rd = io.rd;
   const int* frows = eotl ? nullptr : eot_rows;  // EOT-last: the last layer's rows are compact
-  TRY(clipk_layernorm_bwd_x2(rd, CLIPK_F32, nout, W, b.dlnf, W, t.Xf, W, frows, (const float*)e->head[0], t.meanf,
+  TRY(clipk_layernorm_bwd_x2(rd, CLIPK_F32, nout, W, b.dlnf, W, t.Xf, W, frows, io.lnf_w, t.meanf,
                              t.rstdf, nullptr, CLIPK_F32, W, r16 ? nullptr : dX, b.dX_lp, gd, frows, W, st));
   // residual-gradient update of one LayerNorm backward over n rows: dres (fp32 dX or the
   // 16-bit dX_lp, in place) + LN'(dxn); last: the encoder input's gradient, always fp32 into dX
@@ -530,7 +580,7 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
   // read + written (16-bit stream or fp32), mean / rstd
   auto ln_bwd = [&](int n, const void* x, const float* gamma, const float* mean, const float* rstd, bool last) {
     const double lnbb = (double)n * W * (esize(gd) + esize(rd) + 2.0 * (r16 ? esize(gd) : 4)) + 8.0 * n;
-    ProfScope ps(CLIPK_PROF_NONE, st, 0.0, "text.ln_bwd", lnbb);
+    ProfScope ps(CLIPK_PROF_NONE, st, 0.0, SITE("ln_bwd"), lnbb);
     if (!r16)
       return clipk_layernorm_bwd_x(rd, gd, n, W, b.dxn, W, x, W, nullptr, gamma, mean, rstd, dX, W, dX,
                                    last ? nullptr : b.dX_lp, gd, nullptr, W, st);
@@ -545,19 +595,19 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
     // MLP: dg = dX . Wproj ; dh = dg * qgelu'(h)  (h saved in the act dtype: more precise
     // than saving qgelu'(h), which rounds the saturated region)
     TRY(gemm(gd, gd, CLIPK_EPI_DQGELU, n, 4 * W, W, b.dX_lp, w[15], nullptr, nullptr, b.dh, nullptr,
-             t.h[l], act, st, CLIPK_PROF_GEMM_DGELU, nullptr, 0, "text.proj_dx_dgelu"));
+             t.h[l], act, st, io.text ? CLIPK_PROF_GEMM_DGELU : CLIPK_PROF_NONE, nullptr, 0, SITE("proj_dx_dgelu")));
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, n, W, 4 * W, b.dh, w[14], nullptr, nullptr, b.dxn, nullptr,
-             nullptr, 0, st, CLIPK_PROF_GEMM_ALL, nullptr, 0, "text.fc_dx"));
+             nullptr, 0, st, pg, nullptr, 0, SITE("fc_dx")));
     TRY(ln_bwd(n, t.Xm[l], (const float*)w[6], t.mean2[l], t.rstd2[l], false));
     // attention: do = dXm . Wout ; dqkv ; dxn1 = dqkv . Win
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, n, W, W, b.dX_lp, w[13], nullptr, nullptr, compact ? b.dh : b.do_,
-             nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL, nullptr, 0, "text.out_dx"));
+             nullptr, nullptr, 0, st, pg, nullptr, 0, SITE("out_dx")));
     if (compact) {
       // back to the full row layout: do and the residual gradient (the one LN1's backward
       // reads: the 16-bit stream, or fp32 dX) scattered to the EOT rows of zeroed buffers
       const int gb = W * (int)esize(gd), rb = W * (r16 ? (int)esize(gd) : 4);
       void* res = r16 ? b.dX_lp : (void*)dX;
-      ProfScope ps(CLIPK_PROF_NONE, st, 0.0, "text.eot_scatter",
+      ProfScope ps(CLIPK_PROF_NONE, st, 0.0, SITE("eot_scatter"),
                    2.0 * nout * (gb + 2.0 * rb) + (double)rows * (gb + rb));
       TRY(zero(b.do_, (size_t)rows * gb));
       TRY(clipk_rows_copy(gb, nout, b.dh, nullptr, b.do_, eot_rows, st));
@@ -570,12 +620,22 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
       // kernels also read o (the 16-bit MFMA ones recompute D_i = rowsum(P o dP) instead)
       const double ab = (double)rows * W * ((act == CLIPK_F32 ? 4.0 : 3.0) * esize(act) + 4.0 * esize(gd)) +
                         4.0 * rows * e->heads;
-      ProfScope ps(CLIPK_PROF_ATTN, st, 0.0, "text.attn_bwd", ab);
+      ProfScope ps(io.text ? CLIPK_PROF_ATTN : CLIPK_PROF_NONE, st, 0.0, SITE("attn_bwd"), ab);
       TRY(attn_bwd(e, sh, t.qkv[l], t.o[l], b.do_, t.lse[l], b.dqkv, b.part, st));
     }
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, 3 * W, b.dqkv, w[12], nullptr, nullptr, b.dxn,
-             nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_ALL, nullptr, 0, "text.qkv_dx"));
+             nullptr, nullptr, 0, st, pg, nullptr, 0, SITE("qkv_dx")));
     TRY(ln_bwd(rows, t.X[l], (const float*)w[0], t.mean1[l], t.rstd1[l], l == 0));
+    const DeepPrompts& d = e->deep;
+    if (l >= 1 && l <= d.n_deep && d.grads) {
+      // layer l's replaced rows: their gradient is the prompt's; it stops there
+      if (r16)
+        TRY(clipk_rows_collect(gd, d.n_ctx, d.n_per, W, b.dX_lp, W, nullptr, 0, 0, d.rows,
+                               d.grads + (size_t)(l - 1) * d.n_ctx * W, 0, 1, st));
+      else
+        TRY(clipk_rows_collect(CLIPK_F32, d.n_ctx, d.n_per, W, dX, W, b.dX_lp, gd, W, d.rows,
+                               d.grads + (size_t)(l - 1) * d.n_ctx * W, 0, 1, st));
+    }
   }
   return CLIPK_OK;
 }
@@ -604,7 +664,7 @@ extern "C" int clipk_text_forward(const clipk_encoder* e, int nseq, int L, const
   if (!e || e->kind != 0 || !x0 || !eot_rows || !txt || !ws) return CLIPK_EINVAL;
   if (nseq <= 0 || L <= 0 || L > 77) return CLIPK_ESHAPE;
   return text_forward_impl(e, SeqShape::plain(nseq, L, 1), x0, eot_rows, txt, saved, saved_bytes, ws,
-                           ws_bytes, (hipStream_t)stream);
+                           ws_bytes, (hipStream_t)stream, text_io(e));
 }
 
 extern "C" size_t clipk_text_bwd_ws_bytes(const clipk_encoder* e, int nseq, int L) {
@@ -617,9 +677,9 @@ extern "C" int clipk_text_backward(const clipk_encoder* e, int nseq, int L, cons
                                    void* ws, size_t ws_bytes, void* stream) {
   if (!e || e->kind != 0 || !eot_rows || !dtxt || !saved || !dx0 || !ws) return CLIPK_EINVAL;
   if (!e->head[3]) return CLIPK_EINVAL;  // forward-only encoder
-  if (nseq <= 0 || L <= 0 || L > 64) return CLIPK_ESHAPE;
+  if (nseq <= 0 || L <= 0 || L > 77) return CLIPK_ESHAPE;
   return text_backward_impl(e, SeqShape::plain(nseq, L, 1), eot_rows, dtxt, saved, saved_bytes, dx0, ws,
-                            ws_bytes, (hipStream_t)stream);
+                            ws_bytes, (hipStream_t)stream, text_io(e));
 }
 
 static bool packed_ok(int G, int C, int P, int R, int ntiles) {
@@ -649,7 +709,7 @@ extern "C" int clipk_text_forward_packed(const clipk_encoder* e, int G, int C, i
   if (!e || e->kind != 0 || !tiles || !row_first || !x0 || !eot_rows || !txt || !ws) return CLIPK_EINVAL;
   if (!packed_ok(G, C, P, R, ntiles)) return CLIPK_ESHAPE;
   return text_forward_impl(e, SeqShape::prefix(G, C, P, R, ntiles, tiles, row_first), x0, eot_rows, txt, saved,
-                           saved_bytes, ws, ws_bytes, (hipStream_t)stream);
+                           saved_bytes, ws, ws_bytes, (hipStream_t)stream, text_io(e));
 }
 
 extern "C" int clipk_text_backward_packed(const clipk_encoder* e, int G, int C, int P, int R, int ntiles,
@@ -661,7 +721,7 @@ extern "C" int clipk_text_backward_packed(const clipk_encoder* e, int G, int C, 
   if (!e->head[3]) return CLIPK_EINVAL;
   if (!packed_ok(G, C, P, R, ntiles)) return CLIPK_ESHAPE;
   return text_backward_impl(e, SeqShape::prefix(G, C, P, R, ntiles, tiles, row_first), eot_rows, dtxt, saved,
-                            saved_bytes, dx0, ws, ws_bytes, (hipStream_t)stream);
+                            saved_bytes, dx0, ws, ws_bytes, (hipStream_t)stream, text_io(e));
 }
 
 // ---------------------------------------------------------------- vision
@@ -731,6 +791,146 @@ extern "C" int clipk_vit_forward(const clipk_encoder* e, int B, const float* img
   TRY(gemm(act, CLIPK_F32, CLIPK_EPI_NONE, B, e->E, D, v.cls, e->head[4], nullptr, nullptr, feat,
            nullptr, nullptr, 0, st, CLIPK_PROF_NONE, nullptr, 0, "vit.head"));
   return CLIPK_OK;
+}
+
+// ---------------------------------------------------------------- prompted ViT (training)
+// IVLP / MaPLe / PromptSRC (model.py:191-331, 401-431, 434-485): n_vpt visual prompt rows
+// appended after the image tokens (rows per image L' = L + n_vpt), deep prompts replacing the
+// last n_vpt rows at layers 1..n_deep (clipk_encoder_set_deep_prompts), and -- because those
+// prompts train -- the input-grad backward of the whole ViT: the text encoder's layer loop
+// (text_forward_impl / text_backward_impl) on plain non-causal rows with an fp32 residual
+// stream, ln_post / proj on the CLS rows (the last layer's post-attention half on those rows
+// only, as the text encoder's EOT rows).
+namespace clipk {
+static EncIO vit_io(const clipk_encoder* e, const void* proj_b) {
+  EncIO io;
+  io.rd = CLIPK_F32;
+  io.lnf_w = (const float*)e->head[2]; io.lnf_b = (const float*)e->head[3];
+  io.proj_f = e->head[4]; io.proj_b = proj_b;
+  io.text = false;
+  return io;
+}
+struct VitPBufs {
+  void* patches;
+  float *pout, *x0, *cls_rows;  // cls_rows: int row table [B] (as float storage, reinterpreted)
+  float *dvpt_sum, *vmean, *vrstd;
+  void* sk;
+  size_t sk_bytes;
+  void* rest;  // text_layout ws (forward) / text_bwd_layout (backward)
+  size_t bytes;
+};
+static VitPBufs vitp_layout(const clipk_encoder* e, int B, int n_vpt, void* ws) {
+  VitPBufs v;
+  const size_t a = esize(e->act), D = e->W, L = e->Limg, Lp = L + n_vpt, rows = (size_t)B * Lp;
+  const size_t np = (size_t)B * (L - 1);
+  Carver c(ws);
+  v.patches = c.take(np * e->Kp * a);
+  v.pout = (float*)c.take(np * D * 4);
+  v.x0 = (float*)c.take(rows * D * 4);
+  v.cls_rows = (float*)c.take((size_t)B * 4);
+  v.dvpt_sum = (float*)c.take((size_t)(n_vpt > 0 ? n_vpt : 1) * D * 4);
+  v.vmean = (float*)c.take((size_t)(n_vpt > 0 ? n_vpt : 1) * 4);
+  v.vrstd = (float*)c.take((size_t)(n_vpt > 0 ? n_vpt : 1) * 4);
+  static const bool no_sk = getenv("CLIPK_VIT_NOSPLITK") != nullptr;
+  v.sk_bytes = no_sk ? 0 : vit_splitk_bytes(e->act, (int)rows, (int)D);
+  v.sk = v.sk_bytes ? c.take(v.sk_bytes) : nullptr;
+  v.rest = ws ? (char*)ws + c.off : nullptr;
+  const size_t fwd = text_layout(e, rows, B, nullptr, nullptr, true, CLIPK_F32).ws_bytes;
+  const size_t fwd0 = text_layout(e, rows, B, nullptr, nullptr, false, CLIPK_F32).ws_bytes;
+  const size_t bwd = text_bwd_layout(e, rows, B, 0, nullptr).bytes;
+  v.bytes = c.off + std::max(std::max(fwd, fwd0), bwd);
+  return v;
+}
+__global__ void cls_rows_kernel(int B, int Lp, int* rows) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) rows[b] = b * Lp;
+}
+// out[p] = sum over images b (fixed order) of dx[b * Lp + L + p]
+__global__ __launch_bounds__(256) void vpt_rows_sum_kernel(int B, int Lp, int L, int n_vpt, int D,
+                                                           const float* __restrict__ dx, float* __restrict__ out) {
+  const int p = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  if (p >= n_vpt || c >= D) return;
+  float acc = 0.f;
+  for (int b = 0; b < B; ++b) acc += dx[((size_t)b * Lp + L + p) * D + c];
+  out[(size_t)p * D + c] = acc;
+}
+}  // namespace clipk
+
+extern "C" int clipk_encoder_set_deep_prompts(clipk_encoder* e, int n_deep, int n_ctx, int n_per, const int* rows,
+                                              const float* prompts, float* grads) {
+  if (!e) return CLIPK_EINVAL;
+  if (n_deep < 0 || n_deep >= e->layers || (n_deep > 0 && (n_ctx <= 0 || n_per <= 0))) return CLIPK_ESHAPE;
+  if (n_deep > 0 && (!rows || !prompts)) return CLIPK_EINVAL;
+  e->deep = DeepPrompts();
+  if (n_deep > 0) {
+    e->deep.n_deep = n_deep; e->deep.n_ctx = n_ctx; e->deep.n_per = n_per;
+    e->deep.rows = rows; e->deep.prompts = prompts; e->deep.grads = grads;
+  }
+  return CLIPK_OK;
+}
+
+extern "C" size_t clipk_vit_prompted_saved_bytes(const clipk_encoder* e, int B, int n_vpt) {
+  if (!e || e->kind != 1 || B <= 0 || n_vpt < 0) return 0;
+  return text_layout(e, (size_t)B * (e->Limg + n_vpt), B, nullptr, nullptr, true, CLIPK_F32).saved_bytes;
+}
+
+extern "C" size_t clipk_vit_prompted_ws_bytes(const clipk_encoder* e, int B, int n_vpt) {
+  if (!e || e->kind != 1 || B <= 0 || n_vpt < 0) return 0;
+  return vitp_layout(e, B, n_vpt, nullptr).bytes;
+}
+
+extern "C" int clipk_vit_forward_prompted(const clipk_encoder* e, int B, const float* img, int n_vpt,
+                                          const float* vpt, float* feat, void* saved, size_t saved_bytes, void* ws,
+                                          size_t ws_bytes, void* stream) {
+  if (!e || e->kind != 1 || !img || !feat || !ws || (n_vpt > 0 && !vpt)) return CLIPK_EINVAL;
+  if (B <= 0 || n_vpt < 0) return CLIPK_ESHAPE;
+  VitPBufs v = vitp_layout(e, B, n_vpt, ws);
+  if (ws_bytes < v.bytes) return CLIPK_EWORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int D = e->W, L = e->Limg, Lp = L + n_vpt, np = B * (L - 1), act = e->act;
+  TRY(clipk_im2col(act, B, e->res, e->patch, e->Kp, img, v.patches, st));
+  TRY(gemm(act, CLIPK_F32, CLIPK_EPI_NONE, np, D, e->Kp, v.patches, e->head[5], nullptr, nullptr, v.pout, nullptr,
+           nullptr, 0, st, CLIPK_PROF_NONE,
+           clipk_gemm_splitk_ws_bytes(np, D, clipk_gemm_auto_splits(act, np, D, e->Kp)) <= v.sk_bytes ? v.sk : nullptr,
+           v.sk_bytes, "vit.patch_embed"));
+  TRY(clipk_vit_embed_ln_vpt(B, L, n_vpt, D, v.pout, (const float*)e->head[6], (const float*)e->head[7], vpt,
+                             (const float*)e->head[0], (const float*)e->head[1], v.x0, st));
+  hipLaunchKernelGGL(cls_rows_kernel, dim3((B + 63) / 64), dim3(64), 0, st, B, Lp, (int*)v.cls_rows);
+  CLIPK_CHECK_LAUNCH();
+  EncIO io = vit_io(e, nullptr);
+  io.sk = v.sk; io.skb = v.sk_bytes;
+  return text_forward_impl(e, SeqShape::plain(B, Lp, 0), v.x0, (const int*)v.cls_rows, feat, saved, saved_bytes,
+                           v.rest, ws_bytes - ((char*)v.rest - (char*)ws), st, io);
+}
+
+extern "C" int clipk_vit_backward_prompted(const clipk_encoder* e, int B, int n_vpt, const float* vpt,
+                                           const void* proj_bwd, const float* dfeat, const void* saved,
+                                           size_t saved_bytes, float* dvpt, void* ws, size_t ws_bytes,
+                                           void* stream) {
+  if (!e || e->kind != 1 || !proj_bwd || !dfeat || !saved || !ws || (n_vpt > 0 && (!vpt || !dvpt)))
+    return CLIPK_EINVAL;
+  if (B <= 0 || n_vpt < 0) return CLIPK_ESHAPE;
+  for (int l = 0; l < e->layers; ++l)
+    if (!e->lw[l][12] || !e->lw[l][13] || !e->lw[l][14] || !e->lw[l][15]) return CLIPK_EINVAL;
+  VitPBufs v = vitp_layout(e, B, n_vpt, ws);
+  if (ws_bytes < v.bytes) return CLIPK_EWORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int D = e->W, L = e->Limg, Lp = L + n_vpt;
+  // the layer loop's gradient of the layer-0 input lands in x0's rows (fp32, [B*Lp, D])
+  hipLaunchKernelGGL(cls_rows_kernel, dim3((B + 63) / 64), dim3(64), 0, st, B, Lp, (int*)v.cls_rows);
+  CLIPK_CHECK_LAUNCH();
+  TRY(text_backward_impl(e, SeqShape::plain(B, Lp, 0), (const int*)v.cls_rows, dfeat, saved, saved_bytes, v.x0,
+                         v.rest, ws_bytes - ((char*)v.rest - (char*)ws), st, vit_io(e, proj_bwd)));
+  if (n_vpt == 0) return CLIPK_OK;
+  // first-layer prompts: x0 rows L.. of every image = ln_pre(vpt) (model.py:413-420); the
+  // same vpt in every image, so d vpt = ln_pre'(vpt) . sum_b d x0[b, L + p] (linear in dy)
+  TRY(clipk_layernorm_fwd(CLIPK_F32, n_vpt, D, vpt, D, nullptr, (const float*)e->head[0], (const float*)e->head[1],
+                          v.dvpt_sum, D, v.vmean, v.vrstd, st));  // the statistics (output overwritten next)
+  hipLaunchKernelGGL(vpt_rows_sum_kernel, dim3((D + 255) / 256, n_vpt), dim3(256), 0, st, B, Lp, L, n_vpt, D, v.x0,
+                     v.dvpt_sum);
+  CLIPK_CHECK_LAUNCH();
+  return clipk_layernorm_bwd(CLIPK_F32, n_vpt, D, v.dvpt_sum, D, vpt, D, nullptr, (const float*)e->head[0], v.vmean,
+                             v.vrstd, nullptr, D, dvpt, nullptr, CLIPK_F32, nullptr, D, st);
 }
 
 extern "C" int clipk_prof_enable(int kind) {

@@ -2,6 +2,8 @@
 // ln_pre, prompt assembly (+pos) and its ctx gradient, cosine logits fwd/bwd, CE/focal
 // loss fwd+bwd, CoCoOp Meta-Net fwd/bwd, fused SGD, casts. One wave per row throughout,
 // float4 accesses, fixed-order (deterministic) reductions.
+#include <type_traits>
+
 #include "common.h"
 
 namespace clipk {
@@ -30,19 +32,24 @@ __global__ __launch_bounds__(256) void im2col_kernel(int B, int R, int P, int Kp
 
 // ---------------------------------------------------------------- ViT embed + ln_pre
 // model.py:405-420: x = cat(cls, patches) + pos; ln_pre(x). One wave per token row.
-__global__ __launch_bounds__(256) void vit_embed_ln_kernel(int B, int L, int D,
+// n_vpt > 0 (IVLP / MaPLe / PromptSRC, model.py:413-420 / 465-472): n_vpt visual prompt rows
+// appended after the L image tokens (no positional embedding), rows per image L + n_vpt.
+__global__ __launch_bounds__(256) void vit_embed_ln_kernel(int B, int L, int n_vpt, int D,
                                                            const float* __restrict__ patch,
                                                            const float* __restrict__ cls,
                                                            const float* __restrict__ pos,
+                                                           const float* __restrict__ vpt,
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta,
                                                            float* __restrict__ x) {
   const int lane = threadIdx.x & 63;
+  const int Lo = L + n_vpt;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= B * L) return;
-  const int b = r / L, t = r % L;
-  const float* src = t == 0 ? cls : patch + ((size_t)b * (L - 1) + t - 1) * D;
-  const float* pp = pos + (size_t)t * D;
+  if (r >= B * Lo) return;
+  const int b = r / Lo, t = r % Lo;
+  const bool prompt = t >= L;
+  const float* src = prompt ? vpt + (size_t)(t - L) * D : t == 0 ? cls : patch + ((size_t)b * (L - 1) + t - 1) * D;
+  const float* pp = pos + (size_t)(prompt ? 0 : t) * D;
   const int nv = D >> 2;
   f32x4 v[4];
   float s = 0.f;
@@ -50,7 +57,8 @@ __global__ __launch_bounds__(256) void vit_embed_ln_kernel(int B, int L, int D,
   for (int i = 0; i < 4; ++i) {
     const int c = lane + i * 64;
     if (c < nv) {
-      v[i] = reinterpret_cast<const f32x4*>(src)[c] + reinterpret_cast<const f32x4*>(pp)[c];
+      v[i] = reinterpret_cast<const f32x4*>(src)[c];
+      if (!prompt) v[i] += reinterpret_cast<const f32x4*>(pp)[c];
       s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
     }
   }
@@ -408,6 +416,45 @@ __global__ __launch_bounds__(256) void rows_copy_kernel(int n, int chunks, const
   }
 }
 
+// Deep prompts (model.py:232-252 IVLP, 293-328 MaPLe): the rows a layer's learnable tokens
+// replace. rows[p * n_per + i] = the i-th row that takes prompt row p.
+template <typename TD>
+__global__ __launch_bounds__(256) void rows_inject_kernel(int n_ctx, int n_per, int W, const float* __restrict__ src,
+                                                          const int* __restrict__ rows, TD* __restrict__ dst,
+                                                          int ldd) {
+  const long total = (long)n_ctx * n_per * W;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int c = (int)(e % W);
+    const long ri = e / W;
+    const int p = (int)(ri / n_per);
+    dst[(size_t)rows[ri] * ldd + c] = (TD)src[(size_t)p * W + c];
+  }
+}
+// out[p] (+)= sum_i src[rows[p*n_per+i]] (fixed order), then those rows of src (and of src2,
+// when given) are zeroed: the replaced rows' inputs did not reach the layer.
+template <typename TS, typename TS2>
+__global__ __launch_bounds__(256) void rows_collect_kernel(int n_ctx, int n_per, int W, TS* __restrict__ src, int lds,
+                                                           TS2* __restrict__ src2, int lds2,
+                                                           const int* __restrict__ rows, float* __restrict__ out,
+                                                           int accumulate, int zero_src) {
+  const int p = blockIdx.y;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (p >= n_ctx || c >= W) return;
+  float acc = accumulate ? out[(size_t)p * W + c] : 0.f;
+  for (int i = 0; i < n_per; ++i) {
+    const size_t r = (size_t)rows[(size_t)p * n_per + i];
+    acc += (float)src[r * lds + c];
+  }
+  out[(size_t)p * W + c] = acc;
+  if (zero_src) {
+    for (int i = 0; i < n_per; ++i) {
+      const size_t r = (size_t)rows[(size_t)p * n_per + i];
+      src[r * lds + c] = (TS)0.f;
+      if (src2) src2[r * lds2 + c] = (TS2)0.f;
+    }
+  }
+}
+
 static inline int grid_for(long n) {
   long g = (n + 255) / 256;
   return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
@@ -442,7 +489,19 @@ extern "C" int clipk_vit_embed_ln(int B, int L, int width, const float* patch, c
   if (B < 0 || L < 2 || width % 4 || width > 1024) return CLIPK_ESHAPE;
   if (B == 0) return CLIPK_OK;
   hipLaunchKernelGGL(vit_embed_ln_kernel, dim3((B * L + 3) / 4), dim3(256), 0, (hipStream_t)stream, B,
-                     L, width, patch, cls, pos, gamma, beta, x);
+                     L, 0, width, patch, cls, pos, nullptr, gamma, beta, x);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_vit_embed_ln_vpt(int B, int L, int n_vpt, int width, const float* patch, const float* cls,
+                                      const float* pos, const float* vpt, const float* gamma, const float* beta,
+                                      float* x, void* stream) {
+  if (!patch || !cls || !pos || !gamma || !beta || !x || (n_vpt > 0 && !vpt)) return CLIPK_EINVAL;
+  if (B < 0 || L < 2 || n_vpt < 0 || width % 4 || width > 1024) return CLIPK_ESHAPE;
+  if (B == 0) return CLIPK_OK;
+  hipLaunchKernelGGL(vit_embed_ln_kernel, dim3((B * (L + n_vpt) + 3) / 4), dim3(256), 0, (hipStream_t)stream, B,
+                     L, n_vpt, width, patch, cls, pos, vpt, gamma, beta, x);
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
 }
@@ -583,6 +642,58 @@ extern "C" int clipk_rows_copy(int row_bytes, int n, const void* src, const int*
   const int chunks = row_bytes / 16;
   hipLaunchKernelGGL(rows_copy_kernel, grid_for((long)n * chunks), 256, 0, (hipStream_t)stream, n, chunks,
                      (const uint4*)src, src_rows, (uint4*)dst, dst_rows);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_rows_inject(int dst_dtype, int n_ctx, int n_per, int width, const float* src, const int* rows,
+                                 void* dst, int ldd, void* stream) {
+  if (!src || !rows || !dst) return CLIPK_EINVAL;
+  if (n_ctx < 0 || n_per < 0 || width <= 0 || ldd < width) return CLIPK_ESHAPE;
+  const long total = (long)n_ctx * n_per * width;
+  if (total == 0) return CLIPK_OK;
+  hipStream_t st = (hipStream_t)stream;
+  switch (dst_dtype) {
+    case CLIPK_F32: hipLaunchKernelGGL(rows_inject_kernel<float>, grid_for(total), 256, 0, st, n_ctx, n_per, width, src, rows, (float*)dst, ldd); break;
+    case CLIPK_F16: hipLaunchKernelGGL(rows_inject_kernel<f16>, grid_for(total), 256, 0, st, n_ctx, n_per, width, src, rows, (f16*)dst, ldd); break;
+    case CLIPK_BF16: hipLaunchKernelGGL(rows_inject_kernel<bf16>, grid_for(total), 256, 0, st, n_ctx, n_per, width, src, rows, (bf16*)dst, ldd); break;
+    default: return CLIPK_EDTYPE;
+  }
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_rows_collect(int src_dtype, int n_ctx, int n_per, int width, void* src, int lds, void* src2,
+                                  int src2_dtype, int lds2, const int* rows, float* out, int accumulate,
+                                  int zero_src, void* stream) {
+  if (!src || !rows || !out) return CLIPK_EINVAL;
+  if (n_ctx < 0 || n_per < 0 || width <= 0 || lds < width || (src2 && lds2 < width)) return CLIPK_ESHAPE;
+  if (n_ctx == 0) return CLIPK_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((width + 255) / 256, n_ctx);
+  auto go = [&](auto* s1) {
+    using TS = std::remove_pointer_t<decltype(s1)>;
+    if (!src2) {
+      hipLaunchKernelGGL((rows_collect_kernel<TS, float>), grid, 256, 0, st, n_ctx, n_per, width, s1, lds,
+                         (float*)nullptr, 0, rows, out, accumulate, zero_src);
+      return CLIPK_OK;
+    }
+    switch (src2_dtype) {
+      case CLIPK_F32: hipLaunchKernelGGL((rows_collect_kernel<TS, float>), grid, 256, 0, st, n_ctx, n_per, width, s1, lds, (float*)src2, lds2, rows, out, accumulate, zero_src); break;
+      case CLIPK_F16: hipLaunchKernelGGL((rows_collect_kernel<TS, f16>), grid, 256, 0, st, n_ctx, n_per, width, s1, lds, (f16*)src2, lds2, rows, out, accumulate, zero_src); break;
+      case CLIPK_BF16: hipLaunchKernelGGL((rows_collect_kernel<TS, bf16>), grid, 256, 0, st, n_ctx, n_per, width, s1, lds, (bf16*)src2, lds2, rows, out, accumulate, zero_src); break;
+      default: return CLIPK_EDTYPE;
+    }
+    return CLIPK_OK;
+  };
+  int rc;
+  switch (src_dtype) {
+    case CLIPK_F32: rc = go((float*)src); break;
+    case CLIPK_F16: rc = go((f16*)src); break;
+    case CLIPK_BF16: rc = go((bf16*)src); break;
+    default: return CLIPK_EDTYPE;
+  }
+  if (rc != CLIPK_OK) return rc;
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
 }

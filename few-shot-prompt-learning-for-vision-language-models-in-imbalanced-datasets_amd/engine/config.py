@@ -120,6 +120,21 @@ def get_cfg_default() -> CfgNode:
                      "CLASS_TOKEN_POSITION": "end", "USE_FOCAL_LOSS": False, "LOSS_TYPE": "ce"},
             # PromptSRC/train.py:110-114
             "COCOOP": {"N_CTX": 16, "CTX_INIT": "", "PREC": "fp16", "USE_FOCAL_LOSS": False},
+            # PromptSRC/train.py:116-122
+            "MAPLE": {"N_CTX": 2, "CTX_INIT": "a photo of a", "PREC": "fp16", "PROMPT_DEPTH": 9,
+                      "USE_FOCAL_LOSS": False},
+            # PromptSRC/train.py:125-141 (+ LOGITS_LOSS_WEIGHT and USE_GPA, which the trainer
+            # reads, promptsrc.py:320, 330, but train.py never defines)
+            "PROMPTSRC": {"N_CTX_VISION": 4, "N_CTX_TEXT": 4, "CTX_INIT": "a photo of a", "PREC": "fp16",
+                          "PROMPT_DEPTH_VISION": 9, "PROMPT_DEPTH_TEXT": 9, "TEXT_LOSS_WEIGHT": 25,
+                          "IMAGE_LOSS_WEIGHT": 10, "LOGITS_LOSS_WEIGHT": 1.0, "GPA_MEAN": 15, "GPA_STD": 1,
+                          "USE_GPA": True, "LABEL_SCOPE": "default", "LOSS_TYPE": "ce", "SIMCLR_ALPHA": 0.0},
+            # PromptSRC/train.py:144-159. USE_KD defaults off here: its teacher is a pretrained
+            # timm download (independentVL.py:360-365), which this path cannot fetch.
+            "IVLP": {"N_CTX_VISION": 2, "N_CTX_TEXT": 2, "CTX_INIT": "a photo of a", "PREC": "fp16",
+                     "PROMPT_DEPTH_VISION": 9, "PROMPT_DEPTH_TEXT": 9, "USE_FOCAL_LOSS": False,
+                     "SIMCLR_ALPHA": 0.0, "USE_MIXUP": True, "MIXUP_ALPHA": 1.0, "USE_KD": False,
+                     "KD_TEACHER_MODEL": "resnet50", "KD_ALPHA": 1.0, "KD_T": 4.0},
         },
         # MI355X-native knobs (not in the reference): prompt truncation to the EOT and the
         # max rows per text-encoder launch chunk (memory bound for large B*C).

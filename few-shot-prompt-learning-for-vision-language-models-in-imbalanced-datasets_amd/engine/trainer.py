@@ -35,7 +35,7 @@ from . import checkpoint as ckpt
 from .metrics import Classification
 
 
-def load_clip(cfg, prec, device, text_grad=True):
+def load_clip(cfg, prec, device, text_grad=True, vision_grad=False):
     """Replacement for load_clip_to_cpu (coop.py:165-184): the CLIP weights file at
     MODEL.WEIGHTS_PATH (OpenAI TorchScript archive, torch.save state dict, .npz or
     .safetensors; clip/weights.py), otherwise the seeded synthetic CLIP of
@@ -43,7 +43,7 @@ def load_clip(cfg, prec, device, text_grad=True):
     weights (forward-only text encoder, e.g. zero-shot)."""
     path = cfg.MODEL.get("WEIGHTS_PATH", "")
     sd = load_state_dict(path) if path else synth.make_state_dict(cfg.MODEL.BACKBONE.NAME, seed=0)
-    return build_model(sd, prec=prec, device=device, text_grad=text_grad)
+    return build_model(sd, prec=prec, device=device, text_grad=text_grad, vision_grad=vision_grad)
 
 
 class TrainerX:

@@ -264,3 +264,28 @@ def cast(x, dtype):
     y = torch.empty(x.shape, device=x.device, dtype=dtype)
     N.call("clipk_cast", DT[dtype], x.numel(), _p(x.contiguous()), _p(y), _stream())
     return y
+
+
+def rows_inject(src, rows, dst, n_per):
+    """dst[rows[p*n_per + i]] = src[p] (deep prompts: the rows a layer's learnable tokens
+    replace, model.py:229-256); src fp32 [n_ctx, W], dst [*, W] any dtype, in place."""
+    _need(src, "prompt rows", torch.float32)
+    _need(rows, "row table", torch.int32)
+    _need(dst, "destination")
+    n_ctx, W = src.shape
+    N.call("clipk_rows_inject", DT[dst.dtype], n_ctx, n_per, W, _p(src), _p(rows), _p(dst), dst.shape[-1], _stream())
+    return dst
+
+
+def rows_collect(src, rows, n_ctx, n_per, out=None, zero_src=True, src2=None):
+    """out[p] = sum_i src[rows[p*n_per + i]] (fixed order); those rows of src (and src2) zeroed."""
+    _need(src, "gradient rows")
+    _need(rows, "row table", torch.int32)
+    W = src.shape[-1]
+    acc = out is not None
+    if out is None:
+        out = torch.empty(n_ctx, W, device=src.device, dtype=torch.float32)
+    N.call("clipk_rows_collect", DT[src.dtype], n_ctx, n_per, W, _p(src), W, _p(src2),
+           DT[src2.dtype] if src2 is not None else 0, W if src2 is not None else 0, _p(rows), _p(out), int(acc),
+           int(zero_src), _stream())
+    return out

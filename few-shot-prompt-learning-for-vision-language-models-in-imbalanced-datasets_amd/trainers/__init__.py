@@ -1,2 +1,3 @@
-"""CoOp / CoCoOp / ZeroshotCLIP trainers (registered in fsp_amd.engine.TRAINER_REGISTRY)."""
-from . import coop, cocoop, zsclip  # noqa: F401
+"""CoOp / CoCoOp / ZeroshotCLIP / IVLP / MaPLe / PromptSRC trainers (registered in
+fsp_amd.engine.TRAINER_REGISTRY)."""
+from . import coop, cocoop, zsclip, deep  # noqa: F401

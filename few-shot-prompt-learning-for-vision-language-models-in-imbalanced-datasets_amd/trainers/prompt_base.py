@@ -156,19 +156,23 @@ class PromptLayout:
 
 
 def init_prompts(module: nn.Module, classnames, clip_model, n_ctx, ctx_init, position, csc,
-                 truncate: bool, shared_prefix: bool = True, class_range=None):
+                 truncate: bool, shared_prefix: bool = True, class_range=None, vl_init: bool = False):
     """Common __init__ body; returns (ctx_vectors, prompt_prefix).
 
     class_range (lo, hi): the native layout covers only classes [lo, hi) -- this rank's
     shard under class-sharded text encoding (CoOp); the checkpointed buffers
-    (token_prefix / token_suffix) and ``n_cls`` still cover every class."""
+    (token_prefix / token_suffix) and ``n_cls`` still cover every class.
+    vl_init: the IVLP / MaPLe / PromptSRC rule (independentVL.py:205-215, maple.py:128-137):
+    CTX_INIT is used only when N_CTX <= 4, and then N_CTX (not the word count) context
+    vectors come from its first tokens while the prompt text keeps all its words."""
     n_cls = len(classnames)
     W = clip_model.arch.transformer_width
     dev = clip_model.positional_embedding.device
     emb_layer = clip_model.token_embedding
-    if ctx_init:
+    if ctx_init and (not vl_init or n_ctx <= 4):
         ctx_init = ctx_init.replace("_", " ")
-        n_ctx = len(ctx_init.split(" "))
+        if not vl_init:
+            n_ctx = len(ctx_init.split(" "))
         prompt = torch.from_numpy(tokenize(ctx_init))
         with torch.no_grad():
             embedding = emb_layer(prompt)

@@ -109,6 +109,24 @@ int clipk_image_resample(int B, int S, int rows_max, const void* src, const long
  * only when the process runs with CLIPK_GEMM_STAMP set (synchronises the device). */
 int clipk_gemm_stamps(void* host, size_t bytes);
 
+/* cls cat + pos add + ln_pre with n_vpt visual prompt rows appended per image (IVLP / MaPLe /
+ * PromptSRC, model.py:413-420, 465-472): x[b*(L+n_vpt) + t] = ln_pre(t < L ? embed(b, t) :
+ * vpt[t-L]) (prompts get no positional embedding). */
+int clipk_vit_embed_ln_vpt(int B, int L, int n_vpt, int width, const float* patch, const float* cls,
+                           const float* pos, const float* vpt, const float* gamma, const float* beta, float* x,
+                           void* stream);
+
+/* Deep prompts (ResidualAttentionBlock_IVLP / _MaPLe.forward, model.py:229-256, 287-331): the
+ * rows a layer's learnable tokens replace. rows[p*n_per + i] = i-th row taking prompt row p.
+ * inject: dst[rows[p*n_per+i]] = (dst dtype) src[p]   (src [n_ctx, width] fp32).
+ * collect: out[p] (+= when accumulate) sum_i src[rows[p*n_per+i]] in a fixed order, then those
+ * rows of src (and of src2, a second copy of the same stream, when given) are zeroed. */
+int clipk_rows_inject(int dst_dtype, int n_ctx, int n_per, int width, const float* src, const int* rows,
+                      void* dst, int ldd, void* stream);
+int clipk_rows_collect(int src_dtype, int n_ctx, int n_per, int width, void* src, int lds, void* src2,
+                       int src2_dtype, int lds2, const int* rows, float* out, int accumulate, int zero_src,
+                       void* stream);
+
 /* y = LN(x[row]) for rows r in [0,rows): x row = in_rows ? in_rows[r] : r.
  * out of out_dtype with row stride ldo; mean/rstd (optional, fp32 [rows]). width%64==0, <=1024 */
 int clipk_layernorm_fwd(int out_dtype, int rows, int width, const float* x, int ldx,
@@ -145,8 +163,9 @@ int clipk_layernorm_bwd_x2(int x_dtype, int dy_dtype, int rows, int width, const
 int clipk_attention_fwd(int dtype, int nseq, int L, int heads, int causal,
                         const void* qkv, int ldqkv, void* out, int ldo, float* lse, void* stream);
 
-/* Input-grad backward of the attention core (L <= 64): dqkv (grad_dtype) from qkv and the
- * saved forward output ofwd (dtype), dout (grad_dtype) and lse. */
+/* Input-grad backward of the attention core, any L (L <= 16: one MFMA tile; longer: two MFMA
+ * passes, dK/dV per key tile and dQ per query tile; VALU for fp32): dqkv (grad_dtype) from qkv
+ * and the saved forward output ofwd (dtype), dout (grad_dtype) and lse. */
 int clipk_attention_bwd(int dtype, int grad_dtype, int nseq, int L, int heads, int causal,
                         const void* qkv, int ldqkv, const void* ofwd, int ldof, const void* dout,
                         int lddo, const float* lse, void* dqkv, int lddqkv, void* stream);
@@ -258,6 +277,33 @@ int clipk_encoder_create(int width, int layers, int heads, int embed, int act_dt
                          int grad_dtype, const void* const* layer_ptrs, const void* const* head_ptrs,
                          clipk_encoder** out);
 void clipk_encoder_destroy(clipk_encoder* enc);
+
+/* Deep prompts of an encoder (IVLP / MaPLe / PromptSRC, model.py:191-331): before layer l in
+ * 1..n_deep the rows `rows` ([n_ctx][n_per], see clipk_rows_inject) of the residual stream
+ * are replaced by prompts[l-1] ([n_deep][n_ctx][width] fp32, values as given: the trainers
+ * round them through fp16 as the reference's .half() does); the backward writes the prompts'
+ * gradients into grads[l-1] (when grads != NULL) and stops them there. Text: rows 1..n_ctx of
+ * every sequence (packed layout: of every group); ViT: the last n_vpt rows of every image.
+ * The pointers must stay valid for the calls that follow; n_deep = 0 clears. */
+int clipk_encoder_set_deep_prompts(clipk_encoder* e, int n_deep, int n_ctx, int n_per, const int* rows,
+                                   const float* prompts, float* grads);
+
+/* ViT with visual prompts, forward with saved activations and input-grad backward (the
+ * prompted VisionTransformer of IVLP / PromptSRC, model.py:401-431, and MaPLe, 434-485):
+ * n_vpt prompt rows (vpt [n_vpt, width] fp32) appended after the image tokens before ln_pre,
+ * deep prompts per clipk_encoder_set_deep_prompts, feat [B, E] fp32 from ln_post(CLS) @ proj.
+ * saved == NULL: inference. The backward needs the encoder created with its transposed
+ * layer weights (layer_ptrs 12..15) and proj_bwd = proj [width, E] in the grad dtype; it
+ * writes d vpt [n_vpt, width] fp32 (summed over the images) and the deep prompts' gradients.
+ * One workspace (clipk_vit_prompted_ws_bytes) serves both calls. */
+size_t clipk_vit_prompted_saved_bytes(const clipk_encoder* e, int B, int n_vpt);
+size_t clipk_vit_prompted_ws_bytes(const clipk_encoder* e, int B, int n_vpt);
+int clipk_vit_forward_prompted(const clipk_encoder* e, int B, const float* img, int n_vpt, const float* vpt,
+                               float* feat, void* saved, size_t saved_bytes, void* ws, size_t ws_bytes,
+                               void* stream);
+int clipk_vit_backward_prompted(const clipk_encoder* e, int B, int n_vpt, const float* vpt, const void* proj_bwd,
+                                const float* dfeat, const void* saved, size_t saved_bytes, float* dvpt, void* ws,
+                                size_t ws_bytes, void* stream);
 
 /* Text encoder forward over nseq sequences of length L (x0 fp32 [nseq*L, W], positional
  * embedding already added). eot_rows[s] = s*L + EOT position of sequence s (int32, device).

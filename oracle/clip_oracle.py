@@ -100,6 +100,109 @@ def encode_text(p: dict, prompts: T, tokenized: T) -> T:
     return x[torch.arange(N), eot] @ p["text_projection"]
 
 
+# ---------------------------------------------------------------- deep prompts (§8 f4)
+def half_round(x: T) -> T:
+    """The reference's ``.half()`` on prompt tokens before they join an fp32 stream
+    (model.py:238, 249, 306, 323, 414, 466): values rounded to fp16, and -- applied after the
+    per-sequence expand, as there -- each sequence's gradient contribution rounded to fp16
+    before the fp32 sum over sequences."""
+    return x.half().float()
+
+
+def encode_image_prompted(p: dict, image: T, vpt, deep_vpt=()) -> T:
+    """Prompted VisionTransformer.forward (IVLP / PromptSRC: model.py:401-431 with
+    ResidualAttentionBlock_IVLP 229-256; MaPLe: VisionTransformer_MaPLe 454-485 with
+    ResidualAttentionBlock_MaPLe 287-331 -- the same math). vpt [n_vpt, D] appended after the
+    positional embedding (no pos for prompts) and before ln_pre; deep_vpt[l-1] replaces the last
+    n_vpt tokens before layer l = 1..len(deep_vpt). vpt None: the plain ViT."""
+    w = p["visual.conv1.weight"]
+    D, _, ps, _ = w.shape
+    x = F.conv2d(image, w, stride=ps)
+    B = x.shape[0]
+    x = x.reshape(B, D, -1).permute(0, 2, 1)
+    cls = p["visual.class_embedding"].expand(B, 1, D)
+    x = torch.cat([cls, x], dim=1) + p["visual.positional_embedding"]
+    if vpt is not None:
+        x = torch.cat([x, half_round(vpt.expand(B, -1, -1))], dim=1)  # model.py:413-415
+    x = layer_norm(x, p["visual.ln_pre.weight"], p["visual.ln_pre.bias"])
+    heads = D // 64
+    for i in range(_layers(p, "visual.transformer.resblocks")):
+        if 1 <= i <= len(deep_vpt):  # model.py:234-241
+            n = deep_vpt[i - 1].shape[0]
+            x = torch.cat([x[:, : x.shape[1] - n], half_round(deep_vpt[i - 1].expand(B, -1, -1))], dim=1)
+        x = residual_block(x, p, f"visual.transformer.resblocks.{i}.", heads, causal=False)
+    x = layer_norm(x[:, 0, :], p["visual.ln_post.weight"], p["visual.ln_post.bias"])
+    return x @ p["visual.proj"]
+
+
+def encode_text_deep(p: dict, prompts: T, tokenized: T, deep_ctx=()) -> T:
+    """TextEncoder.forward with deep text prompts (IVLP / PromptSRC: model.py:242-252;
+    MaPLe: 313-328): deep_ctx[l-1] [n_ctx, W] replaces tokens 1..n_ctx before layer l."""
+    N, L, W = prompts.shape
+    x = prompts + p["positional_embedding"][:L]
+    heads = W // 64
+    for i in range(_layers(p, "transformer.resblocks")):
+        if 1 <= i <= len(deep_ctx):
+            n = deep_ctx[i - 1].shape[0]
+            x = torch.cat([x[:, :1], half_round(deep_ctx[i - 1].expand(N, -1, -1)), x[:, 1 + n:]], dim=1)
+        x = residual_block(x, p, f"transformer.resblocks.{i}.", heads, causal=True)
+    x = layer_norm(x, p["ln_final.weight"], p["ln_final.bias"])
+    eot = tokenized.argmax(dim=-1)
+    return x[torch.arange(N), eot] @ p["text_projection"]
+
+
+def ivlp_logits(p, image, ctx, prefix, suffix, tokenized, vpt, deep_ctx=(), deep_vpt=(), L=None):
+    """IVLP / PromptSRC CustomCLIP.forward logits (independentVL.py:315-322,
+    promptsrc.py:183-193): [prefix, ctx, suffix] text prompts with deep text prompts,
+    prompted image features, cosine logits at logit_scale.exp()."""
+    C = prefix.shape[0]
+    prompts = torch.cat([prefix, ctx.unsqueeze(0).expand(C, -1, -1), suffix], dim=1)
+    if L is not None:
+        prompts = prompts[:, :L]
+    txt = normalize(encode_text_deep(p, prompts, tokenized, deep_ctx))
+    img = normalize(encode_image_prompted(p, image, vpt, deep_vpt))
+    return p["logit_scale"].exp() * img @ txt.t()
+
+
+def maple_logits(p, mp, image, ctx, compound, prefix, suffix, tokenized, L=None):
+    """MaPLe CustomCLIP.forward (maple.py:240-256): vision prompts = proj(ctx) and
+    proj_i(compound_i) (MultiModalPromptLearner.forward, maple.py:190-204); mp holds
+    proj.{weight,bias} and compound_prompt_projections.{i}.{weight,bias} (the reference's
+    ``proj.half()`` rounds proj's initial weights: pass them rounded)."""
+    C = prefix.shape[0]
+    prompts = torch.cat([prefix, ctx.unsqueeze(0).expand(C, -1, -1), suffix], dim=1)
+    if L is not None:
+        prompts = prompts[:, :L]
+    shared = ctx @ mp["proj.weight"].t() + mp["proj.bias"]
+    deep_v = [c @ mp[f"compound_prompt_projections.{i}.weight"].t() + mp[f"compound_prompt_projections.{i}.bias"]
+              for i, c in enumerate(compound)]
+    txt = normalize(encode_text_deep(p, prompts, tokenized, list(compound)))
+    img = normalize(encode_image_prompted(p, image, shared, deep_v))
+    return p["logit_scale"].exp() * img @ txt.t()
+
+
+def promptsrc_loss(logits, label, txt_n, fixed_txt_n, img_n, zs_img_n, zs_logits, text_w=25.0, image_w=10.0,
+                   logits_w=1.0):
+    """PromptSRC.forward_backward loss (promptsrc.py:296-323): CE + L1(text features, frozen
+    CLIP text features) * TEXT_LOSS_WEIGHT + L1(image features, frozen CLIP image features) *
+    IMAGE_LOSS_WEIGHT + KL(log_softmax(logits) || log_softmax(zero-shot logits)) summed / numel
+    * LOGITS_LOSS_WEIGHT. All feature arguments L2-normalised."""
+    ce = F.cross_entropy(logits, label)
+    l_text = F.l1_loss(txt_n, fixed_txt_n, reduction="mean") * text_w
+    l_img = F.l1_loss(img_n, zs_img_n, reduction="mean") * image_w
+    l_logits = F.kl_div(F.log_softmax(logits, dim=1), F.log_softmax(zs_logits, dim=1), reduction="sum",
+                        log_target=True) / logits.numel() * logits_w
+    return ce + l_logits + l_text + l_img
+
+
+def gpa_weights(max_epoch: int, mean: float, std: float):
+    """PromptSRC's Gaussian prompt aggregation weights (promptsrc.py:272-276, 380-382)."""
+    g = [(1 / (std * math.sqrt(2 * math.pi))) * math.exp(-0.5 * ((a - mean) / std) ** 2)
+         for a in range(1, max_epoch + 1)]
+    tot = sum(g)
+    return [x / tot for x in g]
+
+
 # ---------------------------------------------------------------- prompt learners
 def token_embed(p: dict, tokenized: T) -> T:
     return p["token_embedding.weight"][tokenized]

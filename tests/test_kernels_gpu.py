@@ -186,18 +186,48 @@ def test_attention_fwd(dev, dtype, nseq, L, H, causal):
 
 
 @pytest.mark.parametrize("dtype,gdtype", [(torch.float16, torch.bfloat16), (torch.float16, torch.float16),
-                                         (torch.float32, torch.float32)])
-@pytest.mark.parametrize("nseq,L,H", [(6, 11, 8), (3, 23, 2), (2, 64, 2), (4, 5, 2)])
-def test_attention_bwd(dev, dtype, gdtype, nseq, L, H):
+                                         (torch.bfloat16, torch.bfloat16), (torch.float32, torch.float32)])
+@pytest.mark.parametrize("nseq,L,H,causal", [(6, 11, 8, 1), (3, 23, 2, 1), (2, 64, 2, 1), (4, 5, 2, 1),
+                                             (2, 77, 8, 1), (3, 50, 4, 0), (2, 100, 2, 1), (2, 201, 12, 0),
+                                             (1, 257, 2, 0), (2, 33, 2, 0)])
+def test_attention_bwd(dev, dtype, gdtype, nseq, L, H, causal):
+    """L <= 16: one MFMA tile; longer (text L_eff 17..77, the prompted ViT's 50..600 rows):
+    the two-pass kernels (MFMA for 16-bit, VALU for fp32)."""
     g = torch.Generator().manual_seed(L + 100 * H)
     qkv = torch.randn(nseq * L, 3 * H * 64, generator=g).to(dev).to(dtype)
-    o, lse = ops.attention(qkv, nseq, L, H, 1, lse=True)
+    o, lse = ops.attention(qkv, nseq, L, H, causal, lse=True)
     do = torch.randn(nseq * L, H * 64, generator=g).to(dev).to(gdtype)
-    dqkv = ops.attention_bwd(qkv, o, do, lse, nseq, L, H, 1, gdtype)
+    dqkv = ops.attention_bwd(qkv, o, do, lse, nseq, L, H, causal, gdtype)
     qr = qkv.float().clone().requires_grad_(True)
-    ro, _ = attn_ref(qr, nseq, L, H, 1)
+    ro, _ = attn_ref(qr, nseq, L, H, causal)
     ro.backward(do.float())
     close(dqkv, qr.grad, gdtype if dtype != torch.float32 else dtype, "attn bwd")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+def test_rows_inject_collect(dev, dtype):
+    """Deep-prompt row replacement and its gradient (sum over the sequences sharing a prompt
+    row, replaced rows zeroed)."""
+    g = torch.Generator().manual_seed(5)
+    n_ctx, n_per, W, rows_total = 3, 5, 256, 40
+    rows = torch.randperm(rows_total, generator=g)[: n_ctx * n_per].to(torch.int32)
+    src = torch.randn(n_ctx, W, generator=g)
+    dst = torch.randn(rows_total, W, generator=g).to(dtype)
+    ref = dst.clone()
+    for p in range(n_ctx):
+        for i in range(n_per):
+            ref[rows[p * n_per + i]] = src[p].to(dtype)
+    out = ops.rows_inject(src.to(dev), rows.to(dev), dst.to(dev), n_per)
+    assert torch.equal(out.cpu(), ref)
+    grad = torch.randn(rows_total, W, generator=g).to(dtype)
+    want = torch.stack([sum(grad[rows[p * n_per + i]].float() for i in range(n_per)) for p in range(n_ctx)])
+    gd = grad.to(dev)
+    twin = grad.float().to(dev)
+    got = ops.rows_collect(gd, rows.to(dev), n_ctx, n_per, src2=twin)
+    torch.testing.assert_close(got.cpu(), want, rtol=1e-6, atol=1e-5)
+    zeroed = grad.clone()
+    zeroed[rows.long()] = 0
+    assert torch.equal(gd.cpu(), zeroed) and torch.equal(twin.cpu(), zeroed.float())
 
 
 @pytest.mark.parametrize("patch,res", [(16, 32), (32, 64), (14, 28)])
