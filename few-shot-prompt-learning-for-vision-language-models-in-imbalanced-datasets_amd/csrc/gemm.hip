@@ -79,10 +79,35 @@ template <> struct Raw<8> { uint2 v; };
 template <> struct Raw<16> { uint4 v; };
 template <> struct Raw<32> { uint4 v[2]; };
 
+// Cache policy of the epilogue's streaming traffic (build-time A/B knobs, tools/ab_bench.sh):
+// CLIPK_GEMM_SPOL = the output stores' cache-policy bits, CLIPK_GEMM_XNT = non-temporal
+// residual / aux loads. Headline step (profiles/r02k_ab_cache_policy.txt): plain 12.70 ms;
+// nt stores (2) 12.43 -- every GEMM 4-9 % faster, their consumers (LayerNorm, attention) a
+// little slower; sc1 stores (16, the line leaves the XCD's L2) 12.72; nt stores + nt aux /
+// residual loads 12.37-12.43 (dgelu 1.61 -> 1.55 ms/step): the default.
+#ifndef CLIPK_GEMM_SPOL
+#define CLIPK_GEMM_SPOL 2
+#endif
+#ifndef CLIPK_GEMM_XNT
+#define CLIPK_GEMM_XNT 1
+#endif
 template <int NB> __device__ __forceinline__ void ld_raw(const void* p, Raw<NB>& r) {
+#if CLIPK_GEMM_XNT
+  typedef unsigned int nt2 __attribute__((ext_vector_type(2)));
+  typedef unsigned int nt4 __attribute__((ext_vector_type(4)));
+  if constexpr (NB == 8) {
+    r.v = __builtin_bit_cast(uint2, __builtin_nontemporal_load(reinterpret_cast<const nt2*>(p)));
+  } else if constexpr (NB == 16) {
+    r.v = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const nt4*>(p)));
+  } else {
+    r.v[0] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const nt4*>(p)));
+    r.v[1] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const nt4*>(p) + 1));
+  }
+#else
   if constexpr (NB == 8) r.v = *reinterpret_cast<const uint2*>(p);
   else if constexpr (NB == 16) r.v = *reinterpret_cast<const uint4*>(p);
   else { r.v[0] = reinterpret_cast<const uint4*>(p)[0]; r.v[1] = reinterpret_cast<const uint4*>(p)[1]; }
+#endif
 }
 template <typename TX, int CW, int NB>
 __device__ __forceinline__ void raw_f32(const Raw<NB>& r, float* o) {
@@ -119,7 +144,7 @@ __device__ __forceinline__ void buf_store16(__amdgpu_buffer_rsrc_t r, int off, c
     for (int c = 0; c < 8; ++c) h[c] = (TO)v[c];
     d = __builtin_bit_cast(u32x4, h);
   }
-  __builtin_amdgcn_raw_buffer_store_b128(d, r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(d, r, off, 0, CLIPK_GEMM_SPOL);
 }
 
 // Start skew (knob CLIPK_GEMM_SKEW, ~us): every other CU of each XCD starts late, so that the
