@@ -3,6 +3,10 @@
 #pragma once
 #include "common.h"
 
+#ifndef CLIPK_ATTN_SNT
+#define CLIPK_ATTN_SNT 0
+#endif
+
 namespace clipk {
 
 constexpr float kScale = 0.125f;  // 1/sqrt(64)
@@ -159,8 +163,14 @@ __device__ __forceinline__ void store_tile64(T* rowp, const f32x4 (&o)[4], float
     }
   if (ok) {
     const int g4 = (threadIdx.x & 63) >> 4;
+#if CLIPK_ATTN_SNT  // build-time A/B knob: non-temporal output stores
+    __builtin_nontemporal_store((u32x4){d[0][0], d[0][1], d[1][0], d[1][1]}, reinterpret_cast<u32x4*>(rowp + 8 * g4));
+    __builtin_nontemporal_store((u32x4){d[2][0], d[2][1], d[3][0], d[3][1]},
+                                reinterpret_cast<u32x4*>(rowp + 32 + 8 * g4));
+#else
     *reinterpret_cast<u32x4*>(rowp + 8 * g4) = (u32x4){d[0][0], d[0][1], d[1][0], d[1][1]};
     *reinterpret_cast<u32x4*>(rowp + 32 + 8 * g4) = (u32x4){d[2][0], d[2][1], d[3][0], d[3][1]};
+#endif
   }
 }
 

@@ -16,12 +16,25 @@ constexpr int LN_MAXV = 4;  // 4-element vectors per lane -> width <= 1024
 
 // VW consecutive elements per lane per chunk: 8 (16-B loads of 16-bit rows, 2x16-B of fp32)
 // when width is a multiple of 512, else 4; NC chunks cover width <= 1024.
+// Cache policy knobs (build-time A/B, tools/ab_bench.sh): CLIPK_LN_NT bit 0 = non-temporal
+// row loads, bit 1 = non-temporal stores (16-bit rows).
+#ifndef CLIPK_LN_NT
+#define CLIPK_LN_NT 0
+#endif
 template <typename T, int VW>
 __device__ __forceinline__ void ldv(const T* p, float* o) {
   if constexpr (VW == 4) {
     load4<T>(p, o);
   } else if constexpr (sizeof(T) == 2) {
+#if CLIPK_LN_NT & 1
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    const t8 v = __builtin_bit_cast(t8, __builtin_nontemporal_load(reinterpret_cast<const u4*>(p)));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (float)v[i];
+#else
     load16_f32<T>(p, o);
+#endif
   } else {
     load16_f32<T>(p, o);
     load16_f32<T>(p + 4, o + 4);
@@ -32,7 +45,16 @@ __device__ __forceinline__ void stv(T* p, const float* v) {
   if constexpr (VW == 4) {
     store4<T>(p, v[0], v[1], v[2], v[3]);
   } else if constexpr (sizeof(T) == 2) {
+#if CLIPK_LN_NT & 2
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    t8 h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = (T)v[i];
+    __builtin_nontemporal_store(__builtin_bit_cast(u4, h), reinterpret_cast<u4*>(p));
+#else
     store16_f32<T>(p, v);
+#endif
   } else {
     store16_f32<T>(p, v);
     store16_f32<T>(p + 4, v + 4);

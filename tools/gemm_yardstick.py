@@ -43,7 +43,21 @@ def timeit(fn, iters=12, warm=3, rounds=3):
     return best
 
 
+VIT = [  # ViT-B/16 layer GEMMs (D = 768) at B = 8 images x 197 tokens
+    ("vit qkv  N2304 K768  BIAS", 2304, 768, "bias"),
+    ("vit out  N768  K768  BIAS_RES", 768, 768, "res"),
+    ("vit fc   N3072 K768  BIAS", 3072, 768, "bias"),
+    ("vit proj N768  K3072 BIAS_RES", 768, 3072, "res"),
+]
+
+
 def main():
+    global SHAPES
+    if "--vit" in sys.argv:
+        sys.argv.remove("--vit")
+        SHAPES = VIT
+        if len(sys.argv) == 1:
+            sys.argv.append("1576")
     M = int(sys.argv[1]) if len(sys.argv) > 1 else 47160
     dev = torch.device("cuda")
     f16 = torch.float16
