@@ -91,6 +91,27 @@ template <> struct Raw<32> { uint4 v[2]; };
 #ifndef CLIPK_GEMM_XNT
 #define CLIPK_GEMM_XNT 1
 #endif
+// CLIPK_GEMM_PP: 192x256 / 256x256 launches with >= 2 K tiles run the ping-pong main loop
+// (1, persistent; 2 = one tile per block, A/B; 0 = the 2-slot loop). Same-box A/B
+// (profiles/r02m_ab_pingpong.txt): headline step 12.60 -> 12.13 ms, input-grad GEMMs
+// 2.65 -> 2.27 ms/step; staging by global_load_lds with per-lane 64-bit addresses instead of
+// buffer LDS-DMA measured 12.80 ms (the address arithmetic sits in the memory segments).
+#ifndef CLIPK_GEMM_PP
+#define CLIPK_GEMM_PP 1
+#endif
+// CLIPK_GEMM_RING (A/B): 192x256 launches as non-persistent 4-slot rings of 64-B K steps.
+#ifndef CLIPK_GEMM_RING
+#define CLIPK_GEMM_RING 0
+#endif
+// Diagnostic builds only (wrong results; tools/gemm_diag.sh): NOLOAD = stage no K step past
+// the first (the loop's compute + LDS + barrier ceiling), NOBAR = no barrier / vmcnt wait per
+// K step either.
+#ifndef CLIPK_GEMM_NOLOAD
+#define CLIPK_GEMM_NOLOAD 0
+#endif
+#ifndef CLIPK_GEMM_NOBAR
+#define CLIPK_GEMM_NOBAR 0
+#endif
 template <int NB> __device__ __forceinline__ void ld_raw(const void* p, Raw<NB>& r) {
 #if CLIPK_GEMM_XNT
   typedef unsigned int nt2 __attribute__((ext_vector_type(2)));
@@ -175,20 +196,40 @@ __device__ __forceinline__ void skew_start(int us, int bid) {
 // its A chunks of the next stage into registers at the top of a K step (where the glds would
 // have been issued), and after the step's MFMAs writes quickgelu(h) to the same lane-linear
 // LDS slots the glds would have filled.
+// PP (ping-pong, non-persistent 8-wave 2x4 tiles of BN = 256, 16-bit): each 64-deep K tile
+// runs as 4 phases, one output quadrant each -- (A half 0, B half 0), (A0, B1), (A1, B1),
+// (A1, B0), where A half h = rows h*BM/4.. of each wave row's BM/2 and B half q = columns
+// q*32.. of each wave column's 64 -- and every phase is a memory segment (this phase's
+// fragment reads + one region's glds restage, lgkmcnt(0)) and an MFMA segment, each ended by a
+// raw barrier. Wave row 1 starts one barrier late, so on every SIMD one wave's MFMAs overlap
+// the other's LDS reads. A region is restaged (for K tile t+2, or t+1 for B0) one phase after
+// its last read; the K tile t+1 wait is a counted vmcnt at phase 4 of tile t that leaves the
+// three regions already issued for t+2 in flight -- the ring never drains in the loop.
 template <typename T, typename TO, typename TX, int EPI, int BM, int BN, int WM, int WN, bool PERSIST,
-          int ROWB = GEMM_ROWB, int DEPTH = 2, bool AG = false>
+          int ROWB = GEMM_ROWB, int DEPTH = 2, bool AG = false, bool PP = false>
 __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
   static_assert(DEPTH == 2 || !PERSIST, "deep ring: non-persistent launches only");
   static_assert(!AG || (!PERSIST && DEPTH == 2 && sizeof(T) == 2 && ROWB == 128), "A-operand QuickGELU path");
+  static_assert(!PP || (PERSIST && !AG && DEPTH == 2 && ROWB == 128 && WM == 2 && WN == 4 && BN == 256 &&
+                        sizeof(T) == 2 && BM % 64 == 0), "ping-pong main loop (K >= 128)");
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int OPA = BM * ROWB, OPB = BN * ROWB, STAGE = OPA + OPB;
   constexpr int RPI = 1024 / ROWB;   // rows per glds wave-instruction (64 lanes x 16 B)
   constexpr int CPR = ROWB / 16;     // 16-B chunks per staged row
   constexpr int KK = ROWB / 64;      // 64-B MFMA k-windows per K step
-  constexpr int IA = BM / RPI / NW, IB = BN / RPI / NW;  // glds per wave per stage
+  // A stage is NG glds units of RPI rows (1 KiB each, A's GA units then B's), unit g landing
+  // at stage offset g * 1024. BLOCKED (every wave the same number of A and of B units): wave w
+  // issues A units w*IA.. and B units GA + w*IB..; otherwise units are dealt round-robin
+  // (g = w + NW*i) and the first NREM waves issue one more than the others.
+  constexpr int GA = BM / RPI, GB = BN / RPI, NG = GA + GB;
+  constexpr bool BLOCKED = GA % NW == 0 && GB % NW == 0;
+  constexpr int IA = BLOCKED ? GA / NW : 0, IB = BLOCKED ? GB / NW : 0;
+  constexpr int NI = (NG + NW - 1) / NW;  // glds slots per wave (the last may be idle)
+  constexpr int PERL = NG / NW, NREM = NG % NW;
   static_assert(ROWB == 128 || (ROWB == 64 && sizeof(T) == 2), "staged row is 128 B (or 64 B for 16-bit)");
-  static_assert(IA >= 1 && IB >= 1 && BM % (RPI * NW) == 0 && BN % (RPI * NW) == 0, "tile/wave mismatch");
+  static_assert(BM % RPI == 0 && BN % RPI == 0 && NG >= NW, "tile/wave mismatch");
+  static_assert(!AG || BLOCKED, "A-operand QuickGELU path: blocked unit split");
   __shared__ CLIPK_LDS_ALIGN char smem[DEPTH * STAGE + NW * EPI_SCRATCH];  // one array (see header)
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -221,38 +262,42 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
   // c ^ ((r >> 2) & 3) -- either way 16 consecutive rows read at one chunk hit 16 distinct
   // 16-B slots of the 256-B bank row
   auto swz = [](int r) { return ROWB == 128 ? (r >> 1) & 7 : (r >> 2) & 3; };
-  const char* srcA[IA];
-  const char* srcB[IB];
+  auto unit = [&](int i) { return BLOCKED ? (i < IA ? w * IA + i : GA + w * IB + (i - IA)) : w + NW * i; };
+  const char* src[NI];
   auto set_tile = [&](int t) {
     const int tm0 = (t / ntn) * BM, tn0 = (t % ntn) * BN;
 #pragma unroll
-    for (int i = 0; i < IA; ++i) {
-      const int row = (w * IA + i) * RPI + lane / CPR;
+    for (int i = 0; i < NI; ++i) {
+      const int u = unit(i);
+      const bool ua = BLOCKED ? i < IA : u < GA;
+      const int row = (ua ? u : u - GA) * RPI + lane / CPR;
       const int c = (lane % CPR) ^ swz(row);  // source-side swizzle
-      int ga = tm0 + row;
-      ga = ga < g.M ? ga : g.M - 1;
-      srcA[i] = g.A + ((size_t)ga * g.lda) * esz + c * 16 + (size_t)kt0 * ROWB;
-    }
-#pragma unroll
-    for (int i = 0; i < IB; ++i) {
-      const int row = (w * IB + i) * RPI + lane / CPR;
-      const int c = (lane % CPR) ^ swz(row);
-      srcB[i] = g.B + ((size_t)(tn0 + row) * g.ldb) * esz + c * 16 + (size_t)kt0 * ROWB;
+      if (ua) {
+        int ga = tm0 + row;
+        ga = ga < g.M ? ga : g.M - 1;
+        src[i] = g.A + ((size_t)ga * g.lda) * esz + c * 16 + (size_t)kt0 * ROWB;
+      } else {
+        const int gb = u < NG ? tn0 + row : tn0;  // idle slot: a valid address, never issued
+        src[i] = g.B + ((size_t)gb * g.ldb) * esz + c * 16 + (size_t)kt0 * ROWB;
+      }
     }
   };
   u32x4 ra[AG ? IA : 1];  // AG: the next stage's A chunks in flight
   auto stage = [&](int s, int kt) {
+    if (CLIPK_GEMM_NOLOAD && kt > 0) return;
     char* base = smem + s * STAGE;
     const size_t koff = (size_t)kt * ROWB;
-    if constexpr (AG) {
 #pragma unroll
-      for (int i = 0; i < IA; ++i) ra[i] = *reinterpret_cast<const u32x4*>(srcA[i] + koff);
-    } else {
-#pragma unroll
-      for (int i = 0; i < IA; ++i) glds16(srcA[i] + koff, base + (w * IA + i) * 1024);
+    for (int i = 0; i < NI; ++i) {
+      if constexpr (AG) {
+        if (i < IA) {
+          ra[i] = *reinterpret_cast<const u32x4*>(src[i] + koff);
+          continue;
+        }
+      }
+      const int u = unit(i);
+      if (BLOCKED || NREM == 0 || u < NG) glds16(src[i] + koff, base + u * 1024);
     }
-#pragma unroll
-    for (int i = 0; i < IB; ++i) glds16(srcB[i] + koff, base + OPA + (w * IB + i) * 1024);
   };
   auto write_a = [&](int s) {  // AG: quickgelu of the loaded chunks into stage s
     if constexpr (AG) {
@@ -276,17 +321,27 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
   constexpr bool HAS_EXT = EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU;
 
   set_tile(tile);
-  constexpr int PER = IA + IB;  // glds per wave per stage
   // deep ring: wait until stage kt+1 has landed while `younger` later stages stay in flight
+  // (this wave's glds per stage: PERL, or PERL + 1 for the first NREM waves)
   auto ring_wait = [&](int younger) {
     if constexpr (DEPTH > 2) {
-      if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
-      else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (NREM != 0 && w < NREM) {
+        constexpr int P = PERL + 1;
+        if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * P) : "memory");
+        else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        constexpr int P = PERL;
+        if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * P) : "memory");
+        else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     }
   };
   static_assert(DEPTH <= 4, "ring_wait covers up to two younger stages");
-  if constexpr (DEPTH == 2) {
+  if constexpr (PP) {
+    // prologue inside the tile loop
+  } else if constexpr (DEPTH == 2) {
     stage(0, 0);
     write_a(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -345,6 +400,141 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       }
     };
     if (stp && ti < STAMP_TILES) stp[2 + 3 * ti] = __builtin_amdgcn_s_memrealtime();
+    if constexpr (PP) {
+      constexpr int TM2 = TM / 2, TN2 = TN / 2;
+      constexpr int HA = BM / 32;        // 8-row units of one wave row's A half (BM/4 rows)
+      constexpr int UA = 2 * HA, UB = 16;  // units per A / B region
+      constexpr int NA_HI = UA - NW;     // waves w < NA_HI issue 2 units of an A region, others 1
+      static_assert(UA >= NW && UA <= 2 * NW && UB == 2 * NW, "region split");
+      // region r: 0 = A half 0, 1 = A half 1, 2 = B half 0, 3 = B half 1; unit u = w + NW*i
+      // (wave-uniform first row row0, a multiple of 8). A lane stages row row0 + lrow, 16-B
+      // chunk (lane % 8) ^ swz(row) = lco ^ (row0 & 8 ? 4 : 0) chunks, by buffer LDS-DMA: the
+      // lane's byte offset within its tile is tile-independent (poff) and the tile enters as
+      // the resource base, whose size drops the rows past M (no clamp, no per-load address math).
+      const int lrow = lane / CPR;
+      const int lco = ((lane % CPR) ^ (lrow >> 1)) * 16;
+      const bool two_a = w < NA_HI;
+      auto unit_row0 = [&](int r, int i) {
+        const int u = w + NW * i;
+        if (r < 2) {
+          const int uu = u < UA ? u : 0;
+          return (uu / HA) * (BM / 2) + r * (BM / 4) + (uu % HA) * 8;
+        }
+        return (u / 4) * 64 + (r - 2) * 32 + (u % 4) * 8;
+      };
+      int poff[4][2];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int row0 = unit_row0(r, i);
+          poff[r][i] = (row0 + lrow) * (r < 2 ? g.lda : g.ldb) * (int)esz + (lco ^ ((row0 & 8) << 3));
+        }
+      auto rsrc_a = [&](int tm0) {
+        return tile_rsrc(g.A + (size_t)tm0 * g.lda * esz, (long long)(g.M - tm0) * g.lda * (long long)esz);
+      };
+      auto rsrc_b = [&](int tn0) {
+        return tile_rsrc(g.B + (size_t)tn0 * g.ldb * esz, (long long)BN * g.ldb * (long long)esz);
+      };
+      typedef __amdgpu_buffer_rsrc_t TRes;
+      // stage region r of K tile kt into buffer buf from the tile resources ra / rb
+      auto pst = [&](int buf, __amdgpu_buffer_rsrc_t ra_, __amdgpu_buffer_rsrc_t rb_, int kt, int r) {
+        const int base = buf * STAGE;
+        const int koff = (kt0 + kt) * ROWB;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          if (r >= 2 || i == 0 || two_a) {
+            const int row0 = unit_row0(r, i);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                r < 2 ? ra_ : rb_, (__attribute__((address_space(3))) void*)(smem + base + (r < 2 ? 0 : OPA) + row0 * ROWB),
+                16, poff[r][i], koff, 0, 0);
+          }
+      };
+      // K step s+1 landed; the three regions already issued for s+2 (A0, B1, A1) stay in flight
+      auto wait_ahead = [&]() {
+        if (two_a) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      };
+      u32x4 fa[KK][TM2], fb[KK][TN2];
+      auto rd_a = [&](int buf, int h) {
+        const char* As = smem + buf * STAGE + (wm * (BM / WM) + h * (BM / WM / 2) + fr) * ROWB;
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+          for (int i = 0; i < TM2; ++i)
+            fa[kk][i] = *reinterpret_cast<const u32x4*>(As + i * 16 * ROWB + ((kk * 4 + fq) ^ sw) * 16);
+      };
+      auto rd_b = [&](int buf, int q) {
+        const char* Bs = smem + buf * STAGE + OPA + (wn * (BN / WN) + q * (BN / WN / 2) + fr) * ROWB;
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+          for (int j = 0; j < TN2; ++j)
+            fb[kk][j] = *reinterpret_cast<const u32x4*>(Bs + j * 16 * ROWB + ((kk * 4 + fq) ^ sw) * 16);
+      };
+      auto mm = [&](int h, int q) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+          for (int i = 0; i < TM2; ++i)
+#pragma unroll
+            for (int j = 0; j < TN2; ++j)
+              acc[h * TM2 + i][q * TN2 + j] = mma<T>(fb[kk][j], fa[kk][i], acc[h * TM2 + i][q * TN2 + j]);
+        __builtin_amdgcn_s_setprio(0);
+      };
+      auto seg_end = [&]() {  // memory segment done: fragments in registers, then the barrier
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        G8_BAR();
+      };
+      // The K steps of this block's tiles form one stream (step `it`, buffer it & 1): the
+      // restages for steps s+1 / s+2 reach into the next tile, so its first two K tiles load
+      // during this tile's last phases and epilogue (nk >= 2).
+      const bool lag = wm == 1;
+      const TRes cra = rsrc_a(m0), crb = rsrc_b(n0);
+      if (it == 0) {
+        pst(0, cra, crb, 0, 0); pst(0, cra, crb, 0, 2); pst(0, cra, crb, 0, 1); pst(0, cra, crb, 0, 3);
+        pst(1, cra, crb, 1, 0); pst(1, cra, crb, 1, 3); pst(1, cra, crb, 1, 1);
+        wait_ahead();
+        G8_BAR();
+      }
+      if (lag) G8_BAR();  // wave row 1 runs one segment behind
+      const TRes xra = rsrc_a(has_next ? (next / ntn) * BM : m0);
+      const TRes xrb = rsrc_b(has_next ? (next % ntn) * BN : n0);
+      for (int kt = 0; kt < nk; ++kt, ++it) {
+        const int b = it & 1;
+        const bool in1 = kt + 1 < nk, in2 = kt + 2 < nk;
+        const bool h1 = in1 || has_next, h2 = in2 || has_next;
+        const int k1 = in1 ? kt + 1 : kt + 1 - nk, k2 = in2 ? kt + 2 : kt + 2 - nk;
+        rd_a(b, 0); rd_b(b, 0);                 // phase 1: A0 x B0
+        if (h1) pst(b ^ 1, cra, in1 ? crb : xrb, k1, 2);
+        if (!in1) load_ext(0, extq[0]);
+        seg_end();
+        mm(0, 0);
+        G8_BAR();
+        rd_b(b, 1);                             // phase 2: A0 x B1
+        if (h2) pst(b, in2 ? cra : xra, crb, k2, 0);
+        seg_end();
+        mm(0, 1);
+        G8_BAR();
+        rd_a(b, 1);                             // phase 3: A1 x B1
+        if (h2) pst(b, cra, in2 ? crb : xrb, k2, 3);
+        seg_end();
+        mm(1, 1);
+        G8_BAR();
+        rd_b(b, 0);                             // phase 4: A1 x B0
+        if (h2) {
+          pst(b, in2 ? cra : xra, crb, k2, 1);
+          wait_ahead();
+        } else if (h1) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        seg_end();
+        mm(1, 0);
+        G8_BAR();
+      }
+      if (!lag) G8_BAR();  // both wave rows level again: the epilogues run side by side
+    } else
     // group 0's operands are loaded at the top of the last K step (its MFMAs hide them)
     for (int kt = 0; kt < nk; ++kt, ++it) {
       const int cur = DEPTH == 2 ? (it & 1) : it % DEPTH;
@@ -378,8 +568,10 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       if (!last) {
         if constexpr (DEPTH == 2) {
           write_a(cur ^ 1);  // AG: slot cur^1 was last read in step kt-1 (before its barrier)
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __syncthreads();
+          if (!CLIPK_GEMM_NOBAR) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+          }
         } else {
           ring_wait(min(DEPTH - 2, nk - 2 - kt));  // stages kt+2 .. issued after kt+1
           G8_BAR();
@@ -468,10 +660,12 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       break;
     }
     tile = next;
-    // the K loop left `it` one past this tile's last step: buffer it & 1 holds the
-    // next tile's prefetched first stage
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if constexpr (!PP) {
+      // the K loop left `it` one past this tile's last step: buffer it & 1 holds the
+      // next tile's prefetched first stage
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
 }
 
@@ -552,6 +746,28 @@ static int num_cus() {
   return g_num_cus;
 }
 
+// ping-pong launches: one block per CU at most, a multiple of 8 (XCD groups of the tile split)
+[[maybe_unused]] static int pp_grid(int nwg, int cus) {
+  const int full = (cus / 8) * 8;
+  const int need = (nwg + 7) / 8 * 8;
+  if (CLIPK_GEMM_PP == 2) return need;  // one tile per block (A/B)
+  return need < full ? need : full;
+}
+
+// BM x 256 ping-pong launch when built in and the shape has >= 2 K tiles (the 256-row forms
+// with an fp32 residual / aux operand would spill: they keep the 2-slot loop)
+template <typename T, typename TO, typename TX, int EPI, int BM>
+static bool try_pp(const GemmArgs& g, int nwg, hipStream_t st) {
+  constexpr bool ext32 = (EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU) && sizeof(TX) == 4;
+  if constexpr (CLIPK_GEMM_PP && sizeof(T) == 2 && !(BM == 256 && ext32)) {
+    if (g.K * (int)sizeof(T) < 2 * GEMM_ROWB) return false;
+    hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, BM, 256, 2, 4, true, GEMM_ROWB, 2, false, true>),
+                       dim3(pp_grid(nwg, num_cus())), dim3(512), 0, st, g);
+    return true;
+  }
+  return false;
+}
+
 template <typename T, typename TO, typename TX, int EPI>
 static int launch_gemm(const GemmArgs& g, hipStream_t st) {
   const int cfg = pick_cfg(g.M, g.N, (int)sizeof(T));
@@ -568,7 +784,8 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
     if (cfg == 1 || cfg == 3) {
       const int nwg = ((g.M + 255) / 256) * (g.N / 256);
       const int cus = num_cus();
-      if (cfg == 1 && nwg > 2 * cus) {
+      if (try_pp<T, TO, TX, EPI, 256>(g, nwg, st)) {
+      } else if (cfg == 1 && nwg > 2 * cus) {
         // persistent: one 8-wave block per CU, grid a multiple of 8 (XCD groups)
         const int grid = (cus / 8) * 8;
         hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 256, 2, 4, true>), dim3(grid), dim3(512), 0, st, g);
@@ -578,7 +795,10 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
     } else if (cfg == 6) {
       const int nwg = ((g.M + 191) / 192) * (g.N / 256);
       const int cus = num_cus();
-      if (nwg > persist_min(cus))
+      if (try_pp<T, TO, TX, EPI, 192>(g, nwg, st)) {
+      } else if constexpr (CLIPK_GEMM_RING)  // 4-slot ring of 64-B K steps: three steps in flight
+        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 192, 256, 2, 4, false, 64, 4>), dim3(nwg), dim3(512), 0, st, g);
+      else if (nwg > persist_min(cus))
         hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 192, 256, 2, 4, true>), dim3((cus / 8) * 8), dim3(512), 0, st, g);
       else
         hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 192, 256, 2, 4, false>), dim3(nwg), dim3(512), 0, st, g);

@@ -339,6 +339,27 @@ def test_gemm_large_m_every_config(dev, cfg, Nn, K):
         lib.clipk_gemm_set_config(-1)
 
 
+@pytest.mark.parametrize("cfg", [1, 6])
+@pytest.mark.parametrize("K", [64, 128, 192, 320])
+def test_gemm_large_tiles_short_k(dev, cfg, K):
+    """The 256- / 192-row tile main loops at 1-5 K tiles (prologue / drain edge cases)."""
+    lib = N.load()
+    M, Nn = 5000, 512
+    g = torch.Generator(device="cpu").manual_seed(K + cfg)
+    A = torch.randn(M, K, generator=g).to(dev).to(torch.float16)
+    B = (torch.randn(Nn, K, generator=g) / math.sqrt(K)).to(dev).to(torch.float16)
+    bias = torch.randn(Nn, generator=g).to(dev)
+    res = torch.randn(M, Nn, generator=g).to(dev)
+    ref = A.float() @ B.float().t()
+    try:
+        N.check(lib.clipk_gemm_set_config(cfg), "set_config")
+        close(ops.gemm(A, B, N.EPI_NONE, torch.float16), ref, torch.float16, f"cfg{cfg} K{K} none")
+        close(ops.gemm(A, B, N.EPI_BIAS_RES, torch.float32, bias=bias, res=res), ref + bias + res,
+              torch.float16, f"cfg{cfg} K{K} res")
+    finally:
+        lib.clipk_gemm_set_config(-1)
+
+
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("M,Nn,K,splits",[(1576, 768, 3072, 0), (1576, 768, 768, 3), (1576, 2304, 768, 2),
                                            (300, 256, 512, 3)])

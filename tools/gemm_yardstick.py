@@ -58,6 +58,17 @@ def main():
         SHAPES = VIT
         if len(sys.argv) == 1:
             sys.argv.append("1576")
+    hot = "--hot" in sys.argv  # one A buffer: re-read from the Infinity Cache / L2
+    if hot:
+        sys.argv.remove("--hot")
+    ref_on = "--no-ref" not in sys.argv
+    if not ref_on:
+        sys.argv.remove("--no-ref")
+    only = None  # --only <name prefix>: one shape (PMC runs)
+    if "--only" in sys.argv:
+        j = sys.argv.index("--only")
+        only = sys.argv[j + 1]
+        del sys.argv[j:j + 2]
     M = int(sys.argv[1]) if len(sys.argv) > 1 else 47160
     dev = torch.device("cuda")
     f16 = torch.float16
@@ -65,27 +76,39 @@ def main():
     rnd = lambda *s: (torch.randn(*s, device=dev, generator=g) * 0.5).to(f16)
     tot_ours = tot_t = 0.0
     for name, n, k, kind in SHAPES:
-        nbuf = max(2, -(-600_000_000 // (M * k * 2)))
+        if only and not name.startswith(only):
+            continue
+        nbuf = 1 if hot else max(2, -(-600_000_000 // (M * k * 2)))
         As = [rnd(M, k) for _ in range(nbuf)]
         B = rnd(n, k)
         bias = torch.randn(n, device=dev)
-        res = rnd(M, n)
+        vit_res = SHAPES is VIT and kind == "res"  # the ViT's residual stream is fp32
+        res = torch.randn(M, n, device=dev) if vit_res else rnd(M, n)
         aux = rnd(M, n)
-        out = torch.empty(M, n, device=dev, dtype=f16)
+        out = torch.empty(M, n, device=dev, dtype=torch.float32 if vit_res else f16)
         if kind == "none":
             ours = lambda i: ops.gemm(As[i % nbuf], B, N.EPI_NONE, f16, out=out)
         elif kind == "bias":
             ours = lambda i: ops.gemm(As[i % nbuf], B, N.EPI_BIAS, f16, bias=bias, out=out)
         elif kind == "res":
-            ours = lambda i: ops.gemm(As[i % nbuf], B, N.EPI_BIAS_RES, f16, bias=bias, res=res, out=out)
+            ours = lambda i: ops.gemm(As[i % nbuf], B, N.EPI_BIAS_RES, out.dtype, bias=bias, res=res, out=out)
         elif kind == "res_ag":
             ours = lambda i: ops.gemm(As[i % nbuf], B, N.EPI_BIAS_RES | N.A_QGELU, f16, bias=bias, res=res,
                                       out=out)
         else:
             ours = lambda i: ops.gemm(As[i % nbuf], B, N.EPI_DQGELU, f16, aux=aux, out=out)
-        ref = lambda i: torch.matmul(As[i % nbuf], B.t(), out=out)
+        outr = torch.empty(M, n, device=dev, dtype=f16)
+        ref = lambda i: torch.matmul(As[i % nbuf], B.t(), out=outr)
+        if SHAPES is VIT and kind in ("bias", "res"):
+            sk = N.load().clipk_gemm_auto_splits(N.F16, M, n, k)
+            epi = N.EPI_BIAS if kind == "bias" else N.EPI_BIAS_RES
+            for s_ in sorted({1, 2, 3, 4, sk}):
+                ms_s = timeit(lambda i: ops.gemm_splitk(As[i % nbuf], B, epi, out.dtype, bias=bias,
+                                                        res=res if kind == "res" else None, splits=s_))
+                print(f"    split-K {s_}{' (auto)' if s_ == sk else ''}: {ms_s*1e3:7.1f} us "
+                      f"{2.0*M*n*k/ms_s/1e9:7.1f} TF/s", flush=True)
         ms_o = timeit(ours)
-        ms_t = timeit(ref)
+        ms_t = timeit(ref) if ref_on else float("nan")
         fl = 2.0 * M * n * k
         tot_ours += ms_o
         tot_t += ms_t

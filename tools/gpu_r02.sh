@@ -12,4 +12,7 @@ cp gpurun_out/pmc_$TAG/traffic.json gpurun_out/pmc_$TAG/summary.txt profiles/r02
 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > gpurun_out/bench_$TAG.log 2>&1 && \
 cd /tmp && export TMPDIR=/tmp && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o p -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extra --eval-images 0 > $R/gpurun_out/prof_$TAG.log 2>&1
-echo exit $?
+rc=$?
+cd $R
+[ $rc -eq 0 ] && [ -n "$YARD" ] && timeout -k 10 300 python -u tools/gemm_yardstick.py --vit > gpurun_out/yard_vit_$TAG.log 2>&1
+echo exit $rc $?
