@@ -45,9 +45,9 @@ PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc", "traffic.json")
 # kernel-name key, for the PMC traffic lookup) -- the text GEMMs by role, attention, LN
 KERNELS = {
     "gemm_dx_n512": (["text.fc_dx", "text.qkv_dx", "text.out_dx"], "EPI_NONE 192x256", "mfma"),
-    "gemm_proj_fwd": (["text.proj_fwd"], "EPI_BIAS_RES A_QGELU", "mfma"),
+    "gemm_proj_fwd": (["text.proj_fwd"], "EPI_BIAS_RES N=512 K=2048", "mfma"),
     "gemm_dgelu": (["text.proj_dx_dgelu"], "EPI_DQGELU", "mfma"),
-    "gemm_fc_fwd": (["text.fc_fwd"], "EPI_BIAS N=2048", "mfma"),
+    "gemm_fc_fwd": (["text.fc_fwd"], "EPI_BIAS_QGELU N=2048 (h and QuickGELU(h))", "mfma"),
     "gemm_qkv_fwd": (["text.qkv_fwd"], "EPI_BIAS N=1536", "mfma"),
     "gemm_out_fwd": (["text.out_fwd"], "EPI_BIAS_RES N=512", "mfma"),
     "attn_bwd": (["text.attn_bwd"], "attn_prefix_bwd_lds", "hbm"),
@@ -59,7 +59,7 @@ KERNELS = {
 }
 ROOF_PMC_KEY = {"gemm_dx_n512": "gemm_nt_kernelIDF16_DF16_fLi4ELi192ELi256",
                 "gemm_dgelu": "gemm_nt_kernelIDF16_DF16_DF16_Li3E",
-                "gemm_proj_fwd": "gemm_nt_kernelIDF16_DF16_DF16_Li1ELi192ELi256ELi2ELi4ELb0ELi128ELi2ELb1E",
+                "gemm_proj_fwd": "gemm_nt_kernelIDF16_DF16_DF16_Li1ELi192ELi256ELi2ELi4ELb1ELi128ELi2ELb0ELb1E",
                 "attn_bwd": "attn_prefix_bwd_lds"}
 
 

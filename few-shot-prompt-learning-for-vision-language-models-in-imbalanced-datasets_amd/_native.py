@@ -65,6 +65,7 @@ SIGNATURES = {
     "clipk_rows_inject": (_I, [_I, _I, _I, _I, _P, _P, _P, _I, _P]),
     "clipk_rows_collect": (_I, [_I, _I, _I, _I, _P, _I, _P, _I, _I, _P, _P, _I, _I, _P]),
     "clipk_encoder_set_deep_prompts": (_I, [_P, _I, _I, _I, _P, _P, _P]),
+    "clipk_encoder_set_input_rows": (_I, [_P, _I]),
     "clipk_vit_prompted_saved_bytes": (_S, [_P, _I, _I]),
     "clipk_vit_prompted_ws_bytes": (_S, [_P, _I, _I]),
     "clipk_vit_forward_prompted": (_I, [_P, _I, _P, _I, _P, _P, _P, _S, _P, _S, _P]),

@@ -165,6 +165,13 @@ class TextEncoderCore(_Encoder):
                                                         ops._p(deep), ops._p(grads)),
                 "clipk_encoder_set_deep_prompts")
 
+    def _input_rows(self, lib, shape):
+        """clipk_encoder_set_input_rows for this call: 1 when the packed layout's class rows are
+        the same in every group and only its prefix rows need an input gradient
+        (TextShape.prefix_input); forward and backward of one call see the same mode."""
+        N.check(lib.clipk_encoder_set_input_rows(self.handle, int(bool(getattr(shape, "prefix_input", False)))),
+                "clipk_encoder_set_input_rows")
+
     def forward(self, x0, shape, save):
         """x0 fp32 [shape.rows, W] -> txt fp32 [shape.nout, E] (+ saved arena if save)."""
         lib = N.load()
@@ -181,6 +188,7 @@ class TextEncoderCore(_Encoder):
         saved = torch.empty(sb, dtype=torch.uint8, device=x0.device) if save else None
         tail = (ops._p(x0), ops._p(shape.eot_rows), ops._p(txt), ops._p(saved), sb, ops._p(ws), ws.numel(),
                 ops._stream())
+        self._input_rows(lib, shape)
         if shape.packed:
             N.check(lib.clipk_text_forward_packed(h, shape.G, shape.C, shape.P, shape.R, shape.ntiles,
                                                   ops._p(shape.tiles), ops._p(shape.row_first), *tail),
@@ -200,6 +208,7 @@ class TextEncoderCore(_Encoder):
         ws = WORKSPACE.get(wsb, dtxt.device, "text_bwd")
         tail = (ops._p(shape.eot_rows), ops._p(dtxt.contiguous()), ops._p(saved), saved.numel(), ops._p(dx0),
                 ops._p(ws), ws.numel(), ops._stream())
+        self._input_rows(lib, shape)
         if shape.packed:
             N.check(lib.clipk_text_backward_packed(h, shape.G, shape.C, shape.P, shape.R, shape.ntiles,
                                                    ops._p(shape.tiles), ops._p(shape.row_first), *tail),

@@ -33,6 +33,10 @@ struct clipk_encoder {
   std::vector<std::array<const void*, 16>> lw;
   std::array<const void*, 8> head;
   DeepPrompts deep;
+  // clipk_encoder_set_input_rows: 1 = on the shared-prefix packed layout only the P prefix rows
+  // of each group carry per-group (trainable) values; the class rows of x0 are the same for
+  // every group and their input gradient is not wanted
+  int prefix_input = 0;
 };
 
 namespace clipk {
@@ -309,13 +313,16 @@ static int block_attn(const clipk_encoder* e, const std::array<const void*, 16>&
 // Post-attention half over `rows` rows: Xm = X + o Wout^T + b; xn = LN2(Xm);
 // Xo = Xm + MLP(xn). (The text encoder's last layer runs it on the EOT rows only.)
 // Residual stream X, Xm, Xo of dtype rd (fp32, or the 16-bit act dtype for the text encoder).
-// Text c_proj consumes quickgelu(h) from its A staging (knob CLIPK_TEXT_AQGELU=0: c_fc writes
-// both h and quickgelu(h) as before)
+// Training: c_fc writes both h (kept for the backward) and quickgelu(h) from its epilogue, and
+// c_proj stages quickgelu(h) like any operand, so it runs the ping-pong loop. Knob
+// CLIPK_TEXT_AQGELU=1: c_fc writes h alone and c_proj applies QuickGELU to A while staging it
+// (register-staged 2-slot loop). Same-box A/B (profiles/r02o_ab_aqgelu.txt): 12.33 -> 12.19 ms
+// per step with the epilogue form (c_proj 1.71 -> 1.22 ms, c_fc 1.19 -> 1.49 ms).
 static bool a_qgelu_on() {
   static int v = -1;
   if (v < 0) {
     const char* s = getenv("CLIPK_TEXT_AQGELU");
-    v = s ? atoi(s) : 1;
+    v = s ? atoi(s) : 0;
   }
   return v != 0;
 }
@@ -334,11 +341,8 @@ static int block_post(const clipk_encoder* e, const std::array<const void*, 16>&
                               m2, r2, st));
   }
   if (text && act != CLIPK_F32 && h && a_qgelu_on()) {
-    // training: c_fc writes only the pre-activation h (kept for the backward) and c_proj
-    // applies QuickGELU to its A operand while staging it, so the g write (rows x 4W x 2 B
-    // per layer) is gone: +2.7 % train images/s. Forward-only (no h kept) stays on the
-    // QuickGELU epilogue: there c_fc writes g alone, and c_proj's glds staging of g beat the
-    // register staging + QuickGELU of h by 3.6 % eval images/s.
+    // knob: c_fc writes only the pre-activation h and c_proj applies QuickGELU to its A
+    // operand while staging it (no g write; measured slower than the ping-pong c_proj)
     TRY(gemm(act, act, CLIPK_EPI_BIAS, rows, 4 * W, W, xn, w[8], (const float*)w[9], nullptr, h,
              nullptr, nullptr, 0, st, CLIPK_PROF_GEMM_FC, nullptr, 0, "text.fc_fwd"));
     TRY(gemm(act, rd, CLIPK_EPI_BIAS_RES | CLIPK_A_QGELU, rows, W, 4 * W, h, w[10], (const float*)w[11], Xm,
@@ -476,6 +480,89 @@ static int deep_inject(const clipk_encoder* e, int l, int rd, void* X, hipStream
                            e->W, st);
 }
 
+// ---- prefix-input mode (clipk_encoder_set_input_rows), shared-prefix packed layout:
+// * forward, layer 0, G >= 2: the class rows of every group enter layer 0 with the same values
+//   (token embedding + position; CoCoOp's pi_b reaches only the context rows, all in the
+//   prefix), and LN1 / the qkv projection are row-wise, so their q|k|v rows are computed once
+//   (group 0) and copied to the other groups; the other groups' prefix rows are computed
+//   compactly. Rows [0, R) of the LN1 statistics hold group 0's, rows [R, R + (G-1) P) the
+//   other groups' prefix rows (layer 0's backward reads only prefix rows).
+// * backward, layer 0: the encoder input's gradient is formed on the prefix rows only (its qkv
+//   input-grad GEMM and LN1 backward run on G*P rows); other rows of dx0 are left unspecified.
+// Exact: the same per-row arithmetic on the rows whose results are used.
+static bool prefix_mode(const clipk_encoder* e, const SeqShape& sh) {
+  return e->prefix_input && sh.packed && sh.P >= 1 && sh.R - sh.P >= sh.G * sh.P;
+}
+// prow[i] = g*R + p for prefix row i = g*P + p; with m/r: mc/rc[i] = the saved LN1 statistics of
+// that row (at its own row, or -- forward sharing, `shared` -- at the layout described above)
+__global__ __launch_bounds__(256) void prefix_tables_kernel(int G, int P, int R, int shared, int* __restrict__ prow,
+                                                            const float* __restrict__ m, const float* __restrict__ r,
+                                                            float* __restrict__ mc, float* __restrict__ rc) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= G * P) return;
+  const int g = i / P, p = i % P;
+  prow[i] = g * R + p;
+  if (m) {
+    const int si = (!shared || g == 0) ? g * R + p : R + (g - 1) * P + p;
+    mc[i] = m[si];
+    rc[i] = r[si];
+  }
+}
+// rows [P, R) of group 0 (16-B chunks per row) copied to groups 1..G-1
+__global__ __launch_bounds__(256) void group_bcast_kernel(int G, int P, int R, int chunks, uint4* __restrict__ buf) {
+  const long per = (long)(R - P) * chunks, total = per * (G - 1);
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int g = 1 + (int)(i / per);
+    const long j = i % per;
+    buf[(long)g * R * chunks + (long)P * chunks + j] = buf[(long)P * chunks + j];
+  }
+}
+static int prefix_tables(const SeqShape& sh, bool shared, int* prow, const float* m, const float* r, float* mc,
+                         float* rc, hipStream_t st) {
+  const int n = sh.G * sh.P;
+  hipLaunchKernelGGL(prefix_tables_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sh.G, sh.P, sh.R, (int)shared, prow,
+                     m, r, mc, rc);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+// Layer 0's attention half under forward sharing (prefix_mode, G >= 2): LN1 + qkv on group 0's
+// rows and, compactly, on the other groups' prefix rows; qkv class rows copied to every group.
+static int block_attn_shared0(const clipk_encoder* e, const std::array<const void*, 16>& w, const SeqShape& sh,
+                              int rd, const void* X, void* xn, void* qkv, void* o, float* lse, float* m1, float* r1,
+                              int* prow, hipStream_t st) {
+  const int W = e->W, act = e->act, G = sh.G, P = sh.P, R = sh.R;
+  const int n = (G - 1) * P;  // other groups' prefix rows
+  const size_t xa = (size_t)W * esize(act), qa = 3 * xa;
+  TRY(prefix_tables(sh, true, prow, nullptr, nullptr, nullptr, nullptr, st));
+  {
+    ProfScope ps(CLIPK_PROF_NONE, st, 0.0, "text.ln_fwd", (double)(R + n) * W * (esize(rd) + esize(act)));
+    TRY(clipk_layernorm_fwd_x(rd, act, R, W, X, W, nullptr, (const float*)w[0], (const float*)w[1], xn, W, m1, r1,
+                              st));
+    TRY(clipk_layernorm_fwd_x(rd, act, n, W, X, W, prow + P, (const float*)w[0], (const float*)w[1],
+                              (char*)xn + (size_t)R * xa, W, m1 ? m1 + R : nullptr, r1 ? r1 + R : nullptr, st));
+  }
+  // one GEMM over [group 0's R rows | the compact prefix rows]: the compact rows land on rows
+  // R.., of which group 1's prefix rows (R..R+P-1) are already in place
+  TRY(gemm(act, act, CLIPK_EPI_BIAS, R + n, 3 * W, W, xn, w[2], (const float*)w[3], nullptr, qkv, nullptr, nullptr,
+           0, st, CLIPK_PROF_GEMM_ALL, nullptr, 0, "text.qkv_fwd"));
+  {
+    ProfScope ps(CLIPK_PROF_NONE, st, 0.0, "text.qkv_bcast", (double)(G - 1) * (R - P) * qa * 2.0);
+    if (G > 2) TRY(clipk_rows_copy((int)qa, (G - 2) * P, (char*)qkv + (size_t)(R + P) * qa, nullptr, qkv, prow + 2 * P, st));
+    const int chunks = (int)(qa / 16);
+    const long total = (long)(R - P) * chunks * (G - 1);
+    hipLaunchKernelGGL(group_bcast_kernel, dim3((unsigned)std::min<long>((total + 255) / 256, 4096)), dim3(256), 0, st,
+                       G, P, R, chunks, (uint4*)qkv);
+    CLIPK_CHECK_LAUNCH();
+  }
+  {
+    const double ab = (double)sh.rows * 4 * W * esize(act) + (lse ? 4.0 * sh.rows * e->heads : 0.0);
+    ProfScope ps(CLIPK_PROF_ATTN, st, 0.0, "text.attn_fwd", ab);
+    TRY(attn_fwd(e, sh, qkv, o, lse, st));
+  }
+  return CLIPK_OK;
+}
+
 static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const float* x0, const int* eot_rows,
                              float* txt, void* saved, size_t saved_bytes, void* ws, size_t ws_bytes,
                              hipStream_t st, const EncIO& io) {
@@ -502,11 +589,17 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
     void* Xo = t.X[l + 1];
     if (!save && Xo == cur) Xo = t.X[l];  // ping-pong (cur may be the caller's x0)
     if (l >= 1) TRY(deep_inject(e, l, rd, const_cast<void*>(cur), st));  // l >= 1: cur is ours
+    const bool share0 = l == 0 && io.text && sh.G >= 2 && prefix_mode(e, sh);
+    if (share0) {
+      TRY(block_attn_shared0(e, e->lw[l], sh, rd, cur, t.xn, t.qkv[l], t.o[l], t.lse[l], t.mean1[l], t.rstd1[l],
+                             (int*)t.g, st));
+    }
     if (eotl && l == nl - 1) {
       // last layer: attention over all rows (the EOT rows attend to their whole prefix),
       // then out_proj / LN2 / MLP on the EOT rows alone; Xm, h, Xo hold nout compact rows
-      TRY(block_attn(e, e->lw[l], sh, rd, cur, t.xn, t.qkv[l], t.o[l], t.lse[l], t.mean1[l], t.rstd1[l], st,
-                     io.text, io.sk, io.skb));
+      if (!share0)
+        TRY(block_attn(e, e->lw[l], sh, rd, cur, t.xn, t.qkv[l], t.o[l], t.lse[l], t.mean1[l], t.rstd1[l], st,
+                       io.text, io.sk, io.skb));
       {
         ProfScope ps(CLIPK_PROF_NONE, st, 0.0, SITE("eot_gather"),
                      2.0 * nout * W * (esize(e->act) + esize(rd)));
@@ -515,6 +608,9 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
       }
       TRY(block_post(e, e->lw[l], nout, rd, t.xc, t.oc, t.Xm[l], Xo, t.xn, save ? t.h[l] : nullptr, t.g,
                      t.mean2[l], t.rstd2[l], st, io.text, nullptr, 0));
+    } else if (share0) {
+      TRY(block_post(e, e->lw[l], sh.rows, rd, cur, t.o[l], t.Xm[l], Xo, t.xn, save ? t.h[l] : nullptr, t.g,
+                     t.mean2[l], t.rstd2[l], st, io.text, io.sk, io.skb));
     } else {
       TRY(block_fwd(e, e->lw[l], sh, rd, cur, t.Xm[l], Xo, t.xn, t.qkv[l], t.o[l], t.lse[l],
                     save ? t.h[l] : nullptr, t.g, t.mean1[l], t.rstd1[l], t.mean2[l], t.rstd2[l], st, io.text,
@@ -622,6 +718,26 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
                         4.0 * rows * e->heads;
       ProfScope ps(io.text ? CLIPK_PROF_ATTN : CLIPK_PROF_NONE, st, 0.0, SITE("attn_bwd"), ab);
       TRY(attn_bwd(e, sh, t.qkv[l], t.o[l], b.do_, t.lse[l], b.dqkv, b.part, st));
+    }
+    if (l == 0 && io.text && prefix_mode(e, sh)) {
+      // the input gradient on the prefix rows only: dqkv gathered to G*P compact rows, their
+      // qkv input-grad GEMM and LN1 backward (scattered back to the prefix rows of dx0)
+      const int np = sh.G * sh.P;
+      int* prow = (int*)b.do_;  // do is free once the attention backward has run
+      float* mc = (float*)(prow + np);
+      float* rc = mc + np;
+      TRY(prefix_tables(sh, sh.G >= 2, prow, t.mean1[0], t.rstd1[0], mc, rc, st));
+      TRY(clipk_rows_copy(3 * W * (int)esize(gd), np, b.dqkv, prow, b.dh, nullptr, st));
+      TRY(gemm(gd, gd, CLIPK_EPI_NONE, np, W, 3 * W, b.dh, w[12], nullptr, nullptr, b.dxn, nullptr, nullptr, 0, st,
+               pg, nullptr, 0, SITE("qkv_dx_prefix")));
+      const float* g0 = (const float*)w[0];
+      if (!r16)
+        TRY(clipk_layernorm_bwd_x(rd, gd, np, W, b.dxn, W, t.X[0], W, prow, g0, mc, rc, dX, W, dX, nullptr, gd, prow,
+                                  W, st));
+      else
+        TRY(clipk_layernorm_bwd_x2(rd, gd, np, W, b.dxn, W, t.X[0], W, prow, g0, mc, rc, b.dX_lp, gd, W, dX, b.dX_lp,
+                                   gd, prow, W, st));
+      continue;
     }
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, 3 * W, b.dqkv, w[12], nullptr, nullptr, b.dxn,
              nullptr, nullptr, 0, st, pg, nullptr, 0, SITE("qkv_dx")));
@@ -855,6 +971,13 @@ __global__ __launch_bounds__(256) void vpt_rows_sum_kernel(int B, int Lp, int L,
   out[(size_t)p * D + c] = acc;
 }
 }  // namespace clipk
+
+extern "C" int clipk_encoder_set_input_rows(clipk_encoder* e, int mode) {
+  if (!e) return CLIPK_EINVAL;
+  if (mode != 0 && mode != 1) return CLIPK_EINVAL;
+  e->prefix_input = mode;
+  return CLIPK_OK;
+}
 
 extern "C" int clipk_encoder_set_deep_prompts(clipk_encoder* e, int n_deep, int n_ctx, int n_per, const int* rows,
                                               const float* prompts, float* grads) {

@@ -103,6 +103,11 @@ template <> struct Raw<32> { uint4 v[2]; };
 #ifndef CLIPK_GEMM_RING
 #define CLIPK_GEMM_RING 0
 #endif
+// CLIPK_GEMM_PPB0 (A/B): the ping-pong loop keeps phase 1's B-half-0 fragments in registers for
+// phase 4 instead of re-reading them (4 of 24 ds_read_b128 per wave and K tile, +16 VGPRs).
+#ifndef CLIPK_GEMM_PPB0
+#define CLIPK_GEMM_PPB0 0
+#endif
 // Diagnostic builds only (wrong results; tools/gemm_diag.sh): NOLOAD = stage no K step past
 // the first (the loop's compute + LDS + barrier ceiling), NOBAR = no barrier / vmcnt wait per
 // K step either.
@@ -111,6 +116,10 @@ template <> struct Raw<32> { uint4 v[2]; };
 #endif
 #ifndef CLIPK_GEMM_NOBAR
 #define CLIPK_GEMM_NOBAR 0
+#endif
+// NOMMA = no MFMA in the ping-pong loop (its load + LDS + barrier time alone).
+#ifndef CLIPK_GEMM_NOMMA
+#define CLIPK_GEMM_NOMMA 0
 #endif
 template <int NB> __device__ __forceinline__ void ld_raw(const void* p, Raw<NB>& r) {
 #if CLIPK_GEMM_XNT
@@ -439,6 +448,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       typedef __amdgpu_buffer_rsrc_t TRes;
       // stage region r of K tile kt into buffer buf from the tile resources ra / rb
       auto pst = [&](int buf, __amdgpu_buffer_rsrc_t ra_, __amdgpu_buffer_rsrc_t rb_, int kt, int r) {
+        if (CLIPK_GEMM_NOLOAD && it >= 1) return;  // diagnostic: first K tiles only
         const int base = buf * STAGE;
         const int koff = (kt0 + kt) * ROWB;
 #pragma unroll
@@ -455,7 +465,8 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         if (two_a) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       };
-      u32x4 fa[KK][TM2], fb[KK][TN2];
+      constexpr int NFB = CLIPK_GEMM_PPB0 ? 2 : 1;
+      u32x4 fa[KK][TM2], fbs[NFB][KK][TN2];
       auto rd_a = [&](int buf, int h) {
         const char* As = smem + buf * STAGE + (wm * (BM / WM) + h * (BM / WM / 2) + fr) * ROWB;
 #pragma unroll
@@ -470,9 +481,10 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
           for (int j = 0; j < TN2; ++j)
-            fb[kk][j] = *reinterpret_cast<const u32x4*>(Bs + j * 16 * ROWB + ((kk * 4 + fq) ^ sw) * 16);
+            fbs[NFB == 2 ? q : 0][kk][j] = *reinterpret_cast<const u32x4*>(Bs + j * 16 * ROWB + ((kk * 4 + fq) ^ sw) * 16);
       };
       auto mm = [&](int h, int q) {
+        if (CLIPK_GEMM_NOMMA) return;
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int kk = 0; kk < KK; ++kk)
@@ -480,7 +492,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
           for (int i = 0; i < TM2; ++i)
 #pragma unroll
             for (int j = 0; j < TN2; ++j)
-              acc[h * TM2 + i][q * TN2 + j] = mma<T>(fb[kk][j], fa[kk][i], acc[h * TM2 + i][q * TN2 + j]);
+              acc[h * TM2 + i][q * TN2 + j] = mma<T>(fbs[NFB == 2 ? q : 0][kk][j], fa[kk][i], acc[h * TM2 + i][q * TN2 + j]);
         __builtin_amdgcn_s_setprio(0);
       };
       auto seg_end = [&]() {  // memory segment done: fragments in registers, then the barrier
@@ -522,7 +534,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         seg_end();
         mm(1, 1);
         G8_BAR();
-        rd_b(b, 0);                             // phase 4: A1 x B0
+        if (NFB == 1) rd_b(b, 0);               // phase 4: A1 x B0
         if (h2) {
           pst(b, in2 ? cra : xra, crb, k2, 1);
           wait_ahead();

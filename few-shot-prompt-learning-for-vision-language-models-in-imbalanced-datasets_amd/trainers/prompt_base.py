@@ -9,6 +9,8 @@ with the context slots zeroed plus the int32 slot tables consumed by
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -25,6 +27,11 @@ def grads_finite(module) -> bool:
     return bool(torch.stack([torch.isfinite(g).all() for g in gs]).all().item())
 
 
+# prefix-input mode on packed layouts whose trainable slots all sit in the shared prefix
+# (knob CLIPK_TEXT_PREFIX_INPUT=0 turns it off; A/B and parity on both)
+PREFIX_INPUT = os.environ.get("CLIPK_TEXT_PREFIX_INPUT", "1") != "0"
+
+
 class TextShape:
     """Row structure of one text-encoder call, as the native encoder takes it.
 
@@ -33,8 +40,13 @@ class TextShape:
             tiles [ntiles,2] int32 (first row, rows) of the <=16-row attention tiles,
             row_first [R] int32, eot_rows[g*C + c] absolute."""
 
-    def __init__(self, eot_rows, nseq=0, L=0, G=0, C=0, P=0, R=0, tiles=None, row_first=None):
+    def __init__(self, eot_rows, nseq=0, L=0, G=0, C=0, P=0, R=0, tiles=None, row_first=None,
+                 prefix_input=False):
         self.eot_rows = eot_rows
+        # packed only: every trainable slot is a prefix row, so the class rows of x0 are the
+        # same in every group and the input gradient is wanted on the prefix rows alone
+        # (clipk_encoder_set_input_rows; dx0's class rows are then unspecified)
+        self.prefix_input = bool(prefix_input) and tiles is not None
         self.packed = tiles is not None
         self.nseq, self.L = nseq, L
         self.G, self.C, self.P, self.R = G, C, P, R
@@ -119,6 +131,7 @@ class PromptLayout:
         self._shapes = {}
         pk = shared_prefix_tables(src_map, ctx_pos, eot, n_ctx, csc) if shared_prefix else None
         self.pack = None
+        self.prefix_input = False
         if pk is not None:
             self.pack = pk
             self.P, self.R = pk["P"], pk["R"]
@@ -127,6 +140,7 @@ class PromptLayout:
             self.row_tab = torch.from_numpy(pk["row_tab"]).to(dev)
             self.slot_ptr = torch.from_numpy(pk["slot_ptr"]).to(dev)
             self.slot_rows = torch.from_numpy(pk["slot_rows"]).to(dev)
+            self.prefix_input = len(pk["slot_rows"]) == n_ctx and bool((pk["slot_rows"] < self.P).all())
 
     @property
     def rows_per_group(self) -> int:
@@ -149,7 +163,8 @@ class PromptLayout:
         if B not in self._shapes:
             if self.pack is not None:
                 self._shapes[B] = TextShape(self.eot_rows(B), G=B, C=self.n_cls, P=self.P, R=self.R,
-                                            tiles=self.tiles, row_first=self.row_first)
+                                            tiles=self.tiles, row_first=self.row_first,
+                                            prefix_input=self.prefix_input and PREFIX_INPUT)
             else:
                 self._shapes[B] = TextShape(self.eot_rows(B), nseq=B * self.n_cls, L=self.L)
         return self._shapes[B]

@@ -288,6 +288,17 @@ void clipk_encoder_destroy(clipk_encoder* enc);
 int clipk_encoder_set_deep_prompts(clipk_encoder* e, int n_deep, int n_ctx, int n_per, const int* rows,
                                    const float* prompts, float* grads);
 
+/* Input-row mode of the next text-encoder calls on the shared-prefix packed layout
+ * (clipk_text_{forward,backward}_packed). mode 0: every row of x0 is an independent input (the
+ * reference's TextEncoder contract, coop.py:195-205). mode 1: only the P prefix rows of each
+ * group carry per-group values -- the context slots of CoOp / CoCoOp with class position "end"
+ * (coop.py:259-270; cocoop.py:173-198, pi_b added to ctx only) -- so the class rows of x0 are
+ * identical in every group: layer 0's LN1 and qkv projection run once for them (group 0) and
+ * are copied to the other groups, and the backward forms dx0 on the prefix rows only (the
+ * rows clipk_ctx_grad_rows reads; the class rows of dx0 are left unspecified). Exact. Forward
+ * and backward of one call must use the same mode. */
+int clipk_encoder_set_input_rows(clipk_encoder* e, int mode);
+
 /* ViT with visual prompts, forward with saved activations and input-grad backward (the
  * prompted VisionTransformer of IVLP / PromptSRC, model.py:401-431, and MaPLe, 434-485):
  * n_vpt prompt rows (vpt [n_vpt, width] fp32) appended after the image tokens before ln_pre,

@@ -250,3 +250,40 @@ def test_zeroshot_clip_vs_oracle(dev, prec, ensemble):
     ref = (float(np.exp(float(p["logit_scale"]))) * imf @ feats.t()).numpy()
     tol = 1e-3 if prec == "fp32" else 5e-4 * 100.0
     assert float(np.abs(logits - ref).max()) <= tol
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+@pytest.mark.parametrize("name,cocoop", [("cocoop_tiny_ctxinit_ce", True), ("cocoop_vitb16_c4", True),
+                                         ("coop_tiny_end_csc0_ce", False), ("coop_tiny_middle_csc0_ce", False)])
+def test_prefix_input_mode_is_exact(dev, name, prec, cocoop, monkeypatch):
+    """clipk_encoder_set_input_rows(1) (layer 0's LN1 / qkv on the class rows once, copied to every
+    group; dx0 formed on the prefix rows only) against mode 0 on the same packed layout: the
+    same per-row arithmetic, so logits, loss and every prompt gradient agree to fp32 rounding
+    (1e-6 relative; 16-bit: 1e-3). cocoop_tiny has 3 images (groups 1 and 2 take the copy and
+    the compact-row scatter); the middle position keeps context slots among the class rows, so
+    it must stay in mode 0."""
+    from fsp_amd.trainers import prompt_base
+    meta, ref = load_fixture(name)
+    outs = {}
+    for mode in (False, True):
+        monkeypatch.setattr(prompt_base, "PREFIX_INPUT", mode)
+        outs[mode] = run_native(meta, ref, prec, cocoop=cocoop, dev=str(dev))
+        assert outs[mode]["packed"]
+    tol = 1e-6 if prec == "fp32" else 1e-3
+    for k in ["logits", "loss", "ctx_after_step"] + [k for k in outs[True] if k.startswith("grad_")]:
+        assert rel_err(outs[True][k], outs[False][k]) <= tol, (k, rel_err(outs[True][k], outs[False][k]))
+    if "middle" in name:
+        assert not _layout_prefix_input(meta, prec, cocoop, dev)
+    else:
+        assert _layout_prefix_input(meta, prec, cocoop, dev)
+
+
+def _layout_prefix_input(meta, prec, cocoop, dev):
+    from parity_util import make_cfg, state_dict
+    from fsp_amd.clip import synth
+    from fsp_amd.clip.model import build_model
+    from fsp_amd.trainers import coop as C, cocoop as CC
+    cfg = make_cfg(meta, prec, cocoop)
+    clip = build_model(state_dict(meta["arch"]), prec=prec, device=str(dev))
+    model = (CC if cocoop else C).CustomCLIP(cfg, synth.synthetic_classnames(meta["n_cls"]), clip)
+    return model.prompt_learner.layout.shape(2).prefix_input
