@@ -103,10 +103,12 @@ template <> struct Raw<32> { uint4 v[2]; };
 #ifndef CLIPK_GEMM_RING
 #define CLIPK_GEMM_RING 0
 #endif
-// CLIPK_GEMM_PPB0 (A/B): the ping-pong loop keeps phase 1's B-half-0 fragments in registers for
-// phase 4 instead of re-reading them (4 of 24 ds_read_b128 per wave and K tile, +16 VGPRs).
+// CLIPK_GEMM_PPB0: the ping-pong loop keeps phase 1's B-half-0 fragments in registers for
+// phase 4 instead of re-reading them (4 of 24 ds_read_b128 per wave and K tile, +13-16 VGPRs,
+// no spill at 256 rows). Same-box A/B (profiles/r02o_ab_ppb0.txt): headline step 11.91 ->
+// 11.82 ms, input-grad GEMMs 2.195 -> 2.166 ms/step.
 #ifndef CLIPK_GEMM_PPB0
-#define CLIPK_GEMM_PPB0 0
+#define CLIPK_GEMM_PPB0 1
 #endif
 // Diagnostic builds only (wrong results; tools/gemm_diag.sh): NOLOAD = stage no K step past
 // the first (the loop's compute + LDS + barrier ceiling), NOBAR = no barrier / vmcnt wait per
