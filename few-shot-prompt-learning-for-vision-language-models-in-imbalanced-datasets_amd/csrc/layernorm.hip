@@ -1,6 +1,6 @@
 // LayerNorm forward / input-grad backward as wavefront row reductions (HBM-bound).
 // Reference: PromptSRC/clip/model.py:153-159 (fp32 upcast, eps 1e-5, affine).
-// One wave per row, the row kept in registers (width <= 1024), two-pass mean/variance from
+// One wave per CLIPK_LN_RPW rows, each row kept in registers (width <= 1024), two-pass mean/variance from
 // registers (no E[x^2]-E[x]^2 cancellation); 8 consecutive elements per lane (16-B accesses
 // of 16-bit rows) when the width is a multiple of 512, else 4. The input row (the residual
 // stream) is fp32 or, for the 16-bit text residual stream, the activation dtype (statistics
@@ -61,64 +61,98 @@ __device__ __forceinline__ void stv(T* p, const float* v) {
   }
 }
 
-template <typename TI, typename TO, int VW>
+// RPW rows per wave: every row's loads are issued before the first reduction, so a wave keeps
+// RPW rows of HBM traffic in flight; gamma / beta loaded once per wave. NC = 64-lane chunks per
+// row (width / VW / 64 rounded up). The per-row arithmetic does not depend on RPW. Same-box A/B
+// (profiles/r02p_ab_ln_rpw.txt, headline step): forward 1 -> 2 rows per wave 0.52 -> 0.50
+// ms/step, 4 rows 0.58; backward 1 row 0.79, 2 rows 0.85, 4 rows 1.06 (its three row streams
+// per row already keep the memory system busy at one row per wave).
+#ifndef CLIPK_LN_RPW
+#define CLIPK_LN_RPW 2
+#endif
+#ifndef CLIPK_LN_RPW_BWD
+#define CLIPK_LN_RPW_BWD 1
+#endif
+template <typename TI, typename TO, int VW, int NC, int RPW>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int width, const TI* __restrict__ x,
                                                      int ldx, const int* __restrict__ in_rows,
                                                      const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, TO* __restrict__ out,
                                                      int ldo, float* __restrict__ mean,
                                                      float* __restrict__ rstd) {
-  constexpr int NC = 1024 / (64 * VW);
   const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= rows) return;
-  const int xr = in_rows ? in_rows[r] : r;
-  const TI* xp = x + (size_t)xr * ldx;
+  const int r0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (r0 >= rows) return;
   const int nv = width / VW;  // vectors per row
-  float v[NC][VW], gg[NC][VW], bb[NC][VW];
-  float s = 0.f;
-  // gamma / beta are issued with x: loaded after the two reductions they were one more
-  // dependent round trip per row
+  float v[RPW][NC][VW], gg[NC][VW], bb[NC][VW];
+#pragma unroll
+  for (int j = 0; j < RPW; ++j) {
+    const int r = min(r0 + j, rows - 1);  // rows past the end: a valid row, never stored
+    const TI* xp = x + (size_t)(in_rows ? in_rows[r] : r) * ldx;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = lane + i * 64;
+      if (c < nv) {
+        ldv<TI, VW>(xp + c * VW, v[j][i]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < VW; ++k) v[j][i][k] = 0.f;
+      }
+    }
+  }
+  // gamma / beta are issued with x: loaded after the reductions they were one more dependent
+  // round trip per row
 #pragma unroll
   for (int i = 0; i < NC; ++i) {
     const int c = lane + i * 64;
     if (c < nv) {
-      ldv<TI, VW>(xp + c * VW, v[i]);
       ldv<float, VW>(gamma + c * VW, gg[i]);
       ldv<float, VW>(beta + c * VW, bb[i]);
-#pragma unroll
-      for (int k = 0; k < VW; ++k) s += v[i][k];
-    } else {
-#pragma unroll
-      for (int k = 0; k < VW; ++k) v[i][k] = 0.f;
     }
   }
   const float inv_w = 1.0f / (float)width;
-  const float mu = wave_sum(s) * inv_w;
-  float q = 0.f;
+  float mu[RPW], rs[RPW];
 #pragma unroll
-  for (int i = 0; i < NC; ++i) {
-    const int c = lane + i * 64;
-    if (c < nv) {
+  for (int j = 0; j < RPW; ++j) {
+    float s = 0.f;
 #pragma unroll
-      for (int k = 0; k < VW; ++k) { const float d = v[i][k] - mu; q += d * d; }
-    }
+    for (int i = 0; i < NC; ++i)
+#pragma unroll
+      for (int k = 0; k < VW; ++k) s += v[j][i][k];
+    mu[j] = wave_sum(s) * inv_w;
   }
-  const float rs = rsqrtf(wave_sum(q) * inv_w + 1e-5f);
-  TO* op = out + (size_t)r * ldo;
 #pragma unroll
-  for (int i = 0; i < NC; ++i) {
-    const int c = lane + i * 64;
-    if (c < nv) {
-      float o[VW];
+  for (int j = 0; j < RPW; ++j) {
+    float q = 0.f;
 #pragma unroll
-      for (int k = 0; k < VW; ++k) o[k] = (v[i][k] - mu) * rs * gg[i][k] + bb[i][k];
-      stv<TO, VW>(op + c * VW, o);
+    for (int i = 0; i < NC; ++i) {
+      const int c = lane + i * 64;
+      if (c < nv) {
+#pragma unroll
+        for (int k = 0; k < VW; ++k) { const float d = v[j][i][k] - mu[j]; q += d * d; }
+      }
     }
+    rs[j] = rsqrtf(wave_sum(q) * inv_w + 1e-5f);
   }
-  if (lane == 0) {
-    if (mean) mean[r] = mu;
-    if (rstd) rstd[r] = rs;
+#pragma unroll
+  for (int j = 0; j < RPW; ++j) {
+    const int r = r0 + j;
+    if (r >= rows) break;
+    TO* op = out + (size_t)r * ldo;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = lane + i * 64;
+      if (c < nv) {
+        float o[VW];
+#pragma unroll
+        for (int k = 0; k < VW; ++k) o[k] = (v[j][i][k] - mu[j]) * rs[j] * gg[i][k] + bb[i][k];
+        stv<TO, VW>(op + c * VW, o);
+      }
+    }
+    if (lane == 0) {
+      if (mean) mean[r] = mu[j];
+      if (rstd) rstd[r] = rs[j];
+    }
   }
 }
 
@@ -126,7 +160,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int width, const 
 // RL: the incoming residual gradient dres is in the low-precision dtype TL (a 16-bit residual-
 // gradient stream, updated in place: dres == dx_lp is allowed, each lane reads its chunk
 // before writing it); dx (fp32) may then be null.
-template <typename TL, typename TD, typename TX, int VW, bool RL = false>
+template <typename TL, typename TD, typename TX, int VW, bool RL, int NC, int RPW>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int width, const TD* __restrict__ dy,
                                                      int lddy, const TX* __restrict__ x, int ldx,
                                                      const int* __restrict__ x_rows,
@@ -136,55 +170,78 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int width, const 
                                                      const void* dres_v, int lddres,
                                                      float* __restrict__ dx, TL* dx_lp,
                                                      const int* __restrict__ out_rows, int ldo) {
-  constexpr int NC = 1024 / (64 * VW);
   const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= rows) return;
-  const int xr = x_rows ? x_rows[r] : r;
-  const int orow = out_rows ? out_rows[r] : r;
-  const float mu = mean[r], rs = rstd[r];
-  const TX* xp = x + (size_t)xr * ldx;
-  const TD* dp = dy + (size_t)r * lddy;
+  const int r0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (r0 >= rows) return;
   const int nv = width / VW;
-  float gv[NC][VW], xh[NC][VW], rv[NC][VW];
-  float s1 = 0.f, s2 = 0.f;
   typedef typename std::conditional<RL, TL, float>::type TR;
-  const TR* rp = dres_v ? (const TR*)dres_v + (size_t)orow * lddres : nullptr;
+  float xv[RPW][NC][VW], dv[RPW][NC][VW], rv[RPW][NC][VW], gg[NC][VW];
+  int orow[RPW];
+  float mu[RPW], rs[RPW];
 #pragma unroll
-  for (int i = 0; i < NC; ++i) {
-    const int c = lane + i * 64;
-    if (c < nv) {
-      float xv[VW], dv[VW], gg[VW];
-      ldv<TX, VW>(xp + c * VW, xv);
-      ldv<TD, VW>(dp + c * VW, dv);
-      ldv<float, VW>(gamma + c * VW, gg);
-      // the residual gradient is issued with the other operands (not after the reductions)
-      if (rp) ldv<TR, VW>(rp + c * VW, rv[i]);
+  for (int j = 0; j < RPW; ++j) {
+    const int r = min(r0 + j, rows - 1);  // rows past the end: loaded, never stored
+    orow[j] = out_rows ? out_rows[r] : r;
+    mu[j] = mean[r];
+    rs[j] = rstd[r];
+    const TX* xp = x + (size_t)(x_rows ? x_rows[r] : r) * ldx;
+    const TD* dp = dy + (size_t)r * lddy;
+    const TR* rp = dres_v ? (const TR*)dres_v + (size_t)orow[j] * lddres : nullptr;
 #pragma unroll
-      for (int k = 0; k < VW; ++k) {
-        xh[i][k] = (xv[k] - mu) * rs;
-        gv[i][k] = dv[k] * gg[k];
-        s1 += gv[i][k];
-        s2 += gv[i][k] * xh[i][k];
+    for (int i = 0; i < NC; ++i) {
+      const int c = lane + i * 64;
+      if (c < nv) {
+        ldv<TX, VW>(xp + c * VW, xv[j][i]);
+        ldv<TD, VW>(dp + c * VW, dv[j][i]);
+        // the residual gradient is issued with the other operands (not after the reductions)
+        if (rp) ldv<TR, VW>(rp + c * VW, rv[j][i]);
       }
     }
   }
-  const float inv_w = 1.0f / (float)width;
-  const float m1 = wave_sum(s1) * inv_w;
-  const float m2 = wave_sum(s2) * inv_w;
 #pragma unroll
   for (int i = 0; i < NC; ++i) {
     const int c = lane + i * 64;
-    if (c < nv) {
-      float o[VW];
+    if (c < nv) ldv<float, VW>(gamma + c * VW, gg[i]);
+  }
+  const float inv_w = 1.0f / (float)width;
+  float m1[RPW], m2[RPW];
 #pragma unroll
-      for (int k = 0; k < VW; ++k) o[k] = rs * (gv[i][k] - m1 - xh[i][k] * m2);
-      if (rp) {
+  for (int j = 0; j < RPW; ++j) {
+    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int k = 0; k < VW; ++k) o[k] += rv[i][k];
+    for (int i = 0; i < NC; ++i) {
+      const int c = lane + i * 64;
+      if (c < nv) {
+#pragma unroll
+        for (int k = 0; k < VW; ++k) {
+          xv[j][i][k] = (xv[j][i][k] - mu[j]) * rs[j];  // xhat
+          dv[j][i][k] = dv[j][i][k] * gg[i][k];         // g = dy * gamma
+          s1 += dv[j][i][k];
+          s2 += dv[j][i][k] * xv[j][i][k];
+        }
       }
-      if (dx) stv<float, VW>(dx + (size_t)orow * ldo + c * VW, o);
-      if (dx_lp) stv<TL, VW>(dx_lp + (size_t)orow * ldo + c * VW, o);
+    }
+    m1[j] = wave_sum(s1) * inv_w;
+    m2[j] = wave_sum(s2) * inv_w;
+  }
+#pragma unroll
+  for (int j = 0; j < RPW; ++j) {
+    if (r0 + j >= rows) break;
+    const bool has_r = dres_v != nullptr;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = lane + i * 64;
+      if (c < nv) {
+        float o[VW];
+#pragma unroll
+        for (int k = 0; k < VW; ++k) o[k] = rs[j] * (dv[j][i][k] - m1[j] - xv[j][i][k] * m2[j]);
+        if (has_r) {
+#pragma unroll
+          for (int k = 0; k < VW; ++k) o[k] += rv[j][i][k];
+        }
+        if (dx) stv<float, VW>(dx + (size_t)orow[j] * ldo + c * VW, o);
+        if (dx_lp) stv<TL, VW>(dx_lp + (size_t)orow[j] * ldo + c * VW, o);
+      }
     }
   }
 }
@@ -197,15 +254,20 @@ template <typename TI>
 static int ln_fwd_launch(int out_dtype, int rows, int width, const TI* x, int ldx, const int* in_rows,
                          const float* gamma, const float* beta, void* out, int ldo, float* mean, float* rstd,
                          hipStream_t st) {
-  dim3 grid((rows + 3) / 4), block(256);
+  constexpr int RPW = CLIPK_LN_RPW;
+  dim3 grid((rows + 4 * RPW - 1) / (4 * RPW)), block(256);
   const bool v8 = width % 512 == 0 && ldx % 8 == 0 && ldo % 8 == 0;
-#define CLIPK_LNF(TOUT)                                                                                       \
-  if (v8)                                                                                                     \
-    hipLaunchKernelGGL((ln_fwd_kernel<TI, TOUT, 8>), grid, block, 0, st, rows, width, x, ldx, in_rows, gamma, \
-                       beta, (TOUT*)out, ldo, mean, rstd);                                                    \
-  else                                                                                                        \
-    hipLaunchKernelGGL((ln_fwd_kernel<TI, TOUT, 4>), grid, block, 0, st, rows, width, x, ldx, in_rows, gamma, \
-                       beta, (TOUT*)out, ldo, mean, rstd);
+  const bool one = v8 && width == 512;  // one 64-lane chunk of 8 elements per row
+#define CLIPK_LNF(TOUT)                                                                                        \
+  if (one)                                                                                                     \
+    hipLaunchKernelGGL((ln_fwd_kernel<TI, TOUT, 8, 1, RPW>), grid, block, 0, st, rows, width, x, ldx, in_rows, \
+                       gamma, beta, (TOUT*)out, ldo, mean, rstd);                                              \
+  else if (v8)                                                                                                 \
+    hipLaunchKernelGGL((ln_fwd_kernel<TI, TOUT, 8, 2, RPW>), grid, block, 0, st, rows, width, x, ldx, in_rows, \
+                       gamma, beta, (TOUT*)out, ldo, mean, rstd);                                              \
+  else                                                                                                         \
+    hipLaunchKernelGGL((ln_fwd_kernel<TI, TOUT, 4, 4, RPW>), grid, block, 0, st, rows, width, x, ldx, in_rows, \
+                       gamma, beta, (TOUT*)out, ldo, mean, rstd);
   switch (out_dtype) {
     case CLIPK_F32: CLIPK_LNF(float) break;
     case CLIPK_F16: CLIPK_LNF(f16) break;
@@ -252,16 +314,21 @@ static int ln_bwd_launch(int rows, int width, const void* dy, int lddy, const TX
                          const int* x_rows, const float* gamma, const float* mean, const float* rstd,
                          const void* dres, bool dres_lp, int lddres, float* dx, void* dx_lp, int lp_dtype,
                          const int* out_rows, int ldo, hipStream_t st) {
-  dim3 grid((rows + 3) / 4), block(256);
+  constexpr int RPW = CLIPK_LN_RPW_BWD;
+  dim3 grid((rows + 4 * RPW - 1) / (4 * RPW)), block(256);
   const TD* d = (const TD*)dy;
   const bool v8 = width % 512 == 0 && ldx % 8 == 0 && ldo % 8 == 0 && lddy % 8 == 0 && (!dres || lddres % 8 == 0);
-#define CLIPK_LNB(TLP, RLV)                                                                                     \
-  if (v8)                                                                                                       \
-    hipLaunchKernelGGL((ln_bwd_kernel<TLP, TD, TX, 8, RLV>), grid, block, 0, st, rows, width, d, lddy, x, ldx,   \
-                       x_rows, gamma, mean, rstd, dres, lddres, dx, (TLP*)dx_lp, out_rows, ldo);                \
-  else                                                                                                          \
-    hipLaunchKernelGGL((ln_bwd_kernel<TLP, TD, TX, 4, RLV>), grid, block, 0, st, rows, width, d, lddy, x, ldx,   \
-                       x_rows, gamma, mean, rstd, dres, lddres, dx, (TLP*)dx_lp, out_rows, ldo);
+  const bool one = v8 && width == 512;
+#define CLIPK_LNB(TLP, RLV)                                                                                      \
+  if (one)                                                                                                       \
+    hipLaunchKernelGGL((ln_bwd_kernel<TLP, TD, TX, 8, RLV, 1, RPW>), grid, block, 0, st, rows, width, d, lddy, x, \
+                       ldx, x_rows, gamma, mean, rstd, dres, lddres, dx, (TLP*)dx_lp, out_rows, ldo);            \
+  else if (v8)                                                                                                   \
+    hipLaunchKernelGGL((ln_bwd_kernel<TLP, TD, TX, 8, RLV, 2, RPW>), grid, block, 0, st, rows, width, d, lddy, x, \
+                       ldx, x_rows, gamma, mean, rstd, dres, lddres, dx, (TLP*)dx_lp, out_rows, ldo);            \
+  else                                                                                                           \
+    hipLaunchKernelGGL((ln_bwd_kernel<TLP, TD, TX, 4, RLV, 4, RPW>), grid, block, 0, st, rows, width, d, lddy, x, \
+                       ldx, x_rows, gamma, mean, rstd, dres, lddres, dx, (TLP*)dx_lp, out_rows, ldo);
   if (!dx_lp || lp_dtype == CLIPK_F32) {
     if (dres_lp) return CLIPK_EDTYPE;
     CLIPK_LNB(float, false)
