@@ -41,6 +41,25 @@ static int lds_slots();
 // (the LDS-staged forward measured best at 4 units per wave, the register one at 8)
 static int fwd_chunk() { static int c = chunk_env("CLIPK_PREFIX_FWD_CHUNK", lds_slots() ? 4 : 8); return c; }
 static int bwd_chunk() { static int c = chunk_env("CLIPK_PREFIX_BWD_CHUNK", 16); return c; }
+static int prefix_num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0, v = 0;
+    n = (hipGetDevice(&dev) == hipSuccess &&
+         hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+            ? v
+            : 256;
+  }
+  return n;
+}
+// Backward units per wave for this shape: bwd_chunk(), halved (down to 4) while the grid would
+// give fewer than 8 waves per CU -- few groups (CoCoOp at 1 image per step, CoOp's single class
+// set) otherwise leave most CUs idle (1 image: 240 waves of 16 units on 256 CUs).
+static int bwd_uc(int G, int ntiles, int H) {
+  int uc = bwd_chunk();
+  while (uc > 4 && (long)G * H * ((ntiles + 1 + uc - 1) / uc) < 8L * prefix_num_cus()) uc /= 2;
+  return uc;
+}
 static int fwd_batch() { static int c = chunk_env("CLIPK_PREFIX_FWD_BATCH", 1); return c; }
 static int bwd_batch() { static int c = chunk_env("CLIPK_PREFIX_BWD_BATCH", 2); return c; }
 // Waves per block (4 or 8; env CLIPK_PREFIX_WPB). Waves are head-fastest, so 8 waves (H = 8)
@@ -1076,7 +1095,7 @@ static int prefix_bwd(int G, int P, int R, int ntiles, const int* tiles, const i
                       const void* qkv, int ldq, const void* ofwd, int ldof, const void* dout, int lddo,
                       const float* lse, void* dqkv, int lddq, float* part, hipStream_t st) {
   constexpr bool mfma = sizeof(TG) == 2 && sizeof(T) == 2;
-  const int uc = mfma ? bwd_chunk() : kValuChunk;
+  const int uc = mfma ? bwd_uc(G, ntiles, H) : kValuChunk;
   const int nchunk = n_chunks(ntiles, uc);
   const long waves = (long)G * nchunk * H;
   if constexpr (mfma && __is_same(T, TG)) {
@@ -1134,7 +1153,8 @@ static int prefix_shape_ok(int G, int P, int R, int ntiles, int heads, int ldq) 
 
 extern "C" size_t clipk_attention_prefix_ws_bytes(int G, int ntiles, int heads) {
   if (G <= 0 || ntiles <= 0 || heads <= 0) return 0;
-  const int uc = bwd_chunk() < kValuChunk ? bwd_chunk() : kValuChunk;  // the larger chunk count
+  const int ub = bwd_uc(G, ntiles, heads);
+  const int uc = ub < kValuChunk ? ub : kValuChunk;  // the larger chunk count
   return (size_t)G * n_chunks(ntiles, uc) * 16 * 2 * heads * 64 * sizeof(float);
 }
 

@@ -705,6 +705,10 @@ static int pick_cfg(int M, int N, int esz) {
   if (M >= 4096 && N % 256 == 0) {
     // 256- vs 192-row tiles: fraction of the last round of CU slots each leaves busy
     const double cus = 256.0;
+    // a big-tile grid under half the CUs (N = 512 at ~6k rows: CoCoOp at 1 image per step):
+    // 128x128 tiles, 3x the blocks (B = 1 step: N = 512 GEMMs 1.06 + 0.52 + 0.22 -> 0.85 + 0.42
+    // + 0.18 ms; N >= 1536 stay on the big tiles, which measured faster there)
+    if (((M + 191) / 192) * (N / 256) < cus / 2) return 0;
     const double w256 = ((M + 255) / 256) * (N / 256) / cus, w192 = ((M + 191) / 192) * (N / 256) / cus;
     const double e256 = w256 / __builtin_ceil(w256), e192 = w192 / __builtin_ceil(w192);
     return e192 > e256 + 0.05 ? 6 : 1;
@@ -735,13 +739,15 @@ static int persist_min(int cus) {
   return v >= 0 ? v : 2 * cus;
 }
 
-// 4-slot ring for 128x128 grids of at most one tile per CU (knob CLIPK_GEMM_DEEP=1; measured
-// equal to the 2-slot ring on the ViT's 1,576-row GEMMs, so off by default)
+// 4-slot ring for 128x128 grids of at most one tile per CU (knob CLIPK_GEMM_DEEP=0 turns it
+// off): three K steps in flight instead of one. Same-box A/B (profiles/r02p_ab_deep_small.txt):
+// ViT forward at 8 images 1.34 -> 1.26 ms, headline step 11.94 -> 11.76 ms; 1-image step
+// 3.92 -> 3.51 ms (its N = 512 text GEMMs run on such grids too)
 static bool deep_small() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("CLIPK_GEMM_DEEP");
-    v = e ? atoi(e) : 0;
+    v = e ? atoi(e) : 1;
   }
   return v != 0;
 }
