@@ -508,13 +508,13 @@ __global__ __launch_bounds__(256) void prefix_tables_kernel(int G, int P, int R,
     rc[i] = r[si];
   }
 }
-// rows [P, R) of group 0 (16-B chunks per row) copied to groups 1..G-1
+// rows [P, R) of group 0 (16-B chunks per row) copied to groups 1..G-1: each chunk read once
+// and stored G-1 times
 __global__ __launch_bounds__(256) void group_bcast_kernel(int G, int P, int R, int chunks, uint4* __restrict__ buf) {
-  const long per = (long)(R - P) * chunks, total = per * (G - 1);
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int g = 1 + (int)(i / per);
-    const long j = i % per;
-    buf[(long)g * R * chunks + (long)P * chunks + j] = buf[(long)P * chunks + j];
+  const long per = (long)(R - P) * chunks;
+  for (long j = (long)blockIdx.x * 256 + threadIdx.x; j < per; j += (long)gridDim.x * 256) {
+    const uint4 v = buf[(long)P * chunks + j];
+    for (int g = 1; g < G; ++g) buf[(long)g * R * chunks + (long)P * chunks + j] = v;
   }
 }
 static int prefix_tables(const SeqShape& sh, bool shared, int* prow, const float* m, const float* r, float* mc,
@@ -550,7 +550,7 @@ static int block_attn_shared0(const clipk_encoder* e, const std::array<const voi
     ProfScope ps(CLIPK_PROF_NONE, st, 0.0, "text.qkv_bcast", (double)(G - 1) * (R - P) * qa * 2.0);
     if (G > 2) TRY(clipk_rows_copy((int)qa, (G - 2) * P, (char*)qkv + (size_t)(R + P) * qa, nullptr, qkv, prow + 2 * P, st));
     const int chunks = (int)(qa / 16);
-    const long total = (long)(R - P) * chunks * (G - 1);
+    const long total = (long)(R - P) * chunks;
     hipLaunchKernelGGL(group_bcast_kernel, dim3((unsigned)std::min<long>((total + 255) / 256, 4096)), dim3(256), 0, st,
                        G, P, R, chunks, (uint4*)qkv);
     CLIPK_CHECK_LAUNCH();
