@@ -711,7 +711,10 @@ static int pick_cfg(int M, int N, int esz) {
     if (((M + 191) / 192) * (N / 256) < cus / 2) return 0;
     const double w256 = ((M + 255) / 256) * (N / 256) / cus, w192 = ((M + 191) / 192) * (N / 256) / cus;
     const double e256 = w256 / __builtin_ceil(w256), e192 = w192 / __builtin_ceil(w192);
-    return e192 > e256 + 0.05 ? 6 : 1;
+    // 192-row tiles only for a clear quantisation win: N = 512 at 47k rows (0.72 -> 0.96 of the
+    // last round busy) measured 4 % faster; N = 1536 (0.87 -> 0.96) 5 % slower
+    // (profiles/r02p_gemm_tile_rows.txt)
+    return e192 > e256 + 0.15 ? 6 : 1;
   }
   return 0;
 }
