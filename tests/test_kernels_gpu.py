@@ -162,6 +162,22 @@ def test_gemm_bias_res_16bit(dev, dtype):
         close(ops.gemm(A, B, N.EPI_BIAS_RES, dtype, bias=bias, res=res), ref, dtype, f"res16 M{M}")
 
 
+@pytest.mark.parametrize("K", [512, 2048])
+def test_gemm_bench_shape_n512(dev, K):
+    """N = 512 at the headline's 47,160 rows (192x256 ping-pong tiles, 1.92 rounds of CUs): the
+    input-grad form (fp16 out) and the 16-bit residual form, every row against torch fp32."""
+    M, dtype = 47160, torch.float16
+    g = torch.Generator().manual_seed(K)
+    A = torch.randn(M, K, generator=g).to(dev).to(dtype)
+    B = (torch.randn(512, K, generator=g) / math.sqrt(K)).to(dev).to(dtype)
+    bias = torch.randn(512, generator=g).to(dev)
+    res = torch.randn(M, 512, generator=g).to(dev).to(dtype)
+    ref = A.float() @ B.float().t()
+    close(ops.gemm(A, B, N.EPI_NONE, dtype), ref, dtype, f"n512 none K{K}")
+    close(ops.gemm(A, B, N.EPI_BIAS_RES, dtype, bias=bias, res=res), ref + bias + res.float(), dtype,
+          f"n512 res16 K{K}")
+
+
 def attn_ref(qkv, nseq, L, H, causal):
     W = H * 64
     q, k, v = qkv.float().view(nseq, L, 3, H, 64).permute(2, 0, 3, 1, 4)

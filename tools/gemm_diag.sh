@@ -8,6 +8,7 @@ for t in "$@"; do
   # cfgN = the in-tree library with CLIPK_GEMM_CFG=N (tile configuration forced)
   case $t in
     base) L=""; CFG="";;
+    env:*) L=""; CFG=""; export ${t#env:};;
     cfg*) L=""; CFG=${t#cfg};;
     *) L=$R/build_ab/$t/libclipk.so; CFG="";;
   esac
