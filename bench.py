@@ -21,6 +21,8 @@ The JSON line also carries (rank 0, N=1 unless noted):
 * ``eval_images_per_sec`` over --eval-images (default 5,000) images, test batch 100;
 * ``fp32``: train / eval images/sec at PREC fp32 (the 1e-3-logit parity path);
 * ``batch1``: train images/sec at 1 image per step (the reference CoCoOp config batch size);
+* ``coop``: BASELINE config 2 -- CoOp n_ctx 16, ViT-B/16, 1000 classes, batch 32: train and
+  eval images/sec;
 * ``cpu_baseline``: the oracle (fp32 restatement) on the host cores, with nproc stated.
 """
 from __future__ import annotations
@@ -165,6 +167,33 @@ def roofline_of(table, prec):
               "flops_per_launch": fl, "algorithmic_bytes": by,
               "traffic_note": "HBM bytes/launch, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (profiles/r02_pmc)"})
     return r
+
+
+def build_coop_trainer(args, prec, batch, dev, rank, n_test=0):
+    """BASELINE config 2: CoOp n_ctx=16 (random init, class token at the end, shared context),
+    ViT-B/16, fp16, 1000 classes (ImageNet-LT size), train batch 32 (configs/trainers/CoOp/
+    vit_b16.yaml:3), test batch 100."""
+    from fsp_amd.engine.config import get_cfg_default
+    from fsp_amd.data.synthetic import SyntheticDataManager
+    from fsp_amd.trainers.coop import CoOp
+    from fsp_amd.clip import synth
+    arch = synth.ARCHS[args.arch]
+    cfg = get_cfg_default()
+    cfg.TRAINER.NAME = "CoOp"
+    cfg.MODEL.BACKBONE.NAME = args.arch
+    cfg.INPUT.SIZE = (arch.image_resolution, arch.image_resolution)
+    c = cfg.TRAINER.COOP
+    c.N_CTX, c.CTX_INIT, c.CSC, c.CLASS_TOKEN_POSITION, c.PREC = 16, "", False, "end", prec
+    cfg.DATALOADER.TRAIN_X.BATCH_SIZE = batch
+    cfg.DATASET.NUM_SHOTS = 16
+    cfg.OPTIM.MAX_EPOCH = 10
+    cfg.TEST.NO_TEST = True
+    dm = SyntheticDataManager(args.classes, arch.image_resolution, batch, n_batches=2, test_batch=100,
+                              n_test=n_test, device=dev, rank=rank)
+    with contextlib.redirect_stdout(io.StringIO()):
+        trainer = CoOp(cfg, dm=dm)
+    trainer.num_batches = 10 ** 9
+    return trainer, dm
 
 
 def build_trainer(args, prec, batch, dev, rank, n_test=0):
@@ -321,13 +350,25 @@ def main():
     }
     del trainer, dm
     torch.cuda.empty_cache()
-    if not args.no_extra:
+    if not args.no_extra and world == 1:  # the N > 1 scaling runs report the headline lines only
         # the reference's batch size for CoCoOp (configs/trainers/CoCoOp/*.yaml: 1 image/step)
         tr1, dm1 = build_trainer(args, args.prec, 1, dev, rank)
         t1, _ = time_train(tr1, dm1, 10, 3)
         out["batch1"] = {"images_per_sec": round(world * 10 / t1, 3), "ms_per_step": round(100 * t1, 3),
                          "images_per_gpu_per_step": 1}
         del tr1, dm1
+        torch.cuda.empty_cache()
+        # BASELINE config 2: CoOp n_ctx 16, ViT-B/16 fp16, 1000 classes, batch 32
+        trc, dmc = build_coop_trainer(args, args.prec, 32, dev, rank, n_test=1000)
+        tc, _ = time_train(trc, dmc, 10, 3)
+        ec, nc = time_eval(trc, dmc, 1000)
+        out["coop"] = {"workload": f"CoOp {args.arch} n_ctx=16 end, {args.classes} classes, 32 images/GPU/step, "
+                                   f"{args.prec}", "images_per_sec": round(world * 32 * 10 / tc, 3),
+                       "ms_per_step": round(100 * tc, 3), "eval_images_per_sec": round(ec, 3),
+                       "eval_images": int(dist.sum_over_ranks(nc)),
+                       "text_layout": ("shared-prefix packed" if trc.model.prompt_learner.layout.pack is not None
+                                       else "plain")}
+        del trc, dmc
         torch.cuda.empty_cache()
         # PREC fp32: f32-input MFMA everywhere, the path that meets |d logit| <= 1e-3
         tr32, dm32 = build_trainer(args, "fp32", args.batch, dev, rank, n_test=500)
