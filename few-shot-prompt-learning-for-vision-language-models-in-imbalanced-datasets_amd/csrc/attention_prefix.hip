@@ -1032,6 +1032,19 @@ __global__ __launch_bounds__(256) void prefix_kv_reduce(int P, int R, int W, int
   const size_t cs = (size_t)16 * 2 * W;  // chunk stride
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // 4 independent chains, fixed order
   int k = 0;
+  // 16 chunks' loads in flight per round trip (the sums keep the 4-chain order)
+  for (; k + 16 <= nchunk; k += 16) {
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = src[(k + i) * cs];
+#pragma unroll
+    for (int i = 0; i < 16; i += 4) {
+      a0 += v[i];
+      a1 += v[i + 1];
+      a2 += v[i + 2];
+      a3 += v[i + 3];
+    }
+  }
   for (; k + 4 <= nchunk; k += 4) {
     a0 += src[k * cs];
     a1 += src[(k + 1) * cs];

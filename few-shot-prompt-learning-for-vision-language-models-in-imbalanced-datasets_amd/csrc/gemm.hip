@@ -953,8 +953,18 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(int S, int M, int N,
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= (long)M * n4) return;
   const int m = (int)(i / n4), c = (int)(i % n4) * 4;
-  f32x4 v = *reinterpret_cast<const f32x4*>(part + (size_t)m * N + c);
-  for (int s = 1; s < S; ++s) v += *reinterpret_cast<const f32x4*>(part + ((size_t)s * M + m) * N + c);
+  // the first 8 slices' loads all issued before the sums (clamped to valid slices: no load
+  // behind a branch), summed in slice order
+  constexpr int SB = 8;
+  f32x4 t[SB];
+#pragma unroll
+  for (int s = 0; s < SB; ++s)
+    t[s] = *reinterpret_cast<const f32x4*>(part + ((size_t)(s < S ? s : S - 1) * M + m) * N + c);
+  f32x4 v = t[0];
+#pragma unroll
+  for (int s = 1; s < SB; ++s)
+    if (s < S) v += t[s];
+  for (int s = SB; s < S; ++s) v += *reinterpret_cast<const f32x4*>(part + ((size_t)s * M + m) * N + c);
   if constexpr (EPI != CLIPK_EPI_NONE) v += *reinterpret_cast<const f32x4*>(bias + c);
   if constexpr (EPI == CLIPK_EPI_BIAS_RES) v += *reinterpret_cast<const f32x4*>(res + (size_t)m * ldr + c);
   if constexpr (EPI == CLIPK_EPI_BIAS_QGELU) {
