@@ -25,8 +25,11 @@
 
 namespace clipk {
 
+// residual / aux lookahead ring of the 256-row tiles, VGPRs: 16 = two row groups of a 16-bit
+// aux (the dgelu GEMM's h) in flight; still no spill at 251 VGPRs. Same-box A/B
+// (profiles/r02r/ab_xbud256.txt): dgelu 1.587 -> 1.488 ms/step, headline 11.92 -> 11.80 ms.
 #ifndef CLIPK_XBUD256
-#define CLIPK_XBUD256 8
+#define CLIPK_XBUD256 16
 #endif
 constexpr int GEMM_ROWB = 128;  // bytes per staged row (BK = 64 halfs / 32 floats)
 constexpr int GEMM_NMIN = 128;  // N granularity accepted by the C-ABI
