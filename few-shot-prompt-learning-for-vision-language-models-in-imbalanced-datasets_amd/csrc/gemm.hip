@@ -31,6 +31,9 @@ namespace clipk {
 #ifndef CLIPK_XBUD256
 #define CLIPK_XBUD256 16
 #endif
+#ifndef CLIPK_XBUD192
+#define CLIPK_XBUD192 32
+#endif
 constexpr int GEMM_ROWB = 128;  // bytes per staged row (BK = 64 halfs / 32 floats)
 constexpr int GEMM_NMIN = 128;  // N granularity accepted by the C-ABI
 constexpr int EPI_SCRATCH = 16 * 64 * 4;  // per-wave epilogue transpose tile [16][64] fp32
@@ -396,7 +399,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
     constexpr int XNB = CW * (int)sizeof(TX);
     typedef Raw<XNB> XR;
     constexpr int XREG = NQ * XNB / 4;
-    constexpr int XBUD = BM == 192 ? 32 : CLIPK_XBUD256;  // ring VGPRs (256-row tiles: little to spare)
+    constexpr int XBUD = BM == 192 ? CLIPK_XBUD192 : CLIPK_XBUD256;  // ring VGPRs (256-row tiles: little to spare)
     constexpr int XD = XBUD / XREG < 1 ? 1 : (XBUD / XREG > TM ? TM : XBUD / XREG);
     XR extq[XD][NQ];
     auto load_ext = [&](int i, XR* dst) {
