@@ -3,7 +3,10 @@
 on the MI355X-native path (BASELINE.json metric, configs[2]).
 
     python bench.py --gpus N --steps K --warmup W
-    (N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...)
+    (N > 1 without a torchrun environment: this process starts
+     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ...
+     bench.py ... as a child -- before anything touches the GPU -- relays its output and exits
+     with its return code; under torchrun every rank runs the benchmark and rank 0 prints)
 
 A step = one CoCoOp.forward_backward on a resident synthetic batch: ViT-B/16 image
 encode -> Meta-Net -> B*C conditional prompts -> text encoder fwd + input-grad bwd ->
@@ -18,12 +21,19 @@ The JSON line also carries (rank 0, N=1 unless noted):
   (events inside the timed region would add ~15 % wall time), and its HBM traffic from the
   committed rocprofv3 PMC passes; ``kernels``: the same for every kernel class of the step
   (GEMMs: fraction of the MFMA peak; attention / LayerNorm: GB/s and fraction of the HBM peak);
-* ``eval_images_per_sec`` over --eval-images (default 5,000) images, test batch 100;
+* ``eval_images_per_sec`` over --eval-images (default 50,000: SURVEY §8(d)'s full ImageNet-val
+  size) distinct synthetic images resident in HBM, test batch 100, sharded over the ranks;
 * ``fp32``: train / eval images/sec at PREC fp32 (the 1e-3-logit parity path);
 * ``batch1``: train images/sec at 1 image per step (the reference CoCoOp config batch size);
 * ``coop``: BASELINE config 2 -- CoOp n_ctx 16, ViT-B/16, 1000 classes, batch 32: train and
   eval images/sec;
-* ``cpu_baseline``: the oracle (fp32 restatement) on the host cores, with nproc stated.
+* ``batch1_class_shard`` (N > 1): the reference's CoCoOp batch of 1 image per step with its
+  1,000 classes sharded over the N ranks (SURVEY §8(e) Option B: logit all-gather + SUM
+  all-reduce of the prompt gradients), strong scaling of that step;
+* ``cpu_baseline``: the oracle (fp32 restatement) on the host cores, with nproc stated, and the
+  reference's own CPU path at 1,000 classes as measured in the build container
+  (tools/ref_cpu_timing.py -> profiles/r03_ref_cpu_timing.jsonl; the reference does not travel
+  to the GPU box).
 """
 from __future__ import annotations
 
@@ -38,7 +48,47 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-METRIC = "CoCoOp ViT-B/16 16-shot train-step images/sec at 1/2/4/8 GPUs; eval images/sec"
+def metric_name(arch):
+    """BASELINE.json's metric, for the --arch being run (ViT-B/16 by default)."""
+    return f"CoCoOp {arch} 16-shot train-step images/sec at 1/2/4/8 GPUs; eval images/sec"
+
+
+REF_CPU_FILE = os.path.join(ROOT, "profiles", "r03_ref_cpu_timing.jsonl")
+
+
+def launcher_cmd(argv, n, port):
+    """The torchrun command bench.py --gpus N (N > 1) starts as its child: one rank per GPU
+    of this node, rendezvous on 127.0.0.1, the same bench arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def reference_cpu(arch, classes):
+    """The reference's own CPU train step (PromptSRC CoCoOp CustomCLIP + torch SGD, fp32) at
+    this config, measured in the build container (8 threads): images/sec, or None."""
+    try:
+        with open(REF_CPU_FILE) as f:
+            rows = [json.loads(l) for l in f if l.strip()]
+    except OSError:
+        return None
+    for r in rows:
+        if r.get("config") == 3 and r.get("arch") == arch and r.get("classes") == classes:
+            return {"value": r["images_per_sec"], "unit": "images/sec", "cores": r["threads"], "kind": "reference",
+                    "sample": (f"reference CoCoOp {arch} (PromptSRC/trainers/cocoop.py CustomCLIP + torch.optim.SGD, "
+                               f"fp32, 77-token prompts), 1 image x {classes} classes per step, median of "
+                               f"{len(r['step_s_all'])} steps ({r['step_s_median']} s/step), {r['threads']} threads "
+                               f"of the build container's {r['nproc']}-core Xeon (not the GPU box: the reference "
+                               f"does not travel); {REF_CPU_FILE[len(ROOT) + 1:]}")}
+    return None
 PEAK = {"fp16": 2500.0, "bf16": 2500.0, "amp": 2500.0, "fp32": 157.3}  # dense TFLOP/s (MI355X guide)
 HBM_PEAK_GBS = 8000.0  # HBM3E, MI355X_MICROARCH.md
 PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc", "traffic.json")
@@ -169,7 +219,7 @@ def roofline_of(table, prec):
     return r
 
 
-def build_coop_trainer(args, prec, batch, dev, rank, n_test=0):
+def build_coop_trainer(args, prec, batch, dev, rank, n_test=0, n_test_device=0):
     """BASELINE config 2: CoOp n_ctx=16 (random init, class token at the end, shared context),
     ViT-B/16, fp16, 1000 classes (ImageNet-LT size), train batch 32 (configs/trainers/CoOp/
     vit_b16.yaml:3), test batch 100."""
@@ -189,14 +239,14 @@ def build_coop_trainer(args, prec, batch, dev, rank, n_test=0):
     cfg.OPTIM.MAX_EPOCH = 10
     cfg.TEST.NO_TEST = True
     dm = SyntheticDataManager(args.classes, arch.image_resolution, batch, n_batches=2, test_batch=100,
-                              n_test=n_test, device=dev, rank=rank)
+                              n_test=n_test, device=dev, rank=rank, n_test_device=n_test_device)
     with contextlib.redirect_stdout(io.StringIO()):
         trainer = CoOp(cfg, dm=dm)
     trainer.num_batches = 10 ** 9
     return trainer, dm
 
 
-def build_trainer(args, prec, batch, dev, rank, n_test=0):
+def build_trainer(args, prec, batch, dev, rank, n_test=0, n_test_device=0, class_shard=False):
     from fsp_amd.engine.config import get_cfg_default
     from fsp_amd.data.synthetic import SyntheticDataManager
     from fsp_amd.trainers.cocoop import CoCoOp
@@ -215,8 +265,9 @@ def build_trainer(args, prec, batch, dev, rank, n_test=0):
     cfg.OPTIM.WARMUP_EPOCH = 1
     cfg.OPTIM.WARMUP_TYPE = "constant"
     cfg.TEST.NO_TEST = True
+    cfg.NATIVE.COCOOP_SHARD = "class" if class_shard else "image"
     dm = SyntheticDataManager(args.classes, arch.image_resolution, batch, n_batches=2, test_batch=100,
-                              n_test=n_test, device=dev, rank=rank)
+                              n_test=n_test, device=dev, rank=rank, n_test_device=n_test_device)
     with contextlib.redirect_stdout(io.StringIO()):
         trainer = CoCoOp(cfg, dm=dm)  # broadcasts the prompt parameters (N>1)
     trainer.num_batches = 10 ** 9  # keep update_lr out of the timed loop (epoch boundary)
@@ -296,13 +347,21 @@ def main():
     ap.add_argument("--classes", type=int, default=1000)
     ap.add_argument("--arch", default="ViT-B/16")
     ap.add_argument("--prec", default="fp16")
-    ap.add_argument("--eval-images", type=int, default=5000)
+    ap.add_argument("--eval-images", type=int, default=50000)
     ap.add_argument("--cpu-classes", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--prof-steps", type=int, default=3, help="steps after the timed ones with per-site hipEvents")
     ap.add_argument("--no-prof", action="store_true", help="no per-site profiling steps")
     ap.add_argument("--no-extra", action="store_true", help="skip the fp32 / batch-1 lines")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one rank per GPU: torchrun as a CHILD process (this process has not touched the GPU)
+        import subprocess
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        rc = subprocess.call(launcher_cmd(sys.argv[1:], args.gpus, _free_port()), env=env)
+        sys.exit(rc)
 
     import torch
     from fsp_amd import dist
@@ -311,24 +370,28 @@ def main():
     local = dist.init_from_env()
     world = dist.world_size()
     rank = dist.rank()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but the process group has {world} ranks")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     arch = synth.ARCHS[args.arch]
+    n_eval_rank = dist.shard_range(args.eval_images)[1] - dist.shard_range(args.eval_images)[0]
 
-    trainer, dm = build_trainer(args, args.prec, args.batch, dev, rank, n_test=1000)
+    trainer, dm = build_trainer(args, args.prec, args.batch, dev, rank, n_test_device=n_eval_rank)
     lay = trainer.model.prompt_learner.layout
     L = lay.L
     n_prof = 0 if args.no_prof else args.prof_steps
     t, sites = time_train(trainer, dm, args.steps, args.warmup, prof_steps=n_prof)
     table = kernel_table(sites, n_prof, args.prec) if sites else None
     roof = roofline_of(table, args.prec) if table else None
-    eval_ips, n_eval = time_eval(trainer, dm, args.eval_images)
+    eval_ips, n_eval = time_eval(trainer, dm, n_eval_rank)
 
     f_img, f_txt, b_txt = flops(arch, args.classes, L)
     step_flops = args.batch * (f_img + args.classes * (f_txt + b_txt))
     value = world * args.batch * args.steps / t
     out = {
-        "metric": METRIC, "value": round(value, 3), "unit": "images/sec", "n_gpus": world,
+        "metric": metric_name(args.arch), "value": round(value, 3), "unit": "images/sec", "n_gpus": world,
+        "rccl_world": world, "backend": torch.distributed.get_backend() if dist.is_dist() else None,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * t / args.steps, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.prec,
         "data": "synthetic (seeded U[0,1) CLIP-normalised images, random-init CLIP weights)",
@@ -341,6 +404,7 @@ def main():
                                   else f"plain [B*C, {L}]"},
         "eval_images_per_sec": round(eval_ips, 3),
         "eval_images": int(dist.sum_over_ranks(n_eval)),
+        "eval_note": "forward only, test batch 100, distinct resident images sharded over the ranks",
         # reference-equivalent FLOPs (plain [B*C, L_eff] layout) per second, not executed FLOPs
         "model_tflops_per_gpu": round(step_flops * args.steps / t / 1e12, 2),
         "roofline": roof,
@@ -350,6 +414,15 @@ def main():
     }
     del trainer, dm
     torch.cuda.empty_cache()
+    if not args.no_extra and world > 1:
+        # the reference's CoCoOp batch (1 image / step) with the classes sharded over the ranks
+        tr1, dm1 = build_trainer(args, args.prec, 1, dev, 0, class_shard=True)
+        t1, _ = time_train(tr1, dm1, 10, 3)
+        out["batch1_class_shard"] = {"images_per_sec": round(10 / t1, 3), "ms_per_step": round(100 * t1, 3),
+                                     "global_batch": 1, "classes_per_rank": tr1.model.prompt_learner.layout.n_cls,
+                                     "scaling": "strong"}
+        del tr1, dm1
+        torch.cuda.empty_cache()
     if not args.no_extra and world == 1:  # the N > 1 scaling runs report the headline lines only
         # the reference's batch size for CoCoOp (configs/trainers/CoCoOp/*.yaml: 1 image/step)
         tr1, dm1 = build_trainer(args, args.prec, 1, dev, rank)
@@ -359,9 +432,9 @@ def main():
         del tr1, dm1
         torch.cuda.empty_cache()
         # BASELINE config 2: CoOp n_ctx 16, ViT-B/16 fp16, 1000 classes, batch 32
-        trc, dmc = build_coop_trainer(args, args.prec, 32, dev, rank, n_test=1000)
+        trc, dmc = build_coop_trainer(args, args.prec, 32, dev, rank, n_test_device=args.eval_images)
         tc, _ = time_train(trc, dmc, 10, 3)
-        ec, nc = time_eval(trc, dmc, 1000)
+        ec, nc = time_eval(trc, dmc, args.eval_images)
         out["coop"] = {"workload": f"CoOp {args.arch} n_ctx=16 end, {args.classes} classes, 32 images/GPU/step, "
                                    f"{args.prec}", "images_per_sec": round(world * 32 * 10 / tc, 3),
                        "ms_per_step": round(100 * tc, 3), "eval_images_per_sec": round(ec, 3),
@@ -386,6 +459,7 @@ def main():
             cb8 = cpu_baseline(args.arch, "a photo of a", args.classes, args.cpu_classes, min(8, threads))
             cb["value_8_threads"] = cb8["value"]
             cb["sample_8_threads"] = cb8["sample"]
+            cb["reference"] = reference_cpu(args.arch, args.classes)
             out["cpu_baseline"] = cb
         except Exception as e:  # report, never fake
             out["cpu_baseline"] = {"value": None, "error": repr(e)}

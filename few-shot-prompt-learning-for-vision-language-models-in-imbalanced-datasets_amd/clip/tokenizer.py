@@ -5,10 +5,12 @@ SOT 49406, EOT 49407, digits one token each) and ``PromptSRC/clip/clip.py:185-22
 (SOT + BPE + EOT, zero-padded to 77, RuntimeError when too long unless truncate).
 
 The merges file (``bpe_simple_vocab_16e6.txt.gz``) is OpenAI's public CLIP vocab; it is
-not shipped here. It is looked up at ``$FSP_BPE_VOCAB``, next to this file, or in the
-reference checkout. Without it, a small word→id table (``bpe_fallback.json``, generated
-from the vocab by ``tests/golden/make_golden.py``) covers the synthetic prompts used by
-tests and benchmarks ("X", "a photo of a", "classK."); anything else raises.
+not shipped here. It is looked up at ``$FSP_BPE_VOCAB`` or next to this file (copy it there
+once on a box with real datasets); no other location is searched. Without it, a small
+word→id table (``bpe_fallback.json``, generated from the vocab by
+``tests/golden/make_golden.py``) covers the synthetic prompts used by tests and benchmarks
+("X", "a photo of a", "classK."); any other word raises a KeyError that names the file and
+the variable.
 """
 from __future__ import annotations
 
@@ -39,7 +41,6 @@ def _vocab_candidates():
     if env:
         yield env
     yield os.path.join(_HERE, "bpe_simple_vocab_16e6.txt.gz")
-    yield "/root/reference/PromptSRC/clip/bpe_simple_vocab_16e6.txt.gz"
 
 
 def find_vocab():
@@ -129,8 +130,9 @@ class BPETokenizer:
     def encode_word(self, word: str):
         if self.encoder is None:
             if word not in self._fallback:
-                raise KeyError(f"BPE vocab not found and '{word}' is not in the fallback "
-                               f"table; set FSP_BPE_VOCAB to bpe_simple_vocab_16e6.txt.gz")
+                raise KeyError(f"CLIP BPE vocab not found and '{word}' is not in the synthetic-name "
+                               f"fallback table: set $FSP_BPE_VOCAB to the path of "
+                               f"bpe_simple_vocab_16e6.txt.gz (or copy it to {_HERE})")
             return list(self._fallback[word])
         ab = _byte_alphabet()
         w = "".join(ab[b] for b in word.encode("utf-8"))

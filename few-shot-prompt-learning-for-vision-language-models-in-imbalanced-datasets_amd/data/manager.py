@@ -18,8 +18,16 @@ SequentialSampler, torch's global RNG, which dist.sync_rng_from(0) makes identic
 rank each epoch), so every rank walks the SAME global index stream; it is cut into global
 batches of BATCH_SIZE x world (drop_last as the reference: when the set holds a full batch)
 and rank r takes its contiguous slice (dist.shard_range). Each batch carries ``n_global``
-so the trainers weight the gradient all-reduce by the rank's share (engine/trainer.py). The
-test split is sharded contiguously; ``TrainerX.test`` gathers the predictions.
+and ``n_local`` so the trainers weight the gradient all-reduce by the rank's share
+(engine/trainer.py). The test split is sharded contiguously; ``TrainerX.test`` gathers the
+predictions. CoCoOp class sharding (dist.batches_replicated) instead gives every rank the
+whole global batch and the whole test split.
+
+Augmentation: the random-resized-crop / flip parameters come from a generator of the
+transform's own (``augment_generator``), not from torch's global RNG -- that one is synced
+across ranks every epoch for the sampler stream, so drawing crops from it would give rank r's
+k-th image the same crop as rank 0's. Data parallel: one stream per rank (seed + rank);
+replicated batches: one stream shared by every rank (they must preprocess identically).
 """
 from __future__ import annotations
 
@@ -38,10 +46,21 @@ def read_image(path):
         return np.asarray(im.convert("RGB"), dtype=np.uint8)
 
 
+def augment_generator(replicated: bool, seed: int | None = None) -> torch.Generator:
+    """CPU generator of the training augmentation stream: seeded from rank 0's torch seed
+    (``seed`` overrides it) + this rank's index (data parallel) or + 0 on every rank
+    (replicated batches)."""
+    base = dist.broadcast_int(torch.initial_seed() if seed is None else seed) & ((1 << 62) - 1)
+    g = torch.Generator()
+    g.manual_seed(base + (0 if replicated else 1_000_003 * (1 + dist.rank())))
+    return g
+
+
 class ShardedBatchSampler(Sampler):
     """Global batches of batch_size x world from ``sampler``; yields rank r's slice of each
-    as a list of (index, global batch size) keys. A rank whose slice of a short last batch
-    would be empty repeats the batch's first item (every rank must join the all-reduce)."""
+    as a list of (index, global batch size, local batch size) keys. A rank whose slice of a
+    short last batch would be empty gets the batch's first item as a pad with local size 0
+    (every rank must join the all-reduce; the pad's loss weight is 0)."""
 
     def __init__(self, sampler, batch_size, drop_last, rank=None, world=None):
         self.sampler = sampler
@@ -62,8 +81,10 @@ class ShardedBatchSampler(Sampler):
     def __iter__(self):
         for chunk in self.global_batches():
             lo, hi = dist.shard_range(len(chunk), self.rank, self.world)
-            mine = chunk[lo:hi] if hi > lo else chunk[:1]
-            yield [(int(i), len(chunk)) for i in mine]
+            if hi > lo:
+                yield [(int(i), len(chunk), hi - lo) for i in chunk[lo:hi]]
+            else:
+                yield [(int(chunk[0]), len(chunk), 0)]
 
     def __len__(self):
         n = len(self.sampler)
@@ -93,10 +114,10 @@ class DatasetWrapper(Dataset):
         return len(self.data_source)
 
     def __getitem__(self, key):
-        idx, n_global = key if isinstance(key, tuple) else (key, 0)
+        idx, n_global, n_local = key if isinstance(key, tuple) else (key, 0, 0)
         item = self.data_source[idx]
         return {"img": self.reader(item.impath), "label": item.label, "domain": item.domain,
-                "impath": item.impath, "index": idx, "n_global": n_global}
+                "impath": item.impath, "index": idx, "n_global": n_global, "n_local": n_local}
 
 
 def _collate(items):
@@ -105,7 +126,7 @@ def _collate(items):
             "domain": torch.tensor([it["domain"] for it in items], dtype=torch.int64),
             "impath": [it["impath"] for it in items],
             "index": torch.tensor([it["index"] for it in items], dtype=torch.int64),
-            "n_global": items[0]["n_global"]}
+            "n_global": items[0]["n_global"], "n_local": items[0]["n_local"]}
 
 
 class GpuLoader:
@@ -131,7 +152,8 @@ class DataManager:
         self.dataset = dataset
         self.device = torch.device(device)
         nw = cfg.DATALOADER.NUM_WORKERS if num_workers is None else num_workers
-        rank, world = dist.rank(), dist.world_size()
+        self.replicated = dist.batches_replicated(cfg)
+        rank, world = (0, 1) if self.replicated else (dist.rank(), dist.world_size())
 
         train = dataset.train_x
         bs = cfg.DATALOADER.TRAIN_X.BATCH_SIZE
@@ -141,7 +163,8 @@ class DataManager:
         self.train_loader_x = GpuLoader(
             DataLoader(DatasetWrapper(train, reader), batch_sampler=self.train_batch_sampler, num_workers=nw,
                        collate_fn=_collate, pin_memory=False),
-            GpuTransform(cfg, is_train=True, device=self.device), self.device)
+            GpuTransform(cfg, is_train=True, device=self.device, generator=augment_generator(self.replicated)),
+            self.device)
 
         def test_loader(data):
             if not data:

@@ -15,9 +15,10 @@ do the integer multiply-accumulate, the uint8 rounding/clipping of both passes, 
 window, the flip and ToTensor/Normalize in fp32 -- bit-exact to the PIL + torch pipeline
 (tests/test_preprocess_*.py check against Pillow itself).
 
-Random crop parameters and the flip coin use torch's CPU generator in torchvision's call
-order (RandomResizedCrop.get_params, RandomHorizontalFlip), restated here: torchvision is
-not installed, so that sequence is parity-unpinned (documented in DESIGN.md).
+Random crop parameters and the flip coin use a torch CPU generator (the transform's own, or
+the global one) in torchvision's call order (RandomResizedCrop.get_params,
+RandomHorizontalFlip), restated here: torchvision is not installed, so that sequence is
+parity-unpinned (documented in DESIGN.md).
 """
 from __future__ import annotations
 
@@ -183,7 +184,7 @@ class GpuTransform:
     """Dassl transform_train / transform_test equivalent for the CoOp/CoCoOp configs
     (random_resized_crop + random_flip + normalize / resize + center_crop + normalize)."""
 
-    def __init__(self, cfg, is_train, device="cuda"):
+    def __init__(self, cfg, is_train, device="cuda", generator=None):
         choices = list(cfg.INPUT.TRANSFORMS)
         allowed = {"random_resized_crop", "random_flip", "normalize"}
         if is_train and not set(choices) <= allowed:
@@ -199,17 +200,17 @@ class GpuTransform:
         self.mean = tuple(cfg.INPUT.PIXEL_MEAN) if norm else (0.0, 0.0, 0.0)
         self.std = tuple(cfg.INPUT.PIXEL_STD) if norm else (1.0, 1.0, 1.0)
         self.device = device
+        self.generator = generator  # None: torch's global CPU RNG
 
     def plan(self, w, h):
         if not self.is_train:
             return test_plan(w, h, self.size)
         if self.rrc:
-            p = train_plan(w, h, self.size, self.scale, 0.5 if self.flip else 0.0)
-            return p
+            return train_plan(w, h, self.size, self.scale, 0.5 if self.flip else 0.0, generator=self.generator)
         rw = rh = self.size  # Resize(input_size) when no random crop
         p = Plan(0, 0, w, h, rw, rh, 0, 0, self.size, False)
         if self.flip:
-            p.flip = bool(torch.rand(1) < 0.5)
+            p.flip = bool(torch.rand(1, generator=self.generator) < 0.5)
         return p
 
     def __call__(self, images):

@@ -9,8 +9,13 @@ per step the collectives are:
   fp32, latency-bound on xGMI) -- ``allreduce_grads``;
 * CoOp with class-sharded text encoding: an all-gather of the [C, E] text
   features and, in backward, a reduce-scatter of dL/dtext to the class owners --
-  ``AllGatherRows``.
+  ``AllGatherRows``;
+* CoCoOp with class sharding (SURVEY §8(e) Option B, the reference's batch-1 configs):
+  every rank scores the same images against its C/W classes, one all-gather of the
+  [B, C_r] logits (``GatherClassColumns``) and a SUM all-reduce of the prompt gradients.
 Eval shards the test set and gathers (label, prediction) pairs -- ``all_gather_varlen``.
+The uneven-shard pad / unpad (``pad_rank_blocks`` / ``unpad_rank_blocks``) is shared by the
+RCCL and gloo branches; only the collective call itself differs.
 With the gloo backend (CPU tests, or several ranks sharing one GPU) CUDA tensors go through
 host copies.
 """
@@ -99,6 +104,15 @@ def broadcast_params(params, src: int = 0):
             off += n
 
 
+def batches_replicated(cfg) -> bool:
+    """True when every rank must see the SAME batches and test images: CoCoOp with class
+    sharding (cfg NATIVE.COCOOP_SHARD "class") at world > 1. Otherwise batches are split over
+    the ranks (data parallel)."""
+    nat = cfg.get("NATIVE", {}) or {}
+    return (world_size() > 1 and str(cfg.TRAINER.get("NAME", "")) == "CoCoOp"
+            and nat.get("COCOOP_SHARD", "image") == "class")
+
+
 def shard_range(n: int, r: int | None = None, w: int | None = None):
     """Contiguous [lo, hi) share of n items for rank r of w (eval-set sharding)."""
     r = rank() if r is None else r
@@ -128,45 +142,98 @@ def all_gather_varlen(t):
     return out.to(t.device)
 
 
+def pad_rank_blocks(x, counts):
+    """Rows [sum(counts), ...] in rank order -> [w * m, ...] (m = max(counts)) with rank i's
+    rows at block i and zero padding after them: the equal-size layout that all-gather /
+    reduce-scatter of uneven row shards need."""
+    w, m = len(counts), max(counts)
+    x = x.contiguous()
+    if x.shape[0] != sum(counts):
+        raise ValueError(f"{x.shape[0]} rows for shard counts {counts}")
+    out = torch.zeros((w * m,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    off = 0
+    for i, k in enumerate(counts):
+        out[i * m:i * m + k] = x[off:off + k]
+        off += k
+    return out
+
+
+def unpad_rank_blocks(padded, counts):
+    """Inverse of pad_rank_blocks: [w * m, ...] blocks -> rows [sum(counts), ...]."""
+    m = max(counts)
+    return torch.cat([padded[i * m:i * m + k] for i, k in enumerate(counts)], 0)
+
+
+def reduce_scatter_rows(g, counts):
+    """Sum ``g`` [sum(counts), ...] over ranks; return this rank's rows (counts[rank]).
+    RCCL: reduce_scatter_tensor on the padded blocks; gloo (no reduce-scatter): the same
+    padded blocks all-reduced on the host, then this rank's block."""
+    r = rank()
+    m = max(counts)
+    padded = pad_rank_blocks(g, counts)
+    if td.get_backend() == "nccl":
+        out = torch.empty((m,) + tuple(g.shape[1:]), dtype=g.dtype, device=g.device)
+        td.reduce_scatter_tensor(out, padded, op=td.ReduceOp.SUM)
+    else:
+        out = _all_reduce(padded)[r * m:(r + 1) * m]
+    return out[:counts[r]].contiguous()
+
+
+def all_gather_rows(x, counts):
+    """Every rank's row block [counts[r], ...] -> [sum(counts), ...] on every rank (rank
+    order), through equal-size padded blocks (all_gather_into_tensor on RCCL)."""
+    w, m = len(counts), max(counts)
+    xc = x.contiguous()
+    pad = torch.zeros((m,) + tuple(xc.shape[1:]), dtype=xc.dtype, device=xc.device)
+    pad[:xc.shape[0]] = xc
+    h = _host(pad)
+    if td.get_backend() == "nccl":
+        full = torch.empty((w * m,) + tuple(h.shape[1:]), dtype=h.dtype, device=h.device)
+        td.all_gather_into_tensor(full, h)
+    else:
+        parts = [torch.empty_like(h) for _ in range(w)]
+        td.all_gather(parts, h)
+        full = torch.cat(parts, 0)
+    return unpad_rank_blocks(full, counts).to(x.device)
+
+
 class AllGatherRows(torch.autograd.Function):
     """Forward: every rank's row block [n_r, E] -> the full [sum n_r, E] on every rank
     (rank order). Backward: each rank's dL_r/d(full) is summed over ranks and the owner
-    keeps its rows (a reduce-scatter; all-reduce + slice on gloo). CoOp class-sharded text
-    features: rank r encodes classes [lo_r, hi_r) (shard_range) and every rank forms the
-    logits against all C classes; the owner backpropagates the summed text-feature gradient
-    through its own slice of the text encoder."""
+    keeps its rows (reduce_scatter_rows). CoOp class-sharded text features: rank r encodes
+    classes [lo_r, hi_r) (shard_range) and every rank forms the logits of ITS images against
+    all C classes; the owner backpropagates the summed text-feature gradient through its own
+    slice of the text encoder."""
+
+    @staticmethod
+    def forward(ctx, x, counts):
+        ctx.counts = counts
+        return all_gather_rows(x, counts)
+
+    @staticmethod
+    def backward(ctx, g):
+        return reduce_scatter_rows(g, ctx.counts), None
+
+
+class GatherClassColumns(torch.autograd.Function):
+    """CoCoOp class sharding (SURVEY §8(e) Option B): rank r holds the logits [B, C_r] of
+    its classes for the SAME B images as every other rank; forward all-gathers them into
+    [B, C] (class order = rank order). Every rank then evaluates the identical full loss, so
+    dL/d(logits) is the same on every rank and the backward only slices out this rank's
+    columns -- no collective. The prompt gradients each rank produces are partial sums over
+    its classes: all-reduce them with SUM (allreduce_grads(average=False))."""
 
     @staticmethod
     def forward(ctx, x, counts):
         ctx.counts = counts
         ctx.r = rank()
-        w = len(counts)
-        m = max(counts)
-        xc = x.contiguous()
-        pad = torch.zeros((m,) + tuple(xc.shape[1:]), dtype=xc.dtype, device=xc.device)
-        pad[:xc.shape[0]] = xc
-        h = _host(pad)
-        parts = [torch.empty_like(h) for _ in range(w)]
-        td.all_gather(parts, h)
-        return torch.cat([p[:k] for p, k in zip(parts, counts)], 0).to(x.device)
+        full_t = all_gather_rows(x.t(), counts)  # [C, B]
+        return full_t.t().contiguous()
 
     @staticmethod
     def backward(ctx, g):
-        counts, r = ctx.counts, ctx.r
-        lo = sum(counts[:r])
-        g = g.contiguous()
-        if td.get_backend() == "nccl":
-            w, m = len(counts), max(counts)
-            padded = torch.zeros((w * m,) + tuple(g.shape[1:]), dtype=g.dtype, device=g.device)
-            off = 0
-            for i, k in enumerate(counts):
-                padded[i * m:i * m + k] = g[off:off + k]
-                off += k
-            out = torch.empty((m,) + tuple(g.shape[1:]), dtype=g.dtype, device=g.device)
-            td.reduce_scatter_tensor(out, padded, op=td.ReduceOp.SUM)
-            return out[:counts[r]], None
-        full = _all_reduce(g.clone())
-        return full[lo:lo + counts[r]].contiguous(), None
+        lo = sum(ctx.counts[:ctx.r])
+        return g[:, lo:lo + ctx.counts[ctx.r]].contiguous(), None
 
 
 def sync_rng_from(src: int = 0):
@@ -180,6 +247,16 @@ def sync_rng_from(src: int = 0):
         st = st.to(torch.device("cuda", torch.cuda.current_device()))
     td.broadcast(st, src)
     torch.set_rng_state(st.cpu())
+
+
+def broadcast_int(v: int, src: int = 0) -> int:
+    """Rank ``src``'s integer on every rank (e.g. a seed)."""
+    if not is_dist() or world_size() == 1:
+        return int(v)
+    dev = torch.device("cuda", torch.cuda.current_device()) if td.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([int(v)], dtype=torch.int64, device=dev)
+    td.broadcast(t, src)
+    return int(t.item())
 
 
 def barrier():

@@ -1,5 +1,9 @@
 """Dassl checkpoint IO (Dassl.pytorch/dassl/utils/torchtools.py:27-157) for the prompt
-learners, readable in both directions with the reference.
+learners. CoOp / CoCoOp files are readable in both directions with the reference (load and
+resume). The deep trainers (IVLP / MaPLe / PromptSRC) register only their prompt parameters,
+where the reference registers the whole CustomCLIP: their files load here either way, and
+the reference's ``load_model`` (strict=False) reads ours, but the reference's strict resume
+of a file written here would report the frozen encoder keys missing.
 
 Layout (save_checkpoint, torchtools.py:27-74): ``<dir>/model.pth.tar-<epoch>`` (or
 ``model_name``) holding {"state_dict", "epoch", "optimizer", "scheduler", "val_result"},
@@ -113,12 +117,20 @@ def save_checkpoint(state, save_dir, is_best=False, remove_module_from_keys=True
 
 
 def resume_from_checkpoint(fdir, model, optimizer=None, scheduler=None):
-    """torchtools.py:118-157: restore weights (+ optimizer, scheduler); returns the epoch."""
+    """torchtools.py:118-157: restore weights (+ optimizer, scheduler); returns the epoch.
+
+    The file may hold more than the registered module: the reference's IVLP / MaPLe /
+    PromptSRC register a CustomCLIP that also carries the frozen CLIP encoders
+    (promptsrc.py:262), where here only the prompt parameters are registered. Keys the module
+    does not have are dropped; every key the module has must be in the file (a strict load
+    on the module's side, so a CoOp / CoCoOp resume is exactly the reference's)."""
     with open(osp.join(fdir, "checkpoint")) as f:
         fpath = osp.join(fdir, f.readlines()[0].strip("\n"))
     print(f'Loading checkpoint from "{fpath}"')
     ck = load_checkpoint(fpath)
-    model.load_state_dict(ck["state_dict"])
+    own = model.state_dict()
+    sd = {k: v for k, v in ck["state_dict"].items() if k in own}
+    model.load_state_dict(sd)
     if optimizer is not None and ck.get("optimizer") is not None:
         optimizer.load_state_dict(ck["optimizer"])
     if scheduler is not None and ck.get("scheduler") is not None:

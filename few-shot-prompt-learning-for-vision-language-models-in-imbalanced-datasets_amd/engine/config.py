@@ -139,6 +139,8 @@ def get_cfg_default() -> CfgNode:
         # MI355X-native knobs (not in the reference): prompt truncation to the EOT and the
         # max rows per text-encoder launch chunk (memory bound for large B*C).
         # CLASS_SHARD: CoOp under torchrun encodes C / world classes per rank.
+        # COCOOP_SHARD: CoCoOp under torchrun, "image" (data parallel) or "class" (every rank
+        # scores the same batch against C / world classes; SURVEY §8(e) Option B).
         "NATIVE": {"TRUNCATE_PROMPTS": True, "SHARED_PREFIX": True, "MAX_TEXT_ROWS": 2_000_000,
-                   "CLASS_SHARD": True},
+                   "CLASS_SHARD": True, "COCOOP_SHARD": "image"},
     })

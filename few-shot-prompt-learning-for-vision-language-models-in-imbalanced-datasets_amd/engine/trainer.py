@@ -129,11 +129,16 @@ class TrainerX:
     def batch_weight(batch, n_local):
         """Scale for this rank's loss before backward, so that the averaged all-reduce
         gives the gradient of the mean loss over the global batch: n_local * world /
-        n_global (1 when every rank holds an equal share)."""
-        n_global = batch.get("n_global") if isinstance(batch, dict) else None
+        n_global (1 when every rank holds an equal share). A batch marked ``n_local`` 0 is a
+        pad (its rank's slice of a short last batch was empty, data/manager.py): weight 0,
+        so it joins the all-reduce with a zero gradient."""
+        if not isinstance(batch, dict):
+            return 1.0
+        n_global = batch.get("n_global")
         w = dist.world_size()
         if not n_global or w == 1:
             return 1.0
+        n_local = batch.get("n_local", n_local)
         return float(n_local) * w / float(n_global)
 
     def model_inference(self, x):
@@ -168,6 +173,23 @@ class TrainerX:
                                   "val_result": val_result}, osp.join(directory, name), is_best=is_best,
                                  model_name=model_name)
 
+    def load_model(self, directory, epoch=None):
+        """trainer.py:172-201 (the base form; CoOp / CoCoOp override it, dropping the token
+        buffers): ``model-best.pth.tar`` by default, ``model.pth.tar-<epoch>`` when given."""
+        if not directory:
+            print("Note that load_model() is skipped as no pretrained model is given")
+            return
+        model_file = "model-best.pth.tar" if epoch is None else f"model.pth.tar-{epoch}"
+        for name in self.get_model_names():
+            model_path = osp.join(directory, name, model_file)
+            if not osp.exists(model_path):
+                raise FileNotFoundError(f"No model at {model_path}")
+            ck = self.load_checkpoint(model_path)
+            vr = ck.get("val_result")
+            print(f"Load {model_path} to {name} (epoch={ck['epoch']}, val_result="
+                  f"{vr if vr is None else format(vr, '.1f')})")
+            self._models[name].load_state_dict(ck["state_dict"])
+
     def resume_model_if_exist(self, directory):
         names = self.get_model_names()
         if any(not osp.exists(osp.join(directory, n)) for n in names):
@@ -182,20 +204,37 @@ class TrainerX:
 
     # ---- loops ----------------------------------------------------------------------
     def train(self, start_epoch=None, max_epoch=None):
-        self.start_epoch = self.resume_model_if_exist(self.output_dir) if start_epoch is None else start_epoch
+        """trainer.py:242-252 + before_train / after_train (388-420): resume from cfg.RESUME
+        (else OUTPUT_DIR), the epoch loop, then the final test -- of the best-val model
+        when TEST.FINAL_MODEL is "best_val"."""
+        directory = self.cfg.get("RESUME", "") or self.output_dir
+        self.start_epoch = self.resume_model_if_exist(directory) if start_epoch is None else start_epoch
         self.max_epoch = self.max_epoch if max_epoch is None else max_epoch
         t0 = time.time()
         for self.epoch in range(self.start_epoch, self.max_epoch):
             self.run_epoch()
             self.after_epoch()
+        print("Finish training")
         if not self.cfg.TEST.NO_TEST:
+            if self.cfg.TEST.get("FINAL_MODEL", "last_step") == "best_val":
+                print("Deploy the model with the best val performance")
+                self.load_model(self.output_dir)
+            else:
+                print("Deploy the last-epoch model")
             self.test()
         print(f"Elapsed: {datetime.timedelta(seconds=round(time.time() - t0))}")
 
     def after_epoch(self):
-        """trainer.py:422-443: checkpoint at CHECKPOINT_FREQ and at the last epoch."""
+        """trainer.py:422-443: with TEST.FINAL_MODEL "best_val" a val test every epoch and
+        ``model-best.pth.tar`` whenever it improves; a checkpoint at CHECKPOINT_FREQ and at
+        the last epoch."""
         last = (self.epoch + 1) == self.max_epoch
         freq = self.cfg.TRAIN.get("CHECKPOINT_FREQ", 0)
+        if not self.cfg.TEST.NO_TEST and self.cfg.TEST.get("FINAL_MODEL", "last_step") == "best_val":
+            curr = self.test(split="val")
+            if curr > self.best_result:
+                self.best_result = curr
+                self.save_model(self.epoch, self.output_dir, val_result=curr, model_name="model-best.pth.tar")
         if last or (freq > 0 and (self.epoch + 1) % freq == 0):
             self.save_model(self.epoch, self.output_dir)
 
@@ -226,6 +265,9 @@ class TrainerX:
             split = "test"
             loader = self.dm.test_loader
         print(f"Evaluate on the *{split}* set")
+        prepare = getattr(self.model, "prepare_eval", None)
+        if prepare is not None:  # every rank joins its collectives, whatever its shard size
+            prepare()
         preds, labels = [], []
         for batch in loader:
             x, y = self.parse_batch_test(batch)
@@ -235,7 +277,8 @@ class TrainerX:
         dev = self.device
         p = torch.cat(preds) if preds else torch.zeros(0, dtype=torch.int64, device=dev)
         y = torch.cat(labels) if labels else torch.zeros(0, dtype=torch.int64, device=dev)
-        p, y = dist.all_gather_varlen(p), dist.all_gather_varlen(y)
+        if not dist.batches_replicated(self.cfg):  # replicated: every rank saw the whole split
+            p, y = dist.all_gather_varlen(p), dist.all_gather_varlen(y)
         y_true, y_pred = y.cpu().numpy(), p.cpu().numpy()
         results = self.evaluator.evaluate_arrays(y_true, y_pred)
         if return_pred:

@@ -7,6 +7,16 @@ Here one launch sequence encodes all B*C conditional prompts at once: the Meta-N
 bias is added inside the prompt-assembly kernel, the text encoder runs over
 B*C sequences truncated to L = max EOT + 1, and the per-image cosine logits come from
 one kernel. Large B*C is split into image chunks bounded by NATIVE.MAX_TEXT_ROWS.
+
+Multi-GPU (one process per GPU, ``NATIVE.COCOOP_SHARD``):
+* "image" (default): data parallel over images -- each rank encodes its images' B_r*C
+  prompts, one averaged all-reduce of the ctx + Meta-Net gradients;
+* "class" (SURVEY §8(e) Option B, for the reference's batch-1 configs,
+  configs/trainers/CoCoOp/vit_b16_c4_ep10_batch1_ctxv1.yaml:3): every rank scores the SAME
+  batch against its C/W classes (shard_range), the [B, C_r] logit slices are all-gathered
+  (dist.GatherClassColumns), every rank evaluates the full loss and back-propagates its own
+  classes, and the partial prompt gradients are SUM all-reduced. The global batch (and so
+  the update) is the single-process one at any world size.
 """
 from __future__ import annotations
 
@@ -16,6 +26,7 @@ from collections import OrderedDict
 import torch
 import torch.nn as nn
 
+from .. import dist
 from ..engine.registry import TRAINER_REGISTRY
 from ..engine.trainer import TrainerX, load_clip
 from ..engine.optim import build_optimizer, build_lr_scheduler
@@ -41,7 +52,7 @@ class MetaNet(nn.Module):
 
 
 class PromptLearner(nn.Module):
-    def __init__(self, cfg, classnames, clip_model):
+    def __init__(self, cfg, classnames, clip_model, class_range=None):
         super().__init__()
         c = cfg.TRAINER.COCOOP
         clip_imsize = clip_model.visual.input_resolution
@@ -52,7 +63,7 @@ class PromptLearner(nn.Module):
         truncate = cfg.get("NATIVE", {}).get("TRUNCATE_PROMPTS", True)
         shared = cfg.get("NATIVE", {}).get("SHARED_PREFIX", True)
         ctx_vectors, self.prompt_prefix = init_prompts(self, classnames, clip_model, c.N_CTX, c.CTX_INIT,
-                                                       "end", False, truncate, shared)
+                                                       "end", False, truncate, shared, class_range)
         self.ctx = nn.Parameter(ctx_vectors)
         self.meta_net = MetaNet(vis_dim, ctx_dim).to(ctx_vectors.device)
 
@@ -76,10 +87,19 @@ class PromptLearner(nn.Module):
 
 
 class CustomCLIP(nn.Module):
-    def __init__(self, cfg, classnames, clip_model):
+    """cocoop.py:200-260. ``class_counts`` (per-rank class counts, rank order) turns on class
+    sharding: this process encodes its classes for every image and the logit slices are
+    all-gathered (module doc)."""
+
+    def __init__(self, cfg, classnames, clip_model, class_counts=None):
         super().__init__()
         self.cfg = cfg
-        self.prompt_learner = PromptLearner(cfg, classnames, clip_model)
+        self.class_counts = class_counts
+        class_range = None
+        if class_counts is not None:
+            lo = sum(class_counts[:dist.rank()])
+            class_range = (lo, lo + class_counts[dist.rank()])
+        self.prompt_learner = PromptLearner(cfg, classnames, clip_model, class_range)
         self.tokenized_prompts = self.prompt_learner.tokenized_prompts
         self.image_encoder = clip_model.visual
         self.text_core = clip_model.text
@@ -105,7 +125,10 @@ class CustomCLIP(nn.Module):
         B = imf_n.shape[0]
         x0 = pl.assemble(imf_n)
         txt = TextEncodeFn.apply(x0, self.text_core, pl.layout.shape(B))
-        return CosineLogitsFn.apply(imf_n, txt, self.logit_scale_value, 1, pl.n_cls)
+        logits = CosineLogitsFn.apply(imf_n, txt, self.logit_scale_value, 1, pl.layout.n_cls)
+        if self.class_counts is not None:
+            logits = dist.GatherClassColumns.apply(logits, self.class_counts)
+        return logits
 
     def forward(self, image, label=None):
         imf = self.image_encoder(image)
@@ -128,6 +151,13 @@ class CoCoOp(TrainerX):
 
     def check_cfg(self, cfg):
         assert cfg.TRAINER.COCOOP.PREC in ["fp16", "fp32", "amp", "bf16"]
+        mode = cfg.get("NATIVE", {}).get("COCOOP_SHARD", "image")
+        if mode not in ("image", "class"):
+            raise ValueError(f"NATIVE.COCOOP_SHARD must be 'image' or 'class', got {mode!r}")
+
+    @property
+    def class_sharded(self) -> bool:
+        return dist.batches_replicated(self.cfg)
 
     def build_model(self):
         cfg = self.cfg
@@ -135,7 +165,11 @@ class CoCoOp(TrainerX):
         print(f"Loading CLIP (backbone: {cfg.MODEL.BACKBONE.NAME})")
         clip_model = load_clip(cfg, cfg.TRAINER.COCOOP.PREC, self.device)
         print("Building custom CLIP")
-        self.model = CustomCLIP(cfg, classnames, clip_model)
+        counts = None
+        if self.class_sharded:
+            w = dist.world_size()
+            counts = [hi - lo for lo, hi in (dist.shard_range(len(classnames), r, w) for r in range(w))]
+        self.model = CustomCLIP(cfg, classnames, clip_model, class_counts=counts)
         print("Turning off gradients in both the image and the text encoder")
         for name, param in self.model.named_parameters():
             if "prompt_learner" not in name:
@@ -153,9 +187,14 @@ class CoCoOp(TrainerX):
         image, label = self.parse_batch_train(batch)
         loss = self.model(image, label)
         self.optim.zero_grad()
-        w = self.batch_weight(batch, image.shape[0])
-        (loss * w if w != 1.0 else loss).backward()
-        self.allreduce_grads(self.model.prompt_learner)
+        if self.class_sharded:  # full loss on every rank, partial gradients: summed
+            loss.backward()
+            dist.allreduce_grads([p for p in self.model.prompt_learner.parameters() if p.requires_grad],
+                                 average=False)
+        else:
+            w = self.batch_weight(batch, image.shape[0])
+            (loss * w if w != 1.0 else loss).backward()
+            self.allreduce_grads(self.model.prompt_learner)
         if self.cfg.TRAINER.COCOOP.PREC != "amp" or grads_finite(self.model.prompt_learner):
             self.optim.step()
         loss_summary = LossSummary()

@@ -153,6 +153,14 @@ class CustomCLIP(nn.Module):
         self._txt_cache = None
         return super().train(mode)
 
+    def prepare_eval(self):
+        """Called by TrainerX.test before its batch loop: encode (and, class-sharded,
+        all-gather) the class prompts now, so every rank joins that collective exactly once
+        -- a rank whose test shard is empty would otherwise never reach it and the others
+        would wait forever."""
+        if not self.training and not torch.is_grad_enabled():
+            self._cached_text_features()
+
     def forward_once(self, image):
         imf = self.image_encoder(image)
         if not self.training and not torch.is_grad_enabled():

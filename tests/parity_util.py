@@ -69,7 +69,8 @@ def run_native(meta, arrays, prec, cocoop=False, dev="cuda", truncate=True, shar
     mod = CC if cocoop else C
     model = mod.CustomCLIP(cfg, names, clip)
     pl = model.prompt_learner
-    out = {"packed": pl.layout.pack is not None}
+    out = {"packed": pl.layout.pack is not None, "P": getattr(pl.layout, "P", 0),
+           "prefix_input": pl.layout.shape(meta["batch"] if cocoop else 1).prefix_input}
     with torch.no_grad():
         if arrays.get("ctx0") is not None:
             pl.ctx.copy_(torch.from_numpy(arrays["ctx0"]).to(dev))

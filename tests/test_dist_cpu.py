@@ -152,12 +152,14 @@ def test_sharded_batches_union_is_the_global_stream():
         assert out[0][name + "_len"] == out[1][name + "_len"] == len(batches)
         for i, gb in enumerate(batches):
             k0, k1 = out[0][name][i], out[1][name][i]
-            assert all(n == len(gb) for _, n in k0 + k1)  # n_global rides along
-            got = [j for j, _ in k0] + [j for j, _ in k1]
+            assert all(n == len(gb) for _, n, _ in k0 + k1)  # n_global rides along
+            got = [j for j, _, _ in k0] + [j for j, _, _ in k1]
             if len(gb) >= 2:
                 assert got == gb
-            else:  # a 1-item last batch: rank 1 repeats it so it still joins the all-reduce
+                assert [nl for _, _, nl in k0 + k1] == [len(k0)] * len(k0) + [len(k1)] * len(k1)
+            else:  # a 1-item last batch: rank 1 gets it as a pad (local size 0, loss weight 0)
                 assert got == gb + gb
+                assert k0[0][2] == 1 and k1[0][2] == 0
 
 
 def _test_sharded_eval(rank, world):
@@ -244,3 +246,120 @@ def test_coop_class_sharded_grad_equals_full_batch():
     for r in (0, 1):
         np.testing.assert_allclose(out[r]["txt"], txt.numpy(), rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(out[r]["ctx"], ctx.grad.numpy(), rtol=1e-4, atol=2e-5)
+
+
+def test_pad_batch_has_zero_loss_weight():
+    """The pad a rank receives when its slice of a short last batch is empty carries
+    n_local 0: TrainerX.batch_weight gives it weight 0 (it joins the all-reduce with a zero
+    gradient instead of counting the item twice)."""
+    from fsp_amd.engine.trainer import TrainerX
+    import fsp_amd.dist as D
+    orig = D.world_size
+    D.world_size = lambda: 2
+    try:
+        assert TrainerX.batch_weight({"n_global": 1, "n_local": 0}, 1) == 0.0
+        assert TrainerX.batch_weight({"n_global": 1, "n_local": 1}, 1) == 2.0
+        assert TrainerX.batch_weight({"n_global": 5, "n_local": 3}, 3) == 1.2
+    finally:
+        D.world_size = orig
+
+
+def _rank_blocks(rank, world):
+    """pad / unpad of uneven row shards (shared by the RCCL and gloo branches), the gloo
+    reduce-scatter and all-gather built on them."""
+    from fsp_amd import dist
+    counts = [3, 2]
+    g = torch.arange(5 * 2, dtype=torch.float32).reshape(5, 2) * (rank + 1)
+    padded = dist.pad_rank_blocks(g, counts)
+    back = dist.unpad_rank_blocks(padded, counts)
+    mine = torch.full((counts[rank], 2), float(rank + 1))
+    return {"padded": padded.numpy(), "back": back.numpy(), "rs": dist.reduce_scatter_rows(g, counts).numpy(),
+            "ag": dist.all_gather_rows(mine, counts).numpy()}
+
+
+def test_pad_reduce_scatter_all_gather_rows():
+    out = _run(_rank_blocks)
+    g = np.arange(10, dtype=np.float32).reshape(5, 2)
+    for r in (0, 1):
+        o = out[r]
+        exp_pad = np.zeros((6, 2), np.float32)
+        exp_pad[:3] = g[:3] * (r + 1)
+        exp_pad[3:5] = g[3:] * (r + 1)
+        np.testing.assert_array_equal(o["padded"], exp_pad)
+        np.testing.assert_array_equal(o["back"], g * (r + 1))
+        np.testing.assert_array_equal(o["rs"], (g * 3)[:3] if r == 0 else (g * 3)[3:])
+        np.testing.assert_array_equal(o["ag"], np.array([[1, 1]] * 3 + [[2, 2]] * 2, np.float32))
+
+
+def _augment_streams(rank, world):
+    from fsp_amd.data.manager import augment_generator
+    from fsp_amd.data.preprocess import train_plan
+    torch.manual_seed(99 + rank)  # ranks' own seeds differ; rank 0's is the base
+    out = {}
+    for rep in (False, True):
+        g = augment_generator(rep)
+        out[rep] = [vars(train_plan(500, 375, 224, generator=g)) for _ in range(6)]
+    return out
+
+
+def test_augmentation_stream_per_rank():
+    """Data parallel: each rank draws its own crop / flip stream (different crops for its
+    different images); replicated batches (CoCoOp class sharding): one stream on every rank."""
+    out = _run(_augment_streams)
+    assert out[0][False] != out[1][False]
+    assert out[0][True] == out[1][True]
+
+
+def _cocoop_class_sharded(rank, world, n_img=1):
+    """CoCoOp class sharding (Option B) on the oracle's math: every rank scores the SAME
+    image(s) against its classes, GatherClassColumns forms the [B, C] logits, every rank
+    evaluates the full CE, the partial prompt gradients are SUM all-reduced."""
+    from oracle import clip_oracle as O
+    from fsp_amd.clip import synth
+    from fsp_amd import dist
+    from parity_util import load_fixture
+    meta, ref = load_fixture("cocoop_tiny_ctxinit_ce")
+    a = synth.ARCHS["tiny"]
+    p = O.as_torch_sd(synth.make_state_dict("tiny", seed=0))
+    mp_ = {k: torch.nn.Parameter(torch.from_numpy(v)) for k, v in
+           synth.make_meta_net(a.embed_dim, a.transformer_width, seed=4).items()}
+    tok = torch.from_numpy(ref["tokenized"].astype(np.int64))
+    emb = O.token_embed(p, tok)
+    C = meta["n_cls"]
+    counts = [hi - lo for lo, hi in (dist.shard_range(C, r, world) for r in range(world))]
+    lo, hi = dist.shard_range(C)
+    ctx = torch.nn.Parameter(torch.from_numpy(ref["ctx0"]))
+    img = torch.from_numpy(synth.make_images(n_img, a.image_resolution, seed=1))
+    y = torch.from_numpy(synth.make_labels(n_img, C, seed=2))
+    local = O.cocoop_logits(p, mp_, img, ctx, emb[lo:hi, :1], emb[lo:hi, 1 + 4:], tok[lo:hi])
+    logits = dist.GatherClassColumns.apply(local, counts)
+    torch.nn.functional.cross_entropy(logits, y).backward()
+    params = [ctx] + list(mp_.values())
+    dist.allreduce_grads(params, average=False)
+    return {"logits": logits.detach().numpy().copy(), "ctx": ctx.grad.numpy().copy(),
+            "w1": mp_["meta_net.linear1.weight"].grad.numpy().copy()}
+
+
+@pytest.mark.parametrize("n_img", [1, 2])
+def test_cocoop_class_sharded_grad_equals_single_process(n_img):
+    import functools
+    out = _run(functools.partial(_cocoop_class_sharded, n_img=n_img))
+    from oracle import clip_oracle as O
+    from fsp_amd.clip import synth
+    from parity_util import load_fixture
+    meta, ref = load_fixture("cocoop_tiny_ctxinit_ce")
+    a = synth.ARCHS["tiny"]
+    p = O.as_torch_sd(synth.make_state_dict("tiny", seed=0))
+    mp_ = {k: torch.nn.Parameter(torch.from_numpy(v)) for k, v in
+           synth.make_meta_net(a.embed_dim, a.transformer_width, seed=4).items()}
+    tok = torch.from_numpy(ref["tokenized"].astype(np.int64))
+    emb = O.token_embed(p, tok)
+    ctx = torch.nn.Parameter(torch.from_numpy(ref["ctx0"]))
+    img = torch.from_numpy(synth.make_images(n_img, a.image_resolution, seed=1))
+    y = torch.from_numpy(synth.make_labels(n_img, meta["n_cls"], seed=2))
+    logits = O.cocoop_logits(p, mp_, img, ctx, emb[:, :1], emb[:, 1 + 4:], tok)
+    torch.nn.functional.cross_entropy(logits, y).backward()
+    for r in (0, 1):
+        np.testing.assert_allclose(out[r]["logits"], logits.detach().numpy(), rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(out[r]["ctx"], ctx.grad.numpy(), rtol=1e-4, atol=2e-6)
+        np.testing.assert_allclose(out[r]["w1"], mp_["meta_net.linear1.weight"].grad.numpy(), rtol=1e-4, atol=2e-6)

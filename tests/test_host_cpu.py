@@ -86,12 +86,19 @@ def test_prompt_layout_matches_reference_cat(position, csc):
         assert src[c, eot[c]] == eot[c]
 
 
+REF_VOCAB = "/root/reference/PromptSRC/clip/bpe_simple_vocab_16e6.txt.gz"  # build container only
+
+
 def test_tokenizer_matches_reference_probes():
+    """The BPE merge loop vs token ids the reference's SimpleTokenizer produced (fixture),
+    with the vocab file passed explicitly: the product never searches the reference checkout
+    (find_vocab looks at $FSP_BPE_VOCAB and the package directory only)."""
     from fsp_amd.clip.tokenizer import BPETokenizer, find_vocab
     probes = json.load(open(os.path.join(ROOT, "tests", "golden", "tokenizer_probes.json")))
-    if find_vocab() is None:
-        pytest.skip("BPE vocab not available (reference checkout absent)")
-    tok = BPETokenizer()
+    path = find_vocab() or (REF_VOCAB if os.path.isfile(REF_VOCAB) else None)
+    if path is None:
+        pytest.skip("BPE vocab not available (no $FSP_BPE_VOCAB, reference checkout absent)")
+    tok = BPETokenizer(path)
     for s, ids in probes.items():
         assert tok.encode(s) == ids, s
 
@@ -106,8 +113,14 @@ def test_tokenizer_fallback_table_covers_synthetic_prompts():
     probes = json.load(open(os.path.join(ROOT, "tests", "golden", "tokenizer_probes.json")))
     for s in ["X X X X class7.", "a photo of a class123.", "X " * 16 + "class999."]:
         assert tok.encode(s) == probes[s]
-    with pytest.raises(KeyError):
+    with pytest.raises(KeyError, match="FSP_BPE_VOCAB"):
         tok.encode("a photo of a dog.")
+
+
+def test_tokenizer_never_searches_the_reference(monkeypatch):
+    from fsp_amd.clip import tokenizer as T
+    monkeypatch.delenv("FSP_BPE_VOCAB", raising=False)
+    assert all("/root/reference" not in c for c in T._vocab_candidates())
 
 
 def test_tokenize_matches_golden_tokens():
@@ -396,3 +409,54 @@ def test_checkpoint_layout_and_resume(tmp_path):
     assert t2.get_current_lr() == lr
     with pytest.raises(KeyError):
         t2.register_model("prompt_learner", t2.model, None, None)
+
+
+def test_best_val_final_model(tmp_path):
+    """TEST.FINAL_MODEL "best_val" (Dassl trainer.py:402-443): a val test after every epoch,
+    model-best.pth.tar written when the val result improves (val_result recorded), and the
+    final test runs on the best-val weights loaded back by load_model."""
+    from fsp_amd.engine import checkpoint as C
+    rs = np.random.RandomState(3)
+    batches = [{"img": torch.from_numpy(rs.randn(5, 3, 2, 2).astype(np.float32)),
+                "label": torch.from_numpy(rs.randint(0, 3, 5))} for _ in range(2)]
+    t = _dummy_trainer(tmp_path, batches)
+    t.dm.val_loader = batches[:1]
+    t.cfg.TEST.NO_TEST = False
+    t.cfg.TEST.FINAL_MODEL = "best_val"
+    vals = iter([10.0, 30.0, 20.0])
+    tests = []
+    orig_test = t.test
+
+    def fake_test(split=None, return_pred=False):
+        if split == "val":
+            return next(vals)
+        tests.append(t.learner.ctx.detach().clone())
+        return orig_test(split, return_pred)
+    t.test = fake_test
+    t.run_epoch = lambda: t.learner.ctx.data.add_(1.0)  # epoch e leaves ctx == e + 1
+    t.train(start_epoch=0, max_epoch=3)
+    best = C.load_checkpoint(str(tmp_path / "prompt_learner" / "model-best.pth.tar"))
+    assert best["epoch"] == 2 and best["val_result"] == 30.0  # the 2nd epoch's val was best
+    assert float(best["state_dict"]["ctx"][0, 0]) == 2.0
+    assert (tmp_path / "prompt_learner" / "model.pth.tar-3").exists()
+    assert len(tests) == 1 and float(tests[0][0, 0]) == 2.0  # final test on the best-val weights
+
+
+def test_resume_keeps_the_modules_own_keys(tmp_path):
+    """A checkpoint holding more than the registered module (the reference's deep trainers
+    register the whole CustomCLIP, frozen encoders included) resumes: extra keys dropped,
+    the module's own keys required."""
+    from fsp_amd.engine import checkpoint as C
+    t = _dummy_trainer(tmp_path, n_ctx=4, W=8, C=3)
+    sd = dict(t.learner.state_dict())
+    sd = {k: v + 1 for k, v in sd.items()}
+    sd["image_encoder.conv1.weight"] = torch.zeros(2, 2)
+    C.save_checkpoint({"state_dict": sd, "epoch": 1, "optimizer": None, "scheduler": None, "val_result": None},
+                      str(tmp_path / "ck" / "prompt_learner"))
+    assert t.resume_model_if_exist(str(tmp_path / "ck")) == 1
+    assert float(t.learner.ctx[0, 0]) == 1.0
+    del sd["ctx"]
+    C.save_checkpoint({"state_dict": sd, "epoch": 1, "optimizer": None, "scheduler": None, "val_result": None},
+                      str(tmp_path / "ck2" / "prompt_learner"))
+    with pytest.raises(RuntimeError, match="Missing key"):
+        t.resume_model_if_exist(str(tmp_path / "ck2"))

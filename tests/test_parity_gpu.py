@@ -287,3 +287,96 @@ def _layout_prefix_input(meta, prec, cocoop, dev):
     clip = build_model(state_dict(meta["arch"]), prec=prec, device=str(dev))
     model = (CC if cocoop else C).CustomCLIP(cfg, synth.synthetic_classnames(meta["n_cls"]), clip)
     return model.prompt_learner.layout.shape(2).prefix_input
+
+
+def _coop_oracle(arch, n_cls, batch, n_ctx=16, seed_ctx=11):
+    """CPU oracle for CoOp (class token "end", shared random context, CE) at a size too large
+    for a committed fixture: logits, loss, d ctx. Prompts truncated to L_eff (exact, SURVEY
+    §8 a6, pinned by test_oracle_golden). Cached per configuration."""
+    key = ("coop", arch, n_cls, batch, n_ctx, seed_ctx)
+    if key in _ORACLE_CACHE:
+        return _ORACLE_CACHE[key]
+    import torch
+    from oracle import clip_oracle as O
+    from fsp_amd.clip import synth
+    from fsp_amd.clip.tokenizer import tokenize
+    a = synth.ARCHS[arch]
+    p = O.as_torch_sd(synth.make_state_dict(arch, seed=0))
+    names = synth.synthetic_classnames(n_cls)
+    tok = torch.from_numpy(tokenize([" ".join(["X"] * n_ctx) + " " + n + "." for n in names]).astype(np.int64))
+    emb = O.token_embed(p, tok)
+    ctx0 = (np.random.RandomState(seed_ctx).standard_normal((n_ctx, a.transformer_width)) * 0.02).astype(np.float32)
+    ctx = torch.from_numpy(ctx0.copy()).requires_grad_(True)
+    img = torch.from_numpy(synth.make_images(batch, a.image_resolution, seed=1))
+    L = int(tok.argmax(-1).max()) + 1
+    logits = O.coop_logits(p, img, ctx, emb[:, :1], emb[:, 1 + n_ctx:], tok, [0] * n_cls, "end", L)
+    y = torch.from_numpy(synth.make_labels(batch, n_cls, seed=2))
+    loss = torch.nn.functional.cross_entropy(logits, y)
+    loss.backward()
+    out = {"logits": logits.detach().numpy(), "loss": float(loss.detach()), "grad_ctx": ctx.grad.numpy(),
+           "ctx0": ctx0, "L": L}
+    _ORACLE_CACHE.clear()
+    _ORACLE_CACHE[key] = out
+    return out
+
+
+def _gate(ref, out, prec, tag):
+    grads = [k for k in ref if k.startswith("grad_")]
+    report = {"logit_abs": float(np.abs(out["logits"] - ref["logits"]).max()),
+              "loss_abs": abs(out["loss"] - ref["loss"])}
+    if prec == "fp32":
+        report.update({g: rel_err(out[g], ref[g]) for g in grads})
+        print(tag, prec, report)
+        assert report["logit_abs"] <= 1e-3
+        assert report["loss_abs"] <= 1e-4 * max(1.0, abs(ref["loss"]))
+        for g in grads:
+            assert report[g] <= 1e-3, (g, report[g])
+    else:
+        fwd_cos, loss_tol, grad_cos = TOL16[prec]
+        report.update({g: cos_err(out[g].reshape(1, -1), ref[g].reshape(1, -1)) for g in grads})
+        print(tag, prec, report)
+        assert report["logit_abs"] <= fwd_cos * 100.0
+        assert report["loss_abs"] <= loss_tol
+        for g in grads:
+            assert report[g] <= grad_cos, (g, report[g])
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_config2_coop_vitb16_c1000_vs_oracle(dev, prec):
+    """BASELINE config 2 at its shape: CoOp n_ctx 16 (random shared context, class token at
+    the end), ViT-B/16, C = 1000 classes, B = 2 images, CE; the shared-prefix packed layout
+    with its prefix capped at P = 16 rows (SOT + 15 context slots), so the 16th context slot
+    is a per-class row (prompt_base.shared_prefix_tables max_prefix) and layer 0 runs the full
+    input (no prefix-input mode). Logits, loss and d ctx vs the CPU oracle."""
+    meta = {"arch": "ViT-B/16", "n_cls": 1000, "batch": 2, "n_ctx": 16, "ctx_init": "", "csc": 0,
+            "position": "end", "loss_type": "ce", "focal": 0}
+    ref = _coop_oracle("ViT-B/16", 1000, 2, 16)
+    out = run_native(meta, {"ctx0": ref["ctx0"], "tokenized": None}, prec, cocoop=False, dev=str(dev))
+    assert out["packed"] and out["P"] == 16 and not out["prefix_input"]
+    _gate(ref, out, prec, "config2")
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_config4_coop_vitl14_c100_vs_oracle(dev, prec):
+    """BASELINE config 4's model and precision (CoOp n_ctx 16, ViT-L/14, bf16) at C = 100
+    classes, B = 2, vs the CPU oracle (config 4's 1,000 classes are config 2's geometry at
+    W = 768: the per-class cost is linear in C)."""
+    meta = {"arch": "ViT-L/14", "n_cls": 100, "batch": 2, "n_ctx": 16, "ctx_init": "", "csc": 0,
+            "position": "end", "loss_type": "ce", "focal": 0}
+    ref = _coop_oracle("ViT-L/14", 100, 2, 16)
+    out = run_native(meta, {"ctx0": ref["ctx0"], "tokenized": None}, prec, cocoop=False, dev=str(dev))
+    assert out["packed"] and out["P"] == 16
+    _gate(ref, out, prec, "config4")
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_config5_cocoop_vitl14_336_c100_vs_oracle(dev, prec):
+    """BASELINE config 5's model and precision (CoCoOp ViT-L/14@336px, bf16, "a photo of a")
+    at C = 100 classes, B = 2 images (577-token ViT, W = 768 text, packed P = 5 prefix +
+    prefix-input mode), vs the CPU oracle: logits, loss, d ctx, d Meta-Net."""
+    meta = {"arch": "ViT-L/14@336px", "n_cls": 100, "batch": 2, "n_ctx": 4, "ctx_init": "a photo of a", "focal": 0}
+    ref = _cocoop_oracle("ViT-L/14@336px", 100, 2)
+    out = run_native(meta, {"ctx0": None, "tokenized": None}, prec, cocoop=True, dev=str(dev))
+    assert out["packed"] and out["P"] == 5 and out["prefix_input"]
+    np.testing.assert_array_equal(out["ctx0"], ref["ctx0"])
+    _gate(ref, out, prec, "config5")

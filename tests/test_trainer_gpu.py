@@ -27,13 +27,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "golden"))
 
 
-def _setup(trainer, outdir, dev, batches_on_dev=True):
+def _setup(trainer, outdir, dev, batches_on_dev=True, cocoop_shard="image"):
     import make_golden_trainer as MT
     from fsp_amd.clip import synth
     from fsp_amd.engine.registry import TRAINER_REGISTRY
     import fsp_amd.trainers  # noqa: F401
     cfg = MT.make_cfg(trainer, str(outdir))
     cfg.TEST.NO_TEST = True
+    cfg.NATIVE.COCOOP_SHARD = cocoop_shard
     names = synth.synthetic_classnames(MT.N_CLS)
     train, test = MT.batches()
     mv = (lambda b: {k: v.to(dev) for k, v in b.items()}) if batches_on_dev else (lambda b: b)
@@ -170,7 +171,7 @@ def _free_port():
     return p
 
 
-def _dp_worker(rank, world, port, trainer, q):
+def _dp_worker(rank, world, port, trainer, q, mode="dp", n_img=5):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0")
     root = os.path.dirname(HERE)
@@ -181,7 +182,7 @@ def _dp_worker(rank, world, port, trainer, q):
     try:
         dist.init_from_env(backend="gloo")
         T.cuda.set_device(0)
-        res = _dp_step(trainer, T.device("cuda:0"), tempfile.mkdtemp())
+        res = _dp_step(trainer, T.device("cuda:0"), tempfile.mkdtemp(), mode, n_img)
         q.put((rank, res))
     except Exception as e:  # report to the parent instead of hanging it
         import traceback
@@ -191,23 +192,34 @@ def _dp_worker(rank, world, port, trainer, q):
             T.distributed.destroy_process_group()
 
 
-def _dp_step(trainer, dev, outdir):
-    """One forward_backward on this rank's slice of a 5-image global batch (uneven 3 / 2,
-    carrying n_global), from the fixture's initial prompt parameters."""
+def _dp_step(trainer, dev, outdir, mode="dp", n_img=5):
+    """One forward_backward from the fixture's initial prompt parameters. mode "dp": this
+    rank's slice of an n_img global batch (5: uneven 3 / 2, carrying n_global); "class"
+    (CoCoOp class sharding, NATIVE.COCOOP_SHARD): the whole batch on every rank, C / 2
+    classes each; then, in "class" mode, test() on the (replicated) test split."""
     from fsp_amd import dist
     from fsp_amd.clip import synth
     meta, ref = load_fixture(f"trainer_{trainer.lower()}")
-    tr, _ = _setup(trainer, outdir, dev)
+    tr, _ = _setup(trainer, outdir, dev, cocoop_shard="class" if mode == "class" else "image")
     _init_like_fixture(tr, trainer, ref)
     tr.sync_trainable()
     a = synth.ARCHS["tiny"]
-    img = torch.from_numpy(synth.make_images(5, a.image_resolution, seed=77)).to(dev)
-    lbl = torch.from_numpy(synth.make_labels(5, meta["n_cls"], seed=78)).to(dev)
-    lo, hi = dist.shard_range(5)
+    img = torch.from_numpy(synth.make_images(n_img, a.image_resolution, seed=77)).to(dev)
+    lbl = torch.from_numpy(synth.make_labels(n_img, meta["n_cls"], seed=78)).to(dev)
+    lo, hi = (0, n_img) if mode == "class" else dist.shard_range(n_img)
     tr.num_batches = 10
-    tr.forward_backward({"img": img[lo:hi], "label": lbl[lo:hi], "n_global": 5})
+    tr.forward_backward({"img": img[lo:hi], "label": lbl[lo:hi], "n_global": n_img, "n_local": hi - lo})
     pl = tr.model.prompt_learner
-    return {k: p.detach().cpu().numpy() for k, p in pl.named_parameters()}
+    out = {k: p.detach().cpu().numpy() for k, p in pl.named_parameters()}
+    if mode == "class":
+        assert pl.layout.n_cls == (meta["n_cls"] if dist.world_size() == 1 else dist.shard_range(meta["n_cls"])[1]
+                                   - dist.shard_range(meta["n_cls"])[0])
+        y_true, y_pred = tr.test(return_pred=True)
+        out["y_true"], out["y_pred"] = y_true, y_pred
+        tr.set_model_mode("eval")
+        with torch.no_grad():
+            out["logits"] = tr.model_inference(tr.dm.test_loader[0]["img"]).cpu().numpy()
+    return out
 
 
 @pytest.mark.parametrize("trainer", ["CoOp", "CoCoOp"])
@@ -231,3 +243,33 @@ def test_two_ranks_match_single_process(dev, trainer):
         assert "error" not in out[r], out[r].get("error")
         for k, v in single.items():
             assert rel_err(out[r][k], v) <= 1e-5, (r, k, rel_err(out[r][k], v))
+
+
+@pytest.mark.parametrize("n_img", [1, 2])
+def test_cocoop_class_sharded_two_ranks_match_single_process(dev, n_img):
+    """CoCoOp class sharding (SURVEY §8(e) Option B; NATIVE.COCOOP_SHARD "class") at the
+    reference's batch of 1 (configs/trainers/CoCoOp/vit_b16_c4_ep10_batch1_ctxv1.yaml:3) and
+    at 2: two ranks (gloo, both on cuda:0) each encode C / 2 classes of the same images through
+    the real CoCoOp.forward_backward; the logit slices are all-gathered, the partial prompt
+    gradients SUM all-reduced. The update, the eval logits and test() predictions equal the
+    single-process ones."""
+    import torch.multiprocessing as mp
+    single = _dp_step("CoCoOp", dev, str(os.path.join("/tmp", "single_cls")), "class", n_img)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, "CoCoOp", q, "class", n_img)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert "error" not in out[r], out[r].get("error")
+        for k, v in single.items():
+            if k in ("y_true", "y_pred"):
+                np.testing.assert_array_equal(out[r][k], v)
+            elif k == "logits":
+                assert float(np.abs(out[r][k] - v).max()) <= 1e-4
+            else:
+                assert rel_err(out[r][k], v) <= 1e-5, (r, k, rel_err(out[r][k], v))
