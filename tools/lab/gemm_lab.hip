@@ -366,6 +366,11 @@ extern "C" int lab_gemm(int variant, int mode, const void* A, const void* B, voi
   V(3, 256, 256, 2, 4, 64, 5)   // 5-slot ring
   V(5, 256, 256, 2, 4, 64, 3)   // 3-slot ring (no stage in flight across the barrier)
   V(6, 256, 256, 2, 2, 128, 2)  // 4 waves (one per SIMD), 128x128 per wave, classic 2-slot
+  // full-N tiles for the N = 512 GEMMs (A row panel staged once per K step, not once per
+  // 256-column tile): 192 x 512, BK 32 (64-B rows), 45 KB per stage
+  V(10, 192, 512, 1, 4, 64, 3)  // 4 waves of 192x128 (384 accumulators), 3-slot pipelined
+  V(11, 192, 512, 1, 4, 64, 2)  // same, classic 2-slot
+  V(13, 192, 512, 2, 2, 64, 3)  // 4 waves of 96x256 (384 accumulators), 3-slot pipelined
 #undef V
 #define R(ID, BM, BN, WM, WN)                                                     \
   if (variant == ID) {                                                             \

@@ -12,7 +12,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 from fsp_amd import ops, _native as N  # noqa: E402
 
 NAMES = {8: "regstage 192x256 PGR2", 9: "regstage 256x256 PGR2", 6: "4-wave 256x256 BK64 2-slot", 7: "4-wave 256x256 BK32 4-slot pipe (spills)", 0: "prod 256x256 BK64 2-slot", 1: "prod 192x256 BK64 2-slot", 2: "256x256 BK32 4-slot pipelined",
-         3: "256x256 BK32 5-slot pipelined", 5: "256x256 BK32 3-slot pipelined"}
+         3: "256x256 BK32 5-slot pipelined", 5: "256x256 BK32 3-slot pipelined",
+         10: "192x512 4w(192x128) BK32 3-slot", 11: "192x512 4w(192x128) BK32 2-slot",
+         12: "192x512 8w(96x128) BK32 3-slot", 13: "192x512 4w(96x256) BK32 3-slot",
+         14: "192x512 8w(96x128) BK32 2-slot"}
 MODES = {0: "full", 1: "no-MFMA", 2: "no-loads", 3: "no-MFMA no-loads"}
 
 
