@@ -24,6 +24,7 @@ model.py:699), so the 16-bit modes are judged against the fp32 oracle.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -106,6 +107,25 @@ def _ptrs(tensors):
     return arr
 
 
+def ln_fold_enabled() -> bool:
+    """Knob FSP_LN_FOLD=0 builds 16-bit text encoders without the LayerNorm fold."""
+    return os.environ.get("FSP_LN_FOLD", "1") != "0"
+
+
+def ln_fold_weights(w, b, gamma, beta, act, device):
+    """LayerNorm folded into the Linear that consumes it (include/clipk.h, clipk_gemm_ln):
+    LN(x) W^T + b = rstd * (x W'^T - mean * s) + c with W' = W diag(gamma) in the operand dtype,
+    s = W' summed over its input dimension (of the rounded W'), c = b + W beta.
+    Returns (W', s, c) on ``device``, or None when W' does not fit the operand dtype."""
+    wd = w.double()
+    wp = (wd * gamma.double()[None, :]).to(act)
+    if not bool(torch.isfinite(wp.float()).all()):
+        return None
+    s = wp.double().sum(1).float()
+    c = (b.double() + wd @ beta.double()).float()
+    return (wp.to(device).contiguous(), s.to(device).contiguous(), c.to(device).contiguous())
+
+
 class _Encoder:
     handle = None
 
@@ -129,6 +149,8 @@ class TextEncoderCore(_Encoder):
         self.W, self.E, self.layers, self.heads = W, arch.embed_dim, nl, W // 64
         keep = []
         table = []
+        # LayerNorm fold of ln_1 / ln_2 into in_proj / c_fc (16-bit encoders; clipk_encoder_set_ln_fold)
+        fold = [] if act != torch.float32 and ln_fold_enabled() else None
         for i in range(nl):
             p = {k: _t(sd[f"transformer.resblocks.{i}.{k}"]).float() for k in _LAYER_KEYS}
             f32 = lambda x: x.to(self.device, torch.float32).contiguous()
@@ -142,6 +164,12 @@ class TextEncoderCore(_Encoder):
                    G(p["mlp.c_proj.weight"])]
             keep += row
             table += row
+            if fold is not None:
+                f_in = ln_fold_weights(p["attn.in_proj_weight"], p["attn.in_proj_bias"], p["ln_1.weight"],
+                                       p["ln_1.bias"], act, self.device)
+                f_fc = ln_fold_weights(p["mlp.c_fc.weight"], p["mlp.c_fc.bias"], p["ln_2.weight"],
+                                       p["ln_2.bias"], act, self.device)
+                fold = fold + list(f_in) + list(f_fc) if f_in and f_fc else None
         P = _t(sd["text_projection"]).float()
         head = [_t(sd["ln_final.weight"]).float().to(self.device).contiguous(),
                 _t(sd["ln_final.bias"]).float().to(self.device).contiguous(),
@@ -154,6 +182,9 @@ class TextEncoderCore(_Encoder):
                                               _ptrs(table), _ptrs(head), ctypes.byref(h)),
                 "clipk_encoder_create(text)")
         self.handle = h
+        if fold:
+            self._keep += fold
+            N.check(N.load().clipk_encoder_set_ln_fold(h, _ptrs(fold)), "clipk_encoder_set_ln_fold")
 
     def set_deep(self, deep, rows, n_per, grads=None):
         """Deep prompts for the next call(s): deep fp32 [n_deep, n_ctx, W] (None clears)."""

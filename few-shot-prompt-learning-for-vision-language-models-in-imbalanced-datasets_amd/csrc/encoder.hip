@@ -37,6 +37,8 @@ struct clipk_encoder {
   // of each group carry per-group (trainable) values; the class rows of x0 are the same for
   // every group and their input gradient is not wanted
   int prefix_input = 0;
+  // clipk_encoder_set_ln_fold: per layer {W_in', s_in, c_in, W_fc', s_fc, c_fc} (empty: off)
+  std::vector<std::array<const void*, 6>> fold;
 };
 
 namespace clipk {
@@ -169,6 +171,9 @@ struct TextBufs {
   // forward temporaries (oc / xc: the last layer's attention output and residual input
   // gathered to the EOT rows, text_eot_last)
   void *xn = nullptr, *g = nullptr, *lnf = nullptr, *oc = nullptr, *xc = nullptr;
+  // LN fold: per (row, 64-column group) statistics partials of the residual stream; mean /
+  // rstd of the un-saved (inference) forward
+  float *lnst = nullptr, *tm = nullptr, *tr = nullptr;
   size_t saved_bytes = 0, ws_bytes = 0;
 };
 
@@ -215,6 +220,9 @@ static TextBufs text_layout(const clipk_encoder* e, size_t rows, int nout, void*
   t.lnf = wk.take((size_t)nout * W * a);
   t.oc = wk.take((size_t)nout * W * a);
   t.xc = wk.take((size_t)nout * W * xs);
+  t.lnst = (float*)wk.take(rows * (W / 64) * 8);
+  t.tm = (float*)wk.take(rows * 4);
+  t.tr = (float*)wk.take(rows * 4);
   t.saved_bytes = save ? sv.off : 0;
   t.ws_bytes = wk.off;
   return t;
@@ -365,6 +373,51 @@ static int block_fwd(const clipk_encoder* e, const std::array<const void*, 16>& 
   return block_post(e, w, sh.rows, rd, X, o, Xm, Xo, xn, h, g, m2, r2, st, text, sk, skb);
 }
 
+// ---- LayerNorm fold (clipk_encoder_set_ln_fold; text encoder, 16-bit residual stream)
+static int gemm_ln(int act, int epi, int M, int N, int K, const void* A, const void* B, const float* bias,
+                   const void* res, void* o, void* o2, float* stats, const float* colsum, const float* m,
+                   const float* r, hipStream_t st, int prof_cls, const char* site) {
+  const double b = gemm_bytes(act, act, epi, M, N, K, o2 != nullptr, act) + (stats ? (double)M * (N / 64) * 8 : 0.0) +
+                   (m ? 8.0 * M : 0.0);
+  ProfScope ps(prof_cls, st, 2.0 * M * N * K, site, b);
+  return clipk_gemm_ln(act, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, stats, colsum, m, r, st);
+}
+static int ln_merge(int rows, int W, const float* lnst, float* m, float* r, hipStream_t st) {
+  ProfScope ps(CLIPK_PROF_NONE, st, 0.0, "text.ln_stats", (double)rows * (W / 64) * 8 + 8.0 * rows);
+  return clipk_ln_stats_merge(rows, W, lnst, m, r, st);
+}
+// attention half: ln_1 statistics of X merged from the partials the previous layer's c_proj
+// epilogue wrote (lnst); the qkv projection reads X itself through the fold
+static int block_attn_fold(const clipk_encoder* e, const std::array<const void*, 6>& f, const SeqShape& sh,
+                           const void* X, void* qkv, void* o, float* lse, float* m1, float* r1, const float* lnst,
+                           hipStream_t st) {
+  const int W = e->W, rows = sh.rows, act = e->act;
+  TRY(ln_merge(rows, W, lnst, m1, r1, st));
+  TRY(gemm_ln(act, CLIPK_EPI_BIAS, rows, 3 * W, W, X, f[0], (const float*)f[2], nullptr, qkv, nullptr,
+              nullptr, (const float*)f[1], m1, r1, st, CLIPK_PROF_GEMM_ALL, "text.qkv_fwd"));
+  const double ab = (double)rows * 4 * W * esize(act) + (lse ? 4.0 * rows * e->heads : 0.0);
+  ProfScope ps(CLIPK_PROF_ATTN, st, 0.0, "text.attn_fwd", ab);
+  return attn_fwd(e, sh, qkv, o, lse, st);
+}
+// post-attention half: out_proj writes Xm and its ln_2 statistics, c_fc reads Xm through the
+// fold, c_proj writes Xo (and, when a next layer folds ln_1, its statistics)
+static int block_post_fold(const clipk_encoder* e, const std::array<const void*, 16>& w,
+                           const std::array<const void*, 6>& f, int rows, const void* X, const void* o, void* Xm,
+                           void* Xo, void* h, void* g, float* m2, float* r2, float* lnst, bool stats_next,
+                           hipStream_t st) {
+  const int W = e->W, act = e->act;
+  TRY(gemm_ln(act, CLIPK_EPI_BIAS_RES, rows, W, W, o, w[4], (const float*)w[5], X, Xm, nullptr, lnst, nullptr,
+              nullptr, nullptr, st, CLIPK_PROF_GEMM_ALL, "text.out_fwd"));
+  TRY(ln_merge(rows, W, lnst, m2, r2, st));
+  TRY(gemm_ln(act, CLIPK_EPI_BIAS_QGELU, rows, 4 * W, W, Xm, f[3], (const float*)f[5], nullptr, g, h, nullptr,
+              (const float*)f[4], m2, r2, st, CLIPK_PROF_GEMM_FC, "text.fc_fwd"));
+  if (stats_next)
+    return gemm_ln(act, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo, nullptr, lnst,
+                   nullptr, nullptr, nullptr, st, CLIPK_PROF_GEMM_ALL, "text.proj_fwd");
+  return gemm(act, act, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo, nullptr, nullptr,
+              0, st, CLIPK_PROF_GEMM_ALL, nullptr, 0, "text.proj_fwd");
+}
+
 }  // namespace clipk
 
 using namespace clipk;
@@ -471,6 +524,19 @@ static EncIO text_io(const clipk_encoder* e) {
   return io;
 }
 #define SITE(n) (io.text ? "text." n : "vit." n)
+
+// LN fold in this call: set on the encoder, 16-bit text residual stream, no deep prompts (they
+// rewrite rows between a producer's statistics and their use) and not the A-operand QuickGELU
+// knob. Knob CLIPK_TEXT_LNFOLD=0 runs the LayerNorm passes.
+static bool ln_fold_on(const clipk_encoder* e, const EncIO& io) {
+  static int v = -1;
+  if (v < 0) {
+    const char* s = getenv("CLIPK_TEXT_LNFOLD");
+    v = s ? atoi(s) : 1;
+  }
+  return v != 0 && io.text && (int)e->fold.size() == e->layers && e->act != CLIPK_F32 && io.rd == e->act &&
+         !(e->deep.n_deep > 0 && e->deep.prompts) && !a_qgelu_on();
+}
 
 // deep prompts of layer l (1..n_deep) into the layer's input rows
 static int deep_inject(const clipk_encoder* e, int l, int rd, void* X, hipStream_t st) {
@@ -585,37 +651,47 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
   }
   const bool eotl = text_eot_last(sh);
   const int nl = e->layers, nout = sh.nout;
+  const bool fold = ln_fold_on(e, io);
+  bool have_stats = false;  // LN fold: t.lnst holds the statistics partials of cur
   for (int l = 0; l < nl; ++l) {
     void* Xo = t.X[l + 1];
     if (!save && Xo == cur) Xo = t.X[l];  // ping-pong (cur may be the caller's x0)
     if (l >= 1) TRY(deep_inject(e, l, rd, const_cast<void*>(cur), st));  // l >= 1: cur is ours
     const bool share0 = l == 0 && io.text && sh.G >= 2 && prefix_mode(e, sh);
-    if (share0) {
+    // LN statistics of the un-saved forward go to temporaries (m1 is consumed before m2 is written)
+    float* m1 = save ? t.mean1[l] : t.tm;
+    float* r1 = save ? t.rstd1[l] : t.tr;
+    float* m2 = save ? t.mean2[l] : t.tm;
+    float* r2 = save ? t.rstd2[l] : t.tr;
+    if (share0)
       TRY(block_attn_shared0(e, e->lw[l], sh, rd, cur, t.xn, t.qkv[l], t.o[l], t.lse[l], t.mean1[l], t.rstd1[l],
                              (int*)t.g, st));
+    else if (fold && have_stats)
+      TRY(block_attn_fold(e, e->fold[l], sh, cur, t.qkv[l], t.o[l], t.lse[l], m1, r1, t.lnst, st));
+    else
+      TRY(block_attn(e, e->lw[l], sh, rd, cur, t.xn, t.qkv[l], t.o[l], t.lse[l], t.mean1[l], t.rstd1[l], st,
+                     io.text, io.sk, io.skb));
+    // post-attention half over every row, or -- last layer -- the EOT rows alone (the EOT rows
+    // attend to their whole prefix, so the attention above covered every row); Xm, h, Xo then
+    // hold nout compact rows
+    const bool compact = eotl && l == nl - 1;
+    const void* xin = cur;
+    const void* oin = t.o[l];
+    if (compact) {
+      ProfScope ps(CLIPK_PROF_NONE, st, 0.0, SITE("eot_gather"), 2.0 * nout * W * (esize(e->act) + esize(rd)));
+      TRY(clipk_rows_copy(W * (int)esize(e->act), nout, t.o[l], eot_rows, t.oc, nullptr, st));
+      TRY(clipk_rows_copy(W * (int)esize(rd), nout, cur, eot_rows, t.xc, nullptr, st));
+      xin = t.xc;
+      oin = t.oc;
     }
-    if (eotl && l == nl - 1) {
-      // last layer: attention over all rows (the EOT rows attend to their whole prefix),
-      // then out_proj / LN2 / MLP on the EOT rows alone; Xm, h, Xo hold nout compact rows
-      if (!share0)
-        TRY(block_attn(e, e->lw[l], sh, rd, cur, t.xn, t.qkv[l], t.o[l], t.lse[l], t.mean1[l], t.rstd1[l], st,
-                       io.text, io.sk, io.skb));
-      {
-        ProfScope ps(CLIPK_PROF_NONE, st, 0.0, SITE("eot_gather"),
-                     2.0 * nout * W * (esize(e->act) + esize(rd)));
-        TRY(clipk_rows_copy(W * (int)esize(e->act), nout, t.o[l], eot_rows, t.oc, nullptr, st));
-        TRY(clipk_rows_copy(W * (int)esize(rd), nout, cur, eot_rows, t.xc, nullptr, st));
-      }
-      TRY(block_post(e, e->lw[l], nout, rd, t.xc, t.oc, t.Xm[l], Xo, t.xn, save ? t.h[l] : nullptr, t.g,
-                     t.mean2[l], t.rstd2[l], st, io.text, nullptr, 0));
-    } else if (share0) {
-      TRY(block_post(e, e->lw[l], sh.rows, rd, cur, t.o[l], t.Xm[l], Xo, t.xn, save ? t.h[l] : nullptr, t.g,
-                     t.mean2[l], t.rstd2[l], st, io.text, io.sk, io.skb));
-    } else {
-      TRY(block_fwd(e, e->lw[l], sh, rd, cur, t.Xm[l], Xo, t.xn, t.qkv[l], t.o[l], t.lse[l],
-                    save ? t.h[l] : nullptr, t.g, t.mean1[l], t.rstd1[l], t.mean2[l], t.rstd2[l], st, io.text,
-                    io.sk, io.skb));
-    }
+    const int n = compact ? nout : sh.rows;
+    if (fold)
+      TRY(block_post_fold(e, e->lw[l], e->fold[l], n, xin, oin, t.Xm[l], Xo, save ? t.h[l] : nullptr, t.g, m2, r2,
+                          t.lnst, l + 1 < nl, st));
+    else
+      TRY(block_post(e, e->lw[l], n, rd, xin, oin, t.Xm[l], Xo, t.xn, save ? t.h[l] : nullptr, t.g, t.mean2[l],
+                     t.rstd2[l], st, io.text, compact ? nullptr : io.sk, compact ? 0 : io.skb));
+    have_stats = fold && l + 1 < nl;
     cur = Xo;
   }
   // final LayerNorm on the output rows only (exact: LayerNorm is per row), then @ projection
@@ -976,6 +1052,23 @@ extern "C" int clipk_encoder_set_input_rows(clipk_encoder* e, int mode) {
   if (!e) return CLIPK_EINVAL;
   if (mode != 0 && mode != 1) return CLIPK_EINVAL;
   e->prefix_input = mode;
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_encoder_set_ln_fold(clipk_encoder* e, const void* const* fold_ptrs) {
+  if (!e || e->kind != 0) return CLIPK_EINVAL;
+  if (!fold_ptrs) {
+    e->fold.clear();
+    return CLIPK_OK;
+  }
+  if (e->act == CLIPK_F32) return CLIPK_EDTYPE;
+  std::vector<std::array<const void*, 6>> f(e->layers);
+  for (int l = 0; l < e->layers; ++l)
+    for (int i = 0; i < 6; ++i) {
+      f[l][i] = fold_ptrs[l * 6 + i];
+      if (!f[l][i]) return CLIPK_EINVAL;
+    }
+  e->fold.swap(f);
   return CLIPK_OK;
 }
 

@@ -50,7 +50,26 @@ struct GemmArgs {
   int ksplit;                 // split-K slices (non-persistent only); slice s writes out + s*split_stride
   long long split_stride;     // elements of TO between slices' fp32 partial outputs
   int skew;                   // persistent kernels: ~us of start delay for every other CU of an XCD
+  // LayerNorm folded into the GEMMs (clipk_gemm_ln): LNM 1 writes per (row, 64-column group)
+  // statistics partials of the rounded output to lnstats; LNM 2 applies LN to A = x through the
+  // epilogue rstd * (acc - mean * colsum) + bias (B = W diag(gamma), bias = b + W beta) with the
+  // rows' mean / rstd (clipk_ln_stats_merge of the producer's partials)
+  float* lnstats;
+  const float* colsum;
+  const float* lnmean;
+  const float* lnrstd;
 };
+
+// Sum over the aligned 8-lane group (DPP: quad xor 1, quad xor 2, half-row mirror i <-> 7 - i).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float sum8(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  return v + dpp_f<0x141>(v);
+}
 constexpr int STAMP_TILES = 8, STAMP_BLOCKS = 2048;
 
 template <typename T>
@@ -96,6 +115,14 @@ template <> struct Raw<32> { uint4 v[2]; };
 #endif
 #ifndef CLIPK_GEMM_XNT
 #define CLIPK_GEMM_XNT 1
+#endif
+// Store policy of a residual stream written with LN statistics (clipk_gemm_ln producers): its
+// consumer is the next GEMM's A operand, re-read by every column tile, so the lines are kept
+// (plain stores) rather than streamed past the caches. Same-box A/B of the fold
+// (profiles/r03c/ab_lnfold.txt): with nt stores the folded c_fc ran 0.24 ms/step slower than
+// the LayerNorm-pass c_fc; with plain stores 0.04 ms.
+#ifndef CLIPK_GEMM_SPOL_LN
+#define CLIPK_GEMM_SPOL_LN 0
 #endif
 // CLIPK_GEMM_PP: 192x256 / 256x256 launches with >= 2 K tiles run the ping-pong main loop
 // (1, persistent; 2 = one tile per block, A/B; 0 = the 2-slot loop). Same-box A/B
@@ -170,7 +197,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, lo
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)n, 0x00020000);
 }
 // 16 bytes of TO (16 / sizeof(TO) fp32 values converted) at byte offset off
-template <typename TO>
+template <typename TO, int POL = CLIPK_GEMM_SPOL>
 __device__ __forceinline__ void buf_store16(__amdgpu_buffer_rsrc_t r, int off, const float* v) {
   u32x4 d;
   if constexpr (sizeof(TO) == 4) {
@@ -182,7 +209,7 @@ __device__ __forceinline__ void buf_store16(__amdgpu_buffer_rsrc_t r, int off, c
     for (int c = 0; c < 8; ++c) h[c] = (TO)v[c];
     d = __builtin_bit_cast(u32x4, h);
   }
-  __builtin_amdgcn_raw_buffer_store_b128(d, r, off, 0, CLIPK_GEMM_SPOL);
+  __builtin_amdgcn_raw_buffer_store_b128(d, r, off, 0, POL);
 }
 
 // Start skew (knob CLIPK_GEMM_SKEW, ~us): every other CU of each XCD starts late, so that the
@@ -222,8 +249,10 @@ __device__ __forceinline__ void skew_start(int us, int bid) {
 // the other's LDS reads. A region is restaged (for K tile t+2, or t+1 for B0) one phase after
 // its last read; the K tile t+1 wait is a counted vmcnt at phase 4 of tile t that leaves the
 // three regions already issued for t+2 in flight -- the ring never drains in the loop.
+// LNM (clipk_gemm_ln): 1 = per-row LayerNorm statistics of the output, 2 = LayerNorm of A
+// folded into the epilogue (see GemmArgs).
 template <typename T, typename TO, typename TX, int EPI, int BM, int BN, int WM, int WN, bool PERSIST,
-          int ROWB = GEMM_ROWB, int DEPTH = 2, bool AG = false, bool PP = false>
+          int ROWB = GEMM_ROWB, int DEPTH = 2, bool AG = false, bool PP = false, int LNM = 0>
 __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
   static_assert(DEPTH == 2 || !PERSIST, "deep ring: non-persistent launches only");
   static_assert(!AG || (!PERSIST && DEPTH == 2 && sizeof(T) == 2 && ROWB == 128), "A-operand QuickGELU path");
@@ -399,7 +428,8 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
     constexpr int XNB = CW * (int)sizeof(TX);
     typedef Raw<XNB> XR;
     constexpr int XREG = NQ * XNB / 4;
-    constexpr int XBUD = BM == 192 ? CLIPK_XBUD192 : CLIPK_XBUD256;  // ring VGPRs (256-row tiles: little to spare)
+    // ring VGPRs (256-row tiles: little to spare; the LN-statistics epilogue needs 8 more)
+    constexpr int XBUD = BM == 192 ? CLIPK_XBUD192 : (LNM == 1 ? CLIPK_XBUD256 / 2 : CLIPK_XBUD256);
     constexpr int XD = XBUD / XREG < 1 ? 1 : (XBUD / XREG > TM ? TM : XBUD / XREG);
     XR extq[XD][NQ];
     auto load_ext = [&](int i, XR* dst) {
@@ -413,6 +443,25 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
             ld_raw<XNB>((const TX*)g.res + (size_t)mc * g.ldr + ncol, dst[q]);
           else
             ld_raw<XNB>((const TX*)g.aux + (size_t)mc * g.ldaux + ncol, dst[q]);
+        }
+      }
+    };
+    // LN fold: mean / rstd of the lane's rows, two 16-row groups ahead of their use. (Merging the
+    // producer's partials here instead of in clipk_ln_stats_merge -- 2 loads + 2 8-lane sums per
+    // row -- measured slower: qkv 86 -> 110 us, c_fc 129 -> 158 us per launch.)
+    constexpr bool LN_IN = LNM == 2, LN_OUT = LNM == 1;
+    static_assert(!LN_OUT || (EPI == CLIPK_EPI_BIAS_RES && sizeof(TO) == 2 && CW == 8), "LN statistics: 16-bit out");
+    static_assert(!LN_IN || ((EPI == CLIPK_EPI_BIAS || EPI == CLIPK_EPI_BIAS_QGELU) && sizeof(T) == 2 && CW == 8),
+                  "LN fold");
+    [[maybe_unused]] f32x2 lnp[LN_IN ? 2 : 1][NQ];
+    auto load_ln = [&](int i, int slot) {
+      if constexpr (LN_IN) {
+        const int mg = m0 + wm * (BM / WM) + i * 16;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          int mc = mg + RPQ * q + er;
+          mc = mc < g.M ? mc : g.M - 1;
+          lnp[slot][q] = (f32x2){g.lnmean[mc], g.lnrstd[mc]};
         }
       }
     };
@@ -528,7 +577,10 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         const int k1 = in1 ? kt + 1 : kt + 1 - nk, k2 = in2 ? kt + 2 : kt + 2 - nk;
         rd_a(b, 0); rd_b(b, 0);                 // phase 1: A0 x B0
         if (h1) pst(b ^ 1, cra, in1 ? crb : xrb, k1, 2);
-        if (!in1) load_ext(0, extq[0]);
+        if (!in1) {
+          load_ext(0, extq[0]);
+          load_ln(0, 0);
+        }
         seg_end();
         mm(0, 0);
         G8_BAR();
@@ -569,7 +621,10 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       } else {
         if (kt + DEPTH - 1 < nk) stage((kt + DEPTH - 1) % DEPTH, kt + DEPTH - 1);  // slot read at kt-1
       }
-      if (last) load_ext(0, extq[0]);
+      if (last) {
+        load_ext(0, extq[0]);
+        load_ln(0, 0);
+      }
       const char* As = smem + cur * STAGE + (wm * (BM / WM) + fr) * ROWB;
       const char* Bs = smem + cur * STAGE + OPA + (wn * (BN / WN) + fr) * ROWB;
 #pragma unroll
@@ -616,8 +671,22 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         bia[c] = b4[0]; bia[c + 1] = b4[1]; bia[c + 2] = b4[2]; bia[c + 3] = b4[3];
       }
     }
+    [[maybe_unused]] float csum[LN_IN ? CW : 1];
+    if constexpr (LN_IN) {
+#pragma unroll
+      for (int c = 0; c < CW; c += 4) {
+        const f32x4 s4 = *reinterpret_cast<const f32x4*>(g.colsum + ncol + c);
+        csum[c] = s4[0]; csum[c + 1] = s4[1]; csum[c + 2] = s4[2]; csum[c + 3] = s4[3];
+      }
+      if (TM > 1) load_ln(1, 1);
+    }
     float* scr = reinterpret_cast<float*>(smem + DEPTH * STAGE + w * EPI_SCRATCH);
     const long long rows_ok = (long long)(g.M - m0 < BM ? g.M - m0 : BM);
+    // LN statistics: (sum, sum of squares about the group mean) of each row's 64 columns
+    // [nbase, nbase + 64), written by the row's first lane (the others store out of range)
+    const int lng = g.N / 64;
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t rst =
+        tile_rsrc(LN_OUT ? g.lnstats + (size_t)m0 * lng * 2 : nullptr, LN_OUT ? rows_ok * lng * 8 : 0);
     const __amdgpu_buffer_rsrc_t ro = tile_rsrc(outb + (size_t)m0 * g.ldo, rows_ok * g.ldo * (long long)sizeof(TO));
     __amdgpu_buffer_rsrc_t ro2 = ro;
     if constexpr (EPI == CLIPK_EPI_BIAS_QGELU)
@@ -647,7 +716,11 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
           v[4 * c] = t[0]; v[4 * c + 1] = t[1]; v[4 * c + 2] = t[2]; v[4 * c + 3] = t[3];
         }
         const int off = ((m - m0) * g.ldo + ncol) * (int)sizeof(TO);  // rows >= M: out of range, dropped
-        if constexpr (HAS_BIAS) {
+        if constexpr (LN_IN) {
+          const float rs = lnp[i & 1][q][1], nb = -rs * lnp[i & 1][q][0];
+#pragma unroll
+          for (int c = 0; c < CW; ++c) v[c] = fmaf(rs, v[c], fmaf(nb, csum[c], bia[c]));
+        } else if constexpr (HAS_BIAS) {
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] += bia[c];
         }
@@ -656,6 +729,25 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
           raw_f32<TX, CW>(ext[q], r);
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] += r[c];
+          if constexpr (LN_OUT) {
+            float vr[CW], s = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int c = 0; c < CW; ++c) {
+              vr[c] = to_f32((TO)v[c]);  // the stored value
+              s += vr[c];
+            }
+            s = sum8(s);
+            const float mu = s * (1.0f / 64.0f);
+#pragma unroll
+            for (int c = 0; c < CW; ++c) {
+              const float d = vr[c] - mu;
+              s2 = fmaf(d, d, s2);
+            }
+            s2 = sum8(s2);
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            const int so = ec == 0 ? ((m - m0) * lng + nbase / 64) * 8 : 0x40000000;
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, (f32x2){s, s2}), rst, so, 0, 0);
+          }
         } else if constexpr (EPI == CLIPK_EPI_BIAS_QGELU) {
           buf_store16<TO>(ro2, off, v);  // no-op when out2 is null (zero-sized resource)
 #pragma unroll
@@ -666,9 +758,10 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] *= quick_gelu_grad(h[c]);
         }
-        buf_store16<TO>(ro, off, v);
+        buf_store16<TO, LN_OUT ? CLIPK_GEMM_SPOL_LN : CLIPK_GEMM_SPOL>(ro, off, v);
       }
       if (i + XD < TM) load_ext(i + XD, extq[i % XD]);  // this group's slot is free again
+      if (i + 2 < TM) load_ln(i + 2, i & 1);
     }
     if (stp && ti < STAMP_TILES) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -785,19 +878,19 @@ static int num_cus() {
 
 // BM x 256 ping-pong launch when built in and the shape has >= 2 K tiles (the 256-row forms
 // with an fp32 residual / aux operand would spill: they keep the 2-slot loop)
-template <typename T, typename TO, typename TX, int EPI, int BM>
+template <typename T, typename TO, typename TX, int EPI, int BM, int LNM = 0>
 static bool try_pp(const GemmArgs& g, int nwg, hipStream_t st) {
   constexpr bool ext32 = (EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU) && sizeof(TX) == 4;
   if constexpr (CLIPK_GEMM_PP && sizeof(T) == 2 && !(BM == 256 && ext32)) {
     if (g.K * (int)sizeof(T) < 2 * GEMM_ROWB) return false;
-    hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, BM, 256, 2, 4, true, GEMM_ROWB, 2, false, true>),
+    hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, BM, 256, 2, 4, true, GEMM_ROWB, 2, false, true, LNM>),
                        dim3(pp_grid(nwg, num_cus())), dim3(512), 0, st, g);
     return true;
   }
   return false;
 }
 
-template <typename T, typename TO, typename TX, int EPI>
+template <typename T, typename TO, typename TX, int EPI, int LNM = 0>
 static int launch_gemm(const GemmArgs& g, hipStream_t st) {
   const int cfg = pick_cfg(g.M, g.N, (int)sizeof(T));
   const_cast<GemmArgs&>(g).stamp = gemm_stamp_buf();
@@ -808,39 +901,39 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
   const_cast<GemmArgs&>(g).skew = g_skew;
   if constexpr (sizeof(T) == 4) {
     const int nwg = ((g.M + 127) / 128) * (g.N / 128);
-    hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 128, 2, 2, false>), dim3(nwg), dim3(256), 0, st, g);
+    hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 2, false, false, LNM>), dim3(nwg), dim3(256), 0, st, g);
   } else {
     if (cfg == 1 || cfg == 3) {
       const int nwg = ((g.M + 255) / 256) * (g.N / 256);
       const int cus = num_cus();
-      if (try_pp<T, TO, TX, EPI, 256>(g, nwg, st)) {
+      if (try_pp<T, TO, TX, EPI, 256, LNM>(g, nwg, st)) {
       } else if (cfg == 1 && nwg > 2 * cus) {
         // persistent: one 8-wave block per CU, grid a multiple of 8 (XCD groups)
         const int grid = (cus / 8) * 8;
-        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 256, 2, 4, true>), dim3(grid), dim3(512), 0, st, g);
+        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 256, 2, 4, true, GEMM_ROWB, 2, false, false, LNM>), dim3(grid), dim3(512), 0, st, g);
       } else {
-        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 256, 2, 4, false>), dim3(nwg), dim3(512), 0, st, g);
+        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 256, 2, 4, false, GEMM_ROWB, 2, false, false, LNM>), dim3(nwg), dim3(512), 0, st, g);
       }
     } else if (cfg == 6) {
       const int nwg = ((g.M + 191) / 192) * (g.N / 256);
       const int cus = num_cus();
-      if (try_pp<T, TO, TX, EPI, 192>(g, nwg, st)) {
+      if (try_pp<T, TO, TX, EPI, 192, LNM>(g, nwg, st)) {
       } else if constexpr (CLIPK_GEMM_RING)  // 4-slot ring of 64-B K steps: three steps in flight
-        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 192, 256, 2, 4, false, 64, 4>), dim3(nwg), dim3(512), 0, st, g);
+        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 192, 256, 2, 4, false, 64, 4, false, false, LNM>), dim3(nwg), dim3(512), 0, st, g);
       else if (nwg > persist_min(cus))
-        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 192, 256, 2, 4, true>), dim3((cus / 8) * 8), dim3(512), 0, st, g);
+        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 192, 256, 2, 4, true, GEMM_ROWB, 2, false, false, LNM>), dim3((cus / 8) * 8), dim3(512), 0, st, g);
       else
-        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 192, 256, 2, 4, false>), dim3(nwg), dim3(512), 0, st, g);
+        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 192, 256, 2, 4, false, GEMM_ROWB, 2, false, false, LNM>), dim3(nwg), dim3(512), 0, st, g);
     } else if (cfg == 2) {
       const int nwg = ((g.M + 255) / 256) * (g.N / 128);
-      hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 128, 4, 2, false>), dim3(nwg), dim3(512), 0, st, g);
+      hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 128, 4, 2, false, GEMM_ROWB, 2, false, false, LNM>), dim3(nwg), dim3(512), 0, st, g);
     } else {
       const int nwg = ((g.M + 127) / 128) * (g.N / 128);
       if (nwg <= num_cus() && deep_small())  // one tile per CU: 4-slot ring (144 KiB LDS), knob
-        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 4>), dim3(nwg),
+        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 4, false, false, LNM>), dim3(nwg),
                            dim3(256), 0, st, g);
       else
-        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 128, 2, 2, false>), dim3(nwg), dim3(256), 0, st, g);
+        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 2, false, false, LNM>), dim3(nwg), dim3(256), 0, st, g);
     }
   }
   CLIPK_CHECK_LAUNCH();
@@ -945,6 +1038,37 @@ extern "C" int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, in
     case CLIPK_F32: return dispatch_out<float>(out_dtype, epi, aux_dtype, g, st);
     default: return CLIPK_EDTYPE;
   }
+}
+
+namespace clipk {
+template <typename T>
+static int dispatch_ln(int epi, const GemmArgs& g, hipStream_t st) {
+  if (!g.colsum) return launch_gemm<T, T, T, CLIPK_EPI_BIAS_RES, 1>(g, st);
+  if (epi == CLIPK_EPI_BIAS) return launch_gemm<T, T, float, CLIPK_EPI_BIAS, 2>(g, st);
+  return launch_gemm<T, T, float, CLIPK_EPI_BIAS_QGELU, 2>(g, st);
+}
+}  // namespace clipk
+
+// LayerNorm folded into the text GEMMs (include/clipk.h): statistics partials out (EPI_BIAS_RES)
+// or colsum + mean + rstd in (EPI_BIAS / EPI_BIAS_QGELU); 16-bit in and out dtype.
+extern "C" int clipk_gemm_ln(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B,
+                             int ldb, const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
+                             float* stats, const float* colsum, const float* mean, const float* rstd,
+                             void* stream) {
+  if (!A || !B || !out || !bias) return CLIPK_EINVAL;
+  if (in_dtype != CLIPK_F16 && in_dtype != CLIPK_BF16) return CLIPK_EDTYPE;
+  if (!colsum) {  // producer: the statistics partials of the output
+    if (!stats || mean || rstd || epi != CLIPK_EPI_BIAS_RES || !res || ldr < N || ldr % 8) return CLIPK_EINVAL;
+  } else {        // fold: mean / rstd of A's rows in
+    if (stats || !mean || !rstd || (epi != CLIPK_EPI_BIAS && epi != CLIPK_EPI_BIAS_QGELU)) return CLIPK_EINVAL;
+  }
+  if (M <= 0) return M == 0 ? CLIPK_OK : CLIPK_ESHAPE;
+  if (N <= 0 || K <= 0 || N % GEMM_NMIN != 0 || (K * 2) % GEMM_ROWB != 0) return CLIPK_ESHAPE;
+  if (lda < K || ldb < K || lda % 8 || ldb % 8 || ldo < N || ldo % 8) return CLIPK_ESHAPE;
+  GemmArgs g{(const char*)A, (const char*)B, M, N, K, lda, ldb, bias, res, ldr, out, ldo, out2, nullptr,
+             0, nullptr, 1, 0, 0, stats, colsum, mean, rstd};
+  hipStream_t st = (hipStream_t)stream;
+  return in_dtype == CLIPK_F16 ? dispatch_ln<f16>(epi, g, st) : dispatch_ln<bf16>(epi, g, st);
 }
 
 namespace clipk {

@@ -410,3 +410,59 @@ extern "C" int clipk_layernorm_bwd(int dy_dtype, int rows, int width, const void
   return clipk_layernorm_bwd_x(CLIPK_F32, dy_dtype, rows, width, dy, lddy, x, ldx, x_rows, gamma, mean, rstd,
                                dres, lddres, dx, dx_lp, lp_dtype, out_rows, ldo, stream);
 }
+
+namespace clipk {
+// LayerNorm statistics from the per-(row, 64-column group) partials a clipk_gemm_ln producer
+// wrote: (sum_g, M2_g = sum over the group of (x - sum_g / 64)^2). Exact merge (Chan et al.):
+// mean = sum_g sum_g / width; M2 = sum_g M2_g + 64 (sum_g / 64 - mean)^2; rstd = 1 / sqrt(M2 /
+// width + 1e-5) as model.py:153-159. One thread per row, fixed group order (deterministic).
+template <int NG>
+__global__ __launch_bounds__(256) void ln_stats_merge_kernel(int rows, const f32x2* __restrict__ st,
+                                                             float* __restrict__ mean, float* __restrict__ rstd) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= rows) return;
+  f32x2 p[NG];
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(st + (size_t)r * NG);
+#pragma unroll
+  for (int g = 0; g < NG / 2; ++g) {
+    const f32x4 v = s4[g];
+    p[2 * g] = (f32x2){v[0], v[1]};
+    p[2 * g + 1] = (f32x2){v[2], v[3]};
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) s += p[g][0];
+  const float mu = s * (1.0f / (64.0f * NG));
+  float m2 = 0.f;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const float d = p[g][0] * (1.0f / 64.0f) - mu;
+    m2 += fmaf(64.0f * d, d, p[g][1]);
+  }
+  mean[r] = mu;
+  rstd[r] = rsqrtf(m2 * (1.0f / (64.0f * NG)) + 1e-5f);
+}
+}  // namespace clipk
+
+extern "C" int clipk_ln_stats_merge(int rows, int width, const float* stats, float* mean, float* rstd,
+                                    void* stream) {
+  if (!stats || !mean || !rstd) return CLIPK_EINVAL;
+  if (rows < 0 || width % 128 || width < 128 || width > 1024) return CLIPK_ESHAPE;
+  if (rows == 0) return CLIPK_OK;
+  const dim3 grid((rows + 255) / 256);
+  hipStream_t st = (hipStream_t)stream;
+  const f32x2* s = reinterpret_cast<const f32x2*>(stats);
+  switch (width / 64) {
+    case 2: hipLaunchKernelGGL(ln_stats_merge_kernel<2>, grid, dim3(256), 0, st, rows, s, mean, rstd); break;
+    case 4: hipLaunchKernelGGL(ln_stats_merge_kernel<4>, grid, dim3(256), 0, st, rows, s, mean, rstd); break;
+    case 6: hipLaunchKernelGGL(ln_stats_merge_kernel<6>, grid, dim3(256), 0, st, rows, s, mean, rstd); break;
+    case 8: hipLaunchKernelGGL(ln_stats_merge_kernel<8>, grid, dim3(256), 0, st, rows, s, mean, rstd); break;
+    case 10: hipLaunchKernelGGL(ln_stats_merge_kernel<10>, grid, dim3(256), 0, st, rows, s, mean, rstd); break;
+    case 12: hipLaunchKernelGGL(ln_stats_merge_kernel<12>, grid, dim3(256), 0, st, rows, s, mean, rstd); break;
+    case 14: hipLaunchKernelGGL(ln_stats_merge_kernel<14>, grid, dim3(256), 0, st, rows, s, mean, rstd); break;
+    case 16: hipLaunchKernelGGL(ln_stats_merge_kernel<16>, grid, dim3(256), 0, st, rows, s, mean, rstd); break;
+    default: return CLIPK_ESHAPE;
+  }
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}

@@ -91,6 +91,24 @@ int clipk_gemm_splitk(int in_dtype, int out_dtype, int epi, int M, int N, int K,
                       void* out, int ldo, void* out2, int splits, void* ws, size_t ws_bytes,
                       void* stream);
 
+/* LayerNorm folded into the GEMM that consumes it (the text encoder's ln_1 -> attn.in_proj
+ * and ln_2 -> mlp.c_fc, PromptSRC/clip/model.py:153-159, 185-188):
+ *   LN(x) W^T + b = rstd * (x W'^T - mean * s) + c,  W' = W diag(gamma) (in_dtype),
+ *   s_j = sum_k W'[j,k], c_j = b_j + sum_k beta_k W[j,k] (fp32),
+ * so the GEMM reads the residual stream x itself and no normalised copy is written.
+ * Two modes, 16-bit in_dtype == out dtype:
+ *  - colsum == NULL: EPI_BIAS_RES (the residual-stream producer); in addition, per row m and
+ *    64-column group g of the ROUNDED output, stats[(m * N/64 + g) * 2 + {0, 1}] = (sum, sum of
+ *    squared deviations from the group's mean) (fp32);
+ *  - colsum != NULL (stats NULL): EPI_BIAS or EPI_BIAS_QGELU with A = x, B = W', bias = c,
+ *    colsum = s and mean / rstd of A's rows (fp32 [M]).
+ * clipk_ln_stats_merge turns a producer's partials into mean / rstd (exact pairwise merge in a
+ * fixed order, eps 1e-5; width / 64 partials per row). Shape constraints as clipk_gemm. */
+int clipk_gemm_ln(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B, int ldb,
+                  const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
+                  float* stats, const float* colsum, const float* mean, const float* rstd, void* stream);
+int clipk_ln_stats_merge(int rows, int width, const float* stats, float* mean, float* rstd, void* stream);
+
 /* Benchmark knob: force the 16-bit GEMM tile configuration (0: 128x128, 1: 256x256
  * (persistent above 2 x CUs tiles), 2: 256x128, 3: 256x256 non-persistent, 6: 192x256;
  * -1 = automatic by shape; other values: CLIPK_EINVAL). Not needed for normal use. */
@@ -298,6 +316,15 @@ int clipk_encoder_set_deep_prompts(clipk_encoder* e, int n_deep, int n_ctx, int 
  * rows clipk_ctx_grad_rows reads; the class rows of dx0 are left unspecified). Exact. Forward
  * and backward of one call must use the same mode. */
 int clipk_encoder_set_input_rows(clipk_encoder* e, int mode);
+
+/* LayerNorm fold of a 16-bit text encoder (see clipk_gemm_ln): fold_ptrs = 6 per layer,
+ * {W_in' [3W, W] act dtype, s_in [3W] fp32, c_in [3W] fp32, W_fc' [4W, W], s_fc [4W], c_fc [4W]}
+ * built from the layer's ln_1 / ln_2 and in_proj / c_fc weights. When set, layers >= 1 take
+ * ln_1 from the previous layer's c_proj epilogue statistics and every layer takes ln_2 from its
+ * out_proj epilogue (layer 0's ln_1 and ln_final stay LayerNorm passes; not used with deep
+ * prompts or an fp32 encoder). The saved mean / rstd are the same quantities the LayerNorm pass
+ * writes, so the backward is unchanged. fold_ptrs == NULL clears. Pointers must stay valid. */
+int clipk_encoder_set_ln_fold(clipk_encoder* e, const void* const* fold_ptrs);
 
 /* ViT with visual prompts, forward with saved activations and input-grad backward (the
  * prompted VisionTransformer of IVLP / PromptSRC, model.py:401-431, and MaPLe, 434-485):

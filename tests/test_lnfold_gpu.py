@@ -1,0 +1,138 @@
+"""LayerNorm folded into the text GEMMs (clipk_gemm_ln / clipk_ln_stats_merge /
+clipk_encoder_set_ln_fold) vs PyTorch fp32/fp64 references of the same ops.
+
+The fold rewrites LN(x) W^T + b (PromptSRC/clip/model.py:153-159 feeding 171-177 / 185-188)
+as rstd * (x W'^T - mean * s) + c, W' = W diag(gamma): the producer GEMM writes per-row
+statistics partials of the residual stream it stores, and the consumer GEMM reads x itself.
+Bars: the statistics match torch on the stored (rounded) values to fp32 rounding; the folded
+GEMM is within the dtype's tolerance of the fp64 reference and no further from it than the
+un-fused path (LayerNorm pass -> 16-bit -> GEMM) by more than a small margin."""
+import math
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from fsp_amd import ops, _native as N
+from fsp_amd.clip import model as M, synth
+from fsp_amd.trainers.prompt_base import TextShape
+
+pytestmark = pytest.mark.gpu
+
+TOL = {torch.float16: 1e-2, torch.bfloat16: 3e-2}
+
+
+def partials(x):
+    """The producer's statistics partials of x (what an EPI_BIAS_RES clipk_gemm_ln writes)."""
+    xg = x.double().reshape(x.shape[0], -1, 64)
+    return torch.stack([xg.sum(-1), ((xg - xg.mean(-1, keepdim=True)) ** 2).sum(-1)], -1).float().contiguous()
+
+
+def _rel(out, ref):
+    return ((out.double() - ref.double()).abs().max() / (ref.double().abs().max() + 1e-30)).item()
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("Mr,Nn,K", [(47160, 512, 2048), (8000, 512, 512), (300, 768, 512), (20000, 768, 3072),
+                                     (1, 512, 512)])
+def test_gemm_ln_stats(dev, dtype, Mr, Nn, K):
+    g = torch.Generator(device="cpu").manual_seed(Mr + Nn + K)
+    a = torch.randn(Mr, K, generator=g).to(dev, dtype)
+    b = (torch.randn(Nn, K, generator=g) / math.sqrt(K)).to(dev, dtype)
+    bias = (0.1 * torch.randn(Nn, generator=g)).to(dev)
+    # residual stream with a per-row offset and an outlier column (CLIP's large-magnitude dims)
+    res = torch.randn(Mr, Nn, generator=g) + 3.0 * torch.randn(Mr, 1, generator=g)
+    res[:, 7] *= 40.0
+    res = res.to(dev, dtype)
+    stats = torch.full((Mr, Nn // 64, 2), float("nan"), device=dev)
+    out = ops.gemm_ln(a, b, N.EPI_BIAS_RES, bias, stats, res=res)
+    plain = ops.gemm(a, b, N.EPI_BIAS_RES, dtype, bias=bias, res=res)
+    assert torch.equal(out, plain), "stats epilogue changed the stored output"
+    mean, rstd = ops.ln_stats_merge(stats, Nn)
+    x = out.double()
+    mu = x.mean(1)
+    var = x.var(1, unbiased=False)
+    assert ((mean.double() - mu).abs() <= 1e-5 * (x.abs().amax(1) + 1)).all()
+    assert ((rstd.double() * torch.sqrt(var + 1e-5) - 1).abs().max().item()) <= 2e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("epi", [N.EPI_BIAS, N.EPI_BIAS_QGELU])
+@pytest.mark.parametrize("Mr,Wd,Nn", [(47160, 512, 1536), (47160, 512, 2048), (8000, 512, 2048), (300, 768, 2304),
+                                      (3, 512, 1536)])
+def test_gemm_ln_fold(dev, dtype, epi, Mr, Wd, Nn):
+    g = torch.Generator(device="cpu").manual_seed(Mr * 3 + Wd + Nn + epi)
+    x = torch.randn(Mr, Wd, generator=g) + 2.0 * torch.randn(Mr, 1, generator=g)
+    x[:, 5] *= 30.0
+    x = x.to(dev, dtype)
+    gamma = (1.0 + 0.2 * torch.randn(Wd, generator=g)).to(dev)
+    beta = (0.1 * torch.randn(Wd, generator=g)).to(dev)
+    w = (torch.randn(Nn, Wd, generator=g) / math.sqrt(Wd)).to(dev)
+    bias = (0.05 * torch.randn(Nn, generator=g)).to(dev)
+    wp, s, c = M.ln_fold_weights(w, bias, gamma, beta, dtype, dev)
+    xd = x.double()
+    ref = F.layer_norm(xd, (Wd,), gamma.double(), beta.double(), eps=1e-5) @ w.double().t() + bias.double()
+    if epi == N.EPI_BIAS_QGELU:
+        ref_g = ref * torch.sigmoid(1.702 * ref)
+    # the un-fused path the fold replaces: LayerNorm pass -> 16-bit -> GEMM with W
+    xn = ops.layernorm(x, gamma, beta, out_dtype=dtype)
+    wq = w.to(dtype)
+    mean, rstd = ops.ln_stats_merge(partials(x), Wd)
+    if epi == N.EPI_BIAS:
+        out = ops.gemm_ln(x, wp, epi, c, colsum=s, mean=mean, rstd=rstd)
+        unf = ops.gemm(xn, wq, N.EPI_BIAS, dtype, bias=bias)
+        e_fold, e_unf = _rel(out, ref), _rel(unf, ref)
+    else:
+        out, h = ops.gemm_ln(x, wp, epi, c, colsum=s, mean=mean, rstd=rstd, want_out2=True)
+        unf, uh = ops.gemm(xn, wq, N.EPI_BIAS_QGELU, dtype, bias=bias, want_out2=True)
+        e_fold, e_unf = max(_rel(out, ref_g), _rel(h, ref)), max(_rel(unf, ref_g), _rel(uh, ref))
+    mu, var = xd.mean(1), xd.var(1, unbiased=False)
+    assert ((mean.double() - mu).abs() <= 1e-5 * (xd.abs().amax(1) + 1)).all()
+    assert ((rstd.double() * torch.sqrt(var + 1e-5) - 1).abs().max().item()) <= 2e-5
+    assert e_fold <= TOL[dtype], f"fold rel err {e_fold:.3e}"
+    assert e_fold <= 1.5 * e_unf + 2e-3, f"fold {e_fold:.3e} vs un-fused {e_unf:.3e}"
+
+
+def _encoder_pair(arch, prec, dev):
+    sd = synth.make_state_dict(arch, seed=0)
+    a = synth.ARCHS[arch]
+    os.environ["FSP_LN_FOLD"] = "0"
+    try:
+        off = M.TextEncoderCore(sd, a, prec, dev)
+    finally:
+        os.environ.pop("FSP_LN_FOLD", None)
+    on = M.TextEncoderCore(sd, a, prec, dev)
+    ref = M.TextEncoderCore(sd, a, "fp32", dev)
+    return a, on, off, ref
+
+
+@pytest.mark.parametrize("prec", ["fp16", "bf16", "amp"])
+def test_text_encoder_fold_on_off(dev, prec):
+    """Whole text encoder (12 layers, plain layout, EOT-last layer): the folded encoder's
+    features and input gradient against the fp32 encoder, no worse than the un-fused one."""
+    a, on, off, ref = _encoder_pair("ViT-B/16", prec, dev)
+    nseq, L = 64, 11
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x0 = (0.3 * torch.randn(nseq * L, a.transformer_width, generator=g)).to(dev)
+    eot = (torch.arange(nseq) * L + (3 + torch.arange(nseq) % 8)).to(torch.int32).to(dev)
+    shape = TextShape(eot, nseq=nseq, L=L)
+    dtxt = torch.randn(nseq, a.embed_dim, generator=g).to(dev)
+    res = {}
+    for nm, core in (("on", on), ("off", off), ("ref", ref)):
+        txt, saved = core.forward(x0, shape, save=True)
+        dx0 = core.backward(dtxt, shape, saved)
+        res[nm] = (txt.double(), dx0.double())
+    def cos(u, v):
+        return (1 - (u * v).sum() / (u.norm() * v.norm())).item()
+    # only the rows that reach an EOT row carry a gradient
+    live = torch.zeros(nseq * L, dtype=torch.bool, device=dev)
+    for s in range(nseq):
+        live[s * L:int(eot[s]) + 1] = True
+    for i, nm in ((0, "txt"), (1, "dx0")):
+        r = res["ref"][i] if i == 0 else res["ref"][i][live]
+        e_on = cos((res["on"][i] if i == 0 else res["on"][i][live]).flatten(), r.flatten())
+        e_off = cos((res["off"][i] if i == 0 else res["off"][i][live]).flatten(), r.flatten())
+        bar = 5e-3 if prec == "bf16" else 1e-3
+        assert e_on <= bar, f"{nm}: fold 1-cos {e_on:.3e}"
+        assert e_on <= 2.0 * e_off + 1e-5, f"{nm}: fold {e_on:.3e} vs un-fused {e_off:.3e}"
