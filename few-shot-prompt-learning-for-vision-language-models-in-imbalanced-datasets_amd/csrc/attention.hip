@@ -405,24 +405,50 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma16(int nseq, int L, int H, i
 
 // ------------------------------------------------------------------ forward, MFMA (any L)
 // Flash-style forward on MFMA for 16-bit operands: block = 4 waves = 64 query rows of one
-// (seq, head); keys streamed through LDS in chunks of 64 (K and V tiles, row-major).
-// Per 16-key sub-chunk: S^T = K Q^T (16x16x32; query on the lane, keys in registers),
-// online softmax per query, O += P V (16x16x16 with P from the S^T registers as the A
-// operand and V through ds_read_b64_tr_b16).
+// (seq, head); keys streamed through LDS in chunks of 64 (K and V tiles, row-major); per 32
+// keys S^T = K Q^T (16x16x32: query on the lane, 8 keys per lane in registers). Built for low
+// VALU per key (the first form -- O in the query-row layout, one softmax update per 16 keys,
+// ds_bpermute shuffles -- ran 6 MFMAs against ~100 VALU per 16 keys: L 577 50.6 -> 33.2 us,
+// 100 x L 197 63.8 -> 48.8 us per launch, profiles/r03c/vit_attn_ab.txt):
+//  * O is accumulated transposed, O^T = V^T P^T (16x16x32: A = V^T by two transposed LDS reads,
+//    B = P^T straight from the S^T registers), so a lane holds its own query's O entries and the
+//    softmax rescale needs no cross-lane broadcast; the row sum l stays lane-partial until the end;
+//  * one softmax update per 32 keys (4 S MFMAs, 8 scores per lane), max over the 4 lane groups by
+//    v_permlane32/16_swap (VALU, no LDS), scores in the log2 domain (exp2);
+//  * the rescale of O is skipped when no query's running max moved (wave vote);
+//  * the next 64-key K/V chunk is loaded into registers while the current one is consumed.
+// Key slot 8 g4 + j of the PV MFMA is key 4 g4 + j (j < 4) or 16 + 4 g4 + j - 4 of the 32.
+__device__ __forceinline__ float xmax4(float v) {  // max over lane bits 4 and 5
+  auto a = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false,
+                                            false);
+  v = fmaxf(__builtin_bit_cast(float, (unsigned)a[0]), __builtin_bit_cast(float, (unsigned)a[1]));
+  auto b = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false,
+                                            false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)b[0]), __builtin_bit_cast(float, (unsigned)b[1]));
+}
+__device__ __forceinline__ float xsum4(float v) {  // sum over lane bits 4 and 5
+  auto a = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false,
+                                            false);
+  v = __builtin_bit_cast(float, (unsigned)a[0]) + __builtin_bit_cast(float, (unsigned)a[1]);
+  auto b = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false,
+                                            false);
+  return __builtin_bit_cast(float, (unsigned)b[0]) + __builtin_bit_cast(float, (unsigned)b[1]);
+}
+
 template <typename T>
-__global__ __launch_bounds__(256) void attn_fwd_mfma(int nseq, int L, int H, int causal,
-                                                     const T* __restrict__ qkv, int ldq,
-                                                     T* __restrict__ out, int ldo,
-                                                     float* __restrict__ lse) {
+__global__ __launch_bounds__(256) void attn_fwd_mfma_t(int nseq, int L, int H, int causal,
+                                                       const T* __restrict__ qkv, int ldq,
+                                                       T* __restrict__ out, int ldo,
+                                                       float* __restrict__ lse) {
   __shared__ CLIPK_LDS_ALIGN short sK[64 * TRS];
   __shared__ CLIPK_LDS_ALIGN short sV[64 * TRS];
+  constexpr float kLog2e = 1.4426950408889634f;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
   const int h = blockIdx.y, s = blockIdx.z;
   const int W = H * 64;
   const size_t row0 = (size_t)s * L;
   const int q0 = blockIdx.x * 64 + w * 16;
-  // Q fragments (B operand of S^T = K Q^T): row q0+r16, 16-B chunks g4 and g4+4
   const int qr = q0 + r16;
   const bool qok = qr < L;
   const T* qp = qkv + (row0 + (qok ? qr : 0)) * ldq + h * 64;
@@ -430,81 +456,102 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(int nseq, int L, int H, int
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) qf[kk] = ld_row16(qp + 8 * g4 + 32 * kk, qok);
 
-  f32x4 o[4];
+  f32x4 o[4];  // o[t][r] = O[query r16][dim 16 t + 4 g4 + r]
 #pragma unroll
   for (int t = 0; t < 4; ++t) o[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;  // for query r16 (replicated over g4)
+  float m = -INFINITY, l = 0.f;  // running max (log2 domain, replicated over g4), lane-partial sum
   const int qmax = min(L, (int)(blockIdx.x + 1) * 64) - 1;
   const int kend = causal ? qmax + 1 : L;
-  for (int k0 = 0; k0 < kend; k0 += 64) {
-    __syncthreads();
-    // cooperative load: 64 rows x 128 B of K and of V (2 x 16 B per thread each)
+  // K / V chunk staging: thread tid moves 16 B of rows (tid >> 3) and 32 + (tid >> 3)
+  s16x8 rk[2], rv[2];
+  auto fetch = [&](int k0) {
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
-      const int idx = it * 256 + tid;
-      const int rr = idx >> 3, ch = idx & 7;
+      const int rr = it * 32 + (tid >> 3), ch = tid & 7;
       const int kr = k0 + rr;
       const bool ok = kr < L;
       const T* base = qkv + (row0 + (ok ? kr : 0)) * ldq + h * 64 + ch * 8;
-      *reinterpret_cast<s16x8*>(sK + rr * TRS + ch * 8) = ld_row16(base + W, ok);
-      *reinterpret_cast<s16x8*>(sV + rr * TRS + ch * 8) = ld_row16(base + 2 * W, ok);
+      rk[it] = ld_row16(base + W, ok);
+      rv[it] = ld_row16(base + 2 * W, ok);
+    }
+  };
+  fetch(0);
+  const float sc2 = kScale * kLog2e;
+  for (int k0 = 0; k0 < kend; k0 += 64) {
+    __syncthreads();  // the previous chunk's readers are done
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int rr = it * 32 + (tid >> 3), ch = tid & 7;
+      *reinterpret_cast<s16x8*>(sK + rr * TRS + ch * 8) = rk[it];
+      *reinterpret_cast<s16x8*>(sV + rr * TRS + ch * 8) = rv[it];
     }
     __syncthreads();
-    const int nsub = min(4, (kend - k0 + 15) / 16);
-    for (int sc = 0; sc < nsub; ++sc) {
-      f32x4 st = {0.f, 0.f, 0.f, 0.f};
+    if (k0 + 64 < kend) fetch(k0 + 64);  // in flight while this chunk is consumed
+    const int npair = min(2, (kend - k0 + 31) / 32);
+    for (int pc = 0; pc < npair; ++pc) {
+      const int kb = pc * 32;  // first key of the 32 within the chunk
+      float sv[8];
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const s16x8 kf = *reinterpret_cast<const s16x8*>(sK + (sc * 16 + r16) * TRS + 8 * g4 + 32 * kk);
-        st = mfma32_t<T>(kf, qf[kk], st);  // st[r] = S[q = r16][key = k0 + sc*16 + 4g4 + r]
-      }
-      float sv[4], mx = -INFINITY;
+      for (int sub = 0; sub < 2; ++sub) {
+        f32x4 st = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = k0 + sc * 16 + 4 * g4 + r;
-        float v = st[r] * kScale;
-        if (key >= L || (causal && key > qr)) v = -INFINITY;
-        sv[r] = v;
-        mx = fmaxf(mx, v);
+        for (int kk = 0; kk < 2; ++kk) {
+          const s16x8 kf = *reinterpret_cast<const s16x8*>(sK + (kb + sub * 16 + r16) * TRS + 8 * g4 + 32 * kk);
+          st = mfma32_t<T>(kf, qf[kk], st);  // st[r] = S[query r16][key kb + 16 sub + 4 g4 + r]
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sv[4 * sub + r] = st[r] * sc2;
       }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const int kabs = k0 + kb;
+      if (kabs + 32 > L || (causal && kabs + 31 > q0)) {  // wave-uniform: edge chunk only
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int key = kabs + (j < 4 ? 4 * g4 + j : 16 + 4 * g4 + j - 4);
+          if (key >= L || (causal && key > qr)) sv[j] = -INFINITY;
+        }
+      }
+      float mx = sv[0];
+#pragma unroll
+      for (int j = 1; j < 8; ++j) mx = fmaxf(mx, sv[j]);
+      mx = xmax4(mx);
       const float mn = fmaxf(m, mx);
-      const float corr = mn == -INFINITY ? 1.f : __expf(m - mn);
-      float p[4], ps = 0.f;
+      const float msafe = mn == -INFINITY ? 0.f : mn;
+      float p[8], ps = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        p[r] = mn == -INFINITY ? 0.f : __expf(sv[r] - mn);
-        ps += p[r];
+      for (int j = 0; j < 8; ++j) {
+        p[j] = __builtin_amdgcn_exp2f(sv[j] - msafe);
+        ps += p[j];
       }
-      ps += __shfl_xor(ps, 16, 64);
-      ps += __shfl_xor(ps, 32, 64);
-      l = l * corr + ps;
+      if (__builtin_amdgcn_ballot_w64(mn > m) != 0) {  // some query's max moved: rescale
+        const float corr = __builtin_amdgcn_exp2f(m - msafe);  // m = -inf -> 0 (O, l are 0)
+        l *= corr;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) o[t] *= corr;
+      }
+      l += ps;
       m = mn;
-      // rescale O rows (query 4g4+r) by that query's corr
+      typedef T t8 __attribute__((ext_vector_type(8)));
+      t8 pv;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float c = __shfl(corr, 4 * g4 + r, 64);
+      for (int j = 0; j < 8; ++j) pv[j] = (T)p[j];
+      const s16x8 pb = __builtin_bit_cast(s16x8, pv);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) o[t][r] *= c;
+      for (int t = 0; t < 4; ++t) {
+        const s16x4 lo = tr_read(sV, kb + 4 * g4, 16 * t, lane), hi = tr_read(sV, kb + 16 + 4 * g4, 16 * t, lane);
+        const s16x8 va = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        o[t] = mfma32_t<T>(va, pb, o[t]);
       }
-      const s16x4 pa = pack4<T>(p[0], p[1], p[2], p[3]);  // A[m=query r16][k=key 4g4+jj]
-#pragma unroll
-      for (int t = 0; t < 4; ++t) o[t] = mfma16_t<T>(pa, tr_read(sV, sc * 16 + 4 * g4, 16 * t, lane), o[t]);
     }
   }
-  // normalise and store rows q0 + 4g4 + r
+  const float lt = xsum4(l);
+  const float inv = 1.0f / lt;
+  if (qok) {
+    T* op = out + (row0 + qr) * ldo + h * 64 + 4 * g4;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int q = q0 + 4 * g4 + r;
-    const float inv = 1.0f / __shfl(l, 4 * g4 + r, 64);
-    if (q < L) {
-      T* op = out + (row0 + q) * ldo + h * 64 + r16;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) op[16 * t] = (T)(o[t][r] * inv);
-    }
+    for (int t = 0; t < 4; ++t)
+      *reinterpret_cast<s16x4*>(op + 16 * t) = pack4<T>(o[t][0] * inv, o[t][1] * inv, o[t][2] * inv, o[t][3] * inv);
+    if (lse && g4 == 0) lse[(row0 + qr) * H + h] = (m + __log2f(lt)) * 0.6931471805599453f;
   }
-  if (lse && g4 == 0 && qok) lse[(row0 + qr) * H + h] = m + __logf(l);
 }
 
 // ------------------------------------------------------------------ backward, any L (vision)
@@ -832,7 +879,7 @@ static int launch_fwd(int nseq, int L, int H, int causal, const void* qkv, int l
   if constexpr (sizeof(T) == 2) {
     if (L > 16) {  // MFMA flash forward (vision L = 50..577, text 16 < L <= 77)
       dim3 grid((L + 63) / 64, H, nseq);
-      hipLaunchKernelGGL((attn_fwd_mfma<T>), grid, dim3(256), 0, st, nseq, L, H, causal, (const T*)qkv, ldq,
+      hipLaunchKernelGGL((attn_fwd_mfma_t<T>), grid, dim3(256), 0, st, nseq, L, H, causal, (const T*)qkv, ldq,
                          (T*)out, ldo, lse);
       CLIPK_CHECK_LAUNCH();
       return CLIPK_OK;

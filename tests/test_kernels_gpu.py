@@ -189,9 +189,10 @@ def attn_ref(qkv, nseq, L, H, causal):
     return o.permute(0, 2, 1, 3).reshape(nseq * L, W), lse.permute(0, 2, 1).reshape(nseq * L, H)
 
 
-@pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("nseq,L,H,causal", [(7, 11, 8, 1), (5, 23, 2, 1), (3, 50, 4, 1), (2, 77, 8, 1),
-                                             (2, 197, 12, 0), (1, 257, 2, 0), (3, 5, 2, 0)])
+                                             (2, 197, 12, 0), (1, 257, 2, 0), (3, 5, 2, 0), (2, 577, 4, 0),
+                                             (2, 130, 2, 1)])
 def test_attention_fwd(dev, dtype, nseq, L, H, causal):
     g = torch.Generator().manual_seed(L * H)
     qkv = torch.randn(nseq * L, 3 * H * 64, generator=g).to(dev).to(dtype)
