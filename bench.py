@@ -91,7 +91,9 @@ def reference_cpu(arch, classes):
     return None
 PEAK = {"fp16": 2500.0, "bf16": 2500.0, "amp": 2500.0, "fp32": 157.3}  # dense TFLOP/s (MI355X guide)
 HBM_PEAK_GBS = 8000.0  # HBM3E, MI355X_MICROARCH.md
-PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc", "traffic.json")
+# the latest round's PMC passes (tools/pmc_bench.sh), else the previous round's
+PMC_FILE = next((f for f in (os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r03_pmc", "r02_pmc"))
+                 if os.path.exists(f)), os.path.join(ROOT, "profiles", "r03_pmc", "traffic.json"))
 
 # kernel classes of the step: launch sites that run the same kernel instantiation (rocprofv3
 # kernel-name key, for the PMC traffic lookup) -- the text GEMMs by role, attention, LN
@@ -99,13 +101,14 @@ KERNELS = {
     "gemm_dx_n512": (["text.fc_dx", "text.qkv_dx", "text.out_dx"], "EPI_NONE 192x256", "mfma"),
     "gemm_proj_fwd": (["text.proj_fwd"], "EPI_BIAS_RES N=512 K=2048", "mfma"),
     "gemm_dgelu": (["text.proj_dx_dgelu"], "EPI_DQGELU", "mfma"),
-    "gemm_fc_fwd": (["text.fc_fwd"], "EPI_BIAS_QGELU N=2048 (h and QuickGELU(h))", "mfma"),
-    "gemm_qkv_fwd": (["text.qkv_fwd"], "EPI_BIAS N=1536", "mfma"),
+    "gemm_fc_fwd": (["text.fc_fwd"], "EPI_BIAS_QGELU N=2048 (h and QuickGELU(h); ln_2 folded)", "mfma"),
+    "gemm_qkv_fwd": (["text.qkv_fwd"], "EPI_BIAS N=1536 (ln_1 folded)", "mfma"),
     "gemm_out_fwd": (["text.out_fwd"], "EPI_BIAS_RES N=512", "mfma"),
     "attn_bwd": (["text.attn_bwd"], "attn_prefix_bwd_lds", "hbm"),
     "attn_fwd": (["text.attn_fwd"], "attn_prefix_fwd_lds", "hbm"),
     "ln_bwd": (["text.ln_bwd"], "ln_bwd_kernel", "hbm"),
     "ln_fwd": (["text.ln_fwd"], "ln_fwd_kernel", "hbm"),
+    "ln_stats": (["text.ln_stats"], "ln_stats_merge_kernel (LN fold statistics)", "hbm"),
     "vit": (["vit.patch_embed", "vit.qkv_fwd", "vit.attn_fwd", "vit.out_fwd", "vit.fc_fwd", "vit.proj_fwd",
              "vit.ln_fwd", "vit.head"], "ViT forward (all sites)", "mfma"),
 }
@@ -215,7 +218,7 @@ def roofline_of(table, prec):
     r.update({"traffic": pmc_traffic(ROOF_PMC_KEY.get(name)) if prec == "fp16" else None,
               "kernel_class": name, "kernel": k["kernel"], "avg_launch_ms": k["avg_launch_ms"],
               "flops_per_launch": fl, "algorithmic_bytes": by,
-              "traffic_note": "HBM bytes/launch, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (profiles/r02_pmc)"})
+              "traffic_note": "HBM bytes/launch, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (" + os.path.relpath(os.path.dirname(PMC_FILE), ROOT) + ")"})
     return r
 
 
