@@ -790,6 +790,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
 // fills the last wave of CUs better than 256-row tiles (N = 512 at 47k rows: 1.45 -> 1.92
 // waves).
 static int g_force_cfg = -2;  // -2: unread, -1: auto
+static int num_cus();
 static int pick_cfg(int M, int N, int esz) {
   if (g_force_cfg == -2) {
     const char* e = getenv("CLIPK_GEMM_CFG");
@@ -798,9 +799,14 @@ static int pick_cfg(int M, int N, int esz) {
   if (esz == 4) return 0;  // fp32 parity path: one configuration
   if (g_force_cfg >= 0) {
     if ((g_force_cfg == 1 || g_force_cfg == 3 || g_force_cfg == 6) && N % 256 == 0) return g_force_cfg;
+    if (g_force_cfg == 7) return g_force_cfg;
     if (g_force_cfg == 2) return g_force_cfg;
     return 0;
   }
+  // small M (the ViT at training batch sizes): 64x128 tiles while their grid is at most two
+  // rounds of CUs (ViT-B/16 at 8 images: qkv 13.2 -> 11.7 us, out_proj 14.1 -> 11.9 us;
+  // profiles/r03c/vit_gemm_ab.txt)
+  if (M < 4096 && (long long)((M + 63) / 64) * (N / 128) <= 2LL * num_cus()) return 7;
   if (M >= 4096 && N % 256 == 0) {
     // 256- vs 192-row tiles: fraction of the last round of CU slots each leaves busy
     const double cus = 256.0;
@@ -924,6 +930,15 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
         hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 192, 256, 2, 4, true, GEMM_ROWB, 2, false, false, LNM>), dim3((cus / 8) * 8), dim3(512), 0, st, g);
       else
         hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 192, 256, 2, 4, false, GEMM_ROWB, 2, false, false, LNM>), dim3(nwg), dim3(512), 0, st, g);
+    } else if (cfg == 7) {
+      // 64x128 (4 waves of 32x64): twice the 128x128 grid for the small-M ViT projections
+      const int nwg = ((g.M + 63) / 64) * (g.N / 128);
+      if (nwg <= num_cus() && deep_small())
+        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 64, 128, 2, 2, false, GEMM_ROWB, 4, false, false, LNM>),
+                           dim3(nwg), dim3(256), 0, st, g);
+      else
+        hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 64, 128, 2, 2, false, GEMM_ROWB, 2, false, false, LNM>),
+                           dim3(nwg), dim3(256), 0, st, g);
     } else if (cfg == 2) {
       const int nwg = ((g.M + 255) / 256) * (g.N / 128);
       hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 128, 4, 2, false, GEMM_ROWB, 2, false, false, LNM>), dim3(nwg), dim3(512), 0, st, g);
@@ -1211,7 +1226,7 @@ extern "C" int clipk_gemm_stamps(void* host, size_t bytes) {
 
 // Benchmark knob: force a tile configuration (-1 = automatic choice).
 extern "C" int clipk_gemm_set_config(int cfg) {
-  if (cfg < -1 || cfg > 6 || cfg == 4 || cfg == 5) return CLIPK_EINVAL;
+  if (cfg < -1 || cfg > 7 || cfg == 4 || cfg == 5) return CLIPK_EINVAL;
   g_force_cfg = cfg;
   return CLIPK_OK;
 }
