@@ -173,7 +173,7 @@ struct TextBufs {
   void *xn = nullptr, *g = nullptr, *lnf = nullptr, *oc = nullptr, *xc = nullptr;
   // LN fold: per (row, 64-column group) statistics partials of the residual stream; mean /
   // rstd of the un-saved (inference) forward
-  float *lnst = nullptr, *tm = nullptr, *tr = nullptr;
+  float *lnst = nullptr, *tm = nullptr, *tr = nullptr, *rnb = nullptr;
   size_t saved_bytes = 0, ws_bytes = 0;
 };
 
@@ -223,6 +223,7 @@ static TextBufs text_layout(const clipk_encoder* e, size_t rows, int nout, void*
   t.lnst = (float*)wk.take(rows * (W / 64) * 8);
   t.tm = (float*)wk.take(rows * 4);
   t.tr = (float*)wk.take(rows * 4);
+  t.rnb = (float*)wk.take(rows * 8);
   t.saved_bytes = save ? sv.off : 0;
   t.ws_bytes = wk.off;
   return t;
@@ -375,26 +376,27 @@ static int block_fwd(const clipk_encoder* e, const std::array<const void*, 16>& 
 
 // ---- LayerNorm fold (clipk_encoder_set_ln_fold; text encoder, 16-bit residual stream)
 static int gemm_ln(int act, int epi, int M, int N, int K, const void* A, const void* B, const float* bias,
-                   const void* res, void* o, void* o2, float* stats, const float* colsum, const float* m,
-                   const float* r, hipStream_t st, int prof_cls, const char* site) {
+                   const void* res, void* o, void* o2, float* stats, const float* colsum, const float* rnb,
+                   hipStream_t st, int prof_cls, const char* site) {
   const double b = gemm_bytes(act, act, epi, M, N, K, o2 != nullptr, act) + (stats ? (double)M * (N / 64) * 8 : 0.0) +
-                   (m ? 8.0 * M : 0.0);
+                   (rnb ? 8.0 * M : 0.0);
   ProfScope ps(prof_cls, st, 2.0 * M * N * K, site, b);
-  return clipk_gemm_ln(act, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, stats, colsum, m, r, st);
+  return clipk_gemm_ln(act, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, stats, colsum, rnb, st);
 }
-static int ln_merge(int rows, int W, const float* lnst, float* m, float* r, hipStream_t st) {
-  ProfScope ps(CLIPK_PROF_NONE, st, 0.0, "text.ln_stats", (double)rows * (W / 64) * 8 + 8.0 * rows);
-  return clipk_ln_stats_merge(rows, W, lnst, m, r, st);
+// mean / rstd (kept for the LayerNorm backward) and the folding GEMM's (rstd, -rstd mean) pairs
+static int ln_merge(int rows, int W, const float* lnst, float* m, float* r, float* rnb, hipStream_t st) {
+  ProfScope ps(CLIPK_PROF_NONE, st, 0.0, "text.ln_stats", (double)rows * (W / 64) * 8 + 16.0 * rows);
+  return clipk_ln_stats_merge(rows, W, lnst, m, r, rnb, st);
 }
 // attention half: ln_1 statistics of X merged from the partials the previous layer's c_proj
 // epilogue wrote (lnst); the qkv projection reads X itself through the fold
 static int block_attn_fold(const clipk_encoder* e, const std::array<const void*, 6>& f, const SeqShape& sh,
                            const void* X, void* qkv, void* o, float* lse, float* m1, float* r1, const float* lnst,
-                           hipStream_t st) {
+                           float* rnb, hipStream_t st) {
   const int W = e->W, rows = sh.rows, act = e->act;
-  TRY(ln_merge(rows, W, lnst, m1, r1, st));
+  TRY(ln_merge(rows, W, lnst, m1, r1, rnb, st));
   TRY(gemm_ln(act, CLIPK_EPI_BIAS, rows, 3 * W, W, X, f[0], (const float*)f[2], nullptr, qkv, nullptr,
-              nullptr, (const float*)f[1], m1, r1, st, CLIPK_PROF_GEMM_ALL, "text.qkv_fwd"));
+              nullptr, (const float*)f[1], rnb, st, CLIPK_PROF_GEMM_ALL, "text.qkv_fwd"));
   const double ab = (double)rows * 4 * W * esize(act) + (lse ? 4.0 * rows * e->heads : 0.0);
   ProfScope ps(CLIPK_PROF_ATTN, st, 0.0, "text.attn_fwd", ab);
   return attn_fwd(e, sh, qkv, o, lse, st);
@@ -403,17 +405,17 @@ static int block_attn_fold(const clipk_encoder* e, const std::array<const void*,
 // fold, c_proj writes Xo (and, when a next layer folds ln_1, its statistics)
 static int block_post_fold(const clipk_encoder* e, const std::array<const void*, 16>& w,
                            const std::array<const void*, 6>& f, int rows, const void* X, const void* o, void* Xm,
-                           void* Xo, void* h, void* g, float* m2, float* r2, float* lnst, bool stats_next,
-                           hipStream_t st) {
+                           void* Xo, void* h, void* g, float* m2, float* r2, float* lnst, float* rnb,
+                           bool stats_next, hipStream_t st) {
   const int W = e->W, act = e->act;
   TRY(gemm_ln(act, CLIPK_EPI_BIAS_RES, rows, W, W, o, w[4], (const float*)w[5], X, Xm, nullptr, lnst, nullptr,
-              nullptr, nullptr, st, CLIPK_PROF_GEMM_ALL, "text.out_fwd"));
-  TRY(ln_merge(rows, W, lnst, m2, r2, st));
+              nullptr, st, CLIPK_PROF_GEMM_ALL, "text.out_fwd"));
+  TRY(ln_merge(rows, W, lnst, m2, r2, rnb, st));
   TRY(gemm_ln(act, CLIPK_EPI_BIAS_QGELU, rows, 4 * W, W, Xm, f[3], (const float*)f[5], nullptr, g, h, nullptr,
-              (const float*)f[4], m2, r2, st, CLIPK_PROF_GEMM_FC, "text.fc_fwd"));
+              (const float*)f[4], rnb, st, CLIPK_PROF_GEMM_FC, "text.fc_fwd"));
   if (stats_next)
     return gemm_ln(act, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo, nullptr, lnst,
-                   nullptr, nullptr, nullptr, st, CLIPK_PROF_GEMM_ALL, "text.proj_fwd");
+                   nullptr, nullptr, st, CLIPK_PROF_GEMM_ALL, "text.proj_fwd");
   return gemm(act, act, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo, nullptr, nullptr,
               0, st, CLIPK_PROF_GEMM_ALL, nullptr, 0, "text.proj_fwd");
 }
@@ -667,7 +669,7 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
       TRY(block_attn_shared0(e, e->lw[l], sh, rd, cur, t.xn, t.qkv[l], t.o[l], t.lse[l], t.mean1[l], t.rstd1[l],
                              (int*)t.g, st));
     else if (fold && have_stats)
-      TRY(block_attn_fold(e, e->fold[l], sh, cur, t.qkv[l], t.o[l], t.lse[l], m1, r1, t.lnst, st));
+      TRY(block_attn_fold(e, e->fold[l], sh, cur, t.qkv[l], t.o[l], t.lse[l], m1, r1, t.lnst, t.rnb, st));
     else
       TRY(block_attn(e, e->lw[l], sh, rd, cur, t.xn, t.qkv[l], t.o[l], t.lse[l], t.mean1[l], t.rstd1[l], st,
                      io.text, io.sk, io.skb));
@@ -687,7 +689,7 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
     const int n = compact ? nout : sh.rows;
     if (fold)
       TRY(block_post_fold(e, e->lw[l], e->fold[l], n, xin, oin, t.Xm[l], Xo, save ? t.h[l] : nullptr, t.g, m2, r2,
-                          t.lnst, l + 1 < nl, st));
+                          t.lnst, t.rnb, l + 1 < nl, st));
     else
       TRY(block_post(e, e->lw[l], n, rd, xin, oin, t.Xm[l], Xo, t.xn, save ? t.h[l] : nullptr, t.g, t.mean2[l],
                      t.rstd2[l], st, io.text, compact ? nullptr : io.sk, compact ? 0 : io.skb));

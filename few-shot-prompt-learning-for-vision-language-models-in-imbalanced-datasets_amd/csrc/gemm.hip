@@ -52,12 +52,11 @@ struct GemmArgs {
   int skew;                   // persistent kernels: ~us of start delay for every other CU of an XCD
   // LayerNorm folded into the GEMMs (clipk_gemm_ln): LNM 1 writes per (row, 64-column group)
   // statistics partials of the rounded output to lnstats; LNM 2 applies LN to A = x through the
-  // epilogue rstd * (acc - mean * colsum) + bias (B = W diag(gamma), bias = b + W beta) with the
-  // rows' mean / rstd (clipk_ln_stats_merge of the producer's partials)
+  // epilogue rstd * acc - rstd * mean * colsum + bias (B = W diag(gamma), bias = b + W beta) with
+  // the rows' (rstd, -rstd * mean) pairs (clipk_ln_stats_merge of the producer's partials)
   float* lnstats;
   const float* colsum;
-  const float* lnmean;
-  const float* lnrstd;
+  const f32x2* lnrnb;
 };
 
 // Sum over the aligned 8-lane group (DPP: quad xor 1, quad xor 2, half-row mirror i <-> 7 - i).
@@ -461,7 +460,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         for (int q = 0; q < NQ; ++q) {
           int mc = mg + RPQ * q + er;
           mc = mc < g.M ? mc : g.M - 1;
-          lnp[slot][q] = (f32x2){g.lnmean[mc], g.lnrstd[mc]};
+          lnp[slot][q] = g.lnrnb[mc];  // one 8-B load per row
         }
       }
     };
@@ -717,7 +716,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         }
         const int off = ((m - m0) * g.ldo + ncol) * (int)sizeof(TO);  // rows >= M: out of range, dropped
         if constexpr (LN_IN) {
-          const float rs = lnp[i & 1][q][1], nb = -rs * lnp[i & 1][q][0];
+          const float rs = lnp[i & 1][q][0], nb = lnp[i & 1][q][1];
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] = fmaf(rs, v[c], fmaf(nb, csum[c], bia[c]));
         } else if constexpr (HAS_BIAS) {
@@ -1065,23 +1064,22 @@ static int dispatch_ln(int epi, const GemmArgs& g, hipStream_t st) {
 }  // namespace clipk
 
 // LayerNorm folded into the text GEMMs (include/clipk.h): statistics partials out (EPI_BIAS_RES)
-// or colsum + mean + rstd in (EPI_BIAS / EPI_BIAS_QGELU); 16-bit in and out dtype.
+// or colsum + per-row (rstd, -rstd * mean) in (EPI_BIAS / EPI_BIAS_QGELU); 16-bit in and out.
 extern "C" int clipk_gemm_ln(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B,
                              int ldb, const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
-                             float* stats, const float* colsum, const float* mean, const float* rstd,
-                             void* stream) {
+                             float* stats, const float* colsum, const float* rnb, void* stream) {
   if (!A || !B || !out || !bias) return CLIPK_EINVAL;
   if (in_dtype != CLIPK_F16 && in_dtype != CLIPK_BF16) return CLIPK_EDTYPE;
   if (!colsum) {  // producer: the statistics partials of the output
-    if (!stats || mean || rstd || epi != CLIPK_EPI_BIAS_RES || !res || ldr < N || ldr % 8) return CLIPK_EINVAL;
-  } else {        // fold: mean / rstd of A's rows in
-    if (stats || !mean || !rstd || (epi != CLIPK_EPI_BIAS && epi != CLIPK_EPI_BIAS_QGELU)) return CLIPK_EINVAL;
+    if (!stats || rnb || epi != CLIPK_EPI_BIAS_RES || !res || ldr < N || ldr % 8) return CLIPK_EINVAL;
+  } else {        // fold: (rstd, -rstd * mean) of A's rows in
+    if (stats || !rnb || (epi != CLIPK_EPI_BIAS && epi != CLIPK_EPI_BIAS_QGELU)) return CLIPK_EINVAL;
   }
   if (M <= 0) return M == 0 ? CLIPK_OK : CLIPK_ESHAPE;
   if (N <= 0 || K <= 0 || N % GEMM_NMIN != 0 || (K * 2) % GEMM_ROWB != 0) return CLIPK_ESHAPE;
   if (lda < K || ldb < K || lda % 8 || ldb % 8 || ldo < N || ldo % 8) return CLIPK_ESHAPE;
   GemmArgs g{(const char*)A, (const char*)B, M, N, K, lda, ldb, bias, res, ldr, out, ldo, out2, nullptr,
-             0, nullptr, 1, 0, 0, stats, colsum, mean, rstd};
+             0, nullptr, 1, 0, 0, stats, colsum, reinterpret_cast<const f32x2*>(rnb)};
   hipStream_t st = (hipStream_t)stream;
   return in_dtype == CLIPK_F16 ? dispatch_ln<f16>(epi, g, st) : dispatch_ln<bf16>(epi, g, st);
 }

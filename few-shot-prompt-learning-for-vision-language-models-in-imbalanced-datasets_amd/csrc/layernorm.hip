@@ -416,9 +416,12 @@ namespace clipk {
 // wrote: (sum_g, M2_g = sum over the group of (x - sum_g / 64)^2). Exact merge (Chan et al.):
 // mean = sum_g sum_g / width; M2 = sum_g M2_g + 64 (sum_g / 64 - mean)^2; rstd = 1 / sqrt(M2 /
 // width + 1e-5) as model.py:153-159. One thread per row, fixed group order (deterministic).
+// Outputs (each optional): mean, rstd (the LayerNorm backward's), and rnb = (rstd, -rstd * mean)
+// pairs (the folding GEMM's one 8-B load per row).
 template <int NG>
 __global__ __launch_bounds__(256) void ln_stats_merge_kernel(int rows, const f32x2* __restrict__ st,
-                                                             float* __restrict__ mean, float* __restrict__ rstd) {
+                                                             float* __restrict__ mean, float* __restrict__ rstd,
+                                                             f32x2* __restrict__ rnb) {
   const int r = blockIdx.x * 256 + threadIdx.x;
   if (r >= rows) return;
   f32x2 p[NG];
@@ -439,28 +442,30 @@ __global__ __launch_bounds__(256) void ln_stats_merge_kernel(int rows, const f32
     const float d = p[g][0] * (1.0f / 64.0f) - mu;
     m2 += fmaf(64.0f * d, d, p[g][1]);
   }
-  mean[r] = mu;
-  rstd[r] = rsqrtf(m2 * (1.0f / (64.0f * NG)) + 1e-5f);
+  const float rs = rsqrtf(m2 * (1.0f / (64.0f * NG)) + 1e-5f);
+  if (mean) mean[r] = mu;
+  if (rstd) rstd[r] = rs;
+  if (rnb) rnb[r] = (f32x2){rs, -rs * mu};
 }
 }  // namespace clipk
 
 extern "C" int clipk_ln_stats_merge(int rows, int width, const float* stats, float* mean, float* rstd,
-                                    void* stream) {
-  if (!stats || !mean || !rstd) return CLIPK_EINVAL;
+                                    float* rnb, void* stream) {
+  if (!stats || (!mean && !rstd && !rnb)) return CLIPK_EINVAL;
   if (rows < 0 || width % 128 || width < 128 || width > 1024) return CLIPK_ESHAPE;
   if (rows == 0) return CLIPK_OK;
   const dim3 grid((rows + 255) / 256);
   hipStream_t st = (hipStream_t)stream;
   const f32x2* s = reinterpret_cast<const f32x2*>(stats);
   switch (width / 64) {
-    case 2: hipLaunchKernelGGL(ln_stats_merge_kernel<2>, grid, dim3(256), 0, st, rows, s, mean, rstd); break;
-    case 4: hipLaunchKernelGGL(ln_stats_merge_kernel<4>, grid, dim3(256), 0, st, rows, s, mean, rstd); break;
-    case 6: hipLaunchKernelGGL(ln_stats_merge_kernel<6>, grid, dim3(256), 0, st, rows, s, mean, rstd); break;
-    case 8: hipLaunchKernelGGL(ln_stats_merge_kernel<8>, grid, dim3(256), 0, st, rows, s, mean, rstd); break;
-    case 10: hipLaunchKernelGGL(ln_stats_merge_kernel<10>, grid, dim3(256), 0, st, rows, s, mean, rstd); break;
-    case 12: hipLaunchKernelGGL(ln_stats_merge_kernel<12>, grid, dim3(256), 0, st, rows, s, mean, rstd); break;
-    case 14: hipLaunchKernelGGL(ln_stats_merge_kernel<14>, grid, dim3(256), 0, st, rows, s, mean, rstd); break;
-    case 16: hipLaunchKernelGGL(ln_stats_merge_kernel<16>, grid, dim3(256), 0, st, rows, s, mean, rstd); break;
+    case 2: hipLaunchKernelGGL(ln_stats_merge_kernel<2>, grid, dim3(256), 0, st, rows, s, mean, rstd, (f32x2*)rnb); break;
+    case 4: hipLaunchKernelGGL(ln_stats_merge_kernel<4>, grid, dim3(256), 0, st, rows, s, mean, rstd, (f32x2*)rnb); break;
+    case 6: hipLaunchKernelGGL(ln_stats_merge_kernel<6>, grid, dim3(256), 0, st, rows, s, mean, rstd, (f32x2*)rnb); break;
+    case 8: hipLaunchKernelGGL(ln_stats_merge_kernel<8>, grid, dim3(256), 0, st, rows, s, mean, rstd, (f32x2*)rnb); break;
+    case 10: hipLaunchKernelGGL(ln_stats_merge_kernel<10>, grid, dim3(256), 0, st, rows, s, mean, rstd, (f32x2*)rnb); break;
+    case 12: hipLaunchKernelGGL(ln_stats_merge_kernel<12>, grid, dim3(256), 0, st, rows, s, mean, rstd, (f32x2*)rnb); break;
+    case 14: hipLaunchKernelGGL(ln_stats_merge_kernel<14>, grid, dim3(256), 0, st, rows, s, mean, rstd, (f32x2*)rnb); break;
+    case 16: hipLaunchKernelGGL(ln_stats_merge_kernel<16>, grid, dim3(256), 0, st, rows, s, mean, rstd, (f32x2*)rnb); break;
     default: return CLIPK_ESHAPE;
   }
   CLIPK_CHECK_LAUNCH();

@@ -59,12 +59,12 @@ def gemm(a, b, epi=N.EPI_NONE, out_dtype=torch.float32, bias=None, res=None, aux
     return (out, out2) if want_out2 else out
 
 
-def gemm_ln(a, b, epi, bias, stats=None, res=None, colsum=None, mean=None, rstd=None, want_out2=False):
+def gemm_ln(a, b, epi, bias, stats=None, res=None, colsum=None, rnb=None, want_out2=False):
     """clipk_gemm_ln (include/clipk.h): 16-bit a[M,K] @ b[N,K]^T with the LayerNorm fold.
     Producer (EPI_BIAS_RES, colsum None): the statistics partials of the output are written to
     stats (fp32 [M, N/64, 2]). Fold (EPI_BIAS / EPI_BIAS_QGELU): a is the LayerNorm input x with
-    per-row mean / rstd (ln_stats_merge of its partials), b = W diag(gamma), bias = b + W beta,
-    colsum = row sums of b. Output in a's dtype."""
+    per-row rnb = (rstd, -rstd * mean) (ln_stats_merge of its partials), b = W diag(gamma),
+    bias = b + W beta, colsum = row sums of b. Output in a's dtype."""
     _need(a, "A")
     _need(b, "B", a.dtype)
     M, K = a.shape
@@ -72,24 +72,26 @@ def gemm_ln(a, b, epi, bias, stats=None, res=None, colsum=None, mean=None, rstd=
     out = torch.empty(M, Nn, device=a.device, dtype=a.dtype)
     out2 = torch.empty_like(out) if want_out2 else None
     _need(bias, "bias", torch.float32)
-    for t, nm in ((stats, "stats"), (colsum, "colsum"), (mean, "mean"), (rstd, "rstd")):
+    for t, nm in ((stats, "stats"), (colsum, "colsum"), (rnb, "rnb")):
         if t is not None:
             _need(t, nm, torch.float32)
     if res is not None:
         _need(res, "res", a.dtype)
     N.call("clipk_gemm_ln", DT[a.dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias), _p(res), Nn, _p(out), Nn,
-           _p(out2), _p(stats), _p(colsum), _p(mean), _p(rstd), _stream())
+           _p(out2), _p(stats), _p(colsum), _p(rnb), _stream())
     return (out, out2) if want_out2 else out
 
 
 def ln_stats_merge(stats, width):
-    """clipk_ln_stats_merge: [M, width/64, 2] partials -> (mean, rstd) fp32 [M]."""
+    """clipk_ln_stats_merge: [M, width/64, 2] partials -> (mean, rstd, rnb): fp32 [M], [M], [M, 2]
+    with rnb = (rstd, -rstd * mean)."""
     _need(stats, "stats", torch.float32)
     M = stats.shape[0]
     mean = torch.empty(M, device=stats.device, dtype=torch.float32)
     rstd = torch.empty_like(mean)
-    N.call("clipk_ln_stats_merge", M, width, _p(stats), _p(mean), _p(rstd), _stream())
-    return mean, rstd
+    rnb = torch.empty(M, 2, device=stats.device, dtype=torch.float32)
+    N.call("clipk_ln_stats_merge", M, width, _p(stats), _p(mean), _p(rstd), _p(rnb), _stream())
+    return mean, rstd, rnb
 
 
 def gemm_splitk(a, b, epi=N.EPI_NONE, out_dtype=torch.float32, bias=None, res=None, want_out2=False,

@@ -101,13 +101,15 @@ int clipk_gemm_splitk(int in_dtype, int out_dtype, int epi, int M, int N, int K,
  *    64-column group g of the ROUNDED output, stats[(m * N/64 + g) * 2 + {0, 1}] = (sum, sum of
  *    squared deviations from the group's mean) (fp32);
  *  - colsum != NULL (stats NULL): EPI_BIAS or EPI_BIAS_QGELU with A = x, B = W', bias = c,
- *    colsum = s and mean / rstd of A's rows (fp32 [M]).
- * clipk_ln_stats_merge turns a producer's partials into mean / rstd (exact pairwise merge in a
- * fixed order, eps 1e-5; width / 64 partials per row). Shape constraints as clipk_gemm. */
+ *    colsum = s and rnb = per-row (rstd, -rstd * mean) pairs of A's rows (fp32 [M][2]).
+ * clipk_ln_stats_merge turns a producer's partials (width / 64 per row) into any of mean, rstd
+ * (fp32 [rows]) and rnb (exact pairwise merge in a fixed order, eps 1e-5). Shape constraints as
+ * clipk_gemm. */
 int clipk_gemm_ln(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B, int ldb,
                   const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
-                  float* stats, const float* colsum, const float* mean, const float* rstd, void* stream);
-int clipk_ln_stats_merge(int rows, int width, const float* stats, float* mean, float* rstd, void* stream);
+                  float* stats, const float* colsum, const float* rnb, void* stream);
+int clipk_ln_stats_merge(int rows, int width, const float* stats, float* mean, float* rstd, float* rnb,
+                         void* stream);
 
 /* Benchmark knob: force the 16-bit GEMM tile configuration (0: 128x128, 1: 256x256
  * (persistent above 2 x CUs tiles), 2: 256x128, 3: 256x256 non-persistent, 6: 192x256;

@@ -49,7 +49,8 @@ def test_gemm_ln_stats(dev, dtype, Mr, Nn, K):
     out = ops.gemm_ln(a, b, N.EPI_BIAS_RES, bias, stats, res=res)
     plain = ops.gemm(a, b, N.EPI_BIAS_RES, dtype, bias=bias, res=res)
     assert torch.equal(out, plain), "stats epilogue changed the stored output"
-    mean, rstd = ops.ln_stats_merge(stats, Nn)
+    mean, rstd, rnb = ops.ln_stats_merge(stats, Nn)
+    assert torch.equal(rnb[:, 0], rstd) and torch.equal(rnb[:, 1], -rstd * mean)
     x = out.double()
     mu = x.mean(1)
     var = x.var(1, unbiased=False)
@@ -78,13 +79,13 @@ def test_gemm_ln_fold(dev, dtype, epi, Mr, Wd, Nn):
     # the un-fused path the fold replaces: LayerNorm pass -> 16-bit -> GEMM with W
     xn = ops.layernorm(x, gamma, beta, out_dtype=dtype)
     wq = w.to(dtype)
-    mean, rstd = ops.ln_stats_merge(partials(x), Wd)
+    mean, rstd, rnb = ops.ln_stats_merge(partials(x), Wd)
     if epi == N.EPI_BIAS:
-        out = ops.gemm_ln(x, wp, epi, c, colsum=s, mean=mean, rstd=rstd)
+        out = ops.gemm_ln(x, wp, epi, c, colsum=s, rnb=rnb)
         unf = ops.gemm(xn, wq, N.EPI_BIAS, dtype, bias=bias)
         e_fold, e_unf = _rel(out, ref), _rel(unf, ref)
     else:
-        out, h = ops.gemm_ln(x, wp, epi, c, colsum=s, mean=mean, rstd=rstd, want_out2=True)
+        out, h = ops.gemm_ln(x, wp, epi, c, colsum=s, rnb=rnb, want_out2=True)
         unf, uh = ops.gemm(xn, wq, N.EPI_BIAS_QGELU, dtype, bias=bias, want_out2=True)
         e_fold, e_unf = max(_rel(out, ref_g), _rel(h, ref)), max(_rel(unf, ref_g), _rel(uh, ref))
     mu, var = xd.mean(1), xd.var(1, unbiased=False)

@@ -24,7 +24,7 @@ def main():
     beta = (0.02 * torch.randn(W, generator=g)).to(dev)
     xg = x.double().reshape(Mr, W // 64, 64)
     st_x = torch.stack([xg.sum(-1), ((xg - xg.mean(-1, keepdim=True)) ** 2).sum(-1)], -1).float().contiguous()
-    mean, rstd = ops.ln_stats_merge(st_x, W)
+    _, _, rnb = ops.ln_stats_merge(st_x, W)
     for Nn, epi, nm in ((1536, N.EPI_BIAS, "qkv"), (2048, N.EPI_BIAS_QGELU, "c_fc")):
         w = (torch.randn(Nn, W, generator=g) / math.sqrt(W)).to(dev)
         b = (0.02 * torch.randn(Nn, generator=g)).to(dev)
@@ -32,7 +32,7 @@ def main():
         wq = w.to(dt)
         q2 = epi == N.EPI_BIAS_QGELU
         t_plain = timeit(lambda: ops.gemm(x, wq, epi, dt, bias=b, want_out2=q2), iters=20)
-        t_fold = timeit(lambda: ops.gemm_ln(x, wp, epi, c, colsum=s, mean=mean, rstd=rstd, want_out2=q2), iters=20)
+        t_fold = timeit(lambda: ops.gemm_ln(x, wp, epi, c, colsum=s, rnb=rnb, want_out2=q2), iters=20)
         fl = 2.0 * Mr * Nn * W
         print(f"{nm:8s} plain {t_plain * 1e3:7.1f} us ({fl / t_plain / 1e9:6.1f} TF/s)   fold {t_fold * 1e3:7.1f} us "
               f"({fl / t_fold / 1e9:6.1f} TF/s)")
