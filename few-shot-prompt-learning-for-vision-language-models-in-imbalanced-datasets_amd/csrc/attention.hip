@@ -418,23 +418,6 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma16(int nseq, int L, int H, i
 //  * the rescale of O is skipped when no query's running max moved (wave vote);
 //  * the next 64-key K/V chunk is loaded into registers while the current one is consumed.
 // Key slot 8 g4 + j of the PV MFMA is key 4 g4 + j (j < 4) or 16 + 4 g4 + j - 4 of the 32.
-__device__ __forceinline__ float xmax4(float v) {  // max over lane bits 4 and 5
-  auto a = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false,
-                                            false);
-  v = fmaxf(__builtin_bit_cast(float, (unsigned)a[0]), __builtin_bit_cast(float, (unsigned)a[1]));
-  auto b = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false,
-                                            false);
-  return fmaxf(__builtin_bit_cast(float, (unsigned)b[0]), __builtin_bit_cast(float, (unsigned)b[1]));
-}
-__device__ __forceinline__ float xsum4(float v) {  // sum over lane bits 4 and 5
-  auto a = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false,
-                                            false);
-  v = __builtin_bit_cast(float, (unsigned)a[0]) + __builtin_bit_cast(float, (unsigned)a[1]);
-  auto b = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false,
-                                            false);
-  return __builtin_bit_cast(float, (unsigned)b[0]) + __builtin_bit_cast(float, (unsigned)b[1]);
-}
-
 template <typename T>
 __global__ __launch_bounds__(256) void attn_fwd_mfma_t(int nseq, int L, int H, int causal,
                                                        const T* __restrict__ qkv, int ldq,

@@ -183,8 +183,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_mfma(int G, int P, i
       vq[r] = (key <= r16 && key >= first) ? so[r] * kScale : -INFINITY;  // key == r16 always valid
       mx = fmaxf(mx, fmaxf(vp[r], vq[r]));
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = xmax4(mx);
     float ep[4], eo[4], ps = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -192,8 +191,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_mfma(int G, int P, i
       eo[r] = __expf(vq[r] - mx);
       ps += ep[r] + eo[r];
     }
-    ps += __shfl_xor(ps, 16, 64);
-    ps += __shfl_xor(ps, 32, 64);
+    ps = xsum4(ps);
     lds_fence();
     // O^T = V^T P^T: the transposed V read doubles as the A operand (A[m=d][k=key]) and the
     // probabilities as B (B[k=key 4g4+jj][n=query r16]), so lane (r16, g4) ends up holding
@@ -343,8 +341,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_bwd_mfma(int G, int P, i
       P2o[r] = (qok && j <= r16 && j >= cur.first2) ? __expf(s2o[r] * kScale - cur.l2) : 0.f;
       Dsum += P2p[r] * p2p[r] + P2o[r] * p2o[r];
     }
-    Dsum += __shfl_xor(Dsum, 16, 64);
-    Dsum += __shfl_xor(Dsum, 32, 64);  // D_i for i = r16
+    Dsum = xsum4(Dsum);  // D_i for i = r16
     float dS2p[4], dS2o[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -570,8 +567,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_lds(int G, int P, in
       vq[r] = (key <= r16 && key >= first) ? so[r] * kScale : -INFINITY;
       mx = fmaxf(mx, fmaxf(vp[r], vq[r]));
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = xmax4(mx);
     float ep[4], eo[4], ps = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -579,8 +575,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_lds(int G, int P, in
       eo[r] = __expf(vq[r] - mx);
       ps += ep[r] + eo[r];
     }
-    ps += __shfl_xor(ps, 16, 64);
-    ps += __shfl_xor(ps, 32, 64);
+    ps = xsum4(ps);
     const s16x4 bp = pack4<T>(ep[0], ep[1], ep[2], ep[3]);
     const s16x4 bo = pack4<T>(eo[0], eo[1], eo[2], eo[3]);
     const float inv = 1.0f / ps;
@@ -703,8 +698,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_bwd_lds(int G, int P, in
       P2o[r] = (qok && j <= r16 && j >= first2) ? __expf(s2o[r] * kScale - l2) : 0.f;
       Dsum += P2p[r] * p2p[r] + P2o[r] * p2o[r];
     }
-    Dsum += __shfl_xor(Dsum, 16, 64);
-    Dsum += __shfl_xor(Dsum, 32, 64);
+    Dsum = xsum4(Dsum);
     float dS2p[4], dS2o[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {

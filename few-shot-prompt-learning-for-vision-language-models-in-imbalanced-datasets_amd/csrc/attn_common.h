@@ -127,6 +127,27 @@ __device__ __forceinline__ s16x4 pack4(float a, float b, float c, float d) {
   return __builtin_bit_cast(s16x4, v);
 }
 
+// Reductions over lane bits 4 and 5 (the four 16-lane rows of an MFMA 16x16 tile) by
+// v_permlane32_swap / v_permlane16_swap: VALU only (a __shfl_xor is an LDS ds_bpermute round
+// trip), and every lane ends with the same value (the adds are the same pairs in the same order).
+__device__ __forceinline__ float xmax4(float v) {  // max over lane bits 4 and 5
+  auto a = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false,
+                                            false);
+  v = fmaxf(__builtin_bit_cast(float, (unsigned)a[0]), __builtin_bit_cast(float, (unsigned)a[1]));
+  auto b = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false,
+                                            false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)b[0]), __builtin_bit_cast(float, (unsigned)b[1]));
+}
+__device__ __forceinline__ float xsum4(float v) {  // sum over lane bits 4 and 5
+  auto a = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false,
+                                            false);
+  v = __builtin_bit_cast(float, (unsigned)a[0]) + __builtin_bit_cast(float, (unsigned)a[1]);
+  auto b = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false,
+                                            false);
+  return __builtin_bit_cast(float, (unsigned)b[0]) + __builtin_bit_cast(float, (unsigned)b[1]);
+}
+
+
 // Store a 16-row x 64-column (one head) tile held in the MFMA accumulator layout -- lane
 // (r16, g4) holds row r16, columns 16t + 4g4 .. +3 in o[t] -- as 16-bit values. The packed
 // values go through a lane/slot butterfly (v_permlane32_swap: lane bit 5 <-> slot bit 0, then
