@@ -31,14 +31,15 @@ def test_library_exports_every_header_symbol():
 
 
 def test_gemm_config_knob_range():
-    """The GEMM tile knob accepts the shipped configurations only: the variants measured
-    slower (4 / 5: 64-B rows, 7: 8-phase ping-pong, 8 / 9: deep-A ring) left the build."""
+    """The GEMM tile knob accepts the shipped configurations only (7 = the round-3 64x128
+    small-M tile); the variants measured slower (4 / 5: 64-B rows, 8 / 9: deep-A ring; round 2's
+    8-phase ping-pong, once cfg 7) left the build."""
     from fsp_amd import _native
     lib = _native.load()
     try:
-        for cfg in (-1, 0, 1, 2, 3, 6):
+        for cfg in (-1, 0, 1, 2, 3, 6, 7):
             assert lib.clipk_gemm_set_config(cfg) == 0, cfg
-        for cfg in (-2, 4, 5, 7, 8, 9, 10):
+        for cfg in (-2, 4, 5, 8, 9, 10):
             assert lib.clipk_gemm_set_config(cfg) == -1, cfg
     finally:
         lib.clipk_gemm_set_config(-1)
