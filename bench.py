@@ -110,7 +110,7 @@ KERNELS = {
     "ln_fwd": (["text.ln_fwd"], "ln_fwd_kernel", "hbm"),
     "ln_stats": (["text.ln_stats"], "ln_stats_merge_kernel (LN fold statistics)", "hbm"),
     "vit": (["vit.patch_embed", "vit.qkv_fwd", "vit.attn_fwd", "vit.out_fwd", "vit.fc_fwd", "vit.proj_fwd",
-             "vit.ln_fwd", "vit.head"], "ViT forward (all sites)", "mfma"),
+             "vit.ln_fwd", "vit.ln_stats", "vit.eot_gather", "vit.head"], "ViT forward (all sites)", "mfma"),
 }
 ROOF_PMC_KEY = {"gemm_dx_n512": "gemm_nt_kernelIDF16_DF16_fLi4ELi192ELi256",
                 "gemm_dgelu": "gemm_nt_kernelIDF16_DF16_DF16_Li3E",

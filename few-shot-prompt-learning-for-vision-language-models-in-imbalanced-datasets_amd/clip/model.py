@@ -328,9 +328,18 @@ class VisionEncoder(nn.Module, _Encoder):
         G = lambda x: _t(x).float().t().contiguous().to(self.dev, act) if with_grad else None
         self.with_grad = with_grad
         table = []
+        # LayerNorm fold of ln_1 / ln_2 for the 16-bit-residual forward (clipk_vit_forward)
+        fold = [] if act != torch.float32 and ln_fold_enabled() else None
         for i in range(nl):
             pre = f"visual.transformer.resblocks.{i}."
             q = {k: sd[pre + k] for k in _LAYER_KEYS}
+            if fold is not None:
+                qf = {k: _t(v).float() for k, v in q.items()}
+                f_in = ln_fold_weights(qf["attn.in_proj_weight"], qf["attn.in_proj_bias"], qf["ln_1.weight"],
+                                       qf["ln_1.bias"], act, self.dev)
+                f_fc = ln_fold_weights(qf["mlp.c_fc.weight"], qf["mlp.c_fc.bias"], qf["ln_2.weight"],
+                                       qf["ln_2.bias"], act, self.dev)
+                fold = fold + list(f_in) + list(f_fc) if f_in and f_fc else None
             table += [f32(q["ln_1.weight"]), f32(q["ln_1.bias"]), A(q["attn.in_proj_weight"]),
                       f32(q["attn.in_proj_bias"]), A(q["attn.out_proj.weight"]), f32(q["attn.out_proj.bias"]),
                       f32(q["ln_2.weight"]), f32(q["ln_2.bias"]), A(q["mlp.c_fc.weight"]), f32(q["mlp.c_fc.bias"]),
@@ -356,6 +365,9 @@ class VisionEncoder(nn.Module, _Encoder):
                                              ops.DT[act], _ptrs(table), _ptrs(head), ctypes.byref(h)),
                 "clipk_vision_create")
         self.handle = h
+        if fold:
+            self._keep += fold
+            N.check(N.load().clipk_encoder_set_ln_fold(h, _ptrs(fold)), "clipk_encoder_set_ln_fold")
 
     def _check_image(self, image):
         image = image.to(self.dev, torch.float32).contiguous()

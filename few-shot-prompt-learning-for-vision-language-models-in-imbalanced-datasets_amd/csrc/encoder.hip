@@ -384,21 +384,22 @@ static int gemm_ln(int act, int epi, int M, int N, int K, const void* A, const v
   return clipk_gemm_ln(act, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, stats, colsum, rnb, st);
 }
 // mean / rstd (kept for the LayerNorm backward) and the folding GEMM's (rstd, -rstd mean) pairs
-static int ln_merge(int rows, int W, const float* lnst, float* m, float* r, float* rnb, hipStream_t st) {
-  ProfScope ps(CLIPK_PROF_NONE, st, 0.0, "text.ln_stats", (double)rows * (W / 64) * 8 + 16.0 * rows);
+static int ln_merge(int rows, int W, const float* lnst, float* m, float* r, float* rnb, hipStream_t st, bool text) {
+  ProfScope ps(CLIPK_PROF_NONE, st, 0.0, text ? "text.ln_stats" : "vit.ln_stats", (double)rows * (W / 64) * 8 + 16.0 * rows);
   return clipk_ln_stats_merge(rows, W, lnst, m, r, rnb, st);
 }
 // attention half: ln_1 statistics of X merged from the partials the previous layer's c_proj
 // epilogue wrote (lnst); the qkv projection reads X itself through the fold
 static int block_attn_fold(const clipk_encoder* e, const std::array<const void*, 6>& f, const SeqShape& sh,
                            const void* X, void* qkv, void* o, float* lse, float* m1, float* r1, const float* lnst,
-                           float* rnb, hipStream_t st) {
+                           float* rnb, hipStream_t st, bool text) {
   const int W = e->W, rows = sh.rows, act = e->act;
-  TRY(ln_merge(rows, W, lnst, m1, r1, rnb, st));
+  TRY(ln_merge(rows, W, lnst, m1, r1, rnb, st, text));
   TRY(gemm_ln(act, CLIPK_EPI_BIAS, rows, 3 * W, W, X, f[0], (const float*)f[2], nullptr, qkv, nullptr,
-              nullptr, (const float*)f[1], rnb, st, CLIPK_PROF_GEMM_ALL, "text.qkv_fwd"));
+              nullptr, (const float*)f[1], rnb, st, text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE,
+              text ? "text.qkv_fwd" : "vit.qkv_fwd"));
   const double ab = (double)rows * 4 * W * esize(act) + (lse ? 4.0 * rows * e->heads : 0.0);
-  ProfScope ps(CLIPK_PROF_ATTN, st, 0.0, "text.attn_fwd", ab);
+  ProfScope ps(text ? CLIPK_PROF_ATTN : CLIPK_PROF_NONE, st, 0.0, text ? "text.attn_fwd" : "vit.attn_fwd", ab);
   return attn_fwd(e, sh, qkv, o, lse, st);
 }
 // post-attention half: out_proj writes Xm and its ln_2 statistics, c_fc reads Xm through the
@@ -406,18 +407,20 @@ static int block_attn_fold(const clipk_encoder* e, const std::array<const void*,
 static int block_post_fold(const clipk_encoder* e, const std::array<const void*, 16>& w,
                            const std::array<const void*, 6>& f, int rows, const void* X, const void* o, void* Xm,
                            void* Xo, void* h, void* g, float* m2, float* r2, float* lnst, float* rnb,
-                           bool stats_next, hipStream_t st) {
+                           bool stats_next, hipStream_t st, bool text) {
   const int W = e->W, act = e->act;
+  const int pg = text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE;
   TRY(gemm_ln(act, CLIPK_EPI_BIAS_RES, rows, W, W, o, w[4], (const float*)w[5], X, Xm, nullptr, lnst, nullptr,
-              nullptr, st, CLIPK_PROF_GEMM_ALL, "text.out_fwd"));
-  TRY(ln_merge(rows, W, lnst, m2, r2, rnb, st));
+              nullptr, st, pg, text ? "text.out_fwd" : "vit.out_fwd"));
+  TRY(ln_merge(rows, W, lnst, m2, r2, rnb, st, text));
   TRY(gemm_ln(act, CLIPK_EPI_BIAS_QGELU, rows, 4 * W, W, Xm, f[3], (const float*)f[5], nullptr, g, h, nullptr,
-              (const float*)f[4], rnb, st, CLIPK_PROF_GEMM_FC, "text.fc_fwd"));
+              (const float*)f[4], rnb, st, text ? CLIPK_PROF_GEMM_FC : CLIPK_PROF_NONE,
+              text ? "text.fc_fwd" : "vit.fc_fwd"));
   if (stats_next)
     return gemm_ln(act, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo, nullptr, lnst,
-                   nullptr, nullptr, st, CLIPK_PROF_GEMM_ALL, "text.proj_fwd");
+                   nullptr, nullptr, st, pg, text ? "text.proj_fwd" : "vit.proj_fwd");
   return gemm(act, act, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo, nullptr, nullptr,
-              0, st, CLIPK_PROF_GEMM_ALL, nullptr, 0, "text.proj_fwd");
+              0, st, pg, nullptr, 0, text ? "text.proj_fwd" : "vit.proj_fwd");
 }
 
 }  // namespace clipk
@@ -527,16 +530,17 @@ static EncIO text_io(const clipk_encoder* e) {
 }
 #define SITE(n) (io.text ? "text." n : "vit." n)
 
-// LN fold in this call: set on the encoder, 16-bit text residual stream, no deep prompts (they
-// rewrite rows between a producer's statistics and their use) and not the A-operand QuickGELU
-// knob. Knob CLIPK_TEXT_LNFOLD=0 runs the LayerNorm passes.
+// LN fold in this call: set on the encoder, 16-bit residual stream (the text encoder's, or the
+// ViT's forward, clipk_vit_forward), no deep prompts (they rewrite rows between a producer's
+// statistics and their use) and not the A-operand QuickGELU knob. Knob CLIPK_TEXT_LNFOLD=0 runs
+// the LayerNorm passes.
 static bool ln_fold_on(const clipk_encoder* e, const EncIO& io) {
   static int v = -1;
   if (v < 0) {
     const char* s = getenv("CLIPK_TEXT_LNFOLD");
     v = s ? atoi(s) : 1;
   }
-  return v != 0 && io.text && (int)e->fold.size() == e->layers && e->act != CLIPK_F32 && io.rd == e->act &&
+  return v != 0 && (int)e->fold.size() == e->layers && e->act != CLIPK_F32 && io.rd == e->act &&
          !(e->deep.n_deep > 0 && e->deep.prompts) && !a_qgelu_on();
 }
 
@@ -669,7 +673,7 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
       TRY(block_attn_shared0(e, e->lw[l], sh, rd, cur, t.xn, t.qkv[l], t.o[l], t.lse[l], t.mean1[l], t.rstd1[l],
                              (int*)t.g, st));
     else if (fold && have_stats)
-      TRY(block_attn_fold(e, e->fold[l], sh, cur, t.qkv[l], t.o[l], t.lse[l], m1, r1, t.lnst, t.rnb, st));
+      TRY(block_attn_fold(e, e->fold[l], sh, cur, t.qkv[l], t.o[l], t.lse[l], m1, r1, t.lnst, t.rnb, st, io.text));
     else
       TRY(block_attn(e, e->lw[l], sh, rd, cur, t.xn, t.qkv[l], t.o[l], t.lse[l], t.mean1[l], t.rstd1[l], st,
                      io.text, io.sk, io.skb));
@@ -689,7 +693,7 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
     const int n = compact ? nout : sh.rows;
     if (fold)
       TRY(block_post_fold(e, e->lw[l], e->fold[l], n, xin, oin, t.Xm[l], Xo, save ? t.h[l] : nullptr, t.g, m2, r2,
-                          t.lnst, t.rnb, l + 1 < nl, st));
+                          t.lnst, t.rnb, l + 1 < nl, st, io.text));
     else
       TRY(block_post(e, e->lw[l], n, rd, xin, oin, t.Xm[l], Xo, t.xn, save ? t.h[l] : nullptr, t.g, t.mean2[l],
                      t.rstd2[l], st, io.text, compact ? nullptr : io.sk, compact ? 0 : io.skb));
@@ -951,8 +955,16 @@ static VitBufs vit_layout(const clipk_encoder* e, int B, void* ws) {
 }
 }  // namespace clipk
 
+namespace clipk {
+static bool vit_res16(const clipk_encoder* e);
+static size_t vit16_bytes(const clipk_encoder* e, int B, void* ws, void** parts);
+static int vit16_forward(const clipk_encoder* e, int B, const float* img, float* feat, void* ws, size_t ws_bytes,
+                         hipStream_t st);
+}  // namespace clipk
+
 extern "C" size_t clipk_vit_ws_bytes(const clipk_encoder* e, int B) {
   if (!e || e->kind != 1) return 0;
+  if (vit_res16(e)) return vit16_bytes(e, B, nullptr, nullptr);
   return vit_layout(e, B, nullptr).bytes;
 }
 
@@ -960,6 +972,7 @@ extern "C" int clipk_vit_forward(const clipk_encoder* e, int B, const float* img
                                  void* ws, size_t ws_bytes, void* stream) {
   if (!e || e->kind != 1 || !img || !feat || !ws) return CLIPK_EINVAL;
   if (B <= 0) return CLIPK_ESHAPE;
+  if (vit_res16(e)) return vit16_forward(e, B, img, feat, ws, ws_bytes, (hipStream_t)stream);
   VitBufs v = vit_layout(e, B, ws);
   if (ws_bytes < v.bytes) return CLIPK_EWORKSPACE;
   hipStream_t st = (hipStream_t)stream;
@@ -1039,6 +1052,61 @@ __global__ void cls_rows_kernel(int B, int Lp, int* rows) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b < B) rows[b] = b * Lp;
 }
+
+// ---- ViT forward with a 16-bit residual stream (round 3; knob CLIPK_VIT_RES16=0 keeps fp32):
+// the text encoder's layer loop (text_forward_impl) on B plain non-causal sequences, so the ViT
+// gets the LayerNorm fold of ln_1 / ln_2 (when set on the handle) and the last layer's
+// post-attention half on the CLS rows alone (the only rows ln_post reads; exact). ln_pre stays in
+// clipk_vit_embed_ln (fp32 out, cast into the stream by the layer loop).
+static bool vit_res16(const clipk_encoder* e) {
+  static int v = -1;
+  if (v < 0) {
+    const char* s = getenv("CLIPK_VIT_RES16");
+    v = s ? atoi(s) : 1;
+  }
+  return v != 0 && e->act != CLIPK_F32;
+}
+// parts: patches, pout, x0, cls_rows, sk, rest (the layer loop's workspace); returns the bytes
+static size_t vit16_bytes(const clipk_encoder* e, int B, void* ws, void** parts) {
+  const size_t a = esize(e->act), D = e->W, L = e->Limg, rows = (size_t)B * L;
+  const size_t np = (size_t)B * (L - 1);
+  Carver c(ws);
+  void* p[6];
+  p[0] = c.take(np * e->Kp * a);
+  p[1] = c.take(np * D * 4);
+  p[2] = c.take(rows * D * 4);
+  p[3] = c.take((size_t)B * 4);
+  static const bool no_sk = getenv("CLIPK_VIT_NOSPLITK") != nullptr;
+  const size_t skb = no_sk ? 0 : vit_splitk_bytes(e->act, (int)rows, (int)D);
+  p[4] = skb ? c.take(skb) : nullptr;
+  p[5] = ws ? (char*)ws + c.off : nullptr;
+  if (parts)
+    for (int i = 0; i < 6; ++i) parts[i] = p[i];
+  return c.off + text_layout(e, rows, B, nullptr, nullptr, false, e->act).ws_bytes;
+}
+static int vit16_forward(const clipk_encoder* e, int B, const float* img, float* feat, void* ws, size_t ws_bytes,
+                         hipStream_t st) {
+  void* p[6];
+  const size_t need = vit16_bytes(e, B, ws, p);
+  if (ws_bytes < need) return CLIPK_EWORKSPACE;
+  const int D = e->W, L = e->Limg, np = B * (L - 1), act = e->act;
+  const size_t skb = p[4] ? (size_t)((char*)p[5] - (char*)p[4]) : 0;
+  TRY(clipk_im2col(act, B, e->res, e->patch, e->Kp, img, p[0], st));
+  TRY(gemm(act, CLIPK_F32, CLIPK_EPI_NONE, np, D, e->Kp, p[0], e->head[5], nullptr, nullptr, p[1], nullptr, nullptr,
+           0, st, CLIPK_PROF_NONE,
+           clipk_gemm_splitk_ws_bytes(np, D, clipk_gemm_auto_splits(act, np, D, e->Kp)) <= skb ? p[4] : nullptr, skb,
+           "vit.patch_embed"));
+  TRY(clipk_vit_embed_ln(B, L, D, (const float*)p[1], (const float*)e->head[6], (const float*)e->head[7],
+                         (const float*)e->head[0], (const float*)e->head[1], (float*)p[2], st));
+  hipLaunchKernelGGL(cls_rows_kernel, dim3((B + 255) / 256), dim3(256), 0, st, B, L, (int*)p[3]);
+  CLIPK_CHECK_LAUNCH();
+  EncIO io = vit_io(e, nullptr);
+  io.rd = act;
+  io.sk = p[4];
+  io.skb = skb;
+  return text_forward_impl(e, SeqShape::plain(B, L, 0), (const float*)p[2], (const int*)p[3], feat, nullptr, 0, p[5],
+                           need - (size_t)((char*)p[5] - (char*)ws), st, io);
+}
 // out[p] = sum over images b (fixed order) of dx[b * Lp + L + p]
 __global__ __launch_bounds__(256) void vpt_rows_sum_kernel(int B, int Lp, int L, int n_vpt, int D,
                                                            const float* __restrict__ dx, float* __restrict__ out) {
@@ -1058,7 +1126,7 @@ extern "C" int clipk_encoder_set_input_rows(clipk_encoder* e, int mode) {
 }
 
 extern "C" int clipk_encoder_set_ln_fold(clipk_encoder* e, const void* const* fold_ptrs) {
-  if (!e || e->kind != 0) return CLIPK_EINVAL;
+  if (!e) return CLIPK_EINVAL;
   if (!fold_ptrs) {
     e->fold.clear();
     return CLIPK_OK;

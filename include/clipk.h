@@ -325,7 +325,10 @@ int clipk_encoder_set_input_rows(clipk_encoder* e, int mode);
  * ln_1 from the previous layer's c_proj epilogue statistics and every layer takes ln_2 from its
  * out_proj epilogue (layer 0's ln_1 and ln_final stay LayerNorm passes; not used with deep
  * prompts or an fp32 encoder). The saved mean / rstd are the same quantities the LayerNorm pass
- * writes, so the backward is unchanged. fold_ptrs == NULL clears. Pointers must stay valid. */
+ * writes, so the backward is unchanged. fold_ptrs == NULL clears. Pointers must stay valid. A ViT
+ * handle (clipk_vision_create) takes the same table for its ln_1 / ln_2: its forward with a
+ * 16-bit act dtype (clipk_vit_forward) runs the residual stream in that dtype through the text
+ * encoder's layer loop and folds them the same way. */
 int clipk_encoder_set_ln_fold(clipk_encoder* e, const void* const* fold_ptrs);
 
 /* ViT with visual prompts, forward with saved activations and input-grad backward (the
@@ -375,7 +378,10 @@ int clipk_text_backward_packed(const clipk_encoder* enc, int G, int C, int P, in
                                const float* dtxt, const void* saved, size_t saved_bytes, float* dx0,
                                void* ws, size_t ws_bytes, void* stream);
 
-/* Vision transformer forward (frozen, no grad): img fp32 [B,3,R,R] -> feat fp32 [B,E].
+/* Vision transformer forward (frozen, no grad): img fp32 [B,3,R,R] -> feat fp32 [B,E]. With a
+ * 16-bit act dtype the residual stream is kept in that dtype (CLIP's half semantics, as the text
+ * encoder's; env CLIPK_VIT_RES16=0: fp32), ln_1 / ln_2 are folded when set
+ * (clipk_encoder_set_ln_fold) and the last layer's post-attention half runs on the CLS rows.
  * Head table for a vision encoder: ln_pre_w, ln_pre_b, ln_post_w, ln_post_b (f32),
  * projT [E,D] act, conv_w [D,Kp] act, class_emb f32[D], pos f32[L,D]. */
 int clipk_vision_create(int width, int layers, int heads, int embed, int res, int patch,
