@@ -415,34 +415,34 @@ namespace clipk {
 // LayerNorm statistics from the per-(row, 64-column group) partials a clipk_gemm_ln producer
 // wrote: (sum_g, M2_g = sum over the group of (x - sum_g / 64)^2). Exact merge (Chan et al.):
 // mean = sum_g sum_g / width; M2 = sum_g M2_g + 64 (sum_g / 64 - mean)^2; rstd = 1 / sqrt(M2 /
-// width + 1e-5) as model.py:153-159. One thread per row, fixed group order (deterministic).
-// Outputs (each optional): mean, rstd (the LayerNorm backward's), and rnb = (rstd, -rstd * mean)
-// pairs (the folding GEMM's one 8-B load per row).
-template <int NG>
-__global__ __launch_bounds__(256) void ln_stats_merge_kernel(int rows, const f32x2* __restrict__ st,
+// width + 1e-5) as model.py:153-159. Outputs (each optional): mean, rstd (the LayerNorm
+// backward's), and rnb = (rstd, -rstd * mean) pairs (the folding GEMM's one 8-B load per row).
+// 16 lanes per row, lane j holding partial j (one 8-B load; idle past width / 64), sums over the
+// 16 lanes by DPP in a fixed pattern (deterministic): the kernel is one memory round trip (the
+// first form, one thread per row reading 64 B, took 5 us at 47k rows).
+template <int CTRL>
+__device__ __forceinline__ float dpp_row(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float sum16(float v) {
+  v += dpp_row<0xB1>(v);   // quad: xor 1
+  v += dpp_row<0x4E>(v);   // quad: xor 2
+  v += dpp_row<0x141>(v);  // half-row mirror: quads 0 <-> 1
+  return v + dpp_row<0x140>(v);  // row mirror: halves 0 <-> 1
+}
+__global__ __launch_bounds__(256) void ln_stats_merge_kernel(int rows, int ng, const f32x2* __restrict__ st,
                                                              float* __restrict__ mean, float* __restrict__ rstd,
                                                              f32x2* __restrict__ rnb) {
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= rows) return;
-  f32x2 p[NG];
-  const f32x4* s4 = reinterpret_cast<const f32x4*>(st + (size_t)r * NG);
-#pragma unroll
-  for (int g = 0; g < NG / 2; ++g) {
-    const f32x4 v = s4[g];
-    p[2 * g] = (f32x2){v[0], v[1]};
-    p[2 * g + 1] = (f32x2){v[2], v[3]};
-  }
-  float s = 0.f;
-#pragma unroll
-  for (int g = 0; g < NG; ++g) s += p[g][0];
-  const float mu = s * (1.0f / (64.0f * NG));
-  float m2 = 0.f;
-#pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    const float d = p[g][0] * (1.0f / 64.0f) - mu;
-    m2 += fmaf(64.0f * d, d, p[g][1]);
-  }
-  const float rs = rsqrtf(m2 * (1.0f / (64.0f * NG)) + 1e-5f);
+  const int lane = threadIdx.x & 63, j = lane & 15;
+  const int r = (blockIdx.x * 256 + threadIdx.x) >> 4;
+  const bool ok = r < rows && j < ng;
+  const f32x2 p = ok ? st[(size_t)r * ng + j] : (f32x2){0.f, 0.f};
+  const float inv_w = 1.0f / (64.0f * ng);
+  const float mu = sum16(p[0]) * inv_w;
+  const float d = p[0] * (1.0f / 64.0f) - mu;
+  const float m2 = sum16(ok ? fmaf(64.0f * d, d, p[1]) : 0.f);
+  if (r >= rows || j != 0) return;
+  const float rs = rsqrtf(m2 * inv_w + 1e-5f);
   if (mean) mean[r] = mu;
   if (rstd) rstd[r] = rs;
   if (rnb) rnb[r] = (f32x2){rs, -rs * mu};
@@ -454,20 +454,9 @@ extern "C" int clipk_ln_stats_merge(int rows, int width, const float* stats, flo
   if (!stats || (!mean && !rstd && !rnb)) return CLIPK_EINVAL;
   if (rows < 0 || width % 128 || width < 128 || width > 1024) return CLIPK_ESHAPE;
   if (rows == 0) return CLIPK_OK;
-  const dim3 grid((rows + 255) / 256);
-  hipStream_t st = (hipStream_t)stream;
-  const f32x2* s = reinterpret_cast<const f32x2*>(stats);
-  switch (width / 64) {
-    case 2: hipLaunchKernelGGL(ln_stats_merge_kernel<2>, grid, dim3(256), 0, st, rows, s, mean, rstd, (f32x2*)rnb); break;
-    case 4: hipLaunchKernelGGL(ln_stats_merge_kernel<4>, grid, dim3(256), 0, st, rows, s, mean, rstd, (f32x2*)rnb); break;
-    case 6: hipLaunchKernelGGL(ln_stats_merge_kernel<6>, grid, dim3(256), 0, st, rows, s, mean, rstd, (f32x2*)rnb); break;
-    case 8: hipLaunchKernelGGL(ln_stats_merge_kernel<8>, grid, dim3(256), 0, st, rows, s, mean, rstd, (f32x2*)rnb); break;
-    case 10: hipLaunchKernelGGL(ln_stats_merge_kernel<10>, grid, dim3(256), 0, st, rows, s, mean, rstd, (f32x2*)rnb); break;
-    case 12: hipLaunchKernelGGL(ln_stats_merge_kernel<12>, grid, dim3(256), 0, st, rows, s, mean, rstd, (f32x2*)rnb); break;
-    case 14: hipLaunchKernelGGL(ln_stats_merge_kernel<14>, grid, dim3(256), 0, st, rows, s, mean, rstd, (f32x2*)rnb); break;
-    case 16: hipLaunchKernelGGL(ln_stats_merge_kernel<16>, grid, dim3(256), 0, st, rows, s, mean, rstd, (f32x2*)rnb); break;
-    default: return CLIPK_ESHAPE;
-  }
+  hipLaunchKernelGGL(ln_stats_merge_kernel, dim3((unsigned)(((long)rows * 16 + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, rows, width / 64, reinterpret_cast<const f32x2*>(stats), mean, rstd,
+                     reinterpret_cast<f32x2*>(rnb));
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
 }
