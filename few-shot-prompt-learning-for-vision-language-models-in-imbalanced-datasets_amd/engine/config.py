@@ -142,5 +142,8 @@ def get_cfg_default() -> CfgNode:
         # COCOOP_SHARD: CoCoOp under torchrun, "image" (data parallel) or "class" (every rank
         # scores the same batch against C / world classes; SURVEY §8(e) Option B).
         "NATIVE": {"TRUNCATE_PROMPTS": True, "SHARED_PREFIX": True, "MAX_TEXT_ROWS": 2_000_000,
-                   "CLASS_SHARD": True, "COCOOP_SHARD": "image"},
+                   "CLASS_SHARD": True, "COCOOP_SHARD": "image",
+                   # OVERLAP_VISION: CoOp runs the frozen image encoder on a side stream while the
+                   # text encoder (independent of the images) runs on the main one
+                   "OVERLAP_VISION": True},
     })

@@ -161,12 +161,38 @@ class CustomCLIP(nn.Module):
         if not self.training and not torch.is_grad_enabled():
             self._cached_text_features()
 
+    def _image_features_async(self, image):
+        """The frozen image encoder on a side stream (NATIVE.OVERLAP_VISION): CoOp's text
+        features do not depend on the images (coop.py:356-363 computes both, then the logits), so
+        the ViT's small, latency-bound launches can fill the CUs the text encoder leaves idle.
+        Returns (imf, join): call join() on the main stream before imf is read there."""
+        main = torch.cuda.current_stream(image.device)
+        side = getattr(self, "_side_stream", None)
+        if side is None or side.device != image.device:
+            side = self._side_stream = torch.cuda.Stream(image.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            imf = self.image_encoder(image)
+
+        def join():
+            main.wait_stream(side)
+            imf.record_stream(main)
+            return imf
+        return imf, join
+
     def forward_once(self, image):
-        imf = self.image_encoder(image)
+        overlap = (image.is_cuda and self.cfg.get("NATIVE", {}).get("OVERLAP_VISION", False)
+                   and (self.training or torch.is_grad_enabled()))
+        if overlap:
+            _, join = self._image_features_async(image)
+        else:
+            imf = self.image_encoder(image)
         if not self.training and not torch.is_grad_enabled():
             txt = self._cached_text_features()
         else:
             txt = self.text_features()
+        if overlap:
+            imf = join()
         return CosineLogitsFn.apply(imf, txt, self.logit_scale_value, 0, self.prompt_learner.n_cls)
 
     def forward(self, img1, lbl=None, img2=None):
