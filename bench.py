@@ -290,6 +290,7 @@ def time_train(trainer, dm, steps, warmup, batch=None, prof_steps=0):
 
     def step(i):
         trainer.batch_idx = i
+        trainer.next_batch = batches[(i + 1) % len(batches)]  # as TrainerX.run_epoch's lookahead
         return trainer.forward_backward(batches[i % len(batches)])
 
     for i in range(warmup):
@@ -404,7 +405,11 @@ def main():
                    "seq_len": L, "parallelism": f"dp{world}",
                    "text_layout": ("shared-prefix packed, %d text rows/image (plain: %d)"
                                    % (lay.rows_per_group, args.classes * L)) if lay.pack is not None
-                                  else f"plain [B*C, {L}]"},
+                                  else f"plain [B*C, {L}]",
+                   "vision": ("each step starts the NEXT batch's (frozen) image encoder on a side stream between "
+                              "its forward and backward (NATIVE.PREFETCH_VISION, as TrainerX.run_epoch does with "
+                              "its one-batch lookahead): one ViT forward and one text fwd+bwd per timed step"
+                              if trainer.cfg.NATIVE.get("PREFETCH_VISION", False) else "in line")},
         "eval_images_per_sec": round(eval_ips, 3),
         "eval_images": int(dist.sum_over_ranks(n_eval)),
         "eval_note": "forward only, test batch 100, distinct resident images sharded over the ranks",

@@ -145,5 +145,8 @@ def get_cfg_default() -> CfgNode:
                    "CLASS_SHARD": True, "COCOOP_SHARD": "image",
                    # OVERLAP_VISION: CoOp runs the frozen image encoder on a side stream while the
                    # text encoder (independent of the images) runs on the main one
-                   "OVERLAP_VISION": True},
+                   "OVERLAP_VISION": True,
+                   # PREFETCH_VISION: CoCoOp starts the next batch's image encoder (frozen) on a side
+                   # stream between a step's forward and backward (the loop names the next batch)
+                   "PREFETCH_VISION": True},
     })

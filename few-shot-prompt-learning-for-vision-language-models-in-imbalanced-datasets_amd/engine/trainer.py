@@ -243,8 +243,17 @@ class TrainerX:
         dist.sync_rng_from(0)  # one global sampler stream on every rank (data/manager.py)
         loader = self.dm.train_loader_x
         self.num_batches = len(loader)
-        for self.batch_idx, batch in enumerate(loader):
+        # one batch of lookahead: forward_backward may start work on the next batch (CoCoOp's
+        # frozen image encoder, NATIVE.PREFETCH_VISION); the batches and their order are unchanged
+        it = iter(loader)
+        batch = next(it, None)
+        self.batch_idx = -1
+        while batch is not None:
+            nxt = next(it, None)
+            self.batch_idx += 1
+            self.next_batch = nxt
             summary = self.forward_backward(batch)
+            batch = nxt
             if (self.batch_idx + 1) % self.cfg.TRAIN.PRINT_FREQ == 0 and dist.rank() == 0:
                 print(f"epoch [{self.epoch + 1}/{self.max_epoch}] batch [{self.batch_idx + 1}/"
                       f"{self.num_batches}] {summary} lr {self.get_current_lr():.4e}")

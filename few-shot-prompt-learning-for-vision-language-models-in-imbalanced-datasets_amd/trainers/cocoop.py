@@ -130,8 +130,35 @@ class CustomCLIP(nn.Module):
             logits = dist.GatherClassColumns.apply(logits, self.class_counts)
         return logits
 
+    def prefetch_image_features(self, image):
+        """Start the frozen image encoder on a LATER step's images, on a side stream
+        (NATIVE.PREFETCH_VISION): called between this step's forward and backward, the ViT's
+        small latency-bound launches run beside the text encoder's backward. Exact: the image
+        encoder does not train, so its output does not depend on this step's update."""
+        main = torch.cuda.current_stream(image.device)
+        side = getattr(self, "_side_stream", None)
+        if side is None or side.device != image.device:
+            side = self._side_stream = torch.cuda.Stream(image.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            imf = self.image_encoder(image)
+        self._prefetched = (image, image._version, imf, side)
+
+    def image_features(self, image):
+        """The image encoder's output for ``image``: the prefetched one when it was started for
+        this very tensor (unmodified since), else computed now."""
+        pf = getattr(self, "_prefetched", None)
+        self._prefetched = None
+        if pf is not None and pf[0] is image and pf[1] == image._version:
+            _, _, imf, side = pf
+            main = torch.cuda.current_stream(image.device)
+            main.wait_stream(side)
+            imf.record_stream(main)
+            return imf
+        return self.image_encoder(image)
+
     def forward(self, image, label=None):
-        imf = self.image_encoder(image)
+        imf = self.image_features(image)
         imf = imf / imf.norm(dim=-1, keepdim=True)
         pl = self.prompt_learner
         per_img = pl.layout.rows_per_group
@@ -186,6 +213,11 @@ class CoCoOp(TrainerX):
         """cocoop.py:313-338 (multi-GPU weighting and the amp skip test as CoOp's)."""
         image, label = self.parse_batch_train(batch)
         loss = self.model(image, label)
+        nb, self.next_batch = getattr(self, "next_batch", None), None
+        if nb is not None and image.is_cuda and self.cfg.get("NATIVE", {}).get("PREFETCH_VISION", False):
+            # the next step's image features, beside this step's backward (run_epoch / bench set
+            # next_batch to the batch the loop will pass next)
+            self.model.prefetch_image_features(self.parse_batch_train(nb)[0])
         self.optim.zero_grad()
         if self.class_sharded:  # full loss on every rank, partial gradients: summed
             loss.backward()
