@@ -325,6 +325,7 @@ def time_eval(trainer, dm, n_images):
     trainer.set_model_mode("eval")
     tl = dm.test_loader
     nb = (n_images + 99) // 100
+    hint = hasattr(trainer.model, "prefetch_image_features")  # as TrainerX.test's lookahead
     with torch.no_grad():
         trainer.model_inference(tl[0]["img"])
         torch.cuda.synchronize()
@@ -333,6 +334,8 @@ def time_eval(trainer, dm, n_images):
         n = 0
         for i in range(nb):
             x = tl[i % len(tl)]["img"]
+            if hint:
+                trainer.model.next_image = tl[(i + 1) % len(tl)]["img"] if i + 1 < nb else None
             trainer.model_inference(x)
             n += x.shape[0]
         torch.cuda.synchronize()

@@ -278,9 +278,18 @@ class TrainerX:
         if prepare is not None:  # every rank joins its collectives, whatever its shard size
             prepare()
         preds, labels = [], []
-        for batch in loader:
+        # one batch of lookahead: the model may start the next batch's image encoder meanwhile
+        # (CoCoOp, NATIVE.PREFETCH_VISION); results do not depend on it
+        hint = hasattr(self.model, "prefetch_image_features")
+        it = iter(loader)
+        batch = next(it, None)
+        while batch is not None:
+            nxt = next(it, None)
             x, y = self.parse_batch_test(batch)
+            if hint:
+                self.model.next_image = self.parse_batch_test(nxt)[0] if nxt is not None else None
             out = self.model_inference(x)
+            batch = nxt
             preds.append(out.argmax(1).to(torch.int64))
             labels.append(y.to(torch.int64))
         dev = self.device

@@ -159,6 +159,11 @@ class CustomCLIP(nn.Module):
 
     def forward(self, image, label=None):
         imf = self.image_features(image)
+        nxt, self.next_image = getattr(self, "next_image", None), None
+        if nxt is not None and not self.training and self.cfg.get("NATIVE", {}).get("PREFETCH_VISION", False):
+            # eval: the next test batch's image encoder beside this batch's text encoder (the test
+            # loop names it, TrainerX.test)
+            self.prefetch_image_features(nxt)
         imf = imf / imf.norm(dim=-1, keepdim=True)
         pl = self.prompt_learner
         per_img = pl.layout.rows_per_group
