@@ -142,6 +142,20 @@ template <> struct Raw<32> { uint4 v[2]; };
 #ifndef CLIPK_GEMM_PPB0
 #define CLIPK_GEMM_PPB0 1
 #endif
+// CLIPK_GEMM_PP2: the ping-pong loop in 2 phases per K tile instead of 4 -- (A half 0 x all of
+// B), (A half 1 x all of B), B's fragments read once and kept in registers -- so each wave
+// crosses 4 barriers per K tile instead of 8 and each MFMA segment is 24 MFMAs instead of 12.
+// Restage: A1 + B1 of K tile t+1 in phase 1, A0 + B0 of t+2 in phase 2 (each one phase after
+// its last read by the lagging wave row); phase 2's counted vmcnt leaves only those in flight.
+// 1 = every ping-pong tile, 2 = the 256-row tiles only (default), 0 = off. Same-box A/Bs
+// (profiles/r03i/ab_pp2.txt): on the 256-row tiles (qkv / c_fc forward, dgelu) 1-3 % faster per
+// launch, headline 10.70 -> 10.57 ms/step; on the 192-row tiles (the N = 512 GEMMs) 1-2 % slower.
+// PMC over both shapes: no LDS bank conflicts or unaligned replays, the LDS array busy ~25 % and
+// the MFMA pipes ~45 % of the kernel's cycles -- the loop is bound by its issue / synchronisation
+// structure rather than by either unit.
+#ifndef CLIPK_GEMM_PP2
+#define CLIPK_GEMM_PP2 2
+#endif
 // Diagnostic builds only (wrong results; tools/gemm_diag.sh): NOLOAD = stage no K step past
 // the first (the loop's compute + LDS + barrier ceiling), NOBAR = no barrier / vmcnt wait per
 // K step either.
@@ -560,15 +574,63 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       // during this tile's last phases and epilogue (nk >= 2).
       const bool lag = wm == 1;
       const TRes cra = rsrc_a(m0), crb = rsrc_b(n0);
+      // PP2: K tile t+1 landed; the A0 + B0 regions just issued for t+2 stay in flight
+      auto wait_ahead2 = [&]() {
+        if (two_a) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      };
+      constexpr bool PP2 = CLIPK_GEMM_PP2 == 1 || (CLIPK_GEMM_PP2 == 2 && BM == 256);
+      static_assert(!PP2 || NFB == 2, "PP2 keeps all of B's fragments");
       if (it == 0) {
-        pst(0, cra, crb, 0, 0); pst(0, cra, crb, 0, 2); pst(0, cra, crb, 0, 1); pst(0, cra, crb, 0, 3);
-        pst(1, cra, crb, 1, 0); pst(1, cra, crb, 1, 3); pst(1, cra, crb, 1, 1);
-        wait_ahead();
+        if constexpr (PP2) {
+          pst(0, cra, crb, 0, 0); pst(0, cra, crb, 0, 2); pst(0, cra, crb, 0, 1); pst(0, cra, crb, 0, 3);
+          pst(1, cra, crb, 1, 0); pst(1, cra, crb, 1, 2);
+          wait_ahead2();
+        } else {
+          pst(0, cra, crb, 0, 0); pst(0, cra, crb, 0, 2); pst(0, cra, crb, 0, 1); pst(0, cra, crb, 0, 3);
+          pst(1, cra, crb, 1, 0); pst(1, cra, crb, 1, 3); pst(1, cra, crb, 1, 1);
+          wait_ahead();
+        }
         G8_BAR();
       }
       if (lag) G8_BAR();  // wave row 1 runs one segment behind
       const TRes xra = rsrc_a(has_next ? (next / ntn) * BM : m0);
       const TRes xrb = rsrc_b(has_next ? (next % ntn) * BN : n0);
+      if constexpr (PP2)
+      for (int kt = 0; kt < nk; ++kt, ++it) {
+        const int b = it & 1;
+        const bool in1 = kt + 1 < nk, in2 = kt + 2 < nk;
+        const bool h1 = in1 || has_next, h2 = in2 || has_next;
+        const int k1 = in1 ? kt + 1 : kt + 1 - nk, k2 = in2 ? kt + 2 : kt + 2 - nk;
+        const TRes ra1 = in1 ? cra : xra, rb1 = in1 ? crb : xrb;
+        const TRes ra2 = in2 ? cra : xra, rb2 = in2 ? crb : xrb;
+        rd_a(b, 0); rd_b(b, 0); rd_b(b, 1);     // phase 1: A0 x B
+        if (h1) {
+          pst(b ^ 1, ra1, rb1, k1, 1);
+          pst(b ^ 1, ra1, rb1, k1, 3);
+        }
+        if (!in1) {
+          load_ext(0, extq[0]);
+          load_ln(0, 0);
+        }
+        seg_end();
+        mm(0, 0);
+        mm(0, 1);
+        G8_BAR();
+        rd_a(b, 1);                             // phase 2: A1 x B
+        if (h2) {
+          pst(b, ra2, rb2, k2, 0);
+          pst(b, ra2, rb2, k2, 2);
+          wait_ahead2();
+        } else if (h1) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        seg_end();
+        mm(1, 0);
+        mm(1, 1);
+        G8_BAR();
+      }
+      else
       for (int kt = 0; kt < nk; ++kt, ++it) {
         const int b = it & 1;
         const bool in1 = kt + 1 < nk, in2 = kt + 2 < nk;

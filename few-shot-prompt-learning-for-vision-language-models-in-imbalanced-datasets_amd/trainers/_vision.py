@@ -1,0 +1,80 @@
+"""Scheduling of the frozen image encoder for the CoOp / CoCoOp CustomCLIPs.
+
+The reference calls ``image_encoder(image)`` inline in every forward (coop.py:356-363,
+cocoop.py:238-251). Its weights never train, so its output for a given image tensor is the
+same whenever it is computed; this mixin uses that to move the ViT's small, latency-bound
+launches next to the text encoder's:
+* ``prefetch_image_features(image)`` starts it on a side stream for a batch the loop will pass
+  later (NATIVE.PREFETCH_VISION; the loops name the next batch: TrainerX.run_epoch / test and
+  bench.py keep one batch of lookahead), so it runs beside the current step's text encoder;
+* ``image_features(image)`` returns the prefetched result when it was started for this very
+  tensor (unmodified since), else the last result for it (CoOp's post-step accuracy forward of
+  the same images, coop.py:464-469), else computes it now.
+Results are bitwise the same as the inline call's."""
+from __future__ import annotations
+
+import torch
+
+
+class ImageFeatureSchedule:
+    def _side(self, device):
+        side = getattr(self, "_side_stream", None)
+        if side is None or side.device != device:
+            side = self._side_stream = torch.cuda.Stream(device)
+        return side
+
+    def prefetch_image_features(self, image):
+        main = torch.cuda.current_stream(image.device)
+        side = self._side(image.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            imf = self.image_encoder(image)
+            done = torch.cuda.Event()
+            done.record(side)
+        # an event, not the stream: later work queued on the side stream (the next prefetch)
+        # must not hold up the step that consumes this result. Two entries: a step may start
+        # the next batch's prefetch before it consumes its own.
+        pend = getattr(self, "_prefetched", None) or []
+        self._prefetched = (pend + [(image, image._version, imf, done)])[-2:]
+
+    def image_features_async(self, image):
+        """The image encoder on the side stream for THIS step's images, beside work the caller
+        queues next on the main stream; returns join() -> features (waits on the main stream)."""
+        main = torch.cuda.current_stream(image.device)
+        side = self._side(image.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            imf = self.image_encoder(image)
+            done = torch.cuda.Event()
+            done.record(side)
+
+        def join():
+            main.wait_event(done)
+            imf.record_stream(main)
+            self._last_imf = (image, image._version, imf)
+            return imf
+        return join
+
+    def cached_image_features(self, image):
+        """The prefetched or last result for this very tensor, or None."""
+        pend = getattr(self, "_prefetched", None) or []
+        hit = [pf for pf in pend if pf[0] is image and pf[1] == image._version]
+        if hit:
+            self._prefetched = [pf for pf in pend if pf is not hit[0]]
+            _, _, imf, done = hit[0]
+            main = torch.cuda.current_stream(image.device)
+            main.wait_event(done)
+            imf.record_stream(main)
+            self._last_imf = (image, image._version, imf)
+            return imf
+        last = getattr(self, "_last_imf", None)
+        if last is not None and last[0] is image and last[1] == image._version:
+            return last[2]
+        return None
+
+    def image_features(self, image):
+        imf = self.cached_image_features(image)
+        if imf is None:
+            imf = self.image_encoder(image)
+            self._last_imf = (image, image._version, imf)
+        return imf

@@ -34,6 +34,7 @@ from ..engine.metrics import LossSummary
 from ..clip.model import TextEncodeFn
 from ._fns import PromptAssembleFn, CosineLogitsFn, MetaNetFn
 from .losses import CrossEntropyLoss, MultiClassFocalLoss, focal_alpha
+from ._vision import ImageFeatureSchedule
 from .prompt_base import init_prompts, grads_finite
 from .coop import TextEncoder  # noqa: F401  (same API-compatible text encoder)
 
@@ -86,7 +87,7 @@ class PromptLearner(nn.Module):
         return torch.stack(out, 0)
 
 
-class CustomCLIP(nn.Module):
+class CustomCLIP(ImageFeatureSchedule, nn.Module):
     """cocoop.py:200-260. ``class_counts`` (per-rank class counts, rank order) turns on class
     sharding: this process encodes its classes for every image and the logit slices are
     all-gathered (module doc)."""
@@ -129,33 +130,6 @@ class CustomCLIP(nn.Module):
         if self.class_counts is not None:
             logits = dist.GatherClassColumns.apply(logits, self.class_counts)
         return logits
-
-    def prefetch_image_features(self, image):
-        """Start the frozen image encoder on a LATER step's images, on a side stream
-        (NATIVE.PREFETCH_VISION): called between this step's forward and backward, the ViT's
-        small latency-bound launches run beside the text encoder's backward. Exact: the image
-        encoder does not train, so its output does not depend on this step's update."""
-        main = torch.cuda.current_stream(image.device)
-        side = getattr(self, "_side_stream", None)
-        if side is None or side.device != image.device:
-            side = self._side_stream = torch.cuda.Stream(image.device)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            imf = self.image_encoder(image)
-        self._prefetched = (image, image._version, imf, side)
-
-    def image_features(self, image):
-        """The image encoder's output for ``image``: the prefetched one when it was started for
-        this very tensor (unmodified since), else computed now."""
-        pf = getattr(self, "_prefetched", None)
-        self._prefetched = None
-        if pf is not None and pf[0] is image and pf[1] == image._version:
-            _, _, imf, side = pf
-            main = torch.cuda.current_stream(image.device)
-            main.wait_stream(side)
-            imf.record_stream(main)
-            return imf
-        return self.image_encoder(image)
 
     def forward(self, image, label=None):
         imf = self.image_features(image)
@@ -217,12 +191,13 @@ class CoCoOp(TrainerX):
     def forward_backward(self, batch):
         """cocoop.py:313-338 (multi-GPU weighting and the amp skip test as CoOp's)."""
         image, label = self.parse_batch_train(batch)
-        loss = self.model(image, label)
         nb, self.next_batch = getattr(self, "next_batch", None), None
         if nb is not None and image.is_cuda and self.cfg.get("NATIVE", {}).get("PREFETCH_VISION", False):
-            # the next step's image features, beside this step's backward (run_epoch / bench set
-            # next_batch to the batch the loop will pass next)
+            # the next step's image features on a side stream for the whole of this step
+            # (run_epoch / bench set next_batch to the batch the loop will pass next;
+            # trainers/_vision.py)
             self.model.prefetch_image_features(self.parse_batch_train(nb)[0])
+        loss = self.model(image, label)
         self.optim.zero_grad()
         if self.class_sharded:  # full loss on every rank, partial gradients: summed
             loss.backward()

@@ -23,6 +23,7 @@ from ..engine.metrics import compute_accuracy, LossSummary
 from ..clip.model import TextEncodeFn
 from ._fns import PromptAssembleFn, CosineLogitsFn
 from .losses import CrossEntropyLoss, MultiClassFocalLoss, LogitsNTXentLoss, focal_alpha
+from ._vision import ImageFeatureSchedule
 from .prompt_base import init_prompts, TextShape, grads_finite
 
 
@@ -95,7 +96,7 @@ class PromptLearner(nn.Module):
         return torch.cat(rows, dim=0)
 
 
-class CustomCLIP(nn.Module):
+class CustomCLIP(ImageFeatureSchedule, nn.Module):
     """coop.py:302-390. ``class_counts`` (per-rank class counts, rank order) turns on
     class-sharded text encoding: this process encodes only its classes and the [C, E] text
     features are all-gathered (dist.AllGatherRows: in backward the text-feature gradient
@@ -161,37 +162,24 @@ class CustomCLIP(nn.Module):
         if not self.training and not torch.is_grad_enabled():
             self._cached_text_features()
 
-    def _image_features_async(self, image):
-        """The frozen image encoder on a side stream (NATIVE.OVERLAP_VISION): CoOp's text
-        features do not depend on the images (coop.py:356-363 computes both, then the logits), so
-        the ViT's small, latency-bound launches can fill the CUs the text encoder leaves idle.
-        Returns (imf, join): call join() on the main stream before imf is read there."""
-        main = torch.cuda.current_stream(image.device)
-        side = getattr(self, "_side_stream", None)
-        if side is None or side.device != image.device:
-            side = self._side_stream = torch.cuda.Stream(image.device)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            imf = self.image_encoder(image)
-
-        def join():
-            main.wait_stream(side)
-            imf.record_stream(main)
-            return imf
-        return imf, join
-
     def forward_once(self, image):
-        overlap = (image.is_cuda and self.cfg.get("NATIVE", {}).get("OVERLAP_VISION", False)
-                   and (self.training or torch.is_grad_enabled()))
-        if overlap:
-            _, join = self._image_features_async(image)
-        else:
-            imf = self.image_encoder(image)
+        """The image features come prefetched (NATIVE.PREFETCH_VISION), or from this step's
+        first forward (the post-step accuracy forward of the same images), or -- NATIVE.
+        OVERLAP_VISION -- from a side stream beside the image-independent text encoder
+        (trainers/_vision.py); all bitwise the inline result."""
+        imf = self.cached_image_features(image)
+        join = None
+        if imf is None:
+            if (image.is_cuda and self.cfg.get("NATIVE", {}).get("OVERLAP_VISION", False)
+                    and (self.training or torch.is_grad_enabled())):
+                join = self.image_features_async(image)
+            else:
+                imf = self.image_features(image)
         if not self.training and not torch.is_grad_enabled():
             txt = self._cached_text_features()
         else:
             txt = self.text_features()
-        if overlap:
+        if join is not None:
             imf = join()
         return CosineLogitsFn.apply(imf, txt, self.logit_scale_value, 0, self.prompt_learner.n_cls)
 
@@ -239,6 +227,12 @@ class CoOp(TrainerX):
         step is skipped when a gradient is not finite, as GradScaler.step does (the bf16
         backward needs no loss scaling)."""
         x1, lbl, x2 = self.parse_batch_train(batch)
+        nb, self.next_batch = getattr(self, "next_batch", None), None
+        if (nb is not None and x1.is_cuda and x2 is None
+                and self.cfg.get("NATIVE", {}).get("PREFETCH_VISION", False)):
+            # the next step's image features on a side stream for the whole of this step
+            # (run_epoch / bench set next_batch; trainers/_vision.py)
+            self.model.prefetch_image_features(self.parse_batch_train(nb)[0])
         loss = self.model(x1, lbl, x2)
         self.optim.zero_grad()
         w = self.batch_weight(batch, x1.shape[0])
