@@ -409,9 +409,9 @@ def main():
                    "text_layout": ("shared-prefix packed, %d text rows/image (plain: %d)"
                                    % (lay.rows_per_group, args.classes * L)) if lay.pack is not None
                                   else f"plain [B*C, {L}]",
-                   "vision": ("each step starts the NEXT batch's (frozen) image encoder on a side stream between "
-                              "its forward and backward (NATIVE.PREFETCH_VISION, as TrainerX.run_epoch does with "
-                              "its one-batch lookahead): one ViT forward and one text fwd+bwd per timed step"
+                   "vision": ("each step starts the NEXT batch's (frozen) image encoder on a side stream at its "
+                              "top (NATIVE.PREFETCH_VISION, as TrainerX.run_epoch does with its one-batch "
+                              "lookahead): one ViT forward and one text fwd+bwd per timed step"
                               if trainer.cfg.NATIVE.get("PREFETCH_VISION", False) else "in line")},
         "eval_images_per_sec": round(eval_ips, 3),
         "eval_images": int(dist.sum_over_ranks(n_eval)),
