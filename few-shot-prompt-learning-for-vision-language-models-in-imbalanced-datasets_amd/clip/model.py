@@ -83,13 +83,18 @@ def arch_from_state_dict(sd) -> ClipArch:
 
 
 class _Workspace:
-    """Grow-only per-device scratch arena (stream-ordered reuse, caller-owned memory)."""
+    """Grow-only scratch arena per (device, slot, stream): stream-ordered reuse, caller-owned
+    memory. Per stream because an encoder may run on two streams at once (the image encoder
+    on the side stream of trainers/_vision.py beside an inline run on the main stream): one
+    shared buffer would be a race."""
 
     def __init__(self):
         self.buf = {}
 
     def get(self, nbytes: int, device, slot: str = "ws") -> torch.Tensor:
-        key = (str(device), slot)
+        dev = torch.device(device)
+        sid = torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0
+        key = (str(dev), slot, sid)
         b = self.buf.get(key)
         if b is None or b.numel() < nbytes:
             b = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)

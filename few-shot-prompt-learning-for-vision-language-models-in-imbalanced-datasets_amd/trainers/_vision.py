@@ -31,6 +31,7 @@ class ImageFeatureSchedule:
             imf = self.image_encoder(image)
             done = torch.cuda.Event()
             done.record(side)
+        image.record_stream(side)  # its memory is not reused while the side stream reads it
         # an event, not the stream: later work queued on the side stream (the next prefetch)
         # must not hold up the step that consumes this result. Two entries: a step may start
         # the next batch's prefetch before it consumes its own.
@@ -47,6 +48,7 @@ class ImageFeatureSchedule:
             imf = self.image_encoder(image)
             done = torch.cuda.Event()
             done.record(side)
+        image.record_stream(side)
 
         def join():
             main.wait_event(done)
