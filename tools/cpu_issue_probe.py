@@ -15,13 +15,14 @@ def main():
     ap.add_argument("--arch", default="ViT-B/16")
     ap.add_argument("--classes", type=int, default=1000)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--batches", default="8,1")
     a = ap.parse_args()
     import torch
     import bench
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     tr, dm = bench.build_trainer(a, "fp16", 8, dev, 0)
-    for b in (8, 1):
+    for b in (int(x) for x in a.batches.split(",")):
         batches = [{"img": x["img"][:b], "label": x["label"][:b]} for x in dm.train_loader_x]
 
         def step(i):
