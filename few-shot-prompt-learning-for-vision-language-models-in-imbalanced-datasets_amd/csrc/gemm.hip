@@ -156,6 +156,12 @@ template <> struct Raw<32> { uint4 v[2]; };
 #ifndef CLIPK_GEMM_PP2
 #define CLIPK_GEMM_PP2 2
 #endif
+// CLIPK_GEMM_PRIO (A/B): wave priority in the ping-pong loop -- 1 = the MFMA segment runs at
+// priority 1 (default), 0 = no priority changes, 2 = the memory segment (fragment reads,
+// restage issue) runs at priority 1 instead.
+#ifndef CLIPK_GEMM_PRIO
+#define CLIPK_GEMM_PRIO 1
+#endif
 // Diagnostic builds only (wrong results; tools/gemm_diag.sh): NOLOAD = stage no K step past
 // the first (the loop's compute + LDS + barrier ceiling), NOBAR = no barrier / vmcnt wait per
 // K step either.
@@ -555,7 +561,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       };
       auto mm = [&](int h, int q) {
         if (CLIPK_GEMM_NOMMA) return;
-        __builtin_amdgcn_s_setprio(1);
+        if (CLIPK_GEMM_PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
@@ -563,10 +569,11 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
 #pragma unroll
             for (int j = 0; j < TN2; ++j)
               acc[h * TM2 + i][q * TN2 + j] = mma<T>(fbs[NFB == 2 ? q : 0][kk][j], fa[kk][i], acc[h * TM2 + i][q * TN2 + j]);
-        __builtin_amdgcn_s_setprio(0);
+        if (CLIPK_GEMM_PRIO == 1) __builtin_amdgcn_s_setprio(0);
       };
       auto seg_end = [&]() {  // memory segment done: fragments in registers, then the barrier
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (CLIPK_GEMM_PRIO == 2) __builtin_amdgcn_s_setprio(0);
         G8_BAR();
       };
       // The K steps of this block's tiles form one stream (step `it`, buffer it & 1): the
@@ -604,6 +611,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         const int k1 = in1 ? kt + 1 : kt + 1 - nk, k2 = in2 ? kt + 2 : kt + 2 - nk;
         const TRes ra1 = in1 ? cra : xra, rb1 = in1 ? crb : xrb;
         const TRes ra2 = in2 ? cra : xra, rb2 = in2 ? crb : xrb;
+        if (CLIPK_GEMM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         rd_a(b, 0); rd_b(b, 0); rd_b(b, 1);     // phase 1: A0 x B
         if (h1) {
           pst(b ^ 1, ra1, rb1, k1, 1);
@@ -617,6 +625,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         mm(0, 0);
         mm(0, 1);
         G8_BAR();
+        if (CLIPK_GEMM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         rd_a(b, 1);                             // phase 2: A1 x B
         if (h2) {
           pst(b, ra2, rb2, k2, 0);
@@ -636,6 +645,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         const bool in1 = kt + 1 < nk, in2 = kt + 2 < nk;
         const bool h1 = in1 || has_next, h2 = in2 || has_next;
         const int k1 = in1 ? kt + 1 : kt + 1 - nk, k2 = in2 ? kt + 2 : kt + 2 - nk;
+        if (CLIPK_GEMM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         rd_a(b, 0); rd_b(b, 0);                 // phase 1: A0 x B0
         if (h1) pst(b ^ 1, cra, in1 ? crb : xrb, k1, 2);
         if (!in1) {
@@ -645,16 +655,19 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         seg_end();
         mm(0, 0);
         G8_BAR();
+        if (CLIPK_GEMM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         rd_b(b, 1);                             // phase 2: A0 x B1
         if (h2) pst(b, in2 ? cra : xra, crb, k2, 0);
         seg_end();
         mm(0, 1);
         G8_BAR();
+        if (CLIPK_GEMM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         rd_a(b, 1);                             // phase 3: A1 x B1
         if (h2) pst(b, cra, in2 ? crb : xrb, k2, 3);
         seg_end();
         mm(1, 1);
         G8_BAR();
+        if (CLIPK_GEMM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         if (NFB == 1) rd_b(b, 0);               // phase 4: A1 x B0
         if (h2) {
           pst(b, in2 ? cra : xra, crb, k2, 1);
