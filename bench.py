@@ -89,28 +89,31 @@ def reference_cpu(arch, classes):
                                f"of the build container's {r['nproc']}-core Xeon (not the GPU box: the reference "
                                f"does not travel); {REF_CPU_FILE[len(ROOT) + 1:]}")}
     return None
-PEAK = {"fp16": 2500.0, "bf16": 2500.0, "amp": 2500.0, "fp32": 157.3}  # dense TFLOP/s (MI355X guide)
+# dense TFLOP/s (MI355X guide); fp32s: the fp16 MFMA peak / 3 (3 fp16 MFMAs per fp32-class product,
+# include/clipk.h CLIPK_F32S), the ceiling for its algorithmic (fp32) FLOPs
+PEAK = {"fp16": 2500.0, "bf16": 2500.0, "amp": 2500.0, "fp32": 157.3, "fp32s": 2500.0 / 3}
 HBM_PEAK_GBS = 8000.0  # HBM3E, MI355X_MICROARCH.md
 # the latest round's PMC passes (tools/pmc_bench.sh), else the previous round's
 PMC_FILE = next((f for f in (os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r03_pmc", "r02_pmc"))
                  if os.path.exists(f)), os.path.join(ROOT, "profiles", "r03_pmc", "traffic.json"))
 
 # kernel classes of the step: launch sites that run the same kernel instantiation (rocprofv3
-# kernel-name key, for the PMC traffic lookup) -- the text GEMMs by role, attention, LN
+# kernel-name key, for the PMC traffic lookup) -- the text GEMMs by role, attention, LN. Each
+# class's bound is decided from its own algorithmic FLOPs and bytes per launch (kernel_table).
 KERNELS = {
-    "gemm_dx_n512": (["text.fc_dx", "text.qkv_dx", "text.out_dx"], "EPI_NONE 192x256", "mfma"),
-    "gemm_proj_fwd": (["text.proj_fwd"], "EPI_BIAS_RES N=512 K=2048", "mfma"),
-    "gemm_dgelu": (["text.proj_dx_dgelu"], "EPI_DQGELU", "mfma"),
-    "gemm_fc_fwd": (["text.fc_fwd"], "EPI_BIAS_QGELU N=2048 (h and QuickGELU(h); ln_2 folded)", "mfma"),
-    "gemm_qkv_fwd": (["text.qkv_fwd"], "EPI_BIAS N=1536 (ln_1 folded)", "mfma"),
-    "gemm_out_fwd": (["text.out_fwd"], "EPI_BIAS_RES N=512", "mfma"),
-    "attn_bwd": (["text.attn_bwd"], "attn_prefix_bwd_lds", "hbm"),
-    "attn_fwd": (["text.attn_fwd"], "attn_prefix_fwd_lds", "hbm"),
-    "ln_bwd": (["text.ln_bwd"], "ln_bwd_kernel", "hbm"),
-    "ln_fwd": (["text.ln_fwd"], "ln_fwd_kernel", "hbm"),
-    "ln_stats": (["text.ln_stats"], "ln_stats_merge_kernel (LN fold statistics)", "hbm"),
+    "gemm_dx_n512": (["text.fc_dx", "text.qkv_dx", "text.out_dx"], "EPI_NONE 192x256"),
+    "gemm_proj_fwd": (["text.proj_fwd"], "EPI_BIAS_RES N=512 K=2048"),
+    "gemm_dgelu": (["text.proj_dx_dgelu"], "EPI_DQGELU"),
+    "gemm_fc_fwd": (["text.fc_fwd"], "EPI_BIAS_QGELU N=2048 (h and QuickGELU(h); ln_2 folded)"),
+    "gemm_qkv_fwd": (["text.qkv_fwd"], "EPI_BIAS N=1536 (ln_1 folded)"),
+    "gemm_out_fwd": (["text.out_fwd"], "EPI_BIAS_RES N=512"),
+    "attn_bwd": (["text.attn_bwd"], "attn_prefix_bwd_lds"),
+    "attn_fwd": (["text.attn_fwd"], "attn_prefix_fwd_lds"),
+    "ln_bwd": (["text.ln_bwd"], "ln_bwd_kernel"),
+    "ln_fwd": (["text.ln_fwd"], "ln_fwd_kernel"),
+    "ln_stats": (["text.ln_stats"], "ln_stats_merge_kernel (LN fold statistics)"),
     "vit": (["vit.patch_embed", "vit.qkv_fwd", "vit.attn_fwd", "vit.out_fwd", "vit.fc_fwd", "vit.proj_fwd",
-             "vit.ln_fwd", "vit.ln_stats", "vit.eot_gather", "vit.head"], "ViT forward (all sites)", "mfma"),
+             "vit.ln_fwd", "vit.ln_stats", "vit.eot_gather", "vit.head"], "ViT forward (all sites)"),
 }
 ROOF_PMC_KEY = {"gemm_dx_n512": "gemm_nt_kernelIDF16_DF16_fLi4ELi192ELi256",
                 "gemm_dgelu": "gemm_nt_kernelIDF16_DF16_DF16_Li3E",
@@ -184,7 +187,7 @@ def kernel_table(sites, steps, prec):
     """Per kernel class: launches, avg ms, algorithmic TF/s and GB/s per launch, fractions."""
     peak = PEAK[prec]
     out = {}
-    for name, (members, desc, bound) in KERNELS.items():
+    for name, (members, desc) in KERNELS.items():
         ms = sum(sites[s][0] for s in members if s in sites)
         n = sum(sites[s][1] for s in members if s in sites)
         fl = sum(sites[s][2] for s in members if s in sites)
@@ -194,9 +197,14 @@ def kernel_table(sites, steps, prec):
         sec = ms * 1e-3
         tf = fl / sec / 1e12 if fl else 0.0
         gbs = by / sec / 1e9
+        # the binding roofline of this class: the longer of its FLOPs at the MFMA peak and its
+        # bytes at the HBM peak (arithmetic intensity vs the ridge point peak / 8 TB/s)
+        bound = "hbm" if (fl == 0 or by / (HBM_PEAK_GBS * 1e9) > fl / (peak * 1e12)) else "mfma"
         out[name] = {"kernel": desc, "launches_per_step": round(n / steps, 2), "ms_per_step": round(ms / steps, 4),
                      "avg_launch_ms": round(ms / n, 4), "tflops": round(tf, 1), "mfma_frac": round(tf / peak, 4),
                      "gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4), "bound": bound,
+                     "roof_frac": round(gbs / HBM_PEAK_GBS if bound == "hbm" else tf / peak, 4),
+                     "flop_per_byte": round(fl / by, 1) if by else None,
                      "flops_per_launch": fl / n, "bytes_per_launch": by / n}
     return out
 
@@ -345,6 +353,53 @@ def time_eval(trainer, dm, n_images):
     return dist.sum_over_ranks(n) / te, n
 
 
+def precision_line(args, prec, dev, rank, world, steps=10, warmup=2, n_eval=5000):
+    """The headline workload at another PREC: train img/s over `steps` timed steps, eval img/s
+    over n_eval distinct resident images, and the roofline of its dominant kernel class
+    (site events in 2 extra steps)."""
+    import torch
+    from fsp_amd import dist
+    tr, dm = build_trainer(args, prec, args.batch, dev, rank, n_test_device=n_eval)
+    t, sites = time_train(tr, dm, steps, warmup, prof_steps=2)
+    table = kernel_table(sites, 2, prec) if sites else None
+    e, n = time_eval(tr, dm, n_eval)
+    line = {"images_per_sec": round(world * args.batch * steps / t, 3), "ms_per_step": round(1000 * t / steps, 3),
+            "steps": steps, "eval_images_per_sec": round(e, 3), "eval_images": int(dist.sum_over_ranks(n)),
+            "roofline": roofline_of(table, prec) if table else None,
+            "kernels": ({k: {kk: v[kk] for kk in ("launches_per_step", "ms_per_step", "bound", "roof_frac", "tflops",
+                                                  "gbs")} for k, v in table.items()} if table else None)}
+    if prec == "fp32s":
+        line["peak_note"] = ("fp32s roofline peak = dense fp16 MFMA peak / 3 (three fp16 MFMAs per fp32-class "
+                             "product); achieved counts the algorithmic fp32 FLOPs")
+    del tr, dm
+    torch.cuda.empty_cache()
+    return line
+
+
+def baseline_config_line(args, dev, rank, world, steps=10, warmup=3, n_eval=5000):
+    """BASELINE.json configs 4 / 5 for --arch ViT-L/14 / ViT-L/14@336px (bf16, 1,000 classes,
+    synthetic data, random-init weights of those architectures): config 4 = CoOp n_ctx 16 at 32
+    images per GPU per step (class-sharded text encoding at N > 1), config 5 = CoCoOp n_ctx 4 at
+    8 images per GPU per step (image data parallel). Train and eval images/sec (whole job)."""
+    import torch
+    from fsp_amd import dist
+    if args.arch == "ViT-L/14":
+        name, batch = "config 4: CoOp ViT-L/14 bf16, n_ctx 16, 1000 classes, 32 images/GPU/step", 32
+        tr, dm = build_coop_trainer(args, "bf16", batch, dev, rank, n_test_device=n_eval)
+    else:
+        name, batch = "config 5: CoCoOp ViT-L/14@336px bf16, n_ctx 4, 1000 classes, 8 images/GPU/step", 8
+        tr, dm = build_trainer(args, "bf16", batch, dev, rank, n_test_device=n_eval)
+    t, _ = time_train(tr, dm, steps, warmup)
+    e, n = time_eval(tr, dm, n_eval)
+    line = {"workload": name, "images_per_sec": round(world * batch * steps / t, 3),
+            "ms_per_step": round(1000 * t / steps, 3), "steps": steps, "eval_images_per_sec": round(e, 3),
+            "eval_images": int(dist.sum_over_ranks(n)), "dtype": "bf16",
+            "text_layout": "shared-prefix packed" if tr.model.prompt_learner.layout.pack is not None else "plain"}
+    del tr, dm
+    torch.cuda.empty_cache()
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -420,11 +475,14 @@ def main():
         "model_tflops_per_gpu": round(step_flops * args.steps / t / 1e12, 2),
         "roofline": roof,
         "kernels": ({k: {kk: v[kk] for kk in ("kernel", "launches_per_step", "ms_per_step", "avg_launch_ms",
-                                               "tflops", "mfma_frac", "gbs", "hbm_frac", "bound")}
+                                               "tflops", "mfma_frac", "gbs", "hbm_frac", "bound", "roof_frac",
+                                               "flop_per_byte")}
                      for k, v in table.items()} if table else None),
     }
     del trainer, dm
     torch.cuda.empty_cache()
+    if not args.no_extra and args.arch in ("ViT-L/14", "ViT-L/14@336px"):
+        out["config4" if args.arch == "ViT-L/14" else "config5"] = baseline_config_line(args, dev, rank, world)
     if not args.no_extra and world > 1:
         # the reference's CoCoOp batch (1 image / step) with the classes sharded over the ranks
         tr1, dm1 = build_trainer(args, args.prec, 1, dev, 0, class_shard=True)
@@ -454,15 +512,10 @@ def main():
                                        else "plain")}
         del trc, dmc
         torch.cuda.empty_cache()
-        # PREC fp32: f32-input MFMA everywhere, the path that meets |d logit| <= 1e-3
-        tr32, dm32 = build_trainer(args, "fp32", args.batch, dev, rank, n_test=500)
-        t32, _ = time_train(tr32, dm32, 3, 1)
-        e32, n32 = time_eval(tr32, dm32, 500)
-        out["fp32"] = {"images_per_sec": round(world * args.batch * 3 / t32, 3),
-                       "ms_per_step": round(1000 * t32 / 3, 3), "eval_images_per_sec": round(e32, 3),
-                       "eval_images": int(dist.sum_over_ranks(n32))}
-        del tr32, dm32
-        torch.cuda.empty_cache()
+        # the fp32-class precisions, the paths that meet the north-star |d logit| <= 1e-3:
+        # PREC fp32s (split-fp16 MFMA GEMMs, fp32 elsewhere) and PREC fp32 (f32-input MFMA)
+        for p in ("fp32s", "fp32"):
+            out[p] = precision_line(args, p, dev, rank, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             threads = min(16, os.cpu_count() or 1)

@@ -12,7 +12,8 @@ import os
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CLIPK_LIB") or os.path.join(_PKG, "libclipk.so")  # override: A/B builds
 
-F32, F16, BF16 = 0, 1, 2
+F32, F16, BF16, F32S = 0, 1, 2, 3  # F32S: fp32 activations x split-packed weights (PREC fp32s)
+SPLIT_SCALE = 64.0  # CLIPK_SPLIT_SCALE: clipk_split_pack stores SPLIT_SCALE * W
 EPI_BIAS, EPI_BIAS_RES, EPI_BIAS_QGELU, EPI_DQGELU, EPI_NONE = 0, 1, 2, 3, 4
 A_QGELU = 0x100  # OR-ed into epi: the GEMM consumes quickgelu(A) (include/clipk.h)
 PROF_NONE, PROF_GEMM_FC, PROF_GEMM_ALL, PROF_ATTN, PROF_LN, PROF_GEMM_DGELU = 0, 1, 2, 3, 4, 5
@@ -34,6 +35,7 @@ SIGNATURES = {
     "clipk_gemm_splitk_ws_bytes": (_S, [_I, _I, _I]),
     "clipk_gemm_splitk": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P, _S, _P]),
     "clipk_gemm_set_config": (_I, [_I]),
+    "clipk_split_pack": (_I, [_I, _I, _P, _I, _P, _P]),
     "clipk_gemm_ln": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P]),
     "clipk_ln_stats_merge": (_I, [_I, _I, _P, _P, _P, _P, _P]),
     "clipk_image_resample": (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P]),
@@ -69,6 +71,7 @@ SIGNATURES = {
     "clipk_encoder_set_deep_prompts": (_I, [_P, _I, _I, _I, _P, _P, _P]),
     "clipk_encoder_set_input_rows": (_I, [_P, _I]),
     "clipk_encoder_set_ln_fold": (_I, [_P, _P]),
+    "clipk_encoder_set_split": (_I, [_P, _I]),
     "clipk_vit_prompted_saved_bytes": (_S, [_P, _I, _I]),
     "clipk_vit_prompted_ws_bytes": (_S, [_P, _I, _I]),
     "clipk_vit_forward_prompted": (_I, [_P, _I, _P, _I, _P, _P, _P, _S, _P, _S, _P]),

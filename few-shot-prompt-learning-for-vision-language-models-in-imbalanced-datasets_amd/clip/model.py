@@ -15,7 +15,10 @@ but the encoders run as libclipk.so launch sequences:
   with per-layer deep prompts).
 
 Precision (cfg ``PREC``; PREC_DTYPES): "fp32" -> fp32 operands on f32-input MFMA, fp32
-residual stream (parity mode); "fp16" -> fp16 forward and backward GEMM operands, a 16-bit
+residual stream (parity mode); "fp32s" -> the fp32 mode's dataflow (fp32 activations, residual
+stream, LayerNorm, attention) with every GEMM on the 16-bit MFMA as a split-fp16 product
+(weights packed once by clipk_split_pack; include/clipk.h CLIPK_F32S): fp32-class results, the
+north-star 1e-3 logit bar, at several times the f32-MFMA rate; "fp16" -> fp16 forward and backward GEMM operands, a 16-bit
 text residual stream and residual-gradient stream; "amp" -> fp16 forward, bf16 backward
 operands; "bf16" -> bf16 both. LayerNorm statistics, softmax and MFMA accumulation are fp32
 in every mode. The reference's own "fp16" runs in fp32 (convert_weights disabled,
@@ -36,6 +39,7 @@ from .synth import ClipArch
 
 PREC_DTYPES = {
     "fp32": (torch.float32, torch.float32),
+    "fp32s": (torch.float32, torch.float32),
     "fp16": (torch.float16, torch.float16),
     "amp": (torch.float16, torch.bfloat16),
     "bf16": (torch.bfloat16, torch.bfloat16),
@@ -59,6 +63,13 @@ def prec_dtypes(prec):
 _LAYER_KEYS = ["ln_1.weight", "ln_1.bias", "attn.in_proj_weight", "attn.in_proj_bias",
                "attn.out_proj.weight", "attn.out_proj.bias", "ln_2.weight", "ln_2.bias",
                "mlp.c_fc.weight", "mlp.c_fc.bias", "mlp.c_proj.weight", "mlp.c_proj.bias"]
+
+
+def _mm_weight(x, device, act, split):
+    """A GEMM weight [N, K] as the encoder consumes it: in the activation dtype, or (PREC fp32s)
+    split-packed for the split-fp16 GEMM (ops.split_pack)."""
+    x = x.to(device, torch.float32 if split else act).contiguous()
+    return ops.split_pack(x) if split else x
 
 
 def _t(v):
@@ -150,6 +161,7 @@ class TextEncoderCore(_Encoder):
         act, grad = prec_dtypes(prec)
         self.arch, self.prec, self.device = arch, prec, torch.device(device)
         self.act, self.grad = act, grad
+        split = prec == "fp32s"
         W, nl = arch.transformer_width, arch.transformer_layers
         self.W, self.E, self.layers, self.heads = W, arch.embed_dim, nl, W // 64
         keep = []
@@ -159,8 +171,8 @@ class TextEncoderCore(_Encoder):
         for i in range(nl):
             p = {k: _t(sd[f"transformer.resblocks.{i}.{k}"]).float() for k in _LAYER_KEYS}
             f32 = lambda x: x.to(self.device, torch.float32).contiguous()
-            A = lambda x: x.to(self.device, act).contiguous()
-            G = lambda x: x.t().contiguous().to(self.device, grad) if with_grad else None
+            A = lambda x: _mm_weight(x, self.device, act, split)
+            G = lambda x: _mm_weight(x.t(), self.device, grad, split) if with_grad else None
             row = [f32(p["ln_1.weight"]), f32(p["ln_1.bias"]), A(p["attn.in_proj_weight"]),
                    f32(p["attn.in_proj_bias"]), A(p["attn.out_proj.weight"]), f32(p["attn.out_proj.bias"]),
                    f32(p["ln_2.weight"]), f32(p["ln_2.bias"]), A(p["mlp.c_fc.weight"]), f32(p["mlp.c_fc.bias"]),
@@ -178,8 +190,8 @@ class TextEncoderCore(_Encoder):
         P = _t(sd["text_projection"]).float()
         head = [_t(sd["ln_final.weight"]).float().to(self.device).contiguous(),
                 _t(sd["ln_final.bias"]).float().to(self.device).contiguous(),
-                P.t().contiguous().to(self.device, act),
-                P.contiguous().to(self.device, grad) if with_grad else None]
+                _mm_weight(P.t(), self.device, act, split),
+                _mm_weight(P, self.device, grad, split) if with_grad else None]
         keep += head
         self._keep = keep
         h = ctypes.c_void_p()
@@ -187,6 +199,8 @@ class TextEncoderCore(_Encoder):
                                               _ptrs(table), _ptrs(head), ctypes.byref(h)),
                 "clipk_encoder_create(text)")
         self.handle = h
+        if split:
+            N.check(N.load().clipk_encoder_set_split(h, 1), "clipk_encoder_set_split(text)")
         if fold:
             self._keep += fold
             N.check(N.load().clipk_encoder_set_ln_fold(h, _ptrs(fold)), "clipk_encoder_set_ln_fold")
@@ -324,13 +338,14 @@ class VisionEncoder(nn.Module, _Encoder):
     def __init__(self, sd, arch: ClipArch, prec: str, device, with_grad: bool = False):
         nn.Module.__init__(self)
         act, _ = PREC_DTYPES[prec]
+        split = prec == "fp32s"
         self.arch, self.act, self.dev = arch, act, torch.device(device)
         self.input_resolution = arch.image_resolution
         self.output_dim = arch.embed_dim
         D, nl, p = arch.vision_width, arch.vision_layers, arch.vision_patch_size
         f32 = lambda x: _t(x).float().to(self.dev).contiguous()
-        A = lambda x: _t(x).float().to(self.dev, act).contiguous()
-        G = lambda x: _t(x).float().t().contiguous().to(self.dev, act) if with_grad else None
+        A = lambda x: _mm_weight(_t(x).float(), self.dev, act, split)
+        G = lambda x: _mm_weight(_t(x).float().t(), self.dev, act, split) if with_grad else None
         self.with_grad = with_grad
         table = []
         # LayerNorm fold of ln_1 / ln_2 for the 16-bit-residual forward (clipk_vit_forward)
@@ -358,11 +373,11 @@ class VisionEncoder(nn.Module, _Encoder):
         conv[:, :k] = _t(sd["visual.conv1.weight"]).float().reshape(D, k)
         head = [f32(sd["visual.ln_pre.weight"]), f32(sd["visual.ln_pre.bias"]),
                 f32(sd["visual.ln_post.weight"]), f32(sd["visual.ln_post.bias"]),
-                _t(sd["visual.proj"]).float().t().contiguous().to(self.dev, act),
-                conv.to(self.dev, act).contiguous(), f32(sd["visual.class_embedding"]),
+                _mm_weight(_t(sd["visual.proj"]).float().t(), self.dev, act, split),
+                _mm_weight(conv, self.dev, act, split), f32(sd["visual.class_embedding"]),
                 f32(sd["visual.positional_embedding"])]
         # backward of the head: d ln_post(CLS) = dfeat . proj^T  (proj [D, E], B operand [N=D, K=E])
-        self.proj_bwd = _t(sd["visual.proj"]).float().contiguous().to(self.dev, act) if with_grad else None
+        self.proj_bwd = _mm_weight(_t(sd["visual.proj"]).float(), self.dev, act, split) if with_grad else None
         self._keep = [t for t in table if t is not None] + head
         self.width, self.n_tokens = D, (arch.image_resolution // p) ** 2 + 1
         h = ctypes.c_void_p()
@@ -370,6 +385,8 @@ class VisionEncoder(nn.Module, _Encoder):
                                              ops.DT[act], _ptrs(table), _ptrs(head), ctypes.byref(h)),
                 "clipk_vision_create")
         self.handle = h
+        if split:
+            N.check(N.load().clipk_encoder_set_split(h, 1), "clipk_encoder_set_split(vision)")
         if fold:
             self._keep += fold
             N.check(N.load().clipk_encoder_set_ln_fold(h, _ptrs(fold)), "clipk_encoder_set_ln_fold")

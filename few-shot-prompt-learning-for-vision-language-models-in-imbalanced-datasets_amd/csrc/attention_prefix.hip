@@ -765,252 +765,263 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_bwd_lds(int G, int P, in
   }
 }
 
-// ------------------------------------------------------------------ VALU versions (fp32 path)
-// One wave per (group, chunk of kValuChunk units, head); 4 tiles in flight (lane group
-// grp = lane>>4), lane r16 = row of the tile (query for the forward and dQ, key for dK/dV).
-// K/V rows staged in LDS as fp32.
-__device__ __forceinline__ void valu_unit(const int* __restrict__ tiles, const int* __restrict__ row_first,
-                                          int P, int u, int r16, int& t0, int& n, int& pre, int& first) {
+// ------------------------------------------------------------------ fp32 kernels (PREC fp32 / fp32s)
+// One wave per (group, chunk of kValuChunk units, head); blocks of kF32Wpb waves share one
+// (group, head), so the prefix K/V rows are staged into LDS once per block. Lane = 4 r + s: row
+// r of the unit (query in the forward and for dQ, key for dK / dV) and 16-column slice s of
+// the head; a dot product is 16 FMAs on the lane's slice plus a quad sum (2 DPP adds). K/V
+// (and, for the backward's key phases, Q / dO) rows are read from LDS, where the 16 lanes of
+// one slice read the same 64 B (a broadcast). All arithmetic fp32, the reference's
+// nn.MultiheadAttention math (model.py:183), exact softmax (online max / rescale, fwd).
+constexpr int kF32Wpb = 4;
+
+__device__ __forceinline__ float quad_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+}
+__device__ __forceinline__ void ld16(const float* __restrict__ p, float* v) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const f32x4 t = reinterpret_cast<const f32x4*>(p)[c];
+    v[4 * c] = t[0]; v[4 * c + 1] = t[1]; v[4 * c + 2] = t[2]; v[4 * c + 3] = t[3];
+  }
+}
+__device__ __forceinline__ void st16(float* __restrict__ p, const float* v) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    reinterpret_cast<f32x4*>(p)[c] = (f32x4){v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]};
+}
+__device__ __forceinline__ float dot16(const float* a, const float* b) {
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; d += 2) {
+    s0 = fmaf(a[d], b[d], s0);
+    s1 = fmaf(a[d + 1], b[d + 1], s1);
+  }
+  return s0 + s1;
+}
+// a wave's own LDS writes visible to its other lanes (program order on the LDS; no reordering
+// by the compiler across this point)
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// unit u of group-relative tiles: first row t0, rows n (<= 16), prefix keys pre, and for row rr
+// the first row of its class (causal block-diagonal mask inside the tile)
+__device__ __forceinline__ void f32_unit(const int* __restrict__ tiles, const int* __restrict__ row_first, int P,
+                                         int u, int r, int& t0, int& n, int& pre, int& rr, int& first) {
   if (u == 0) {
-    t0 = 0; n = P; pre = 0; first = 0;
+    t0 = 0; n = P; pre = 0;
   } else {
     t0 = tiles[2 * (u - 1)];
     n = min(tiles[2 * (u - 1) + 1], 16);
     pre = P;
-    first = row_first[t0 + min(r16, n - 1)] - t0;
   }
+  rr = min(r, n - 1);
+  first = u == 0 ? 0 : row_first[t0 + rr] - t0;
 }
 
-template <typename T>
-__device__ __forceinline__ void stage_prefix_f32(const T* __restrict__ qkv, int row0, int P, int ldq, int hW,
-                                                 int W, int lane, float* sKp, float* sVp) {
-  const int row = lane >> 2, qtr = lane & 3;  // 16 rows x 4 quarters of 16 values
-  float kv[16], vv[16];
-  if (row < P) {
-    const T* b = qkv + (size_t)(row0 + row) * ldq + hW + qtr * 16;
-    constexpr int V = Vec16<T>::N;
-#pragma unroll
-    for (int c = 0; c < 16 / V; ++c) {
-      load16_f32<T>(b + W + c * V, kv + c * V);
-      load16_f32<T>(b + 2 * W + c * V, vv + c * V);
+// block (g, h, chunk block kb): waves take chunks kb * kF32Wpb + w; stages the prefix K / V rows
+// of (g, h) (P <= 16 rows x 64 fp32) into sKp / sVp
+__device__ __forceinline__ void f32_block(int H, int nchunk, int& g, int& h, int& k, int& w) {
+  const int nkb = (nchunk + kF32Wpb - 1) / kF32Wpb;
+  const int b = blockIdx.x;
+  h = b % H;
+  const int kb = (b / H) % nkb;
+  g = b / (H * nkb);
+  w = threadIdx.x >> 6;
+  k = kb * kF32Wpb + w;
+}
+__device__ __forceinline__ void f32_stage_prefix(const float* __restrict__ qkv, size_t row0, int P, int ldq, int col,
+                                                 int W, float* sKp, float* sVp) {
+  for (int i = threadIdx.x; i < 16 * 16; i += kF32Wpb * 64) {  // 16 rows x 16 float4
+    const int j = i >> 4, c = i & 15;
+    f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = kv;
+    if (j < P) {
+      const float* b = qkv + (row0 + j) * ldq + col + 4 * c;
+      kv = *reinterpret_cast<const f32x4*>(b + W);
+      vv = *reinterpret_cast<const f32x4*>(b + 2 * W);
     }
-  } else {
-#pragma unroll
-    for (int c = 0; c < 16; ++c) { kv[c] = 0.f; vv[c] = 0.f; }
-  }
-#pragma unroll
-  for (int c = 0; c < 16; ++c) {
-    sKp[row * 64 + qtr * 16 + c] = kv[c];
-    sVp[row * 64 + qtr * 16 + c] = vv[c];
+    reinterpret_cast<f32x4*>(sKp)[i] = kv;
+    reinterpret_cast<f32x4*>(sVp)[i] = vv;
   }
 }
 
-template <typename T>
-__global__ __launch_bounds__(64) void attn_prefix_fwd_valu(int G, int P, int R, int ntiles,
-                                                           const int* __restrict__ tiles,
-                                                           const int* __restrict__ row_first, int H,
-                                                           int nchunk, const T* __restrict__ qkv,
-                                                           int ldq, T* __restrict__ out, int ldo,
-                                                           float* __restrict__ lse) {
-  __shared__ CLIPK_LDS_ALIGN float sKp[16 * 64];
-  __shared__ CLIPK_LDS_ALIGN float sVp[16 * 64];
-  __shared__ CLIPK_LDS_ALIGN float sK[4][16 * 64];
-  __shared__ CLIPK_LDS_ALIGN float sV[4][16 * 64];
-  const int lane = threadIdx.x, grp = lane >> 4, r16 = lane & 15;
-  const int wid = blockIdx.x;
-  const int h = wid % H, k = (wid / H) % nchunk, g = wid / (H * nchunk);
+__global__ __launch_bounds__(kF32Wpb * 64) void attn_prefix_fwd_f32(
+    int G, int P, int R, int ntiles, const int* __restrict__ tiles, const int* __restrict__ row_first, int H,
+    int nchunk, const float* __restrict__ qkv, int ldq, float* __restrict__ out, int ldo, float* __restrict__ lse) {
+  __shared__ CLIPK_LDS_ALIGN float sKp[16 * 64], sVp[16 * 64];
+  __shared__ CLIPK_LDS_ALIGN float sK[kF32Wpb][16 * 64], sV[kF32Wpb][16 * 64];
+  int g, h, k, w;
+  f32_block(H, nchunk, g, h, k, w);
   const int W = H * 64;
-  stage_prefix_f32<T>(qkv, g * R, P, ldq, h * 64, W, lane, sKp, sVp);
+  f32_stage_prefix(qkv, (size_t)g * R, P, ldq, h * 64, W, sKp, sVp);
+  __syncthreads();
+  if (k >= nchunk) return;  // wave-uniform; no block barrier follows
+  const int lane = threadIdx.x & 63, r = lane >> 2, s = lane & 3;
+  float* sk = sK[w];
+  float* sv = sV[w];
   const int u_end = min((k + 1) * kValuChunk, ntiles + 1);
-  for (int base = k * kValuChunk; base < u_end; base += 4) {
-    const int u = base + grp;
-    const bool active = u < u_end;
-    int t0 = 0, n = 1, pre = 0, first = 0;
-    if (active) valu_unit(tiles, row_first, P, u, r16, t0, n, pre, first);
-    const bool qok = active && r16 < n;
-    const size_t row = (size_t)g * R + t0 + min(r16, n - 1);
-    const T* qp = qkv + row * ldq + h * 64;
-    float q[64], t64[64];
-    load_row64<T>(qp, q);
+  for (int u = k * kValuChunk; u < u_end; ++u) {
+    int t0, n, pre, rr, first;
+    f32_unit(tiles, row_first, P, u, r, t0, n, pre, rr, first);
+    const size_t row = (size_t)g * R + t0 + rr;
+    const float* qp = qkv + row * ldq + h * 64 + 16 * s;
+    float q[16], t[16];
+    ld16(qp, q);
 #pragma unroll
-    for (int dd = 0; dd < 64; ++dd) q[dd] *= kScale;
-    load_row64<T>(qp + W, t64);
+    for (int d = 0; d < 16; ++d) q[d] *= kScale;
+    ld16(qp + W, t);
+    st16(sk + r * 64 + 16 * s, t);
+    ld16(qp + 2 * W, t);
+    st16(sv + r * 64 + 16 * s, t);
+    lds_sync();
+    float m = -INFINITY, l = 0.f, o[16];
 #pragma unroll
-    for (int dd = 0; dd < 64; ++dd) sK[grp][r16 * 64 + dd] = t64[dd];
-    load_row64<T>(qp + 2 * W, t64);
+    for (int d = 0; d < 16; ++d) o[d] = 0.f;
+    // online softmax over the prefix keys, then the row's own class keys first..rr
+    auto key = [&](const float* kr, const float* vr, bool ok) {
+      float kv[16];
+      ld16(kr + 16 * s, kv);
+      const float sc = quad_sum(dot16(q, kv));
+      if (ok) {
+        if (sc > m) {
+          const float a = __expf(m - sc);  // 0 for the first key (m = -inf)
+          l *= a;
 #pragma unroll
-    for (int dd = 0; dd < 64; ++dd) sV[grp][r16 * 64 + dd] = t64[dd];
-    __syncthreads();
-    float sc[32], m = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      sc[j] = j < pre ? dot64(q, &sKp[j * 64]) : -INFINITY;
-      sc[16 + j] = (j <= r16 && j >= first) ? dot64(q, &sK[grp][j * 64]) : -INFINITY;
-      m = fmaxf(m, fmaxf(sc[j], sc[16 + j]));
-    }
-    float l = 0.f;
-#pragma unroll
-    for (int dd = 0; dd < 64; ++dd) t64[dd] = 0.f;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      if (sc[j] != -INFINITY) {
-        const float p = __expf(sc[j] - m);
+          for (int d = 0; d < 16; ++d) o[d] *= a;
+          m = sc;
+        }
+        const float p = __expf(sc - m);
         l += p;
-        const float* vr = j < 16 ? &sVp[j * 64] : &sV[grp][(j - 16) * 64];
+        ld16(vr + 16 * s, kv);
 #pragma unroll
-        for (int dd = 0; dd < 64; ++dd) t64[dd] = fmaf(p, vr[dd], t64[dd]);
+        for (int d = 0; d < 16; ++d) o[d] = fmaf(p, kv[d], o[d]);
       }
-    }
-    if (qok) {
+    };
+    for (int j = 0; j < pre; ++j) key(sKp + j * 64, sVp + j * 64, true);
+    for (int j = 0; j < n; ++j) key(sk + j * 64, sv + j * 64, j <= rr && j >= first);
+    if (r < n) {
       const float inv = 1.0f / l;
 #pragma unroll
-      for (int dd = 0; dd < 64; ++dd) t64[dd] *= inv;
-      store_row64<T>(out + row * ldo + h * 64, t64);
-      if (lse) lse[row * H + h] = m + __logf(l);
+      for (int d = 0; d < 16; ++d) o[d] *= inv;
+      st16(out + row * ldo + h * 64 + 16 * s, o);
+      if (lse && s == 0) lse[row * H + h] = m + __logf(l);
     }
-    __syncthreads();  // sK/sV reused by the next 4 tiles
+    lds_sync();  // this unit's sK / sV reads done before the next unit's writes (program order)
   }
 }
 
-template <typename T, typename TG>
-__global__ __launch_bounds__(64) void attn_prefix_bwd_valu(
+// Backward per unit: phase 1 (lane = query): P, dS over the prefix + own keys, dQ; P / dS kept in
+// LDS ([16 queries][16 prefix | 16 own keys], zero where masked). Phase 2 (lane = own key):
+// dK, dV over the unit's queries (the prefix unit's own keys ARE the prefix rows: accumulated).
+// Phase 3 (lane = prefix key): the prefix rows' dK, dV partial of this unit, accumulated over
+// the chunk in registers and written once per chunk (prefix_kv_reduce sums the chunks).
+__global__ __launch_bounds__(kF32Wpb * 64) void attn_prefix_bwd_f32(
     int G, int P, int R, int ntiles, const int* __restrict__ tiles, const int* __restrict__ row_first, int H,
-    int nchunk, const T* __restrict__ qkv, int ldq, const T* __restrict__ o_fwd, int ldof,
-    const TG* __restrict__ dout, int lddo, const float* __restrict__ lse, TG* __restrict__ dqkv, int lddq,
+    int nchunk, const float* __restrict__ qkv, int ldq, const float* __restrict__ o_fwd, int ldof,
+    const float* __restrict__ dout, int lddo, const float* __restrict__ lse, float* __restrict__ dqkv, int lddq,
     float* __restrict__ part) {
-  __shared__ CLIPK_LDS_ALIGN float sKp[16 * 64];
-  __shared__ CLIPK_LDS_ALIGN float sVp[16 * 64];
-  __shared__ CLIPK_LDS_ALIGN float sQ[4][16 * 64];   // scaled q
-  __shared__ CLIPK_LDS_ALIGN float sK[4][16 * 64];
-  __shared__ CLIPK_LDS_ALIGN float sV[4][16 * 64];
-  __shared__ CLIPK_LDS_ALIGN float sdO[4][16 * 64];
-  __shared__ CLIPK_LDS_ALIGN float sAk[4][16 * 64];  // prefix dK accumulators, per lane group
-  __shared__ CLIPK_LDS_ALIGN float sAv[4][16 * 64];
-  __shared__ float slse[4][16], sD[4][16];
-  __shared__ int sfirst[4][16];
-  const int lane = threadIdx.x, grp = lane >> 4, r16 = lane & 15;
-  const int wid = blockIdx.x;
-  const int h = wid % H, k = (wid / H) % nchunk, g = wid / (H * nchunk);
+  __shared__ CLIPK_LDS_ALIGN float sKp[16 * 64], sVp[16 * 64];
+  __shared__ CLIPK_LDS_ALIGN float sA[kF32Wpb][16 * 64], sB[kF32Wpb][16 * 64];  // K|V, then Q|dO
+  __shared__ CLIPK_LDS_ALIGN float sP[kF32Wpb][16 * 32], sS[kF32Wpb][16 * 32];
+  int g, h, k, w;
+  f32_block(H, nchunk, g, h, k, w);
   const int W = H * 64;
-  stage_prefix_f32<T>(qkv, g * R, P, ldq, h * 64, W, lane, sKp, sVp);
-  for (int i = lane; i < 4 * 16 * 64; i += 64) {
-    (&sAk[0][0])[i] = 0.f;
-    (&sAv[0][0])[i] = 0.f;
-  }
+  f32_stage_prefix(qkv, (size_t)g * R, P, ldq, h * 64, W, sKp, sVp);
+  __syncthreads();
+  if (k >= nchunk) return;
+  const int lane = threadIdx.x & 63, r = lane >> 2, s = lane & 3;
+  float* sa = sA[w];
+  float* sb = sB[w];
+  float* sp = sP[w];
+  float* ss = sS[w];
+  float akp[16], avp[16];  // prefix row r's dK / dV slice, summed over the chunk
+#pragma unroll
+  for (int d = 0; d < 16; ++d) { akp[d] = 0.f; avp[d] = 0.f; }
   const int u_end = min((k + 1) * kValuChunk, ntiles + 1);
-  for (int base = k * kValuChunk; base < u_end; base += 4) {
-    const int u = base + grp;
-    const bool active = u < u_end;
-    int t0 = 0, n = 1, pre = 0, first = 0;
-    if (active) valu_unit(tiles, row_first, P, u, r16, t0, n, pre, first);
-    const bool qok = active && r16 < n;
-    const size_t row = (size_t)g * R + t0 + min(r16, n - 1);
-    const T* qp = qkv + row * ldq + h * 64;
-    float a[64], dO[64];
-    load_row64<T>(qp, a);
+  for (int u = k * kValuChunk; u < u_end; ++u) {
+    int t0, n, pre, rr, first;
+    f32_unit(tiles, row_first, P, u, r, t0, n, pre, rr, first);
+    const bool qok = r < n;
+    const size_t row = (size_t)g * R + t0 + rr;
+    const float* qp = qkv + row * ldq + h * 64 + 16 * s;
+    float q[16], dO[16], t[16];
+    ld16(qp, q);
 #pragma unroll
-    for (int dd = 0; dd < 64; ++dd) sQ[grp][r16 * 64 + dd] = a[dd] * kScale;
-    load_row64<T>(qp + W, a);
+    for (int d = 0; d < 16; ++d) q[d] *= kScale;
+    ld16(dout + row * lddo + h * 64 + 16 * s, dO);
+    ld16(o_fwd + row * ldof + h * 64 + 16 * s, t);
+    const float Di = quad_sum(dot16(dO, t));
+    const float li = lse[row * H + h];
+    ld16(qp + W, t);
+    st16(sa + r * 64 + 16 * s, t);
+    ld16(qp + 2 * W, t);
+    st16(sb + r * 64 + 16 * s, t);
+    lds_sync();
+    // phase 1: lane = query row rr
+    float dq[16];
 #pragma unroll
-    for (int dd = 0; dd < 64; ++dd) sK[grp][r16 * 64 + dd] = a[dd];
-    load_row64<T>(qp + 2 * W, a);
+    for (int d = 0; d < 16; ++d) dq[d] = 0.f;
+    auto key = [&](const float* kr, const float* vr, bool ok, int col) {
+      float kv[16], vv[16];
+      ld16(kr + 16 * s, kv);
+      ld16(vr + 16 * s, vv);
+      const float sc = quad_sum(dot16(q, kv));
+      const float dp = quad_sum(dot16(dO, vv));
+      const float p = ok ? __expf(sc - li) : 0.f;
+      const float ds = p * (dp - Di);
 #pragma unroll
-    for (int dd = 0; dd < 64; ++dd) sV[grp][r16 * 64 + dd] = a[dd];
-    load_row64<TG>(dout + row * lddo + h * 64, dO);
-    load_row64<T>(o_fwd + row * ldof + h * 64, a);
-    const float Di = qok ? dot64(dO, a) : 0.f;
-#pragma unroll
-    for (int dd = 0; dd < 64; ++dd) sdO[grp][r16 * 64 + dd] = qok ? dO[dd] : 0.f;
-    const float li = qok ? lse[row * H + h] : 0.f;
-    slse[grp][r16] = li;
-    sD[grp][r16] = Di;
-    sfirst[grp][r16] = first;
-    __syncthreads();
-    // phase 1 (lane = query): dq = sum_j P (dP - D) k_j / 8 over prefix + own keys
-    {
-      const float* qi = &sQ[grp][r16 * 64];
-#pragma unroll
-      for (int dd = 0; dd < 64; ++dd) a[dd] = 0.f;
-      for (int j = 0; j < 32; ++j) {
-        const bool ok = j < 16 ? j < pre : (j - 16 <= r16 && j - 16 >= first);
-        if (!qok || !ok) continue;
-        const float* kr = j < 16 ? &sKp[j * 64] : &sK[grp][(j - 16) * 64];
-        const float* vr = j < 16 ? &sVp[j * 64] : &sV[grp][(j - 16) * 64];
-        const float p = __expf(dot64(qi, kr) - li);
-        const float ds = p * (dot64(dO, vr) - Di);
-#pragma unroll
-        for (int dd = 0; dd < 64; ++dd) a[dd] = fmaf(ds, kr[dd], a[dd]);
+      for (int d = 0; d < 16; ++d) dq[d] = fmaf(ds, kv[d], dq[d]);
+      if (s == 0) {
+        sp[r * 32 + col] = p;
+        ss[r * 32 + col] = ds;
       }
-      if (qok) {
+    };
+    for (int j = 0; j < pre; ++j) key(sKp + j * 64, sVp + j * 64, qok, j);
+    for (int j = 0; j < n; ++j) key(sa + j * 64, sb + j * 64, qok && j <= rr && j >= first, 16 + j);
+    if (qok) {
 #pragma unroll
-        for (int dd = 0; dd < 64; ++dd) a[dd] *= kScale;
-        store_row64<TG>(dqkv + row * lddq + h * 64, a);
-      }
+      for (int d = 0; d < 16; ++d) dq[d] *= kScale;
+      st16(dqkv + row * lddq + h * 64 + 16 * s, dq);
     }
-    // phase 2 (lane = own key j = r16): over the queries i >= j of the same class
-    {
-      const float* kj = &sK[grp][r16 * 64];
-      const float* vj = &sV[grp][r16 * 64];
-      float dk[64], dv[64];
-#pragma unroll
-      for (int dd = 0; dd < 64; ++dd) { dk[dd] = 0.f; dv[dd] = 0.f; }
-      for (int i = r16; i < n; ++i) {
-        if (sfirst[grp][i] > r16) break;  // past this key's class
-        const float* qr = &sQ[grp][i * 64];
-        const float* dr = &sdO[grp][i * 64];
-        const float p = __expf(dot64(qr, kj) - slse[grp][i]);
-        const float ds = p * (dot64(dr, vj) - sD[grp][i]);
-#pragma unroll
-        for (int dd = 0; dd < 64; ++dd) {
-          dv[dd] = fmaf(p, dr[dd], dv[dd]);
-          dk[dd] = fmaf(ds, qr[dd], dk[dd]);
-        }
-      }
-      if (qok) {
-        if (u == 0) {  // the prefix tile's own keys are the prefix rows: accumulate
-#pragma unroll
-          for (int dd = 0; dd < 64; ++dd) {
-            sAk[grp][r16 * 64 + dd] += dk[dd];
-            sAv[grp][r16 * 64 + dd] += dv[dd];
-          }
-        } else {
-          store_row64<TG>(dqkv + row * lddq + W + h * 64, dk);
-          store_row64<TG>(dqkv + row * lddq + 2 * W + h * 64, dv);
-        }
-      }
-    }
-    // phase 3 (lane = prefix key j = r16): partial over every query of this tile
-    if (active && r16 < pre) {
-      const float* kj = &sKp[r16 * 64];
-      const float* vj = &sVp[r16 * 64];
-      float dk[64], dv[64];
-#pragma unroll
-      for (int dd = 0; dd < 64; ++dd) { dk[dd] = 0.f; dv[dd] = 0.f; }
+    // sA / sB: the unit's scaled q and dO rows for the key phases (after every lane's phase-1
+    // reads of K / V: program order)
+    st16(sa + r * 64 + 16 * s, q);
+    st16(sb + r * 64 + 16 * s, dO);
+    lds_sync();
+    // phases 2 / 3: lane = key; sum over the unit's queries i of dS[i][key] q_i, P[i][key] dO_i
+    auto keysum = [&](int col, float* dk, float* dv) {
       for (int i = 0; i < n; ++i) {
-        const float* qr = &sQ[grp][i * 64];
-        const float* dr = &sdO[grp][i * 64];
-        const float p = __expf(dot64(qr, kj) - slse[grp][i]);
-        const float ds = p * (dot64(dr, vj) - sD[grp][i]);
+        const float pv = sp[i * 32 + col], dsv = ss[i * 32 + col];
+        float a[16], b[16];
+        ld16(sa + i * 64 + 16 * s, a);
+        ld16(sb + i * 64 + 16 * s, b);
 #pragma unroll
-        for (int dd = 0; dd < 64; ++dd) {
-          dv[dd] = fmaf(p, dr[dd], dv[dd]);
-          dk[dd] = fmaf(ds, qr[dd], dk[dd]);
+        for (int d = 0; d < 16; ++d) {
+          dk[d] = fmaf(dsv, a[d], dk[d]);
+          dv[d] = fmaf(pv, b[d], dv[d]);
         }
       }
+    };
+    if (u == 0) {  // the prefix unit: its own keys are the prefix rows
+      keysum(16 + r, akp, avp);
+    } else {
+      float dk[16], dv[16];
 #pragma unroll
-      for (int dd = 0; dd < 64; ++dd) {
-        sAk[grp][r16 * 64 + dd] += dk[dd];
-        sAv[grp][r16 * 64 + dd] += dv[dd];
+      for (int d = 0; d < 16; ++d) { dk[d] = 0.f; dv[d] = 0.f; }
+      keysum(16 + r, dk, dv);
+      if (qok) {
+        st16(dqkv + row * lddq + W + h * 64 + 16 * s, dk);
+        st16(dqkv + row * lddq + 2 * W + h * 64 + 16 * s, dv);
       }
+      keysum(r, akp, avp);  // prefix key r (zero columns past pre)
     }
-    __syncthreads();  // staging buffers reused by the next 4 tiles
+    lds_sync();
   }
-  float* pb = part + ((size_t)g * nchunk + k) * 16 * (2 * W);
-  for (int idx = lane; idx < P * 64; idx += 64) {
-    const int j = idx >> 6, dd = idx & 63;
-    const int o = j * 64 + dd;
-    pb[(size_t)j * 2 * W + h * 64 + dd] = ((sAk[0][o] + sAk[1][o]) + sAk[2][o]) + sAk[3][o];
-    pb[(size_t)j * 2 * W + W + h * 64 + dd] = ((sAv[0][o] + sAv[1][o]) + sAv[2][o]) + sAv[3][o];
+  if (r < P) {
+    // (dK = sum dS q with q already scaled: no further factor)
+    float* pb = part + (((size_t)g * nchunk + k) * 16 + r) * (2 * W) + h * 64 + 16 * s;
+    st16(pb, akp);
+    st16(pb + W, avp);
   }
 }
 
@@ -1089,9 +1100,9 @@ static int prefix_fwd(int G, int P, int R, int ntiles, const int* tiles, const i
     }
   } else {
     const int nchunk = n_chunks(ntiles, kValuChunk);
-    const long waves = (long)G * nchunk * H;
-    hipLaunchKernelGGL((attn_prefix_fwd_valu<T>), dim3(waves), dim3(64), 0, st, G, P, R, ntiles, tiles,
-                       row_first, H, nchunk, (const T*)qkv, ldq, (T*)out, ldo, lse);
+    const long blocks = (long)G * ((nchunk + kF32Wpb - 1) / kF32Wpb) * H;
+    hipLaunchKernelGGL(attn_prefix_fwd_f32, dim3(blocks), dim3(64 * kF32Wpb), 0, st, G, P, R, ntiles, tiles,
+                       row_first, H, nchunk, (const float*)qkv, ldq, (float*)out, ldo, lse);
   }
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
@@ -1137,9 +1148,11 @@ static int prefix_bwd(int G, int P, int R, int ntiles, const int* tiles, const i
       else go(attn_prefix_bwd_mfma<T, TG, 2>);
     }
   } else {
-    hipLaunchKernelGGL((attn_prefix_bwd_valu<T, TG>), dim3(waves), dim3(64), 0, st, G, P, R, ntiles, tiles,
-                       row_first, H, nchunk, (const T*)qkv, ldq, (const T*)ofwd, ldof, (const TG*)dout, lddo,
-                       lse, (TG*)dqkv, lddq, part);
+    static_assert(mfma || (sizeof(T) == 4 && sizeof(TG) == 4), "fp32 backward");
+    const long blocks = (long)G * ((nchunk + kF32Wpb - 1) / kF32Wpb) * H;
+    hipLaunchKernelGGL(attn_prefix_bwd_f32, dim3(blocks), dim3(64 * kF32Wpb), 0, st, G, P, R, ntiles, tiles,
+                       row_first, H, nchunk, (const float*)qkv, ldq, (const float*)ofwd, ldof, (const float*)dout,
+                       lddo, lse, (float*)dqkv, lddq, part);
   }
   CLIPK_CHECK_LAUNCH();
   const int W = H * 64;

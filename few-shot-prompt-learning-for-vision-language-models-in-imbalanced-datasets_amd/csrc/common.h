@@ -20,10 +20,15 @@ namespace clipk {
 
 constexpr int kWave = 64;
 
+// GEMM input tag of the split-fp16 fp32-class path (CLIPK_F32S): A fp32, B split-packed
+// (clipk_split_pack); 4 bytes per element on both operands.
+struct f32s { float v; };
+
 template <typename T> struct DT;
 template <> struct DT<float> { static constexpr int id = CLIPK_F32; };
 template <> struct DT<f16>   { static constexpr int id = CLIPK_F16; };
 template <> struct DT<bf16>  { static constexpr int id = CLIPK_BF16; };
+template <> struct DT<f32s>  { static constexpr int id = CLIPK_F32S; };
 
 __device__ __forceinline__ float to_f32(float x) { return x; }
 __device__ __forceinline__ float to_f32(f16 x) { return (float)x; }

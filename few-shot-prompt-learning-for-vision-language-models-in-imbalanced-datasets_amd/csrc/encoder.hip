@@ -39,11 +39,24 @@ struct clipk_encoder {
   int prefix_input = 0;
   // clipk_encoder_set_ln_fold: per layer {W_in', s_in, c_in, W_fc', s_fc, c_fc} (empty: off)
   std::vector<std::array<const void*, 6>> fold;
+  // clipk_encoder_set_split: PREC fp32s -- fp32 activations, every GEMM weight split-packed
+  // (clipk_split_pack) and every GEMM on the split-fp16 MFMA path (CLIPK_F32S)
+  int split = 0;
 };
 
 namespace clipk {
 
-static inline size_t esize(int dt) { return dt == CLIPK_F32 ? 4 : 2; }
+static inline size_t esize(int dt) { return (dt == CLIPK_F32 || dt == CLIPK_F32S) ? 4 : 2; }
+
+// PREC fp32s: while an encoder call of a split encoder runs, its fp32 GEMMs take the split-packed
+// weights (CLIPK_F32S). Set per call (RAII, per host thread) by the entry points below, so the
+// shared layer-loop code keeps passing the activation dtype.
+static thread_local int t_split = 0;
+struct SplitScope {
+  int prev;
+  explicit SplitScope(const clipk_encoder* e) : prev(t_split) { t_split = e->split; }
+  ~SplitScope() { t_split = prev; }
+};
 static inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
 // Residual stream dtype of the TEXT encoder: the 16-bit activation dtype under PREC
@@ -141,6 +154,7 @@ static double gemm_bytes(int in, int out, int epi, int M, int N, int K, bool has
 static int gemm(int in, int out, int epi, int M, int N, int K, const void* A, const void* B,
                 const float* bias, const void* res, void* o, void* o2, const void* aux, int auxdt,
                 hipStream_t st, int prof_cls, void* sk = nullptr, size_t skb = 0, const char* site = nullptr) {
+  if (t_split && in == CLIPK_F32) in = CLIPK_F32S;
   ProfScope ps(prof_cls, st, 2.0 * M * N * K, site,
                site ? gemm_bytes(in, out, epi, M, N, K, o2 != nullptr, auxdt) : 0.0);
   if (sk && epi != CLIPK_EPI_DQGELU)
@@ -229,9 +243,12 @@ static TextBufs text_layout(const clipk_encoder* e, size_t rows, int nout, void*
   return t;
 }
 
+constexpr int kAmaxBlocks = 256;  // partial maxima of the fp32s gradient-scale reduction
+
 struct TextBwdBufs {
   void *dtg, *dX_lp, *dh, *do_, *dqkv, *dxn;  // dxn: LN-output grads in the grad dtype
   float* dlnf;
+  float* gscale;  // PREC fp32s: the backward's gradient scale s and 1 / s (+ amax partials)
   void* part;  // shared-prefix attention: per-chunk prefix dK/dV partials
   size_t bytes;
 };
@@ -249,8 +266,57 @@ static TextBwdBufs text_bwd_layout(const clipk_encoder* e, size_t rows, int nout
   b.do_ = c.take(rows * W * g);
   b.dqkv = c.take(rows * 3 * W * g);
   b.part = part_bytes ? c.take(part_bytes) : nullptr;
+  b.gscale = (float*)c.take((2 + kAmaxBlocks) * sizeof(float));
   b.bytes = c.off;
   return b;
+}
+
+// ---- PREC fp32s gradient scaling. The split-fp16 GEMMs keep ~22 bits of an operand only while
+// its values sit in fp16's normal range (|x| >= 2^-2 for the lo part); gradients here are
+// ~1e-4-sized. The text backward is linear in dtxt, so it runs on s * dtxt with s a power of
+// two putting max |dtxt| in [64, 128) (1/512 of the fp16 maximum: headroom for growth through
+// the layers), and the results are multiplied by 1 / s at the end -- both exact.
+__global__ __launch_bounds__(256) void amax_partial_kernel(long n, const float* __restrict__ x,
+                                                           float* __restrict__ part) {
+  __shared__ float sm[4];
+  float m = 0.f;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) m = fmaxf(m, fabsf(x[i]));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+}
+// sc[0] = s, sc[1] = 1 / s from the partial maxima sc[2 ..]
+__global__ __launch_bounds__(64) void grad_scale_pick_kernel(int nparts, float* __restrict__ sc) {
+  float m = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += 64) m = fmaxf(m, sc[2 + i]);
+  m = wave_max(m);
+  if (threadIdx.x == 0) {
+    int ex = 0;
+    if (m > 0.f && m < INFINITY) (void)frexpf(m, &ex);  // m = f 2^ex, f in [0.5, 1)
+    const int k = min(max(7 - ex, -120), 120);           // m * 2^k in [64, 128)
+    sc[0] = ldexpf(1.0f, k);
+    sc[1] = ldexpf(1.0f, -k);
+  }
+}
+__global__ __launch_bounds__(256) void scale_by_kernel(long n, const float* __restrict__ x, float* __restrict__ y,
+                                                       const float* __restrict__ sc, int which) {
+  const float s = sc[which];
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) y[i] = x[i] * s;
+}
+static int grad_scale_in(const clipk_encoder*, long n, const float* x, float* y, float* sc, hipStream_t st) {
+  hipLaunchKernelGGL(amax_partial_kernel, dim3(kAmaxBlocks), dim3(256), 0, st, n, x, sc + 2);
+  hipLaunchKernelGGL(grad_scale_pick_kernel, dim3(1), dim3(64), 0, st, kAmaxBlocks, sc);
+  hipLaunchKernelGGL(scale_by_kernel, dim3((unsigned)std::min<long>((n + 255) / 256, 4096)), dim3(256), 0, st, n, x, y,
+                     (const float*)sc, 0);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+static int grad_scale_out(long n, float* x, const float* sc, hipStream_t st) {
+  hipLaunchKernelGGL(scale_by_kernel, dim3((unsigned)std::min<long>((n + 255) / 256, 8192)), dim3(256), 0, st, n, x, x,
+                     sc, 1);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
 }
 
 // Row structure of one encoder call: nseq plain sequences of length L (vision, unpacked
@@ -540,8 +606,10 @@ static bool ln_fold_on(const clipk_encoder* e, const EncIO& io) {
     const char* s = getenv("CLIPK_TEXT_LNFOLD");
     v = s ? atoi(s) : 1;
   }
+  // clipk_ln_stats_merge covers widths that are multiples of 128 up to 1024; wider encoders run
+  // the LayerNorm passes
   return v != 0 && (int)e->fold.size() == e->layers && e->act != CLIPK_F32 && io.rd == e->act &&
-         !(e->deep.n_deep > 0 && e->deep.prompts) && !a_qgelu_on();
+         e->W % 128 == 0 && e->W <= 1024 && !(e->deep.n_deep > 0 && e->deep.prompts) && !a_qgelu_on();
 }
 
 // deep prompts of layer l (1..n_deep) into the layer's input rows
@@ -638,6 +706,7 @@ static int block_attn_shared0(const clipk_encoder* e, const std::array<const voi
 static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const float* x0, const int* eot_rows,
                              float* txt, void* saved, size_t saved_bytes, void* ws, size_t ws_bytes,
                              hipStream_t st, const EncIO& io) {
+  SplitScope split_scope(e);
   const bool save = saved != nullptr;
   TextBufs t = text_layout(e, sh.rows, sh.nout, saved, ws, save, io.rd);
   if (ws_bytes < t.ws_bytes || (save && saved_bytes < t.saved_bytes)) return CLIPK_EWORKSPACE;
@@ -727,6 +796,7 @@ static bool text_dres16(const clipk_encoder* e) {
 static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const int* eot_rows,
                               const float* dtxt, const void* saved, size_t saved_bytes, float* dx0,
                               void* ws, size_t ws_bytes, hipStream_t st, const EncIO& io) {
+  SplitScope split_scope(e);
   TextBufs t = text_layout(e, sh.rows, sh.nout, const_cast<void*>(saved), nullptr, true, io.rd);
   TextBwdBufs b = text_bwd_layout(e, sh.rows, sh.nout, sh.part_bytes(e->heads), ws);
   if (saved_bytes < t.saved_bytes || ws_bytes < b.bytes) return CLIPK_EWORKSPACE;
@@ -734,7 +804,12 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
   const int pg = io.text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE;
   float* dX = dx0;
   // d lnf = dtxt . P^T   (txt = lnf @ P, P = projection [W,E])
-  TRY(clipk_cast(gd, (long)nout * e->E, dtxt, b.dtg, st));
+  if (e->split) {
+    // PREC fp32s: the whole backward runs on s * dtxt (grad_scale_pick), unscaled at the end
+    TRY(grad_scale_in(e, (long)nout * e->E, dtxt, (float*)b.dtg, b.gscale, st));
+  } else {
+    TRY(clipk_cast(gd, (long)nout * e->E, dtxt, b.dtg, st));
+  }
   TRY(gemm(gd, CLIPK_F32, CLIPK_EPI_NONE, nout, W, e->E, b.dtg, io.proj_b, nullptr, nullptr, b.dlnf,
            nullptr, nullptr, 0, st, pg));
   // the ViT's residual stream is fp32: its gradient stays fp32 too
@@ -834,6 +909,12 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
         TRY(clipk_rows_collect(CLIPK_F32, d.n_ctx, d.n_per, W, dX, W, b.dX_lp, gd, W, d.rows,
                                d.grads + (size_t)(l - 1) * d.n_ctx * W, 0, 1, st));
     }
+  }
+  if (e->split) {
+    // undo the gradient scale (exact: a power of two) on everything this backward returned
+    TRY(grad_scale_out((long)rows * W, dX, b.gscale, st));
+    const DeepPrompts& d = e->deep;
+    if (d.n_deep > 0 && d.grads) TRY(grad_scale_out((long)d.n_deep * d.n_ctx * W, d.grads, b.gscale, st));
   }
   return CLIPK_OK;
 }
@@ -973,6 +1054,7 @@ extern "C" int clipk_vit_forward(const clipk_encoder* e, int B, const float* img
   if (!e || e->kind != 1 || !img || !feat || !ws) return CLIPK_EINVAL;
   if (B <= 0) return CLIPK_ESHAPE;
   if (vit_res16(e)) return vit16_forward(e, B, img, feat, ws, ws_bytes, (hipStream_t)stream);
+  SplitScope split_scope(e);
   VitBufs v = vit_layout(e, B, ws);
   if (ws_bytes < v.bytes) return CLIPK_EWORKSPACE;
   hipStream_t st = (hipStream_t)stream;
@@ -1142,6 +1224,13 @@ extern "C" int clipk_encoder_set_ln_fold(clipk_encoder* e, const void* const* fo
   return CLIPK_OK;
 }
 
+extern "C" int clipk_encoder_set_split(clipk_encoder* e, int on) {
+  if (!e || (on != 0 && on != 1)) return CLIPK_EINVAL;
+  if (on && (e->act != CLIPK_F32 || e->grad != CLIPK_F32)) return CLIPK_EDTYPE;
+  e->split = on;
+  return CLIPK_OK;
+}
+
 extern "C" int clipk_encoder_set_deep_prompts(clipk_encoder* e, int n_deep, int n_ctx, int n_per, const int* rows,
                                               const float* prompts, float* grads) {
   if (!e) return CLIPK_EINVAL;
@@ -1170,6 +1259,7 @@ extern "C" int clipk_vit_forward_prompted(const clipk_encoder* e, int B, const f
                                           size_t ws_bytes, void* stream) {
   if (!e || e->kind != 1 || !img || !feat || !ws || (n_vpt > 0 && !vpt)) return CLIPK_EINVAL;
   if (B <= 0 || n_vpt < 0) return CLIPK_ESHAPE;
+  SplitScope split_scope(e);
   VitPBufs v = vitp_layout(e, B, n_vpt, ws);
   if (ws_bytes < v.bytes) return CLIPK_EWORKSPACE;
   hipStream_t st = (hipStream_t)stream;

@@ -90,6 +90,32 @@ __device__ __forceinline__ f32x4 mma(u32x4 a, u32x4 b, f32x4 c) {
   }
 }
 
+// ---- PREC fp32s (CLIPK_F32S): fp32-class products on the 16-bit MFMA.
+// 8 fp32 values (a lane's two 16-B fragment chunks, k = 8 fq .. 8 fq + 7) -> fp16 hi = fp16(x)
+// and lo = fp16(x - hi): hi + lo carries ~22 significant bits of x.
+__device__ __forceinline__ void split8(u32x4 a0, u32x4 a1, u32x4& hi, u32x4& lo) {
+  const f32x4 x0 = __builtin_bit_cast(f32x4, a0), x1 = __builtin_bit_cast(f32x4, a1);
+  f16x8 h, l;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    h[c] = (f16)x0[c];
+    h[4 + c] = (f16)x1[c];
+    l[c] = (f16)(x0[c] - (float)h[c]);
+    l[4 + c] = (f16)(x1[c] - (float)h[4 + c]);
+  }
+  hi = __builtin_bit_cast(u32x4, h);
+  lo = __builtin_bit_cast(u32x4, l);
+}
+// a . b ~= hi(a) hi(b) + hi(a) lo(b) + lo(a) hi(b) (lo . lo ~ 2^-22 relative is dropped); the
+// weight's parts (packed, clipk_split_pack) are the instruction's A operand (swapped operands)
+__device__ __forceinline__ f32x4 mma_split(u32x4 bh, u32x4 bl, u32x4 ah, u32x4 al, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, bl), __builtin_bit_cast(f16x8, ah), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, bh), __builtin_bit_cast(f16x8, al), c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, bh), __builtin_bit_cast(f16x8, ah), c, 0,
+                                                0, 0);
+}
+constexpr float kSplitAlpha = 1.0f / CLIPK_SPLIT_SCALE;  // the packed weights' scale, undone
+
 __device__ __forceinline__ void glds16(const char* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(
       (const __attribute__((address_space(1))) void*)src,
@@ -275,8 +301,12 @@ template <typename T, typename TO, typename TX, int EPI, int BM, int BN, int WM,
 __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
   static_assert(DEPTH == 2 || !PERSIST, "deep ring: non-persistent launches only");
   static_assert(!AG || (!PERSIST && DEPTH == 2 && sizeof(T) == 2 && ROWB == 128), "A-operand QuickGELU path");
+  // PREC fp32s: 4-byte elements (A fp32, B split-packed), staged as fp32; a 128-B K step is
+  // one 32-deep k-window read as two 16-B chunks per fragment (2 fq, 2 fq + 1), 3 MFMAs each
+  constexpr bool SPLIT = __is_same(T, f32s);
+  static_assert(!SPLIT || (ROWB == 128 && !AG), "split-fp16 GEMM: 128-B staged rows");
   static_assert(!PP || (PERSIST && !AG && DEPTH == 2 && ROWB == 128 && WM == 2 && WN == 4 && BN == 256 &&
-                        sizeof(T) == 2 && BM % 64 == 0), "ping-pong main loop (K >= 128)");
+                        (sizeof(T) == 2 || SPLIT) && BM % 64 == 0), "ping-pong main loop (K >= 128)");
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int OPA = BM * ROWB, OPB = BN * ROWB, STAGE = OPA + OPB;
@@ -549,7 +579,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
           for (int i = 0; i < TM2; ++i)
-            fa[kk][i] = *reinterpret_cast<const u32x4*>(As + i * 16 * ROWB + ((kk * 4 + fq) ^ sw) * 16);
+            fa[kk][i] = *reinterpret_cast<const u32x4*>(As + i * 16 * ROWB + (((SPLIT ? 2 * fq + kk : kk * 4 + fq)) ^ sw) * 16);
       };
       auto rd_b = [&](int buf, int q) {
         const char* Bs = smem + buf * STAGE + OPA + (wn * (BN / WN) + q * (BN / WN / 2) + fr) * ROWB;
@@ -557,11 +587,23 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
           for (int j = 0; j < TN2; ++j)
-            fbs[NFB == 2 ? q : 0][kk][j] = *reinterpret_cast<const u32x4*>(Bs + j * 16 * ROWB + ((kk * 4 + fq) ^ sw) * 16);
+            fbs[NFB == 2 ? q : 0][kk][j] =
+                *reinterpret_cast<const u32x4*>(Bs + j * 16 * ROWB + (((SPLIT ? 2 * fq + kk : kk * 4 + fq)) ^ sw) * 16);
       };
       auto mm = [&](int h, int q) {
         if (CLIPK_GEMM_NOMMA) return;
         if (CLIPK_GEMM_PRIO == 1) __builtin_amdgcn_s_setprio(1);
+        if constexpr (SPLIT) {
+#pragma unroll
+          for (int i = 0; i < TM2; ++i) {
+            u32x4 ah, al;
+            split8(fa[0][i], fa[1][i], ah, al);
+#pragma unroll
+            for (int j = 0; j < TN2; ++j)
+              acc[h * TM2 + i][q * TN2 + j] = mma_split(fbs[NFB == 2 ? q : 0][0][j], fbs[NFB == 2 ? q : 0][1][j], ah, al,
+                                                        acc[h * TM2 + i][q * TN2 + j]);
+          }
+        } else {
 #pragma unroll
         for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
@@ -569,6 +611,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
 #pragma unroll
             for (int j = 0; j < TN2; ++j)
               acc[h * TM2 + i][q * TN2 + j] = mma<T>(fbs[NFB == 2 ? q : 0][kk][j], fa[kk][i], acc[h * TM2 + i][q * TN2 + j]);
+        }
         if (CLIPK_GEMM_PRIO == 1) __builtin_amdgcn_s_setprio(0);
       };
       auto seg_end = [&]() {  // memory segment done: fragments in registers, then the barrier
@@ -701,6 +744,23 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       }
       const char* As = smem + cur * STAGE + (wm * (BM / WM) + fr) * ROWB;
       const char* Bs = smem + cur * STAGE + OPA + (wn * (BN / WN) + fr) * ROWB;
+      if constexpr (SPLIT) {
+        const int p0 = ((2 * fq) ^ sw) * 16, p1 = ((2 * fq + 1) ^ sw) * 16;
+        u32x4 bh[TN], bl[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          bh[j] = *reinterpret_cast<const u32x4*>(Bs + j * 16 * ROWB + p0);
+          bl[j] = *reinterpret_cast<const u32x4*>(Bs + j * 16 * ROWB + p1);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          u32x4 ah, al;
+          split8(*reinterpret_cast<const u32x4*>(As + i * 16 * ROWB + p0),
+                 *reinterpret_cast<const u32x4*>(As + i * 16 * ROWB + p1), ah, al);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mma_split(bh[j], bl[j], ah, al, acc[i][j]);
+        }
+      } else
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
         const int p = ((kk * 4 + fq) ^ sw) * 16;
@@ -790,6 +850,10 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
           v[4 * c] = t[0]; v[4 * c + 1] = t[1]; v[4 * c + 2] = t[2]; v[4 * c + 3] = t[3];
         }
         const int off = ((m - m0) * g.ldo + ncol) * (int)sizeof(TO);  // rows >= M: out of range, dropped
+        if constexpr (SPLIT) {
+#pragma unroll
+          for (int c = 0; c < CW; ++c) v[c] *= kSplitAlpha;  // exact (power of 2)
+        }
         if constexpr (LN_IN) {
           const float rs = lnp[i & 1][q][0], nb = lnp[i & 1][q][1];
 #pragma unroll
@@ -961,7 +1025,7 @@ static int num_cus() {
 template <typename T, typename TO, typename TX, int EPI, int BM, int LNM = 0>
 static bool try_pp(const GemmArgs& g, int nwg, hipStream_t st) {
   constexpr bool ext32 = (EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU) && sizeof(TX) == 4;
-  if constexpr (CLIPK_GEMM_PP && sizeof(T) == 2 && !(BM == 256 && ext32)) {
+  if constexpr (CLIPK_GEMM_PP && (sizeof(T) == 2 || __is_same(T, f32s)) && !(BM == 256 && ext32)) {
     if (g.K * (int)sizeof(T) < 2 * GEMM_ROWB) return false;
     hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, BM, 256, 2, 4, true, GEMM_ROWB, 2, false, true, LNM>),
                        dim3(pp_grid(nwg, num_cus())), dim3(512), 0, st, g);
@@ -979,7 +1043,7 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
     g_skew = e ? atoi(e) : 0;
   }
   const_cast<GemmArgs&>(g).skew = g_skew;
-  if constexpr (sizeof(T) == 4) {
+  if constexpr (__is_same(T, float)) {
     const int nwg = ((g.M + 127) / 128) * (g.N / 128);
     hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 2, false, false, LNM>), dim3(nwg), dim3(256), 0, st, g);
   } else {
@@ -1027,6 +1091,67 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
   }
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
+}
+
+// PREC fp32s (CLIPK_F32S) launches: fp32 out / residual / aux. Large M (where the 16-bit policy
+// picks the 192- or 256-row tiles): the ping-pong loop on 192x256 tiles (256-row ones spill at
+// 256 VGPRs with the split's temporaries); otherwise 128x128 tiles (a 4-slot ring when the grid
+// is at most one tile per CU).
+template <int EPI>
+static int launch_gemm_split(const GemmArgs& g, hipStream_t st) {
+  const int cus = num_cus();
+  const_cast<GemmArgs&>(g).stamp = gemm_stamp_buf();
+  const_cast<GemmArgs&>(g).skew = 0;
+  const int cfg = pick_cfg(g.M, g.N, 2);
+  if (cfg == 1 || cfg == 6) {
+    if (try_pp<f32s, float, float, EPI, 192>(g, ((g.M + 191) / 192) * (g.N / 256), st)) {
+      CLIPK_CHECK_LAUNCH();
+      return CLIPK_OK;
+    }
+  }
+  const int nwg = ((g.M + 127) / 128) * (g.N / 128);
+  if (nwg <= cus && deep_small())
+    hipLaunchKernelGGL((gemm_nt_kernel<f32s, float, float, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 4>), dim3(nwg),
+                       dim3(256), 0, st, g);
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<f32s, float, float, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 2>), dim3(nwg),
+                       dim3(256), 0, st, g);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+static int dispatch_split(int out_dtype, int epi, int aux_dtype, const GemmArgs& g, hipStream_t st) {
+  if (out_dtype != CLIPK_F32) return CLIPK_EDTYPE;
+  switch (epi) {
+    case CLIPK_EPI_BIAS: return launch_gemm_split<CLIPK_EPI_BIAS>(g, st);
+    case CLIPK_EPI_BIAS_RES: return launch_gemm_split<CLIPK_EPI_BIAS_RES>(g, st);
+    case CLIPK_EPI_BIAS_QGELU: return launch_gemm_split<CLIPK_EPI_BIAS_QGELU>(g, st);
+    case CLIPK_EPI_DQGELU:
+      return aux_dtype == CLIPK_F32 ? launch_gemm_split<CLIPK_EPI_DQGELU>(g, st) : CLIPK_EDTYPE;
+    case CLIPK_EPI_NONE: return launch_gemm_split<CLIPK_EPI_NONE>(g, st);
+    default: return CLIPK_EINVAL;
+  }
+}
+
+// weight W [N, K] fp32 -> CLIPK_SPLIT_SCALE * W as (hi, lo) fp16 parts, per 8 consecutive k:
+// 8 hi then 8 lo (one thread per 8-element group)
+__global__ __launch_bounds__(256) void split_pack_kernel(int N, int K, const float* __restrict__ W, int ldw,
+                                                         f16* __restrict__ out) {
+  const int kg = K / 8;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)N * kg) return;
+  const int n = (int)(i / kg), g8 = (int)(i % kg);
+  const float* src = W + (size_t)n * ldw + 8 * g8;
+  f16x8 h, l;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const float x = src[c] * CLIPK_SPLIT_SCALE;
+    h[c] = (f16)x;
+    l[c] = (f16)(x - (float)h[c]);
+  }
+  f16x8* dst = reinterpret_cast<f16x8*>(out + ((size_t)n * K + 8 * g8) * 2);
+  dst[0] = h;
+  dst[1] = l;
 }
 
 // CLIPK_A_QGELU launches: non-persistent 2-slot kernels of the tile the shape would get
@@ -1108,9 +1233,9 @@ extern "C" int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, in
   if (!A || !B || !out) return CLIPK_EINVAL;
   const bool ag = (epi & CLIPK_A_QGELU) != 0;
   epi &= ~CLIPK_A_QGELU;
-  if (ag && (in_dtype == CLIPK_F32 || epi != CLIPK_EPI_BIAS_RES)) return CLIPK_EINVAL;
+  if (ag && (in_dtype == CLIPK_F32 || in_dtype == CLIPK_F32S || epi != CLIPK_EPI_BIAS_RES)) return CLIPK_EINVAL;
   if (M <= 0) return M == 0 ? CLIPK_OK : CLIPK_ESHAPE;
-  const int esz = in_dtype == CLIPK_F32 ? 4 : 2;
+  const int esz = (in_dtype == CLIPK_F32 || in_dtype == CLIPK_F32S) ? 4 : 2;
   if (N <= 0 || K <= 0 || N % GEMM_NMIN != 0 || (K * esz) % GEMM_ROWB != 0) return CLIPK_ESHAPE;
   if (lda < K || ldb < K || (lda * esz) % 16 || (ldb * esz) % 16 || ldo < N || ldo % 4)
     return CLIPK_ESHAPE;
@@ -1125,8 +1250,19 @@ extern "C" int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, in
     case CLIPK_F16: return dispatch_out<f16>(out_dtype, epi, aux_dtype, g, st, ag);
     case CLIPK_BF16: return dispatch_out<bf16>(out_dtype, epi, aux_dtype, g, st, ag);
     case CLIPK_F32: return dispatch_out<float>(out_dtype, epi, aux_dtype, g, st);
+    case CLIPK_F32S: return dispatch_split(out_dtype, epi, aux_dtype, g, st);
     default: return CLIPK_EDTYPE;
   }
+}
+
+extern "C" int clipk_split_pack(int N, int K, const float* W, int ldw, void* out, void* stream) {
+  if (!W || !out) return CLIPK_EINVAL;
+  if (N <= 0 || K <= 0 || K % 32 != 0 || ldw < K) return CLIPK_ESHAPE;
+  const long n = (long)N * (K / 8);
+  hipLaunchKernelGGL(split_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, N, K, W,
+                     ldw, (f16*)out);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
 }
 
 namespace clipk {
@@ -1210,7 +1346,7 @@ static int auto_splits(int M, int N, int K, int esz) {
 }  // namespace clipk
 
 extern "C" int clipk_gemm_auto_splits(int in_dtype, int M, int N, int K) {
-  return auto_splits(M, N, K, in_dtype == CLIPK_F32 ? 4 : 2);
+  return auto_splits(M, N, K, (in_dtype == CLIPK_F32 || in_dtype == CLIPK_F32S) ? 4 : 2);
 }
 
 extern "C" size_t clipk_gemm_splitk_ws_bytes(int M, int N, int splits) {
@@ -1232,7 +1368,7 @@ extern "C" int clipk_gemm_splitk(int in_dtype, int out_dtype, int epi, int M, in
                                  const float* bias, const void* res, int ldr,
                                  void* out, int ldo, void* out2, int splits, void* ws, size_t ws_bytes,
                                  void* stream) {
-  const int esz = in_dtype == CLIPK_F32 ? 4 : 2;
+  const int esz = (in_dtype == CLIPK_F32 || in_dtype == CLIPK_F32S) ? 4 : 2;
   if (splits <= 0) splits = auto_splits(M, N, K, esz);
   if (splits <= 1 || M <= 0)
     return clipk_gemm(in_dtype, out_dtype, epi, M, N, K, A, lda, B, ldb, bias, res, ldr, out, ldo, out2,
@@ -1262,6 +1398,10 @@ extern "C" int clipk_gemm_splitk(int in_dtype, int out_dtype, int epi, int M, in
       break;
     case CLIPK_F32:
       hipLaunchKernelGGL((gemm_nt_kernel<float, float, float, CLIPK_EPI_NONE, 128, 128, 2, 2, false>), dim3(nwg),
+                         dim3(256), 0, st, p);
+      break;
+    case CLIPK_F32S:  // slice partials already carry the 1 / CLIPK_SPLIT_SCALE (EPI_NONE epilogue)
+      hipLaunchKernelGGL((gemm_nt_kernel<f32s, float, float, CLIPK_EPI_NONE, 128, 128, 2, 2, false>), dim3(nwg),
                          dim3(256), 0, st, p);
       break;
     default: return CLIPK_EDTYPE;

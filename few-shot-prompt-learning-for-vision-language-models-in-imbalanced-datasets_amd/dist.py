@@ -40,10 +40,13 @@ def world_size() -> int:
 
 
 def init_from_env(backend: str | None = None) -> int:
-    """Initialise from torchrun env (RANK/WORLD_SIZE/MASTER_*). Returns local rank."""
+    """Initialise from torchrun env (RANK/WORLD_SIZE/MASTER_*). Returns local rank. A
+    1-rank torchrun launch (WORLD_SIZE=1 with RANK / MASTER_PORT) also forms a group, so every
+    RCCL branch below runs (tests/test_dist_nccl_gpu.py); otherwise this stays a plain process."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if ws > 1 and not is_dist():
+    launched = ws > 1 or (ws == 1 and "RANK" in os.environ and "MASTER_PORT" in os.environ)
+    if launched and not is_dist():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
@@ -70,7 +73,7 @@ def _all_reduce(t, op=td.ReduceOp.SUM):
 
 def allreduce_grads(params, average: bool = True):
     """Sum (mean) the gradients of ``params`` across ranks in ONE fused bucket."""
-    if not is_dist() or world_size() == 1:
+    if not is_dist():
         return
     grads = [p.grad for p in params if p.grad is not None]
     if not grads:
@@ -88,7 +91,7 @@ def allreduce_grads(params, average: bool = True):
 
 def broadcast_params(params, src: int = 0):
     """Make the trainable prompt parameters identical on every rank (one bucket)."""
-    if not is_dist() or world_size() == 1:
+    if not is_dist():
         return
     ps = list(params)
     flat = torch.cat([p.detach().reshape(-1) for p in ps])
@@ -125,7 +128,7 @@ def shard_range(n: int, r: int | None = None, w: int | None = None):
 def all_gather_varlen(t):
     """Concatenate every rank's ``t`` (same trailing shape, any leading length) in rank
     order; returned on every rank, on t's device."""
-    if not is_dist() or world_size() == 1:
+    if not is_dist():
         return t
     w = world_size()
     h = _host(t.contiguous())
@@ -240,7 +243,7 @@ def sync_rng_from(src: int = 0):
     """Make torch's CPU RNG state identical on every rank (rank ``src``'s), so samplers that
     draw from the global generator (RandomSampler, WeightedRandomSampler, as the reference's
     DataManager builds them) produce the same global index stream on every rank."""
-    if not is_dist() or world_size() == 1:
+    if not is_dist():
         return
     st = torch.get_rng_state()
     if td.get_backend() == "nccl":
@@ -251,7 +254,7 @@ def sync_rng_from(src: int = 0):
 
 def broadcast_int(v: int, src: int = 0) -> int:
     """Rank ``src``'s integer on every rank (e.g. a seed)."""
-    if not is_dist() or world_size() == 1:
+    if not is_dist():
         return int(v)
     dev = torch.device("cuda", torch.cuda.current_device()) if td.get_backend() == "nccl" else torch.device("cpu")
     t = torch.tensor([int(v)], dtype=torch.int64, device=dev)

@@ -218,6 +218,9 @@ class TrainerX:
         if not self.cfg.TEST.NO_TEST:
             if self.cfg.TEST.get("FINAL_MODEL", "last_step") == "best_val":
                 print("Deploy the model with the best val performance")
+                # rank 0 alone writes model-best.pth.tar (save_model): every rank waits for it
+                # before reading it back, so no rank loads a missing, partial or older file
+                dist.barrier()
                 self.load_model(self.output_dir)
             else:
                 print("Deploy the last-epoch model")

@@ -35,11 +35,28 @@ def _need(t, name, dtype=None, cuda=True):
     return t
 
 
+def split_pack(w):
+    """clipk_split_pack: fp32 weight [N, K] -> its split-fp16 packing for PREC fp32s
+    (SPLIT_SCALE * w as fp16 hi + lo parts, 4 bytes per element; int32 storage [N, K])."""
+    _need(w, "W", torch.float32)
+    n, k = w.shape
+    if k % 32:
+        raise N.ClipkError(f"split_pack needs K % 32 == 0, got {k}")
+    amax = float(w.abs().max()) if w.numel() else 0.0
+    if not amax * N.SPLIT_SCALE < 65504.0:
+        raise N.ClipkError(f"split_pack: |W| max {amax} exceeds the fp16 range at scale {N.SPLIT_SCALE}")
+    out = torch.empty(n, k, dtype=torch.int32, device=w.device)
+    N.call("clipk_split_pack", n, k, _p(w), k, _p(out), _stream())
+    return out
+
+
 def gemm(a, b, epi=N.EPI_NONE, out_dtype=torch.float32, bias=None, res=None, aux=None,
          want_out2=False, out=None):
-    """out[M,N] = epi(a[M,K] @ b[N,K]^T); returns out (and out2 for EPI_BIAS_QGELU)."""
+    """out[M,N] = epi(a[M,K] @ b[N,K]^T); returns out (and out2 for EPI_BIAS_QGELU). With a
+    fp32 and b an int32 split_pack(...) weight: the fp32-class split-fp16 GEMM (CLIPK_F32S)."""
     _need(a, "A")
-    _need(b, "B", a.dtype)
+    split = a.dtype == torch.float32 and b.dtype == torch.int32
+    _need(b, "B", torch.int32 if split else a.dtype)
     M, K = a.shape
     Nn = b.shape[0]
     if b.shape[1] != K:
@@ -53,7 +70,7 @@ def gemm(a, b, epi=N.EPI_NONE, out_dtype=torch.float32, bias=None, res=None, aux
         _need(res, "res", torch.float32 if out.dtype == torch.float32 else out.dtype)
     if aux is not None:
         _need(aux, "aux")
-    N.call("clipk_gemm", DT[a.dtype], DT[out.dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias),
+    N.call("clipk_gemm", N.F32S if split else DT[a.dtype], DT[out.dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias),
            _p(res), Nn, _p(out), Nn, _p(out2), _p(aux), DT[aux.dtype] if aux is not None else 0, Nn,
            _stream())
     return (out, out2) if want_out2 else out
@@ -251,7 +268,9 @@ def cosine_logits_bwd(imf, txt, inv_t, inv_i, dlogits, scale, per_image):
     return dtxt
 
 
-def ce_loss(logits, labels, alpha=None, gamma=2.0, focal=False, grad=True):
+def ce_loss(logits, labels, alpha=None, gamma=2.0, focal=False, grad=True, grad_scale=None):
+    """Per-row CE / focal loss [B] and dlogits = grad_scale * d(row loss)/d logits (default
+    grad_scale 1/B: the gradient of the mean)."""
     _need(logits, "logits", torch.float32)
     _need(labels, "labels", torch.int64)
     B, C = logits.shape
@@ -264,7 +283,7 @@ def ce_loss(logits, labels, alpha=None, gamma=2.0, focal=False, grad=True):
     row = torch.empty(B, device=logits.device)
     dl = torch.empty_like(logits) if grad else None
     N.call("clipk_ce_loss", B, C, _p(logits), _p(labels), _p(alpha), float(gamma), int(focal),
-           1.0 / B, _p(row), _p(dl), _stream())
+           float(1.0 / B if grad_scale is None else grad_scale), _p(row), _p(dl), _stream())
     return row, dl
 
 

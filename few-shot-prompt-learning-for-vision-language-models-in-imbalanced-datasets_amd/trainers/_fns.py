@@ -100,17 +100,27 @@ class CosineLogitsFn(torch.autograd.Function):
 
 
 class CrossEntropyFn(torch.autograd.Function):
-    """mean CE (nn.CrossEntropyLoss) or MultiClassFocalLoss (coop.py:145-163), fused fwd+bwd."""
+    """nn.CrossEntropyLoss (mean) or MultiClassFocalLoss (coop.py:145-163) with the reference's
+    reductions 'mean' | 'sum' | 'none' (coop.py:158-163), fused fwd+bwd."""
 
     @staticmethod
-    def forward(ctx, logits, labels, alpha, gamma, focal):
-        row, dl = ops.ce_loss(logits.contiguous(), labels, alpha, gamma, focal, grad=logits.requires_grad)
-        ctx.dl = dl
-        return row.mean()
+    def forward(ctx, logits, labels, alpha, gamma, focal, reduction="mean"):
+        B = logits.shape[0]
+        scale = 1.0 / B if reduction == "mean" else 1.0
+        row, dl = ops.ce_loss(logits.contiguous(), labels, alpha, gamma, focal, grad=logits.requires_grad,
+                              grad_scale=scale)
+        ctx.dl, ctx.reduction = dl, reduction
+        if reduction == "mean":
+            return row.mean()
+        if reduction == "sum":
+            return row.sum()
+        return row
 
     @staticmethod
     def backward(ctx, g):
-        return ctx.dl * g, None, None, None, None
+        # 'none': g is [B], each row's gradient scales its own row of d(row loss)/d logits
+        dl = ctx.dl * (g[:, None] if ctx.reduction == "none" else g)
+        return dl, None, None, None, None, None
 
 
 class MetaNetFn(torch.autograd.Function):

@@ -10,7 +10,11 @@ launches next to the text encoder's:
 * ``image_features(image)`` returns the prefetched result when it was started for this very
   tensor (unmodified since), else the last result for it (CoOp's post-step accuracy forward of
   the same images, coop.py:464-469), else computes it now.
-Results are bitwise the same as the inline call's."""
+Results are bitwise the same as the inline call's.
+Contract: a tensor passed to ``prefetch_image_features`` is read by the side stream until the
+prefetch completes; the caller must not write it in place before then (consume the result with
+``image_features`` first, or synchronise the side stream). A later in-place write is detected
+(``_version``) and the stale result is not used."""
 from __future__ import annotations
 
 import torch

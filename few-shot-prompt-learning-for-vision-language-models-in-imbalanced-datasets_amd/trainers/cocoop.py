@@ -98,6 +98,8 @@ class CustomCLIP(ImageFeatureSchedule, nn.Module):
         self.class_counts = class_counts
         class_range = None
         if class_counts is not None:
+            if min(class_counts) < 1:
+                raise ValueError(f"class sharding needs >= 1 class per rank, got counts {class_counts}")
             lo = sum(class_counts[:dist.rank()])
             class_range = (lo, lo + class_counts[dist.rank()])
         self.prompt_learner = PromptLearner(cfg, classnames, clip_model, class_range)
@@ -109,6 +111,12 @@ class CustomCLIP(ImageFeatureSchedule, nn.Module):
         self.logit_scale_value = clip_model.logit_scale_value
         self.dtype = clip_model.dtype
         self.max_rows = int(cfg.get("NATIVE", {}).get("MAX_TEXT_ROWS", 2_000_000))
+        # class-sharded: every rank must split a batch into the same number of logits_for calls
+        # (each runs a GatherClassColumns collective), so the chunking uses the largest rank's
+        # text rows per image (one MAX all-reduce here, at construction on every rank)
+        self._rows_per_img = self.prompt_learner.layout.rows_per_group
+        if class_counts is not None:
+            self._rows_per_img = int(dist.max_over_ranks(float(self._rows_per_img)))
         self.use_focal_loss = cfg.TRAINER.COCOOP.get("USE_FOCAL_LOSS", False)
         print(f">> USE_FOCAL_LOSS = {self.use_focal_loss}")
         if self.use_focal_loss:
@@ -140,8 +148,7 @@ class CustomCLIP(ImageFeatureSchedule, nn.Module):
             self.prefetch_image_features(nxt)
         imf = imf / imf.norm(dim=-1, keepdim=True)
         pl = self.prompt_learner
-        per_img = pl.layout.rows_per_group
-        chunk = max(1, self.max_rows // per_img)
+        chunk = max(1, self.max_rows // self._rows_per_img)
         if imf.shape[0] <= chunk:
             logits = self.logits_for(imf)
         else:
@@ -156,7 +163,7 @@ class CoCoOp(TrainerX):
     """cocoop.py:262-370 trainer contract."""
 
     def check_cfg(self, cfg):
-        assert cfg.TRAINER.COCOOP.PREC in ["fp16", "fp32", "amp", "bf16"]
+        assert cfg.TRAINER.COCOOP.PREC in ["fp16", "fp32", "amp", "bf16", "fp32s"]
         mode = cfg.get("NATIVE", {}).get("COCOOP_SHARD", "image")
         if mode not in ("image", "class"):
             raise ValueError(f"NATIVE.COCOOP_SHARD must be 'image' or 'class', got {mode!r}")

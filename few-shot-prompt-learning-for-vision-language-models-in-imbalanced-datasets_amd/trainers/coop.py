@@ -200,7 +200,7 @@ class CoOp(TrainerX):
     load_model. Multi-GPU: one process per GPU (see fsp_amd.dist), not nn.DataParallel."""
 
     def check_cfg(self, cfg):
-        assert cfg.TRAINER.COOP.PREC in ["fp16", "fp32", "amp", "bf16"]
+        assert cfg.TRAINER.COOP.PREC in ["fp16", "fp32", "amp", "bf16", "fp32s"]
 
     def build_model(self):
         cfg = self.cfg

@@ -214,7 +214,7 @@ class _DeepTrainer(TrainerX):
         return self.cfg.TRAINER[self.SEC]
 
     def check_cfg(self, cfg):
-        assert cfg.TRAINER[self.SEC].PREC in ["fp16", "fp32", "amp", "bf16"]
+        assert cfg.TRAINER[self.SEC].PREC in ["fp16", "fp32", "amp", "bf16", "fp32s"]
 
     def _vision_trains(self):
         raise NotImplementedError

@@ -30,9 +30,8 @@ class MultiClassFocalLoss(nn.Module):
             self.alpha = None
         else:
             raise TypeError("alpha must be None, list, or torch.Tensor")
-        if reduction != "mean":
-            raise NotImplementedError("the trainers use reduction='mean'")
         self.gamma = float(gamma)
+        self.reduction = reduction
 
     def forward(self, inputs, targets):
         a = None
@@ -40,7 +39,9 @@ class MultiClassFocalLoss(nn.Module):
             if self.alpha.device != inputs.device:
                 self.alpha = self.alpha.to(inputs.device)
             a = self.alpha
-        return CrossEntropyFn.apply(inputs, targets, a, self.gamma, True)
+        # reduction: 'mean' / 'sum', anything else returns the per-sample losses (coop.py:158-163)
+        red = self.reduction if self.reduction in ("mean", "sum") else "none"
+        return CrossEntropyFn.apply(inputs, targets, a, self.gamma, True, red)
 
 
 class LogitsNTXentLoss(nn.Module):

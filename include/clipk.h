@@ -38,8 +38,9 @@
 extern "C" {
 #endif
 
-/* element types */
-enum { CLIPK_F32 = 0, CLIPK_F16 = 1, CLIPK_BF16 = 2 };
+/* element types. CLIPK_F32S (GEMM input type only): fp32 activations times a weight packed by
+ * clipk_split_pack -- the fp32-class GEMM on 16-bit MFMA of PREC "fp32s" (clipk_gemm) */
+enum { CLIPK_F32 = 0, CLIPK_F16 = 1, CLIPK_BF16 = 2, CLIPK_F32S = 3 };
 
 /* status codes (hipError_t values > 0 pass through) */
 enum {
@@ -76,6 +77,19 @@ int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, int K,
                const float* bias, const void* res, int ldr,
                void* out, int ldo, void* out2, const void* aux, int aux_dtype, int ldaux,
                void* stream);
+
+/* fp32-class GEMM on the 16-bit MFMA (PREC "fp32s"; the reference runs these Linear layers in
+ * fp32, PromptSRC/clip/model.py:171-177, 699). clipk_split_pack stores W [N, K] (fp32, row
+ * stride ldw) as CLIPK_SPLIT_SCALE * W split into fp16 parts hi = fp16(x), lo = fp16(x - hi):
+ * per 8 consecutive k, 16 B of hi then 16 B of lo (4 B per element, the out buffer holds
+ * N * K * 4 bytes; K % 32 == 0). |W| must stay below 65504 / CLIPK_SPLIT_SCALE (the caller
+ * checks). clipk_gemm(in_dtype = CLIPK_F32S, ...) then takes A fp32 [M, K] and B = the packed
+ * weight (ldb = K) and forms every product as hi(a) hi(b) + hi(a) lo(b) + lo(a) hi(b) with
+ * v_mfma_f32_16x16x32_f16 (fp32 accumulate; A split in registers as its fragments are read),
+ * scaled by 1 / CLIPK_SPLIT_SCALE before the epilogue: ~22 significant bits per operand, the
+ * fp32 result to ~1e-6 relative. out / res / aux fp32 (epilogues as above). */
+#define CLIPK_SPLIT_SCALE 64.0f
+int clipk_split_pack(int N, int K, const float* W, int ldw, void* out, void* stream);
 
 /* Split-K form of clipk_gemm for small M (the ViT at training batch sizes, whose 128x128
  * tile grid would leave most CUs idle): the K range is cut into `splits` slices whose fp32
@@ -330,6 +344,15 @@ int clipk_encoder_set_input_rows(clipk_encoder* e, int mode);
  * 16-bit act dtype (clipk_vit_forward) runs the residual stream in that dtype through the text
  * encoder's layer loop and folds them the same way. */
 int clipk_encoder_set_ln_fold(clipk_encoder* e, const void* const* fold_ptrs);
+
+/* PREC fp32s on an fp32 encoder (act and grad dtype CLIPK_F32): on = 1 declares every GEMM weight
+ * of the handle's tables (layer weights 2, 4, 8, 10 and their transposes 12-15; text head 2-3,
+ * ViT head 4-5 and the prompted backward's proj) packed by clipk_split_pack, and runs every GEMM
+ * of its calls as CLIPK_F32S (the fp32-class split-fp16 MFMA product). LayerNorm, attention and
+ * the residual stream stay fp32. The text backward then runs on s * dtxt with s a power of two
+ * from max |dtxt| (exact, undone on dx0 and the deep-prompt gradients), so the gradient operands
+ * sit in fp16's normal range. Reference semantics: PromptSRC/clip/model.py:699 (fp32 model). */
+int clipk_encoder_set_split(clipk_encoder* e, int on);
 
 /* ViT with visual prompts, forward with saved activations and input-grad backward (the
  * prompted VisionTransformer of IVLP / PromptSRC, model.py:401-431, and MaPLe, 434-485):

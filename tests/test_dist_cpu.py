@@ -363,3 +363,43 @@ def test_cocoop_class_sharded_grad_equals_single_process(n_img):
         np.testing.assert_allclose(out[r]["logits"], logits.detach().numpy(), rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(out[r]["ctx"], ctx.grad.numpy(), rtol=1e-4, atol=2e-6)
         np.testing.assert_allclose(out[r]["w1"], mp_["meta_net.linear1.weight"].grad.numpy(), rtol=1e-4, atol=2e-6)
+
+
+def _best_val_ranks(directory, rank, world):
+    """TEST.FINAL_MODEL "best_val" with 2 ranks sharing OUTPUT_DIR: rank 0 alone writes
+    model-best.pth.tar (and writes it slowly here); every rank must load the best-val weights
+    it wrote -- never a missing, partial or older file -- before the final test."""
+    import time
+    from test_host_cpu import _dummy_trainer
+    rs = np.random.RandomState(3)
+    batches = [{"img": torch.from_numpy(rs.randn(5, 3, 2, 2).astype(np.float32)),
+                "label": torch.from_numpy(rs.randint(0, 3, 5))} for _ in range(2)]
+    t = _dummy_trainer(directory, batches)
+    t.dm.val_loader = batches[:1]
+    t.cfg.TEST.NO_TEST = False
+    t.cfg.TEST.FINAL_MODEL = "best_val"
+    vals = iter([10.0, 30.0, 20.0])
+    tests = []
+    orig_test, orig_save = t.test, t.save_model
+
+    def fake_test(split=None, return_pred=False):
+        if split == "val":
+            return next(vals)
+        tests.append(float(t.learner.ctx.detach()[0, 0]))
+        return orig_test(split, return_pred)
+
+    def slow_save(*a, **k):
+        if rank == 0:  # the writer lags behind the other rank
+            time.sleep(0.5)
+        return orig_save(*a, **k)
+    t.test = fake_test
+    t.save_model = slow_save
+    t.run_epoch = lambda: t.learner.ctx.data.add_(1.0)  # epoch e leaves ctx == e + 1
+    t.train(start_epoch=0, max_epoch=3)
+    return tests
+
+
+def test_best_val_final_model_two_ranks(tmp_path):
+    import functools
+    out = _run(functools.partial(_best_val_ranks, str(tmp_path)))
+    assert out[0] == [2.0] and out[1] == [2.0]  # both ranks test the 2nd epoch's (best) weights

@@ -356,6 +356,98 @@ def test_gemm_large_m_every_config(dev, cfg, Nn, K):
         lib.clipk_gemm_set_config(-1)
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("Nn,K", [(768, 3072), (768, 2304), (768, 768), (2304, 768), (3072, 768)])
+def test_gemm_large_m_w768(dev, dtype, Nn, K):
+    """The W = 768 text GEMMs of BASELINE configs 4 / 5 at their full-size M (C = 1,000 classes:
+    ~44k packed rows), automatic tile choice (the persistent / ping-pong 192- and 256-row
+    tiles), every epilogue the text encoder uses on that shape, 16-bit residual stream, vs a
+    torch fp32 reference."""
+    M = 44000
+    g = torch.Generator(device="cpu").manual_seed(Nn * 3 + K)
+    A = torch.randn(M, K, generator=g).to(dev).to(dtype)
+    B = (torch.randn(Nn, K, generator=g) / math.sqrt(K)).to(dev).to(dtype)
+    bias = torch.randn(Nn, generator=g).to(dev)
+    res = torch.randn(M, Nn, generator=g).to(dev).to(dtype)
+    aux = torch.randn(M, Nn, generator=g).to(dev).to(dtype)
+    ref = A.float() @ B.float().t()
+    close(ops.gemm(A, B, N.EPI_NONE, dtype), ref, dtype, f"{Nn}x{K} none")
+    close(ops.gemm(A, B, N.EPI_NONE, torch.float32), ref, dtype, f"{Nn}x{K} none f32")
+    close(ops.gemm(A, B, N.EPI_BIAS, dtype, bias=bias), ref + bias, dtype, f"{Nn}x{K} bias")
+    close(ops.gemm(A, B, N.EPI_BIAS_RES, dtype, bias=bias, res=res), ref + bias + res.float(), dtype,
+          f"{Nn}x{K} res16")
+    gq, hq = ops.gemm(A, B, N.EPI_BIAS_QGELU, dtype, bias=bias, want_out2=True)
+    hr = ref + bias
+    close(hq, hr, dtype, f"{Nn}x{K} qgelu.h")
+    close(gq, hr * torch.sigmoid(1.702 * hr), dtype, f"{Nn}x{K} qgelu.g")
+    s = torch.sigmoid(1.702 * aux.float())
+    close(ops.gemm(A, B, N.EPI_DQGELU, dtype, aux=aux), ref * (s + 1.702 * aux.float() * s * (1 - s)), dtype,
+          f"{Nn}x{K} dqgelu")
+
+
+@pytest.mark.parametrize("M,Nn,K", [(300, 384, 192), (517, 1536, 512), (4600, 768, 3072), (47160, 512, 2048),
+                                     (47160, 2048, 512), (8000, 512, 512)])
+def test_gemm_split_fp32_class(dev, M, Nn, K):
+    """PREC fp32s GEMM (CLIPK_F32S: fp32 A split into fp16 hi + lo in registers, split-packed B,
+    3 fp16 MFMAs per product) against an fp64 reference, every epilogue: within 4e-6 of the
+    output scale (measured 3e-7 .. 1.8e-6, growing with K; the dropped lo x lo term is ~2^-22 of
+    each product) -- the fp32 class, two orders of magnitude under fp16 operands; the 128x128
+    grids, the 4-slot ring and the 192x256 ping-pong tiles all run here."""
+    g = torch.Generator(device="cpu").manual_seed(M + Nn + K)
+    a = torch.randn(M, K, generator=g).to(dev)
+    b = (torch.randn(Nn, K, generator=g) * 0.03).to(dev)  # CLIP-like weight scale
+    bias = torch.randn(Nn, generator=g).to(dev)
+    res = torch.randn(M, Nn, generator=g).to(dev)
+    aux = torch.randn(M, Nn, generator=g).to(dev)
+    bp = ops.split_pack(b)
+    ref = a.double() @ b.double().t()
+    tol = 4e-6
+
+    def chk(out, r, what):
+        err = ((out.double() - r).abs().max() / (r.abs().max() + 1e-30)).item()
+        assert err <= tol, f"{what}: rel err {err:.3e} > {tol}"
+        return err
+    e_none = chk(ops.gemm(a, bp, N.EPI_NONE), ref, "none")
+    chk(ops.gemm(a, bp, N.EPI_BIAS, bias=bias), ref + bias.double(), "bias")
+    chk(ops.gemm(a, bp, N.EPI_BIAS_RES, bias=bias, res=res), ref + bias.double() + res.double(), "res")
+    gq, hq = ops.gemm(a, bp, N.EPI_BIAS_QGELU, bias=bias, want_out2=True)
+    hr = ref + bias.double()
+    chk(hq, hr, "qgelu.h")
+    chk(gq, hr * torch.sigmoid(1.702 * hr), "qgelu.g")
+    s = torch.sigmoid(1.702 * aux.double())
+    chk(ops.gemm(a, bp, N.EPI_DQGELU, aux=aux), ref * (s + 1.702 * aux.double() * s * (1 - s)), "dqgelu")
+    # for scale: the fp16 operands' error on the same product is ~1e-3
+    e16 = ((ops.gemm(a.half(), b.half(), N.EPI_NONE).double() - ref).abs().max() / ref.abs().max()).item()
+    e32 = ((ops.gemm(a, b, N.EPI_NONE).double() - ref).abs().max() / ref.abs().max()).item()
+    print(f"split {M}x{Nn}x{K}: {e_none:.2e}  f32 MFMA: {e32:.2e}  fp16: {e16:.2e}")
+    assert e_none * 50 < e16
+
+
+@pytest.mark.parametrize("reduction", ["mean", "sum", "none"])
+def test_focal_loss_reductions(dev, reduction):
+    """MultiClassFocalLoss(reduction=...) (PromptSRC/trainers/coop.py:131-163): loss and
+    d logits vs the reference's formula in torch fp32 autograd, for each reduction."""
+    from fsp_amd.trainers.losses import MultiClassFocalLoss
+    g = torch.Generator(device="cpu").manual_seed(5)
+    logits = (torch.randn(6, 37, generator=g) * 3).to(dev)
+    y = torch.randint(0, 37, (6,), generator=g).to(dev)
+    alpha = (torch.rand(37, generator=g) + 0.5).tolist()
+    up = torch.randn(6, generator=g).to(dev)  # upstream gradient for 'none'
+    fl = MultiClassFocalLoss(alpha=alpha, gamma=2, reduction=reduction)
+    x = logits.clone().requires_grad_(True)
+    out = fl(x, y)
+    (out * up).sum().backward() if reduction == "none" else out.backward()
+    xr = logits.clone().requires_grad_(True)
+    ce = F.cross_entropy(xr, y, reduction="none")
+    pt = torch.exp(-ce)
+    fr = torch.tensor(alpha, device=dev)[y] * (1 - pt) ** 2 * ce
+    ref = fr.mean() if reduction == "mean" else fr.sum() if reduction == "sum" else fr
+    (ref * up).sum().backward() if reduction == "none" else ref.backward()
+    assert out.shape == ref.shape
+    close(out.detach(), ref.detach(), torch.float32, f"focal {reduction}")
+    close(x.grad, xr.grad, torch.float32, f"focal {reduction} grad")
+
+
 @pytest.mark.parametrize("cfg", [1, 6])
 @pytest.mark.parametrize("K", [64, 128, 192, 320])
 def test_gemm_large_tiles_short_k(dev, cfg, K):

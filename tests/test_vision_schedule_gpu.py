@@ -58,8 +58,11 @@ def test_features_only_for_the_same_unmodified_tensor(dev, tmp_path):
     # equal values in another tensor: not reused
     y = x.clone()
     assert m.cached_image_features(y) is None
-    # the same tensor modified in place: not reused, recomputed from the new values
+    # the same tensor modified in place: not reused, recomputed from the new values (the
+    # write waits for the prefetch's reads of x: a prefetched tensor is not written in place
+    # before the side stream is done with it, trainers/_vision.py)
     m.prefetch_image_features(x)
+    m._side(x.device).synchronize()
     x.mul_(0.5)
     assert m.cached_image_features(x) is None
     fresh = m.image_features(x)
