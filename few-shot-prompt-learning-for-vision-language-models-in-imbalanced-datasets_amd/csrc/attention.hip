@@ -96,88 +96,72 @@ __global__ __launch_bounds__(256) void attn_fwd_short(int nseq, int L, int H, in
   }
 }
 
-// ------------------------------------------------------------------ forward, any L
-template <typename T>
-__global__ __launch_bounds__(256) void attn_fwd_long(int nseq, int L, int H, int causal,
-                                                     const T* __restrict__ qkv, int ldq,
-                                                     T* __restrict__ out, int ldo,
-                                                     float* __restrict__ lse) {
+// ------------------------------------------------------------------ forward, any L, fp32
+// (PREC fp32 / fp32s: the ViT's L = 50..577, plain text 64 < L <= 77). Block = 64 query rows of
+// one (sequence, head), 4 waves of 16 rows; lane = 4 r + s holds row r's 16-column slice s of q
+// and o; K / V in 64-key LDS chunks, a score is 16 FMAs + a quad sum, exact online softmax.
+__global__ __launch_bounds__(256) void attn_fwd_f32(int nseq, int L, int H, int causal, const float* __restrict__ qkv,
+                                                    int ldq, float* __restrict__ out, int ldo,
+                                                    float* __restrict__ lse) {
   __shared__ CLIPK_LDS_ALIGN float sk[64 * 64];
   __shared__ CLIPK_LDS_ALIGN float sv[64 * 64];
-  const int tid = threadIdx.x;
-  const int i = blockIdx.x * 256 + tid;
-  const int h = blockIdx.y, s = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane >> 2, s = lane & 3;
+  const int h = blockIdx.y, sq = blockIdx.z;
   const int W = H * 64;
+  const int i = blockIdx.x * 64 + (tid >> 6) * 16 + r;  // query row
   const bool row_ok = i < L;
-  const size_t row = (size_t)s * L + (row_ok ? i : 0);
-  float q[64];
-  load_row64<T>(qkv + row * ldq + h * 64, q);
+  const size_t row = (size_t)sq * L + (row_ok ? i : L - 1);
+  float q[16], o[16];
+  ld16(qkv + row * ldq + h * 64 + 16 * s, q);
 #pragma unroll
-  for (int d = 0; d < 64; ++d) q[d] *= kScale;
-  float o[64];
-#pragma unroll
-  for (int d = 0; d < 64; ++d) o[d] = 0.f;
+  for (int d = 0; d < 16; ++d) {
+    q[d] *= kScale;
+    o[d] = 0.f;
+  }
   float m = -INFINITY, l = 0.f;
-  const int qmax = min(L, (int)(blockIdx.x + 1) * 256) - 1;
+  const int qmax = min(L, (int)(blockIdx.x + 1) * 64) - 1;
   const int jend = causal ? qmax + 1 : L;
   for (int j0 = 0; j0 < jend; j0 += 64) {
     __syncthreads();
-    // cooperative load of 64 key/value rows (fp32 in LDS): thread -> (row, 16-element quarter)
-    {
-      const int r = tid >> 2, part = tid & 3;
-      const int jr = j0 + r;
-      float tk[16], tv[16];
+    {  // 64 key / value rows: thread -> (row tid / 4, 16-column quarter)
+      const int jr = j0 + (tid >> 2), part = tid & 3;
+      float t[16];
       if (jr < L) {
-        const T* base = qkv + ((size_t)s * L + jr) * ldq + h * 64 + part * 16;
-        constexpr int V = Vec16<T>::N;
-#pragma unroll
-        for (int c = 0; c < 16 / V; ++c) {
-          load16_f32<T>(base + W + c * V, tk + c * V);
-          load16_f32<T>(base + 2 * W + c * V, tv + c * V);
-        }
-      } else {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) { tk[c] = 0.f; tv[c] = 0.f; }
-      }
-#pragma unroll
-      for (int c = 0; c < 16; c += 4) {
-        *reinterpret_cast<f32x4*>(&sk[r * 64 + part * 16 + c]) = (f32x4){tk[c], tk[c + 1], tk[c + 2], tk[c + 3]};
-        *reinterpret_cast<f32x4*>(&sv[r * 64 + part * 16 + c]) = (f32x4){tv[c], tv[c + 1], tv[c + 2], tv[c + 3]};
+        const float* base = qkv + ((size_t)sq * L + jr) * ldq + h * 64 + part * 16;
+        ld16(base + W, t);
+        st16(&sk[(tid >> 2) * 64 + part * 16], t);
+        ld16(base + 2 * W, t);
+        st16(&sv[(tid >> 2) * 64 + part * 16], t);
       }
     }
     __syncthreads();
-    float sc[64];
-    float cm = -INFINITY;
+    const int nj = min(64, jend - j0);
+    for (int j = 0; j < nj; ++j) {
+      float kv[16];
+      ld16(&sk[j * 64 + 16 * s], kv);
+      const float sc = quad_sum(dot16(q, kv));
+      if (!causal || j0 + j <= i) {
+        if (sc > m) {
+          const float a = __expf(m - sc);  // 0 for the first key (m = -inf)
+          l *= a;
 #pragma unroll
-    for (int j = 0; j < 64; ++j) {
-      const int jj = j0 + j;
-      float v = dot64(q, &sk[j * 64]);
-      if (jj >= L || (causal && jj > i)) v = -INFINITY;
-      sc[j] = v;
-      cm = fmaxf(cm, v);
-    }
-    const float mn = fmaxf(m, cm);
-    if (mn == -INFINITY) continue;  // fully masked chunk for this row
-    const float corr = __expf(m - mn);
-    l *= corr;
+          for (int d = 0; d < 16; ++d) o[d] *= a;
+          m = sc;
+        }
+        const float p = __expf(sc - m);
+        l += p;
+        ld16(&sv[j * 64 + 16 * s], kv);
 #pragma unroll
-    for (int d = 0; d < 64; ++d) o[d] *= corr;
-    m = mn;
-#pragma unroll
-    for (int j = 0; j < 64; ++j) {
-      const float p = __expf(sc[j] - m);
-      l += p;
-      const float* vr = &sv[j * 64];
-#pragma unroll
-      for (int d = 0; d < 64; ++d) o[d] = fmaf(p, vr[d], o[d]);
+        for (int d = 0; d < 16; ++d) o[d] = fmaf(p, kv[d], o[d]);
+      }
     }
   }
   if (row_ok) {
     const float inv = 1.0f / l;
 #pragma unroll
-    for (int d = 0; d < 64; ++d) o[d] *= inv;
-    store_row64<T>(out + row * ldo + h * 64, o);
-    if (lse) lse[row * H + h] = m + __logf(l);
+    for (int d = 0; d < 16; ++d) o[d] *= inv;
+    st16(out + row * ldo + h * 64 + 16 * s, o);
+    if (lse && s == 0) lse[row * H + h] = m + __logf(l);
   }
 }
 
@@ -872,9 +856,12 @@ static int launch_fwd(int nseq, int L, int H, int causal, const void* qkv, int l
   else if (L <= 32) short_launch(std::integral_constant<int, 32>{});
   else if (L <= 64) short_launch(std::integral_constant<int, 64>{});
   else {
-    dim3 grid((L + 255) / 256, H, nseq);
-    hipLaunchKernelGGL((attn_fwd_long<T>), grid, dim3(256), 0, st, nseq, L, H, causal,
-                       (const T*)qkv, ldq, (T*)out, ldo, lse);
+    static_assert(sizeof(T) == 2 || __is_same(T, float), "fp32 long forward");
+    if constexpr (__is_same(T, float)) {
+      dim3 grid((L + 63) / 64, H, nseq);
+      hipLaunchKernelGGL(attn_fwd_f32, grid, dim3(256), 0, st, nseq, L, H, causal, (const float*)qkv, ldq,
+                         (float*)out, ldo, lse);
+    }
   }
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;

@@ -775,31 +775,6 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_bwd_lds(int G, int P, in
 // nn.MultiheadAttention math (model.py:183), exact softmax (online max / rescale, fwd).
 constexpr int kF32Wpb = 4;
 
-__device__ __forceinline__ float quad_sum(float v) {
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
-  return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
-}
-__device__ __forceinline__ void ld16(const float* __restrict__ p, float* v) {
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const f32x4 t = reinterpret_cast<const f32x4*>(p)[c];
-    v[4 * c] = t[0]; v[4 * c + 1] = t[1]; v[4 * c + 2] = t[2]; v[4 * c + 3] = t[3];
-  }
-}
-__device__ __forceinline__ void st16(float* __restrict__ p, const float* v) {
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-    reinterpret_cast<f32x4*>(p)[c] = (f32x4){v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]};
-}
-__device__ __forceinline__ float dot16(const float* a, const float* b) {
-  float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-  for (int d = 0; d < 16; d += 2) {
-    s0 = fmaf(a[d], b[d], s0);
-    s1 = fmaf(a[d + 1], b[d + 1], s1);
-  }
-  return s0 + s1;
-}
 // a wave's own LDS writes visible to its other lanes (program order on the LDS; no reordering
 // by the compiler across this point)
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }

@@ -593,16 +593,13 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       auto mm = [&](int h, int q) {
         if (CLIPK_GEMM_NOMMA) return;
         if (CLIPK_GEMM_PRIO == 1) __builtin_amdgcn_s_setprio(1);
-        if constexpr (SPLIT) {
+        if constexpr (SPLIT) {  // fa[0][i] / fa[1][i]: the A half's hi / lo parts (split_a)
 #pragma unroll
-          for (int i = 0; i < TM2; ++i) {
-            u32x4 ah, al;
-            split8(fa[0][i], fa[1][i], ah, al);
+          for (int i = 0; i < TM2; ++i)
 #pragma unroll
             for (int j = 0; j < TN2; ++j)
-              acc[h * TM2 + i][q * TN2 + j] = mma_split(fbs[NFB == 2 ? q : 0][0][j], fbs[NFB == 2 ? q : 0][1][j], ah, al,
-                                                        acc[h * TM2 + i][q * TN2 + j]);
-          }
+              acc[h * TM2 + i][q * TN2 + j] = mma_split(fbs[NFB == 2 ? q : 0][0][j], fbs[NFB == 2 ? q : 0][1][j],
+                                                        fa[0][i], fa[1][i], acc[h * TM2 + i][q * TN2 + j]);
         } else {
 #pragma unroll
         for (int kk = 0; kk < KK; ++kk)
@@ -614,8 +611,17 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         }
         if (CLIPK_GEMM_PRIO == 1) __builtin_amdgcn_s_setprio(0);
       };
-      auto seg_end = [&]() {  // memory segment done: fragments in registers, then the barrier
+      // PREC fp32s: an A half just read is split into its hi / lo parts in place, once for both
+      // B quadrants it meets, in the memory segment (beside the partner wave's MFMAs)
+      auto split_a = [&]() {
+        if constexpr (SPLIT) {
+#pragma unroll
+          for (int i = 0; i < TM2; ++i) split8(fa[0][i], fa[1][i], fa[0][i], fa[1][i]);
+        }
+      };
+      auto seg_end = [&](bool new_a = false) {  // memory segment done: fragments in registers, then the barrier
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (new_a) split_a();
         if (CLIPK_GEMM_PRIO == 2) __builtin_amdgcn_s_setprio(0);
         G8_BAR();
       };
@@ -664,7 +670,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
           load_ext(0, extq[0]);
           load_ln(0, 0);
         }
-        seg_end();
+        seg_end(true);
         mm(0, 0);
         mm(0, 1);
         G8_BAR();
@@ -677,7 +683,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         } else if (h1) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        seg_end();
+        seg_end(true);
         mm(1, 0);
         mm(1, 1);
         G8_BAR();
@@ -695,7 +701,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
           load_ext(0, extq[0]);
           load_ln(0, 0);
         }
-        seg_end();
+        seg_end(true);
         mm(0, 0);
         G8_BAR();
         if (CLIPK_GEMM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
@@ -707,7 +713,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         if (CLIPK_GEMM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         rd_a(b, 1);                             // phase 3: A1 x B1
         if (h2) pst(b, cra, in2 ? crb : xrb, k2, 3);
-        seg_end();
+        seg_end(true);
         mm(1, 1);
         G8_BAR();
         if (CLIPK_GEMM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
@@ -1103,6 +1109,17 @@ static int launch_gemm_split(const GemmArgs& g, hipStream_t st) {
   const_cast<GemmArgs&>(g).stamp = gemm_stamp_buf();
   const_cast<GemmArgs&>(g).skew = 0;
   const int cfg = pick_cfg(g.M, g.N, 2);
+  if (cfg == 7) {  // small M (the ViT): 64x128 tiles, twice the 128x128 grid
+    const int nwg = ((g.M + 63) / 64) * (g.N / 128);
+    if (nwg <= cus && deep_small())
+      hipLaunchKernelGGL((gemm_nt_kernel<f32s, float, float, EPI, 64, 128, 2, 2, false, GEMM_ROWB, 4>), dim3(nwg),
+                         dim3(256), 0, st, g);
+    else
+      hipLaunchKernelGGL((gemm_nt_kernel<f32s, float, float, EPI, 64, 128, 2, 2, false, GEMM_ROWB, 2>), dim3(nwg),
+                         dim3(256), 0, st, g);
+    CLIPK_CHECK_LAUNCH();
+    return CLIPK_OK;
+  }
   if (cfg == 1 || cfg == 6) {
     if (try_pp<f32s, float, float, EPI, 192>(g, ((g.M + 191) / 192) * (g.N / 256), st)) {
       CLIPK_CHECK_LAUNCH();
@@ -1332,9 +1349,9 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(int S, int M, int N,
 // the grid covers under half of the CUs (the ViT's N = 768 projections at B = 8: 78 tiles;
 // grids of 234-312 tiles measured no better split), enough slices for ~2 blocks per CU,
 // each slice >= 8 K steps, at most 8 slices.
-static int auto_splits(int M, int N, int K, int esz) {
+static int auto_splits(int M, int N, int K, int esz, int tile_rows = 128) {
   if (M <= 0 || N % GEMM_NMIN) return 1;
-  const int tiles = ((M + 127) / 128) * (N / 128);
+  const int tiles = ((M + tile_rows - 1) / tile_rows) * (N / 128);
   if (2 * tiles >= num_cus()) return 1;
   const int nk = K * esz / GEMM_ROWB;
   int s = (2 * num_cus()) / tiles;  // slices x tiles within one round of 2 blocks per CU
@@ -1346,6 +1363,8 @@ static int auto_splits(int M, int N, int K, int esz) {
 }  // namespace clipk
 
 extern "C" int clipk_gemm_auto_splits(int in_dtype, int M, int N, int K) {
+  // fp32s small-M GEMMs run 64x128 tiles (launch_gemm_split): their grid is the one to fill
+  if (in_dtype == CLIPK_F32S) return auto_splits(M, N, K, 4, M < 4096 ? 64 : 128);
   return auto_splits(M, N, K, (in_dtype == CLIPK_F32 || in_dtype == CLIPK_F32S) ? 4 : 2);
 }
 
@@ -1369,7 +1388,7 @@ extern "C" int clipk_gemm_splitk(int in_dtype, int out_dtype, int epi, int M, in
                                  void* out, int ldo, void* out2, int splits, void* ws, size_t ws_bytes,
                                  void* stream) {
   const int esz = (in_dtype == CLIPK_F32 || in_dtype == CLIPK_F32S) ? 4 : 2;
-  if (splits <= 0) splits = auto_splits(M, N, K, esz);
+  if (splits <= 0) splits = clipk_gemm_auto_splits(in_dtype, M, N, K);
   if (splits <= 1 || M <= 0)
     return clipk_gemm(in_dtype, out_dtype, epi, M, N, K, A, lda, B, ldb, bias, res, ldr, out, ldo, out2,
                       nullptr, 0, 0, stream);
