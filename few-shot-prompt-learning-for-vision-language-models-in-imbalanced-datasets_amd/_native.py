@@ -31,6 +31,8 @@ SIGNATURES = {
     "clipk_strerror": (ctypes.c_char_p, [_I]),
     "clipk_device_arch_ok": (_I, []),
     "clipk_gemm": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P, _I, _I, _P]),
+    "clipk_gemm_ws_bytes": (_S, []),
+    "clipk_gemm_ws": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P, _I, _I, _P, _S, _P]),
     "clipk_gemm_auto_splits": (_I, [_I, _I, _I, _I]),
     "clipk_gemm_splitk_ws_bytes": (_S, [_I, _I, _I]),
     "clipk_gemm_splitk": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P, _S, _P]),
@@ -38,6 +40,7 @@ SIGNATURES = {
     "clipk_split_pack": (_I, [_I, _I, _P, _I, _P, _P]),
     "clipk_gemm_ln": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P]),
     "clipk_ln_stats_merge": (_I, [_I, _I, _P, _P, _P, _P, _P]),
+    "clipk_gemm_ln_ws": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _S, _P]),
     "clipk_image_resample": (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P]),
     "clipk_gemm_stamps": (_I, [_P, _S]),
     "clipk_layernorm_fwd": (_I, [_I, _I, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P]),

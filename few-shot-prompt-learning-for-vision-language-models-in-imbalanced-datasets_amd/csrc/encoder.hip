@@ -57,6 +57,22 @@ struct SplitScope {
   explicit SplitScope(const clipk_encoder* e) : prev(t_split) { t_split = e->split; }
   ~SplitScope() { t_split = prev; }
 };
+// The GEMMs of an encoder call get the call's split-tail workspace (clipk_gemm_ws: the N = 512
+// text GEMMs' tiles past the first round run as K halves on paired blocks); its pair flags are
+// zeroed once per call.
+static thread_local void* t_gemm_ws = nullptr;
+struct GemmWsScope {
+  void* prev;
+  int rc = CLIPK_OK;
+  GemmWsScope(void* ws, hipStream_t st) : prev(t_gemm_ws) {
+    t_gemm_ws = ws;
+    if (ws) {
+      const size_t fb = 128 * sizeof(unsigned);  // the flags at the end of clipk_gemm_ws_bytes()
+      if (hipMemsetAsync((char*)ws + clipk_gemm_ws_bytes() - fb, 0, fb, st) != hipSuccess) rc = (int)hipGetLastError();
+    }
+  }
+  ~GemmWsScope() { t_gemm_ws = prev; }
+};
 static inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
 // Residual stream dtype of the TEXT encoder: the 16-bit activation dtype under PREC
@@ -159,7 +175,8 @@ static int gemm(int in, int out, int epi, int M, int N, int K, const void* A, co
                site ? gemm_bytes(in, out, epi, M, N, K, o2 != nullptr, auxdt) : 0.0);
   if (sk && epi != CLIPK_EPI_DQGELU)
     return clipk_gemm_splitk(in, out, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, 0, sk, skb, st);
-  return clipk_gemm(in, out, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, aux, auxdt, N, st);
+  return clipk_gemm_ws(in, out, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, aux, auxdt, N, t_gemm_ws,
+                       t_gemm_ws ? clipk_gemm_ws_bytes() : 0, st);
 }
 
 // split-K workspace for the block GEMMs of a vision forward at `rows` rows (0 when none splits)
@@ -188,6 +205,7 @@ struct TextBufs {
   // LN fold: per (row, 64-column group) statistics partials of the residual stream; mean /
   // rstd of the un-saved (inference) forward
   float *lnst = nullptr, *tm = nullptr, *tr = nullptr, *rnb = nullptr;
+  void* gemm_ws = nullptr;  // clipk_gemm_ws split-tail workspace
   size_t saved_bytes = 0, ws_bytes = 0;
 };
 
@@ -238,6 +256,7 @@ static TextBufs text_layout(const clipk_encoder* e, size_t rows, int nout, void*
   t.tm = (float*)wk.take(rows * 4);
   t.tr = (float*)wk.take(rows * 4);
   t.rnb = (float*)wk.take(rows * 8);
+  t.gemm_ws = wk.take(clipk_gemm_ws_bytes());
   t.saved_bytes = save ? sv.off : 0;
   t.ws_bytes = wk.off;
   return t;
@@ -249,6 +268,7 @@ struct TextBwdBufs {
   void *dtg, *dX_lp, *dh, *do_, *dqkv, *dxn;  // dxn: LN-output grads in the grad dtype
   float* dlnf;
   float* gscale;  // PREC fp32s: the backward's gradient scale s and 1 / s (+ amax partials)
+  void* gemm_ws;  // clipk_gemm_ws split-tail workspace
   void* part;  // shared-prefix attention: per-chunk prefix dK/dV partials
   size_t bytes;
 };
@@ -267,6 +287,7 @@ static TextBwdBufs text_bwd_layout(const clipk_encoder* e, size_t rows, int nout
   b.dqkv = c.take(rows * 3 * W * g);
   b.part = part_bytes ? c.take(part_bytes) : nullptr;
   b.gscale = (float*)c.take((2 + kAmaxBlocks) * sizeof(float));
+  b.gemm_ws = c.take(clipk_gemm_ws_bytes());
   b.bytes = c.off;
   return b;
 }
@@ -447,7 +468,8 @@ static int gemm_ln(int act, int epi, int M, int N, int K, const void* A, const v
   const double b = gemm_bytes(act, act, epi, M, N, K, o2 != nullptr, act) + (stats ? (double)M * (N / 64) * 8 : 0.0) +
                    (rnb ? 8.0 * M : 0.0);
   ProfScope ps(prof_cls, st, 2.0 * M * N * K, site, b);
-  return clipk_gemm_ln(act, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, stats, colsum, rnb, st);
+  return clipk_gemm_ln_ws(act, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, stats, colsum, rnb, t_gemm_ws,
+                          t_gemm_ws ? clipk_gemm_ws_bytes() : 0, st);
 }
 // mean / rstd (kept for the LayerNorm backward) and the folding GEMM's (rstd, -rstd mean) pairs
 static int ln_merge(int rows, int W, const float* lnst, float* m, float* r, float* rnb, hipStream_t st, bool text) {
@@ -710,6 +732,8 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
   const bool save = saved != nullptr;
   TextBufs t = text_layout(e, sh.rows, sh.nout, saved, ws, save, io.rd);
   if (ws_bytes < t.ws_bytes || (save && saved_bytes < t.saved_bytes)) return CLIPK_EWORKSPACE;
+  GemmWsScope gemm_ws_scope(t.gemm_ws, st);
+  TRY(gemm_ws_scope.rc);
   const int W = e->W, rows = sh.rows, rd = io.rd;
   const int pg = io.text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE;
   // layer-0 input: x0 (fp32) into X[0] (the residual dtype) when saving (LN1 backward reads
@@ -800,6 +824,8 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
   TextBufs t = text_layout(e, sh.rows, sh.nout, const_cast<void*>(saved), nullptr, true, io.rd);
   TextBwdBufs b = text_bwd_layout(e, sh.rows, sh.nout, sh.part_bytes(e->heads), ws);
   if (saved_bytes < t.saved_bytes || ws_bytes < b.bytes) return CLIPK_EWORKSPACE;
+  GemmWsScope gemm_ws_scope(b.gemm_ws, st);
+  TRY(gemm_ws_scope.rc);
   const int W = e->W, rows = sh.rows, nout = sh.nout, gd = e->grad, act = e->act;
   const int pg = io.text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE;
   float* dX = dx0;

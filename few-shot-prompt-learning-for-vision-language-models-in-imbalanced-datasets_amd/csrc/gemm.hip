@@ -57,6 +57,12 @@ struct GemmArgs {
   float* lnstats;
   const float* colsum;
   const f32x2* lnrnb;
+  // split tail (TAIL launches, clipk_gemm_ws): the grid's G blocks take tiles 0..G-1 one each,
+  // then the remaining tiles as two K halves on blocks 8 apart (one XCD); the first half's
+  // fp32 accumulators go to tail_ws, published by tail_flags[pair] (release / acquire, agent
+  // scope), and the second half adds them before the epilogue and clears the flag
+  float* tail_ws;
+  unsigned* tail_flags;
 };
 
 // Sum over the aligned 8-lane group (DPP: quad xor 1, quad xor 2, half-row mirror i <-> 7 - i).
@@ -297,7 +303,7 @@ __device__ __forceinline__ void skew_start(int us, int bid) {
 // LNM (clipk_gemm_ln): 1 = per-row LayerNorm statistics of the output, 2 = LayerNorm of A
 // folded into the epilogue (see GemmArgs).
 template <typename T, typename TO, typename TX, int EPI, int BM, int BN, int WM, int WN, bool PERSIST,
-          int ROWB = GEMM_ROWB, int DEPTH = 2, bool AG = false, bool PP = false, int LNM = 0>
+          int ROWB = GEMM_ROWB, int DEPTH = 2, bool AG = false, bool PP = false, int LNM = 0, bool TAIL = false>
 __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
   static_assert(DEPTH == 2 || !PERSIST, "deep ring: non-persistent launches only");
   static_assert(!AG || (!PERSIST && DEPTH == 2 && sizeof(T) == 2 && ROWB == 128), "A-operand QuickGELU path");
@@ -307,6 +313,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
   static_assert(!SPLIT || (ROWB == 128 && !AG), "split-fp16 GEMM: 128-B staged rows");
   static_assert(!PP || (PERSIST && !AG && DEPTH == 2 && ROWB == 128 && WM == 2 && WN == 4 && BN == 256 &&
                         (sizeof(T) == 2 || SPLIT) && BM % 64 == 0), "ping-pong main loop (K >= 128)");
+  static_assert(!TAIL || PP, "split tail: ping-pong launches");
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int OPA = BM * ROWB, OPB = BN * ROWB, STAGE = OPA + OPB;
@@ -343,7 +350,22 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
   const int t_end = t_beg + (xcd < r ? q + 1 : q);
   const int t_step = PERSIST ? (int)(gridDim.x >> 3) : 1;
   int tile = t_beg + (bid >> 3);
-  if (tile >= t_end) return;  // block-uniform
+  // TAIL: work item 0 = data-parallel tile xcd * G/8 + slot (the launcher guarantees G < ntiles
+  // <= 1.5 G), item 1 = tail pair p = xcd * G/16 + slot / 2 (tile G + p), K half slot & 1; the
+  // second half runs on the block 8 ids later (same XCD, dispatched after the first: no wait
+  // on a block that cannot be resident)
+  const int tail_g = TAIL ? (int)gridDim.x : 0;
+  auto tail_item = [&](int& t, int& k0, int& n, int& role, int nk_total) {
+    const int slot = bid >> 3, pr = xcd * (tail_g >> 4) + (slot >> 1);
+    t = tail_g + pr;
+    const int h = slot & 1;
+    k0 = h ? nk_total / 2 : 0;
+    n = h ? nk_total - nk_total / 2 : nk_total / 2;
+    role = h ? 2 : 1;
+    return t < ntiles;
+  };
+  if constexpr (TAIL) tile = xcd * (tail_g >> 3) + (bid >> 3);
+  else if (tile >= t_end) return;  // block-uniform
   if constexpr (PERSIST) skew_start(g.skew, bid);
   const int ks = PERSIST ? 0 : tile / ntiles;
   if (!PERSIST) tile -= ks * ntiles;
@@ -453,10 +475,12 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
                                 ? g.stamp + (size_t)bid * (STAMP_TILES * 3 + 4) : nullptr;
   if (stp) { stp[0] = __builtin_amdgcn_s_memtime(); stp[1] = __builtin_amdgcn_s_memrealtime(); }
 
+  int kt0c = kt0, nkc = nk, role = 0;  // this item's K range and role (TAIL: 1 publish, 2 combine)
   while (true) {
     const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
-    const int next = tile + t_step;
-    const bool has_next = PERSIST && next < t_end;
+    int next = tile + t_step, kt0n = 0, nkn = nk, role_n = 0;
+    bool has_next = PERSIST && next < t_end;
+    if constexpr (TAIL) has_next = role == 0 && tail_item(next, kt0n, nkn, role_n, nk_all);
     f32x4 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -553,10 +577,11 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       };
       typedef __amdgpu_buffer_rsrc_t TRes;
       // stage region r of K tile kt into buffer buf from the tile resources ra / rb
+      // kt: absolute K tile (the item's kt0c + local index; the next item's kt0n + ...)
       auto pst = [&](int buf, __amdgpu_buffer_rsrc_t ra_, __amdgpu_buffer_rsrc_t rb_, int kt, int r) {
         if (CLIPK_GEMM_NOLOAD && it >= 1) return;  // diagnostic: first K tiles only
         const int base = buf * STAGE;
-        const int koff = (kt0 + kt) * ROWB;
+        const int koff = kt * ROWB;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
           if (r >= 2 || i == 0 || two_a) {
@@ -638,13 +663,14 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       constexpr bool PP2 = CLIPK_GEMM_PP2 == 1 || (CLIPK_GEMM_PP2 == 2 && BM == 256);
       static_assert(!PP2 || NFB == 2, "PP2 keeps all of B's fragments");
       if (it == 0) {
+        const int q0 = kt0c, q1 = kt0c + 1;
         if constexpr (PP2) {
-          pst(0, cra, crb, 0, 0); pst(0, cra, crb, 0, 2); pst(0, cra, crb, 0, 1); pst(0, cra, crb, 0, 3);
-          pst(1, cra, crb, 1, 0); pst(1, cra, crb, 1, 2);
+          pst(0, cra, crb, q0, 0); pst(0, cra, crb, q0, 2); pst(0, cra, crb, q0, 1); pst(0, cra, crb, q0, 3);
+          pst(1, cra, crb, q1, 0); pst(1, cra, crb, q1, 2);
           wait_ahead2();
         } else {
-          pst(0, cra, crb, 0, 0); pst(0, cra, crb, 0, 2); pst(0, cra, crb, 0, 1); pst(0, cra, crb, 0, 3);
-          pst(1, cra, crb, 1, 0); pst(1, cra, crb, 1, 3); pst(1, cra, crb, 1, 1);
+          pst(0, cra, crb, q0, 0); pst(0, cra, crb, q0, 2); pst(0, cra, crb, q0, 1); pst(0, cra, crb, q0, 3);
+          pst(1, cra, crb, q1, 0); pst(1, cra, crb, q1, 3); pst(1, cra, crb, q1, 1);
           wait_ahead();
         }
         G8_BAR();
@@ -653,11 +679,11 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       const TRes xra = rsrc_a(has_next ? (next / ntn) * BM : m0);
       const TRes xrb = rsrc_b(has_next ? (next % ntn) * BN : n0);
       if constexpr (PP2)
-      for (int kt = 0; kt < nk; ++kt, ++it) {
+      for (int kt = 0; kt < nkc; ++kt, ++it) {
         const int b = it & 1;
-        const bool in1 = kt + 1 < nk, in2 = kt + 2 < nk;
+        const bool in1 = kt + 1 < nkc, in2 = kt + 2 < nkc;
         const bool h1 = in1 || has_next, h2 = in2 || has_next;
-        const int k1 = in1 ? kt + 1 : kt + 1 - nk, k2 = in2 ? kt + 2 : kt + 2 - nk;
+        const int k1 = in1 ? kt0c + kt + 1 : kt0n + kt + 1 - nkc, k2 = in2 ? kt0c + kt + 2 : kt0n + kt + 2 - nkc;
         const TRes ra1 = in1 ? cra : xra, rb1 = in1 ? crb : xrb;
         const TRes ra2 = in2 ? cra : xra, rb2 = in2 ? crb : xrb;
         if (CLIPK_GEMM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
@@ -689,11 +715,11 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         G8_BAR();
       }
       else
-      for (int kt = 0; kt < nk; ++kt, ++it) {
+      for (int kt = 0; kt < nkc; ++kt, ++it) {
         const int b = it & 1;
-        const bool in1 = kt + 1 < nk, in2 = kt + 2 < nk;
+        const bool in1 = kt + 1 < nkc, in2 = kt + 2 < nkc;
         const bool h1 = in1 || has_next, h2 = in2 || has_next;
-        const int k1 = in1 ? kt + 1 : kt + 1 - nk, k2 = in2 ? kt + 2 : kt + 2 - nk;
+        const int k1 = in1 ? kt0c + kt + 1 : kt0n + kt + 1 - nkc, k2 = in2 ? kt0c + kt + 2 : kt0n + kt + 2 - nkc;
         if (CLIPK_GEMM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         rd_a(b, 0); rd_b(b, 0);                 // phase 1: A0 x B0
         if (h1) pst(b ^ 1, cra, in1 ? crb : xrb, k1, 2);
@@ -729,6 +755,37 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         G8_BAR();
       }
       if (!lag) G8_BAR();  // both wave rows level again: the epilogues run side by side
+      if constexpr (TAIL) {
+        // The pair's fp32 accumulators, lane-major per (wave, sub-tile) (1 KB per instruction),
+        // and its flag travel with sc1 (write-through past the XCD's L2; loads sc0 | sc1, from the
+        // coherent point): correct whichever XCDs the two blocks run on, with no L2 write-back.
+        // A store is counted by vmcnt until it is acknowledged, so the data is out before the
+        // flag. The wait is bounded (~0.1 s): a lost flag gives wrong numbers, never a hang.
+        const int pr = tile - tail_g;
+        const __amdgpu_buffer_rsrc_t frs = tile_rsrc(pr >= 0 ? (const void*)(g.tail_flags + pr) : nullptr, 4);
+        if (role == 1) {
+          const __amdgpu_buffer_rsrc_t wrs =
+              tile_rsrc(reinterpret_cast<f32x4*>(g.tail_ws) + (size_t)pr * (NW * TM * TN * 64),
+                        (long long)NW * TM * TN * 64 * 16);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), wrs,
+                                                     (((w * TM + i) * TN + j) * 64 + lane) * 16, 0, 16);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          G8_BAR();
+          if (threadIdx.x == 0) __builtin_amdgcn_raw_buffer_store_b32(1u, frs, 0, 0, 16);
+        } else if (role == 2) {
+          if (threadIdx.x == 0) {
+            for (int spin = 0; spin < (1 << 22); ++spin) {
+              if (__builtin_amdgcn_raw_buffer_load_b32(frs, 0, 0, 17) != 0u) break;
+              __builtin_amdgcn_s_sleep(2);
+            }
+          }
+          G8_BAR();
+        }
+      }
     } else
     // group 0's operands are loaded at the top of the last K step (its MFMAs hide them)
     for (int kt = 0; kt < nk; ++kt, ++it) {
@@ -801,6 +858,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
     // on both the write and the read-back side).
     if (stp && ti < STAMP_TILES) stp[3 + 3 * ti] = __builtin_amdgcn_s_memrealtime();
     static_assert(TN == 4, "epilogue assumes 64 columns per wave");
+    if (!TAIL || role != 1) {
     float bia[CW];
 #pragma unroll
     for (int c = 0; c < CW; ++c) bia[c] = 0.f;
@@ -832,6 +890,12 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
     if constexpr (EPI == CLIPK_EPI_BIAS_QGELU)
       ro2 = tile_rsrc(g.out2 ? (const TO*)g.out2 + (size_t)m0 * g.ldo : nullptr,
                       g.out2 ? rows_ok * g.ldo * (long long)sizeof(TO) : 0);
+    [[maybe_unused]] __amdgpu_buffer_rsrc_t prs = tile_rsrc(nullptr, 0);
+    if constexpr (TAIL) {
+      const int pr = tile - tail_g;
+      if (role == 2) prs = tile_rsrc(reinterpret_cast<f32x4*>(g.tail_ws) + (size_t)pr * (NW * TM * TN * 64),
+                                     (long long)NW * TM * TN * 64 * 16);
+    }
 #pragma unroll
     for (int d = 1; d < XD; ++d) load_ext(d, extq[d]);
 #pragma unroll
@@ -841,6 +905,15 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
 #pragma unroll
       for (int q = 0; q < NQ; ++q) ext[q] = extq[i % XD][q];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous group's read-back done
+      if constexpr (TAIL) {
+        // a split tail's second half: + the first half's accumulators (a resource that is empty
+        // unless this tile combines: out-of-range loads return 0, no branch around acc -- a
+        // branch there made hipcc keep two copies of the accumulators and spill)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     prs, (((w * TM + i) * TN + j) * 64 + lane) * 16, 0, 17));
+      }
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         *reinterpret_cast<f32x4*>(scr + fr * 64 + (((4 * j + fq) ^ fr) << 2)) = acc[i][j];
@@ -907,6 +980,15 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       if (i + XD < TM) load_ext(i + XD, extq[i % XD]);  // this group's slot is free again
       if (i + 2 < TM) load_ln(i + 2, i & 1);
     }
+    }  // epilogue (skipped by a split tail's first half)
+    if constexpr (TAIL) {
+      if (role == 2) {  // every wave has read the partial (its epilogue consumed it): clear the flag
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        G8_BAR();
+        if (threadIdx.x == 0)
+          __builtin_amdgcn_raw_buffer_store_b32(0u, tile_rsrc(g.tail_flags + (tile - tail_g), 4), 0, 0, 16);
+      }
+    }
     if (stp && ti < STAMP_TILES) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       stp[4 + 3 * ti] = __builtin_amdgcn_s_memrealtime();
@@ -917,6 +999,9 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       break;
     }
     tile = next;
+    kt0c = kt0n;
+    nkc = nkn;
+    role = role_n;
     if constexpr (!PP) {
       // the K loop left `it` one past this tile's last step: buffer it & 1 holds the
       // next tile's prefetched first stage
@@ -1040,8 +1125,44 @@ static bool try_pp(const GemmArgs& g, int nwg, hipStream_t st) {
   return false;
 }
 
+// Split tail (caller workspace, clipk_gemm_ws): 256x256 ping-pong tiles when the grid of G = 256
+// blocks would run 1 < rounds <= 1.5 -- the N = 512 text GEMMs at 47k rows: 370 tiles, where
+// the 192-row tiles take 2 rounds -- with the tiles past the first round cut in two K halves
+// on paired blocks (GemmArgs::tail_ws). EPI_NONE and the 16-bit residual epilogue (the N = 512
+// producers / input-grad GEMMs of the text encoder).
+constexpr int kTailPairs = 128;  // max pairs (G / 2)
+constexpr size_t kTailPairBytes = 8 * 64 * 64 * 16;  // 8 waves x 32 sub-tiles x 64 lanes x 16 B
+static size_t tail_ws_bytes() { return kTailPairs * kTailPairBytes + kTailPairs * sizeof(unsigned); }
+static int tail_mode() {  // knob CLIPK_GEMM_TAIL=0: off
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLIPK_GEMM_TAIL");
+    v = e ? atoi(e) : 1;
+  }
+  return v;
+}
+template <typename T, typename TO, typename TX, int EPI, int LNM>
+static bool try_tail(const GemmArgs& g, hipStream_t st) {
+  constexpr bool ok_epi = EPI == CLIPK_EPI_NONE || (EPI == CLIPK_EPI_BIAS_RES && sizeof(TX) == 2);
+  if constexpr (!CLIPK_GEMM_PP || sizeof(T) != 2 || sizeof(TO) != 2 || !ok_epi) {
+    return false;
+  } else {
+    if (!g.tail_ws || !tail_mode() || g.N % 256 || g.K * (int)sizeof(T) < 4 * GEMM_ROWB) return false;
+    const int G = (num_cus() / 16) * 16;
+    const int nt = ((g.M + 255) / 256) * (g.N / 256);
+    if (G < 16 || G / 2 > kTailPairs || !(nt > G && nt - G <= G / 2)) return false;
+    hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 256, 2, 4, true, GEMM_ROWB, 2, false, true, LNM, true>),
+                       dim3(G), dim3(512), 0, st, g);
+    return true;
+  }
+}
+
 template <typename T, typename TO, typename TX, int EPI, int LNM = 0>
 static int launch_gemm(const GemmArgs& g, hipStream_t st) {
+  if (try_tail<T, TO, TX, EPI, LNM>(g, st)) {
+    CLIPK_CHECK_LAUNCH();
+    return CLIPK_OK;
+  }
   const int cfg = pick_cfg(g.M, g.N, (int)sizeof(T));
   const_cast<GemmArgs&>(g).stamp = gemm_stamp_buf();
   if (g_skew < 0) {
@@ -1242,11 +1363,36 @@ static int dispatch_out(int out_dtype, int epi, int aux_dtype, const GemmArgs& g
 
 using namespace clipk;
 
+namespace clipk {
+static int gemm_entry(int in_dtype, int out_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B,
+                      int ldb, const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
+                      const void* aux, int aux_dtype, int ldaux, void* ws, void* stream);
+}
+
 extern "C" int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, int K,
                           const void* A, int lda, const void* B, int ldb,
                           const float* bias, const void* res, int ldr,
                           void* out, int ldo, void* out2, const void* aux, int aux_dtype,
                           int ldaux, void* stream) {
+  return gemm_entry(in_dtype, out_dtype, epi, M, N, K, A, lda, B, ldb, bias, res, ldr, out, ldo, out2, aux,
+                    aux_dtype, ldaux, nullptr, stream);
+}
+
+extern "C" size_t clipk_gemm_ws_bytes(void) { return tail_ws_bytes(); }
+
+extern "C" int clipk_gemm_ws(int in_dtype, int out_dtype, int epi, int M, int N, int K, const void* A, int lda,
+                             const void* B, int ldb, const float* bias, const void* res, int ldr, void* out, int ldo,
+                             void* out2, const void* aux, int aux_dtype, int ldaux, void* ws, size_t ws_bytes,
+                             void* stream) {
+  if (ws && ws_bytes < tail_ws_bytes()) return CLIPK_EWORKSPACE;
+  return gemm_entry(in_dtype, out_dtype, epi, M, N, K, A, lda, B, ldb, bias, res, ldr, out, ldo, out2, aux,
+                    aux_dtype, ldaux, ws, stream);
+}
+
+namespace clipk {
+static int gemm_entry(int in_dtype, int out_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B,
+                      int ldb, const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
+                      const void* aux, int aux_dtype, int ldaux, void* ws, void* stream) {
   if (!A || !B || !out) return CLIPK_EINVAL;
   const bool ag = (epi & CLIPK_A_QGELU) != 0;
   epi &= ~CLIPK_A_QGELU;
@@ -1262,6 +1408,10 @@ extern "C" int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, in
   if (epi == CLIPK_EPI_DQGELU && (!aux || ldaux < N || ldaux % 4)) return CLIPK_EINVAL;
   GemmArgs g{(const char*)A, (const char*)B, M, N, K, lda, ldb, bias, res, ldr, out, ldo, out2, aux,
              ldaux, nullptr, 1, 0};
+  if (ws) {  // split-tail workspace: partials, then the pair flags (zero between launches)
+    g.tail_ws = (float*)ws;
+    g.tail_flags = (unsigned*)((char*)ws + kTailPairs * kTailPairBytes);
+  }
   hipStream_t st = (hipStream_t)stream;
   switch (in_dtype) {
     case CLIPK_F16: return dispatch_out<f16>(out_dtype, epi, aux_dtype, g, st, ag);
@@ -1271,6 +1421,7 @@ extern "C" int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, in
     default: return CLIPK_EDTYPE;
   }
 }
+}  // namespace clipk
 
 extern "C" int clipk_split_pack(int N, int K, const float* W, int ldw, void* out, void* stream) {
   if (!W || !out) return CLIPK_EINVAL;
@@ -1293,10 +1444,25 @@ static int dispatch_ln(int epi, const GemmArgs& g, hipStream_t st) {
 
 // LayerNorm folded into the text GEMMs (include/clipk.h): statistics partials out (EPI_BIAS_RES)
 // or colsum + per-row (rstd, -rstd * mean) in (EPI_BIAS / EPI_BIAS_QGELU); 16-bit in and out.
+extern "C" int clipk_gemm_ln_ws(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B,
+                                int ldb, const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
+                                float* stats, const float* colsum, const float* rnb, void* ws, size_t ws_bytes,
+                                void* stream);
+
 extern "C" int clipk_gemm_ln(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B,
                              int ldb, const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
                              float* stats, const float* colsum, const float* rnb, void* stream) {
+  return clipk_gemm_ln_ws(in_dtype, epi, M, N, K, A, lda, B, ldb, bias, res, ldr, out, ldo, out2, stats, colsum, rnb,
+                          nullptr, 0, stream);
+}
+
+// clipk_gemm_ln with the split-tail workspace of clipk_gemm_ws (the LN-statistics producers)
+extern "C" int clipk_gemm_ln_ws(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B,
+                                int ldb, const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
+                                float* stats, const float* colsum, const float* rnb, void* ws, size_t ws_bytes,
+                                void* stream) {
   if (!A || !B || !out || !bias) return CLIPK_EINVAL;
+  if (ws && ws_bytes < tail_ws_bytes()) return CLIPK_EWORKSPACE;
   if (in_dtype != CLIPK_F16 && in_dtype != CLIPK_BF16) return CLIPK_EDTYPE;
   if (!colsum) {  // producer: the statistics partials of the output
     if (!stats || rnb || epi != CLIPK_EPI_BIAS_RES || !res || ldr < N || ldr % 8) return CLIPK_EINVAL;
@@ -1308,6 +1474,10 @@ extern "C" int clipk_gemm_ln(int in_dtype, int epi, int M, int N, int K, const v
   if (lda < K || ldb < K || lda % 8 || ldb % 8 || ldo < N || ldo % 8) return CLIPK_ESHAPE;
   GemmArgs g{(const char*)A, (const char*)B, M, N, K, lda, ldb, bias, res, ldr, out, ldo, out2, nullptr,
              0, nullptr, 1, 0, 0, stats, colsum, reinterpret_cast<const f32x2*>(rnb)};
+  if (ws) {
+    g.tail_ws = (float*)ws;
+    g.tail_flags = (unsigned*)((char*)ws + kTailPairs * kTailPairBytes);
+  }
   hipStream_t st = (hipStream_t)stream;
   return in_dtype == CLIPK_F16 ? dispatch_ln<f16>(epi, g, st) : dispatch_ln<bf16>(epi, g, st);
 }

@@ -35,6 +35,11 @@ def _need(t, name, dtype=None, cuda=True):
     return t
 
 
+def gemm_ws(device):
+    """A zeroed workspace for clipk_gemm_ws (the split-tail partials and pair flags)."""
+    return torch.zeros(int(N.load().clipk_gemm_ws_bytes()), dtype=torch.uint8, device=device)
+
+
 def split_pack(w):
     """clipk_split_pack: fp32 weight [N, K] -> its split-fp16 packing for PREC fp32s
     (SPLIT_SCALE * w as fp16 hi + lo parts, 4 bytes per element; int32 storage [N, K])."""
@@ -51,7 +56,7 @@ def split_pack(w):
 
 
 def gemm(a, b, epi=N.EPI_NONE, out_dtype=torch.float32, bias=None, res=None, aux=None,
-         want_out2=False, out=None):
+         want_out2=False, out=None, ws=None):
     """out[M,N] = epi(a[M,K] @ b[N,K]^T); returns out (and out2 for EPI_BIAS_QGELU). With a
     fp32 and b an int32 split_pack(...) weight: the fp32-class split-fp16 GEMM (CLIPK_F32S)."""
     _need(a, "A")
@@ -70,9 +75,12 @@ def gemm(a, b, epi=N.EPI_NONE, out_dtype=torch.float32, bias=None, res=None, aux
         _need(res, "res", torch.float32 if out.dtype == torch.float32 else out.dtype)
     if aux is not None:
         _need(aux, "aux")
-    N.call("clipk_gemm", N.F32S if split else DT[a.dtype], DT[out.dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias),
-           _p(res), Nn, _p(out), Nn, _p(out2), _p(aux), DT[aux.dtype] if aux is not None else 0, Nn,
-           _stream())
+    args = (N.F32S if split else DT[a.dtype], DT[out.dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias),
+            _p(res), Nn, _p(out), Nn, _p(out2), _p(aux), DT[aux.dtype] if aux is not None else 0, Nn)
+    if ws is not None:  # clipk_gemm_ws: split-tail workspace (uint8, zeroed flags; gemm_ws())
+        N.call("clipk_gemm_ws", *args, _p(ws), ws.numel(), _stream())
+    else:
+        N.call("clipk_gemm", *args, _stream())
     return (out, out2) if want_out2 else out
 
 

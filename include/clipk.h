@@ -78,6 +78,21 @@ int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, int K,
                void* out, int ldo, void* out2, const void* aux, int aux_dtype, int ldaux,
                void* stream);
 
+/* clipk_gemm with a caller workspace (ws_bytes >= clipk_gemm_ws_bytes(); ws NULL: clipk_gemm):
+ * when a 256x256 grid would take between 1 and 1.5 rounds of the CUs (the N = 512 text GEMMs
+ * at ~47k rows), its tiles past the first round run as two K halves on paired blocks of one XCD
+ * (the first half's fp32 partial through ws, a release / acquire flag pair), so the second
+ * round takes half a tile instead of a whole one. 16-bit in / out, EPI_NONE or the 16-bit
+ * residual epilogue; other calls behave as clipk_gemm. The flags at the end of ws must be zero
+ * before a call (each call leaves them zero); the two K halves are summed in a fixed order
+ * (deterministic), which differs from the single-tile order in the last bits. */
+size_t clipk_gemm_ws_bytes(void);
+int clipk_gemm_ws(int in_dtype, int out_dtype, int epi, int M, int N, int K,
+                  const void* A, int lda, const void* B, int ldb,
+                  const float* bias, const void* res, int ldr,
+                  void* out, int ldo, void* out2, const void* aux, int aux_dtype, int ldaux,
+                  void* ws, size_t ws_bytes, void* stream);
+
 /* fp32-class GEMM on the 16-bit MFMA (PREC "fp32s"; the reference runs these Linear layers in
  * fp32, PromptSRC/clip/model.py:171-177, 699). clipk_split_pack stores W [N, K] (fp32, row
  * stride ldw) as CLIPK_SPLIT_SCALE * W split into fp16 parts hi = fp16(x), lo = fp16(x - hi):
@@ -124,6 +139,10 @@ int clipk_gemm_ln(int in_dtype, int epi, int M, int N, int K, const void* A, int
                   float* stats, const float* colsum, const float* rnb, void* stream);
 int clipk_ln_stats_merge(int rows, int width, const float* stats, float* mean, float* rstd, float* rnb,
                          void* stream);
+/* clipk_gemm_ln with the split-tail workspace of clipk_gemm_ws (same ws contract). */
+int clipk_gemm_ln_ws(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B, int ldb,
+                     const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
+                     float* stats, const float* colsum, const float* rnb, void* ws, size_t ws_bytes, void* stream);
 
 /* Benchmark knob: force the 16-bit GEMM tile configuration (0: 128x128, 1: 256x256
  * (persistent above 2 x CUs tiles), 2: 256x128, 3: 256x256 non-persistent, 6: 192x256;

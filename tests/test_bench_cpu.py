@@ -46,3 +46,22 @@ def test_metric_label_follows_arch():
     assert bench.metric_name("ViT-B/16") == \
         "CoCoOp ViT-B/16 16-shot train-step images/sec at 1/2/4/8 GPUs; eval images/sec"
     assert "ViT-L/14@336px" in bench.metric_name("ViT-L/14@336px")
+
+
+def test_kernel_table_bound_from_intensity():
+    """Each kernel class's roofline bound comes from its own FLOP/byte ratio against the ridge
+    point (peak / 8 TB/s), not a fixed label: a K = 512 GEMM whose bytes outweigh its FLOPs is
+    HBM-bound, a K = 2,048 one MFMA-bound, attention / LayerNorm (no FLOPs counted) HBM-bound."""
+    sites = {  # site: (total ms, launches, flops, bytes)
+        "text.out_fwd": (0.5, 12, 12 * 24.7e9, 12 * 150e6),     # 165 FLOP/B < 312
+        "text.fc_dx": (1.0, 12, 12 * 98.9e9, 12 * 200e6),       # 495 FLOP/B > 312
+        "text.attn_bwd": (1.0, 12, 0.0, 12 * 350e6),
+    }
+    t = bench.kernel_table(sites, 1, "fp16")
+    assert t["gemm_out_fwd"]["bound"] == "hbm"
+    assert abs(t["gemm_out_fwd"]["roof_frac"] - t["gemm_out_fwd"]["hbm_frac"]) < 1e-9
+    assert t["gemm_dx_n512"]["bound"] == "mfma"
+    assert abs(t["gemm_dx_n512"]["roof_frac"] - t["gemm_dx_n512"]["mfma_frac"]) < 1e-9
+    assert t["attn_bwd"]["bound"] == "hbm"
+    r = bench.roofline_of(t, "fp16")
+    assert r["kernel_class"] == "gemm_dx_n512" and r["bound"] == "mfma"

@@ -423,6 +423,37 @@ def test_gemm_split_fp32_class(dev, M, Nn, K):
     assert e_none * 50 < e16
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("K", [256, 512, 1536, 2048])
+@pytest.mark.parametrize("M", [47160, 33000, 45000])
+def test_gemm_split_tail(dev, dtype, K, M):
+    """clipk_gemm_ws (split tail: 256x256 tiles, the tiles past the first round as two K halves on
+    paired blocks, partial + flag through the workspace) vs a torch fp32 reference and vs plain
+    clipk_gemm: EPI_NONE and the 16-bit residual epilogue at the N = 512 text shapes (47,160 rows:
+    370 tiles on 256 CUs). Reruns are bitwise equal and the pair flags are left zero."""
+    lib = N.load()
+    Nn = 512
+    g = torch.Generator(device="cpu").manual_seed(M + K)
+    A = torch.randn(M, K, generator=g).to(dev).to(dtype)
+    B = (torch.randn(Nn, K, generator=g) / math.sqrt(K)).to(dev).to(dtype)
+    bias = torch.randn(Nn, generator=g).to(dev)
+    res = torch.randn(M, Nn, generator=g).to(dev).to(dtype)
+    ws = ops.gemm_ws(dev)
+    nflag = 128 * 4
+    ref = A.float() @ B.float().t()
+    o1 = ops.gemm(A, B, N.EPI_NONE, dtype, ws=ws)
+    o2 = ops.gemm(A, B, N.EPI_NONE, dtype, ws=ws)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+    assert int(ws[-nflag:].sum()) == 0
+    close(o1, ref, dtype, f"tail none K{K}")
+    plain = ops.gemm(A, B, N.EPI_NONE, dtype)
+    close(o1, plain, dtype, f"tail vs plain K{K}")
+    r1 = ops.gemm(A, B, N.EPI_BIAS_RES, dtype, bias=bias, res=res, ws=ws)
+    close(r1, ref + bias + res.float(), dtype, f"tail res K{K}")
+    assert int(ws[-nflag:].sum()) == 0
+
+
 @pytest.mark.parametrize("reduction", ["mean", "sum", "none"])
 def test_focal_loss_reductions(dev, reduction):
     """MultiClassFocalLoss(reduction=...) (PromptSRC/trainers/coop.py:131-163): loss and
