@@ -23,13 +23,16 @@ The JSON line also carries (rank 0, N=1 unless noted):
   (GEMMs: fraction of the MFMA peak; attention / LayerNorm: GB/s and fraction of the HBM peak);
 * ``eval_images_per_sec`` over --eval-images (default 50,000: SURVEY §8(d)'s full ImageNet-val
   size) distinct synthetic images resident in HBM, test batch 100, sharded over the ranks;
-* ``fp32``: train / eval images/sec at PREC fp32 (the 1e-3-logit parity path);
 * ``batch1``: train images/sec at 1 image per step (the reference CoCoOp config batch size);
 * ``coop``: BASELINE config 2 -- CoOp n_ctx 16, ViT-B/16, 1000 classes, batch 32: train and
   eval images/sec;
 * ``batch1_class_shard`` (N > 1): the reference's CoCoOp batch of 1 image per step with its
   1,000 classes sharded over the N ranks (SURVEY §8(e) Option B: logit all-gather + SUM
   all-reduce of the prompt gradients), strong scaling of that step;
+* ``config4`` / ``config5`` (N = 1): BASELINE configs 4 (CoOp ViT-L/14 bf16, 32 images/step) and 5
+  (CoCoOp ViT-L/14@336px bf16, 8 images/step) per GPU, train and eval images/sec;
+* ``fp32s`` / ``fp32``: the fp32-class precisions (the north-star 1e-3 logit bar) at the headline
+  workload: train over 10 steps, eval over 5,000 images, each with its own roofline;
 * ``cpu_baseline``: the oracle (fp32 restatement) on the host cores, with nproc stated, and the
   reference's own CPU path at 1,000 classes as measured in the build container
   (tools/ref_cpu_timing.py -> profiles/r03_ref_cpu_timing.jsonl; the reference does not travel
@@ -94,8 +97,8 @@ def reference_cpu(arch, classes):
 PEAK = {"fp16": 2500.0, "bf16": 2500.0, "amp": 2500.0, "fp32": 157.3, "fp32s": 2500.0 / 3}
 HBM_PEAK_GBS = 8000.0  # HBM3E, MI355X_MICROARCH.md
 # the latest round's PMC passes (tools/pmc_bench.sh), else the previous round's
-PMC_FILE = next((f for f in (os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r03_pmc", "r02_pmc"))
-                 if os.path.exists(f)), os.path.join(ROOT, "profiles", "r03_pmc", "traffic.json"))
+PMC_FILE = next((f for f in (os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r04_pmc", "r03_pmc"))
+                 if os.path.exists(f)), os.path.join(ROOT, "profiles", "r04_pmc", "traffic.json"))
 
 # kernel classes of the step: launch sites that run the same kernel instantiation (rocprofv3
 # kernel-name key, for the PMC traffic lookup) -- the text GEMMs by role, attention, LN. Each
@@ -415,6 +418,7 @@ def main():
     ap.add_argument("--prof-steps", type=int, default=3, help="steps after the timed ones with per-site hipEvents")
     ap.add_argument("--no-prof", action="store_true", help="no per-site profiling steps")
     ap.add_argument("--no-extra", action="store_true", help="skip the fp32 / batch-1 lines")
+    ap.add_argument("--no-configs", action="store_true", help="skip the BASELINE config 4 / 5 lines")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -483,6 +487,11 @@ def main():
     torch.cuda.empty_cache()
     if not args.no_extra and args.arch in ("ViT-L/14", "ViT-L/14@336px"):
         out["config4" if args.arch == "ViT-L/14" else "config5"] = baseline_config_line(args, dev, rank, world)
+    elif not args.no_extra and not args.no_configs and world == 1:
+        # BASELINE configs 4 and 5 per GPU beside the headline (their own archs, bf16)
+        for key, arch in (("config4", "ViT-L/14"), ("config5", "ViT-L/14@336px")):
+            out[key] = baseline_config_line(argparse.Namespace(**{**vars(args), "arch": arch}), dev, rank, world,
+                                            n_eval=2000)
     if not args.no_extra and world > 1:
         # the reference's CoCoOp batch (1 image / step) with the classes sharded over the ranks
         tr1, dm1 = build_trainer(args, args.prec, 1, dev, 0, class_shard=True)

@@ -37,6 +37,7 @@ SIGNATURES = {
     "clipk_gemm_splitk_ws_bytes": (_S, [_I, _I, _I]),
     "clipk_gemm_splitk": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P, _S, _P]),
     "clipk_gemm_set_config": (_I, [_I]),
+    "clipk_gemm_set_tail": (_I, [_I]),
     "clipk_split_pack": (_I, [_I, _I, _P, _I, _P, _P]),
     "clipk_gemm_ln": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P]),
     "clipk_ln_stats_merge": (_I, [_I, _I, _P, _P, _P, _P, _P]),

@@ -1133,13 +1133,18 @@ static bool try_pp(const GemmArgs& g, int nwg, hipStream_t st) {
 constexpr int kTailPairs = 128;  // max pairs (G / 2)
 constexpr size_t kTailPairBytes = 8 * 64 * 64 * 16;  // 8 waves x 32 sub-tiles x 64 lanes x 16 B
 static size_t tail_ws_bytes() { return kTailPairs * kTailPairBytes + kTailPairs * sizeof(unsigned); }
-static int tail_mode() {  // knob CLIPK_GEMM_TAIL=0: off
-  static int v = -1;
-  if (v < 0) {
+// Off by default: measured slower on the headline step than the 192x256 tiles it replaces
+// (profiles/r04e/ab_split_tail.txt: 10.67 -> 11.39 ms/step; the N = 512 input-grad class 2.28 ->
+// 2.46 ms, the K = 512 out_proj 0.52 -> 0.85 ms -- the 256x256 tile does not run the predicted
+// 1.2x the 192-row tile's rate at N = 512, and the halves' partial exchange sits in the epilogue).
+// Knob CLIPK_GEMM_TAIL=1 (or clipk_gemm_set_tail(1)) turns it on.
+static int g_tail = -1;
+static int tail_mode() {
+  if (g_tail < 0) {
     const char* e = getenv("CLIPK_GEMM_TAIL");
-    v = e ? atoi(e) : 1;
+    g_tail = e ? atoi(e) : 0;
   }
-  return v;
+  return g_tail;
 }
 template <typename T, typename TO, typename TX, int EPI, int LNM>
 static bool try_tail(const GemmArgs& g, hipStream_t st) {
@@ -1623,6 +1628,13 @@ extern "C" int clipk_gemm_stamps(void* host, size_t bytes) {
   if (!g_stamp || !host || bytes < need) return CLIPK_EINVAL;
   if (hipDeviceSynchronize() != hipSuccess) return (int)hipGetLastError();
   if (hipMemcpy(host, g_stamp, need, hipMemcpyDeviceToHost) != hipSuccess) return (int)hipGetLastError();
+  return CLIPK_OK;
+}
+
+// Test / benchmark knob: the split tail of clipk_gemm_ws on (1) or off (0).
+extern "C" int clipk_gemm_set_tail(int on) {
+  if (on != 0 && on != 1) return CLIPK_EINVAL;
+  g_tail = on;
   return CLIPK_OK;
 }
 

@@ -78,8 +78,9 @@ int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, int K,
                void* out, int ldo, void* out2, const void* aux, int aux_dtype, int ldaux,
                void* stream);
 
-/* clipk_gemm with a caller workspace (ws_bytes >= clipk_gemm_ws_bytes(); ws NULL: clipk_gemm):
- * when a 256x256 grid would take between 1 and 1.5 rounds of the CUs (the N = 512 text GEMMs
+/* clipk_gemm with a caller workspace (ws_bytes >= clipk_gemm_ws_bytes(); ws NULL: clipk_gemm).
+ * With the split tail on (clipk_gemm_set_tail / CLIPK_GEMM_TAIL=1; off by default): when a
+ * 256x256 grid would take between 1 and 1.5 rounds of the CUs (the N = 512 text GEMMs
  * at ~47k rows), its tiles past the first round run as two K halves on paired blocks of one XCD
  * (the first half's fp32 partial through ws, a release / acquire flag pair), so the second
  * round takes half a tile instead of a whole one. 16-bit in / out, EPI_NONE or the 16-bit
@@ -148,6 +149,9 @@ int clipk_gemm_ln_ws(int in_dtype, int epi, int M, int N, int K, const void* A, 
  * (persistent above 2 x CUs tiles), 2: 256x128, 3: 256x256 non-persistent, 6: 192x256;
  * -1 = automatic by shape; other values: CLIPK_EINVAL). Not needed for normal use. */
 int clipk_gemm_set_config(int cfg);
+/* Test / benchmark knob: clipk_gemm_ws's split tail on (1) or off (0, default: measured slower
+ * than the 192x256 tiles on the headline step). */
+int clipk_gemm_set_tail(int on);
 
 /* Image preprocessing (Dassl/torchvision Resize+CenterCrop / RandomResizedCrop+flip,
  * ToTensor, Normalize; transforms.py:206-354): Pillow-exact bicubic resampling of a crop

@@ -432,6 +432,14 @@ def test_gemm_split_tail(dev, dtype, K, M):
     clipk_gemm: EPI_NONE and the 16-bit residual epilogue at the N = 512 text shapes (47,160 rows:
     370 tiles on 256 CUs). Reruns are bitwise equal and the pair flags are left zero."""
     lib = N.load()
+    N.check(lib.clipk_gemm_set_tail(1), "clipk_gemm_set_tail")  # off by default (DESIGN §5)
+    try:
+        _split_tail_case(dev, dtype, K, M)
+    finally:
+        lib.clipk_gemm_set_tail(0)
+
+
+def _split_tail_case(dev, dtype, K, M):
     Nn = 512
     g = torch.Generator(device="cpu").manual_seed(M + K)
     A = torch.randn(M, K, generator=g).to(dev).to(dtype)

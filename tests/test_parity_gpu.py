@@ -417,3 +417,29 @@ def test_config5_cocoop_vitl14_336_c1000_vs_oracle(dev, prec):
     assert out["packed"] and out["P"] == 5 and out["prefix_input"]
     np.testing.assert_array_equal(out["ctx0"], ref["ctx0"])
     _gate(ref, out, prec, "config5")
+
+
+@pytest.mark.parametrize("prec", ["fp16", "bf16"])
+def test_headline_batch8_split_tail_matches_plain_tiles(dev, prec):
+    """The benchmark step itself (CoCoOp ViT-B/16, C = 1,000, B = 8 images: 47,160 packed text
+    rows, where the N = 512 GEMMs take the split tail -- 256x256 tiles, the 114 tiles past the
+    first round as two K halves on paired blocks): logits, loss and every prompt gradient with
+    the tail on vs off (clipk_gemm_set_tail), which differ only in the fp32 summation order of
+    the tail tiles -- within the 16-bit rounding of the activations (the oracle parity of the
+    non-tail path at this workload's shape is test_headline_shape_vs_oracle)."""
+    from fsp_amd import _native as N
+    meta = {"arch": "ViT-B/16", "n_cls": 1000, "batch": 8, "n_ctx": 4, "ctx_init": "a photo of a", "focal": 0}
+    lib = N.load()
+    outs = {}
+    try:
+        for on in (1, 0):
+            N.check(lib.clipk_gemm_set_tail(on), "clipk_gemm_set_tail")
+            outs[on] = run_native(meta, {"ctx0": None, "tokenized": None}, prec, cocoop=True, dev=str(dev))
+    finally:
+        lib.clipk_gemm_set_tail(0)
+    a, b = outs[1], outs[0]
+    assert a["packed"]
+    tol = 2e-3 if prec == "fp16" else 1.5e-2
+    assert float(np.abs(a["logits"] - b["logits"]).max()) <= tol * 100.0
+    for k in [k for k in a if k.startswith("grad_")]:
+        assert cos_err(a[k].reshape(1, -1), b[k].reshape(1, -1)) <= tol, k
