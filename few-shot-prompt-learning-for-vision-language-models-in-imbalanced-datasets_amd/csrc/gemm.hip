@@ -1042,7 +1042,16 @@ static int pick_cfg(int M, int N, int esz) {
     // a big-tile grid under half the CUs (N = 512 at ~6k rows: CoCoOp at 1 image per step):
     // 128x128 tiles, 3x the blocks (B = 1 step: N = 512 GEMMs 1.06 + 0.52 + 0.22 -> 0.85 + 0.42
     // + 0.18 ms; N >= 1536 stay on the big tiles, which measured faster there)
-    if (((M + 191) / 192) * (N / 256) < cus / 2) return 0;
+    if (((M + 191) / 192) * (N / 256) < cus / 2) {
+      // knob CLIPK_GEMM_SMALL64 (A/B): 64x128 tiles where the 128x128 grid is one round or less
+      static int s64 = -1;
+      if (s64 < 0) {
+        const char* e = getenv("CLIPK_GEMM_SMALL64");
+        s64 = e ? atoi(e) : 0;
+      }
+      if (s64 && ((M + 127) / 128) * (N / 128) <= num_cus()) return 7;
+      return 0;
+    }
     const double w256 = ((M + 255) / 256) * (N / 256) / cus, w192 = ((M + 191) / 192) * (N / 256) / cus;
     const double e256 = w256 / __builtin_ceil(w256), e192 = w192 / __builtin_ceil(w192);
     // 192-row tiles only for a clear quantisation win: N = 512 at 47k rows (0.72 -> 0.96 of the
