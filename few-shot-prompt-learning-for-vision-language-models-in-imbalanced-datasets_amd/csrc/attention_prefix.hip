@@ -29,7 +29,7 @@
 namespace clipk {
 
 // tiles whose loads are issued together (template parameter; env CLIPK_PREFIX_*_BATCH)
-constexpr int kValuChunk = 16;                // units per wave, VALU kernels
+constexpr int kValuChunk = 8;                 // units per wave, fp32 kernels (16: one round of ~7 waves per CU at the bench shape)
 
 // Units per wave of the MFMA kernels (env CLIPK_PREFIX_FWD_CHUNK / _BWD_CHUNK, read once).
 static int chunk_env(const char* name, int def) {
@@ -766,14 +766,16 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_bwd_lds(int G, int P, in
 }
 
 // ------------------------------------------------------------------ fp32 kernels (PREC fp32 / fp32s)
-// One wave per (group, chunk of kValuChunk units, head); blocks of kF32Wpb waves share one
+// One wave per (group, chunk of kValuChunk units, head); blocks of WPB waves (f32_wpb) share one
 // (group, head), so the prefix K/V rows are staged into LDS once per block. Lane = 4 r + s: row
 // r of the unit (query in the forward and for dQ, key for dK / dV) and 16-column slice s of
 // the head; a dot product is 16 FMAs on the lane's slice plus a quad sum (2 DPP adds). K/V
 // (and, for the backward's key phases, Q / dO) rows are read from LDS, where the 16 lanes of
 // one slice read the same 64 B (a broadcast). All arithmetic fp32, the reference's
 // nn.MultiheadAttention math (model.py:183), exact softmax (online max / rescale, fwd).
-constexpr int kF32Wpb = 4;
+// waves per block (template WPB; knob CLIPK_F32ATTN_WPB: 2 (default), 4 or 8). fp32s headline
+// (profiles/r04h/): backward 2.86 -> 2.76 ms/step at 2 vs 4, forward equal, 8 no better
+static int f32_wpb() { static int c = chunk_env("CLIPK_F32ATTN_WPB", 2); return c == 4 || c == 8 ? c : 2; }
 
 // a wave's own LDS writes visible to its other lanes (program order on the LDS; no reordering
 // by the compiler across this point)
@@ -794,20 +796,22 @@ __device__ __forceinline__ void f32_unit(const int* __restrict__ tiles, const in
   first = u == 0 ? 0 : row_first[t0 + rr] - t0;
 }
 
-// block (g, h, chunk block kb): waves take chunks kb * kF32Wpb + w; stages the prefix K / V rows
+// block (g, h, chunk block kb): waves take chunks kb * WPB + w; stages the prefix K / V rows
 // of (g, h) (P <= 16 rows x 64 fp32) into sKp / sVp
+template <int WPB>
 __device__ __forceinline__ void f32_block(int H, int nchunk, int& g, int& h, int& k, int& w) {
-  const int nkb = (nchunk + kF32Wpb - 1) / kF32Wpb;
+  const int nkb = (nchunk + WPB - 1) / WPB;
   const int b = blockIdx.x;
   h = b % H;
   const int kb = (b / H) % nkb;
   g = b / (H * nkb);
   w = threadIdx.x >> 6;
-  k = kb * kF32Wpb + w;
+  k = kb * WPB + w;
 }
+template <int WPB>
 __device__ __forceinline__ void f32_stage_prefix(const float* __restrict__ qkv, size_t row0, int P, int ldq, int col,
                                                  int W, float* sKp, float* sVp) {
-  for (int i = threadIdx.x; i < 16 * 16; i += kF32Wpb * 64) {  // 16 rows x 16 float4
+  for (int i = threadIdx.x; i < 16 * 16; i += WPB * 64) {  // 16 rows x 16 float4
     const int j = i >> 4, c = i & 15;
     f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = kv;
     if (j < P) {
@@ -820,15 +824,16 @@ __device__ __forceinline__ void f32_stage_prefix(const float* __restrict__ qkv, 
   }
 }
 
-__global__ __launch_bounds__(kF32Wpb * 64) void attn_prefix_fwd_f32(
+template <int WPB>
+__global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
     int G, int P, int R, int ntiles, const int* __restrict__ tiles, const int* __restrict__ row_first, int H,
     int nchunk, const float* __restrict__ qkv, int ldq, float* __restrict__ out, int ldo, float* __restrict__ lse) {
   __shared__ CLIPK_LDS_ALIGN float sKp[16 * 64], sVp[16 * 64];
-  __shared__ CLIPK_LDS_ALIGN float sK[kF32Wpb][16 * 64], sV[kF32Wpb][16 * 64];
+  __shared__ CLIPK_LDS_ALIGN float sK[WPB][16 * 64], sV[WPB][16 * 64];
   int g, h, k, w;
-  f32_block(H, nchunk, g, h, k, w);
+  f32_block<WPB>(H, nchunk, g, h, k, w);
   const int W = H * 64;
-  f32_stage_prefix(qkv, (size_t)g * R, P, ldq, h * 64, W, sKp, sVp);
+  f32_stage_prefix<WPB>(qkv, (size_t)g * R, P, ldq, h * 64, W, sKp, sVp);
   __syncthreads();
   if (k >= nchunk) return;  // wave-uniform; no block barrier follows
   const int lane = threadIdx.x & 63, r = lane >> 2, s = lane & 3;
@@ -890,18 +895,19 @@ __global__ __launch_bounds__(kF32Wpb * 64) void attn_prefix_fwd_f32(
 // dK, dV over the unit's queries (the prefix unit's own keys ARE the prefix rows: accumulated).
 // Phase 3 (lane = prefix key): the prefix rows' dK, dV partial of this unit, accumulated over
 // the chunk in registers and written once per chunk (prefix_kv_reduce sums the chunks).
-__global__ __launch_bounds__(kF32Wpb * 64) void attn_prefix_bwd_f32(
+template <int WPB>
+__global__ __launch_bounds__(WPB * 64) void attn_prefix_bwd_f32(
     int G, int P, int R, int ntiles, const int* __restrict__ tiles, const int* __restrict__ row_first, int H,
     int nchunk, const float* __restrict__ qkv, int ldq, const float* __restrict__ o_fwd, int ldof,
     const float* __restrict__ dout, int lddo, const float* __restrict__ lse, float* __restrict__ dqkv, int lddq,
     float* __restrict__ part) {
   __shared__ CLIPK_LDS_ALIGN float sKp[16 * 64], sVp[16 * 64];
-  __shared__ CLIPK_LDS_ALIGN float sA[kF32Wpb][16 * 64], sB[kF32Wpb][16 * 64];  // K|V, then Q|dO
-  __shared__ CLIPK_LDS_ALIGN float sP[kF32Wpb][16 * 32], sS[kF32Wpb][16 * 32];
+  __shared__ CLIPK_LDS_ALIGN float sA[WPB][16 * 64], sB[WPB][16 * 64];  // K|V, then Q|dO
+  __shared__ CLIPK_LDS_ALIGN float sP[WPB][16 * 32], sS[WPB][16 * 32];
   int g, h, k, w;
-  f32_block(H, nchunk, g, h, k, w);
+  f32_block<WPB>(H, nchunk, g, h, k, w);
   const int W = H * 64;
-  f32_stage_prefix(qkv, (size_t)g * R, P, ldq, h * 64, W, sKp, sVp);
+  f32_stage_prefix<WPB>(qkv, (size_t)g * R, P, ldq, h * 64, W, sKp, sVp);
   __syncthreads();
   if (k >= nchunk) return;
   const int lane = threadIdx.x & 63, r = lane >> 2, s = lane & 3;
@@ -1075,9 +1081,15 @@ static int prefix_fwd(int G, int P, int R, int ntiles, const int* tiles, const i
     }
   } else {
     const int nchunk = n_chunks(ntiles, kValuChunk);
-    const long blocks = (long)G * ((nchunk + kF32Wpb - 1) / kF32Wpb) * H;
-    hipLaunchKernelGGL(attn_prefix_fwd_f32, dim3(blocks), dim3(64 * kF32Wpb), 0, st, G, P, R, ntiles, tiles,
-                       row_first, H, nchunk, (const float*)qkv, ldq, (float*)out, ldo, lse);
+    auto go = [&](auto kern, int wpb) {
+      const long blocks = (long)G * ((nchunk + wpb - 1) / wpb) * H;
+      hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * wpb), 0, st, G, P, R, ntiles, tiles, row_first, H, nchunk,
+                         (const float*)qkv, ldq, (float*)out, ldo, lse);
+    };
+    const int wpb = f32_wpb();
+    if (wpb == 2) go(attn_prefix_fwd_f32<2>, 2);
+    else if (wpb == 8) go(attn_prefix_fwd_f32<8>, 8);
+    else go(attn_prefix_fwd_f32<4>, 4);
   }
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
@@ -1124,10 +1136,16 @@ static int prefix_bwd(int G, int P, int R, int ntiles, const int* tiles, const i
     }
   } else {
     static_assert(mfma || (sizeof(T) == 4 && sizeof(TG) == 4), "fp32 backward");
-    const long blocks = (long)G * ((nchunk + kF32Wpb - 1) / kF32Wpb) * H;
-    hipLaunchKernelGGL(attn_prefix_bwd_f32, dim3(blocks), dim3(64 * kF32Wpb), 0, st, G, P, R, ntiles, tiles,
-                       row_first, H, nchunk, (const float*)qkv, ldq, (const float*)ofwd, ldof, (const float*)dout,
-                       lddo, lse, (float*)dqkv, lddq, part);
+    auto go = [&](auto kern, int wpb) {
+      const long blocks = (long)G * ((nchunk + wpb - 1) / wpb) * H;
+      hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * wpb), 0, st, G, P, R, ntiles, tiles, row_first, H, nchunk,
+                         (const float*)qkv, ldq, (const float*)ofwd, ldof, (const float*)dout, lddo, lse,
+                         (float*)dqkv, lddq, part);
+    };
+    const int wpb = f32_wpb();
+    if (wpb == 2) go(attn_prefix_bwd_f32<2>, 2);
+    else if (wpb == 8) go(attn_prefix_bwd_f32<8>, 8);
+    else go(attn_prefix_bwd_f32<4>, 4);
   }
   CLIPK_CHECK_LAUNCH();
   const int W = H * 64;
