@@ -99,18 +99,44 @@ __device__ __forceinline__ f32x4 mma(u32x4 a, u32x4 b, f32x4 c) {
 // ---- PREC fp32s (CLIPK_F32S): fp32-class products on the 16-bit MFMA.
 // 8 fp32 values (a lane's two 16-B fragment chunks, k = 8 fq .. 8 fq + 7) -> fp16 hi = fp16(x)
 // and lo = fp16(x - hi): hi + lo carries ~22 significant bits of x.
+// The lo part is one mixed-precision FMA per element: fp16(a * 1 - f32(h)) reads h straight
+// from the packed fp16 register and rounds once (exact: x - hi is representable in fp32), so
+// a pair costs 1 cvt_pk + 2 fma_mix instead of cvt_pk + 2 cvt + sub + cvt_pk (the split sits in
+// the ping-pong loop's memory segment, where its VALU count is on the critical path).
+#ifndef CLIPK_SPLIT_MIX
+#define CLIPK_SPLIT_MIX 1
+#endif
+__device__ __forceinline__ unsigned split_lo2(float a, float b, unsigned h) {
+  unsigned l;
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%3 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %2, 1.0, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(l)
+      : "v"(a), "v"(b), "v"(h));
+  return l;
+}
 __device__ __forceinline__ void split8(u32x4 a0, u32x4 a1, u32x4& hi, u32x4& lo) {
   const f32x4 x0 = __builtin_bit_cast(f32x4, a0), x1 = __builtin_bit_cast(f32x4, a1);
-  f16x8 h, l;
+  f16x8 h;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     h[c] = (f16)x0[c];
     h[4 + c] = (f16)x1[c];
+  }
+  hi = __builtin_bit_cast(u32x4, h);
+#if CLIPK_SPLIT_MIX == 0  // A/B knob: the cvt + sub + cvt form
+  f16x8 l;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
     l[c] = (f16)(x0[c] - (float)h[c]);
     l[4 + c] = (f16)(x1[c] - (float)h[4 + c]);
   }
-  hi = __builtin_bit_cast(u32x4, h);
   lo = __builtin_bit_cast(u32x4, l);
+  return;
+#endif
+  lo[0] = split_lo2(x0[0], x0[1], hi[0]);
+  lo[1] = split_lo2(x0[2], x0[3], hi[1]);
+  lo[2] = split_lo2(x1[0], x1[1], hi[2]);
+  lo[3] = split_lo2(x1[2], x1[3], hi[3]);
 }
 // a . b ~= hi(a) hi(b) + hi(a) lo(b) + lo(a) hi(b) (lo . lo ~ 2^-22 relative is dropped); the
 // weight's parts (packed, clipk_split_pack) are the instruction's A operand (swapped operands)

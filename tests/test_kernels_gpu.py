@@ -7,6 +7,7 @@ import os
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
@@ -421,6 +422,24 @@ def test_gemm_split_fp32_class(dev, M, Nn, K):
     e32 = ((ops.gemm(a, b, N.EPI_NONE).double() - ref).abs().max() / ref.abs().max()).item()
     print(f"split {M}x{Nn}x{K}: {e_none:.2e}  f32 MFMA: {e32:.2e}  fp16: {e16:.2e}")
     assert e_none * 50 < e16
+
+
+@pytest.mark.parametrize("M", [96, 1576, 47160])
+def test_gemm_split_parts_exact(dev, M):
+    """The in-register split itself, bit for bit: with B = I (packed hi = 64, lo = 0) every output
+    is 64 (hi + lo) / 64 with hi = fp16(x), lo = fp16(x - hi) -- exact in fp32 -- so the result
+    must equal the numpy split of A exactly, on the small-M, 128x128 and ping-pong tiles."""
+    K = 512
+    g = torch.Generator(device="cpu").manual_seed(M)
+    a = torch.randn(M, K, generator=g) * torch.exp2(torch.randint(-6, 7, (M, K), generator=g).float())
+    x = a.numpy()
+    hi = x.astype(np.float16)
+    lo = (x - hi.astype(np.float32)).astype(np.float16)
+    want = hi.astype(np.float32) + lo.astype(np.float32)
+    out = ops.gemm(a.to(dev), ops.split_pack(torch.eye(K).to(dev)), N.EPI_NONE).cpu().numpy()
+    bad = int((out != want).sum())
+    assert bad == 0, f"{bad} of {out.size} outputs differ from hi + lo"
+    assert np.abs(want - x).max() <= np.abs(x).max() * 2.0 ** -21
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
