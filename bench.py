@@ -106,8 +106,8 @@ PMC_FILE = next((f for f in (os.path.join(ROOT, "profiles", r, "traffic.json") f
 KERNELS = {
     "gemm_dx_n512": (["text.fc_dx", "text.qkv_dx", "text.out_dx"], "EPI_NONE 192x256"),
     "gemm_proj_fwd": (["text.proj_fwd"], "EPI_BIAS_RES N=512 K=2048"),
-    "gemm_dgelu": (["text.proj_dx_dgelu"], "EPI_DQGELU"),
-    "gemm_fc_fwd": (["text.fc_fwd"], "EPI_BIAS_QGELU N=2048 (h and QuickGELU(h); ln_2 folded)"),
+    "gemm_dgelu": (["text.proj_dx_dgelu"], "EPI_DQGELU | QGELU_DERIV (acc x the saved quickgelu')"),
+    "gemm_fc_fwd": (["text.fc_fwd"], "EPI_BIAS_QGELU | QGELU_DERIV N=2048 (QuickGELU(h) and quickgelu'(h); ln_2 folded)"),
     "gemm_qkv_fwd": (["text.qkv_fwd"], "EPI_BIAS N=1536 (ln_1 folded)"),
     "gemm_out_fwd": (["text.out_fwd"], "EPI_BIAS_RES N=512"),
     "attn_bwd": (["text.attn_bwd"], "attn_prefix_bwd_lds"),
@@ -119,7 +119,7 @@ KERNELS = {
              "vit.ln_fwd", "vit.ln_stats", "vit.eot_gather", "vit.head"], "ViT forward (all sites)"),
 }
 ROOF_PMC_KEY = {"gemm_dx_n512": "gemm_nt_kernelIDF16_DF16_fLi4ELi192ELi256",
-                "gemm_dgelu": "gemm_nt_kernelIDF16_DF16_DF16_Li3E",
+                "gemm_dgelu": "gemm_nt_kernelIDF16_DF16_DF16_Li6E",
                 "gemm_proj_fwd": "gemm_nt_kernelIDF16_DF16_DF16_Li1ELi192ELi256ELi2ELi4ELb1ELi128ELi2ELb0ELb1E",
                 "attn_bwd": "attn_prefix_bwd_lds"}
 

@@ -16,6 +16,7 @@ F32, F16, BF16, F32S = 0, 1, 2, 3  # F32S: fp32 activations x split-packed weigh
 SPLIT_SCALE = 64.0  # CLIPK_SPLIT_SCALE: clipk_split_pack stores SPLIT_SCALE * W
 EPI_BIAS, EPI_BIAS_RES, EPI_BIAS_QGELU, EPI_DQGELU, EPI_NONE = 0, 1, 2, 3, 4
 A_QGELU = 0x100  # OR-ed into epi: the GEMM consumes quickgelu(A) (include/clipk.h)
+QGELU_DERIV = 0x200  # OR-ed into epi: out2 = quickgelu' (EPI_BIAS_QGELU) / aux is quickgelu' (EPI_DQGELU)
 PROF_NONE, PROF_GEMM_FC, PROF_GEMM_ALL, PROF_ATTN, PROF_LN, PROF_GEMM_DGELU = 0, 1, 2, 3, 4, 5
 
 _P = ctypes.c_void_p

@@ -61,12 +61,13 @@ struct SplitScope {
 // text GEMMs' tiles past the first round run as K halves on paired blocks); its pair flags are
 // zeroed once per call.
 static thread_local void* t_gemm_ws = nullptr;
+bool gemm_tail_enabled();  // gemm.hip
 struct GemmWsScope {
   void* prev;
   int rc = CLIPK_OK;
   GemmWsScope(void* ws, hipStream_t st) : prev(t_gemm_ws) {
     t_gemm_ws = ws;
-    if (ws) {
+    if (ws && gemm_tail_enabled()) {  // no split tail (the default): no flags to clear, no launch
       const size_t fb = 128 * sizeof(unsigned);  // the flags at the end of clipk_gemm_ws_bytes()
       if (hipMemsetAsync((char*)ws + clipk_gemm_ws_bytes() - fb, 0, fb, st) != hipSuccess) rc = (int)hipGetLastError();
     }
@@ -160,7 +161,7 @@ struct ProfScope {
 static double gemm_bytes(int in, int out, int epi, int M, int N, int K, bool has_o2, int auxdt) {
   const double a = esize(in), o = esize(out);
   double b = (double)M * K * a + (double)N * K * a + (double)M * N * o * (has_o2 ? 2 : 1);
-  const int e = epi & ~CLIPK_A_QGELU;
+  const int e = epi & ~(CLIPK_A_QGELU | CLIPK_QGELU_DERIV);
   if (e == CLIPK_EPI_BIAS_RES) b += (double)M * N * o;
   if (e == CLIPK_EPI_DQGELU) b += (double)M * N * esize(auxdt);
   return b;
@@ -173,7 +174,7 @@ static int gemm(int in, int out, int epi, int M, int N, int K, const void* A, co
   if (t_split && in == CLIPK_F32) in = CLIPK_F32S;
   ProfScope ps(prof_cls, st, 2.0 * M * N * K, site,
                site ? gemm_bytes(in, out, epi, M, N, K, o2 != nullptr, auxdt) : 0.0);
-  if (sk && epi != CLIPK_EPI_DQGELU)
+  if (sk && (epi & ~CLIPK_QGELU_DERIV) != CLIPK_EPI_DQGELU)
     return clipk_gemm_splitk(in, out, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, 0, sk, skb, st);
   return clipk_gemm_ws(in, out, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, aux, auxdt, N, t_gemm_ws,
                        t_gemm_ws ? clipk_gemm_ws_bytes() : 0, st);
@@ -423,6 +424,17 @@ static bool a_qgelu_on() {
   return v != 0;
 }
 
+// Training's c_fc saves quickgelu'(h) for the backward (CLIPK_QGELU_DERIV) instead of h itself;
+// knob CLIPK_QGELU_DERIV=0 (A/B) saves h and the backward recomputes the derivative.
+static bool qgelu_deriv_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char* s = getenv("CLIPK_QGELU_DERIV");
+    v = s ? atoi(s) : 1;
+  }
+  return v != 0;
+}
+
 static int block_post(const clipk_encoder* e, const std::array<const void*, 16>& w, int rows, int rd,
                       const void* X, const void* o, void* Xm, void* Xo, void* xn, void* h, void* g, float* m2,
                       float* r2, hipStream_t st, bool text, void* sk, size_t skb) {
@@ -445,8 +457,9 @@ static int block_post(const clipk_encoder* e, const std::array<const void*, 16>&
              Xo, nullptr, nullptr, 0, st, pg, nullptr, 0, "text.proj_fwd"));
     return CLIPK_OK;
   }
-  TRY(gemm(act, act, CLIPK_EPI_BIAS_QGELU, rows, 4 * W, W, xn, w[8], (const float*)w[9], nullptr, g,
-           h, nullptr, 0, st, text ? CLIPK_PROF_GEMM_FC : CLIPK_PROF_NONE, sk, skb, text ? "text.fc_fwd" : "vit.fc_fwd"));
+  // training (h given): h receives quickgelu'(xn Wfc^T + b) for the backward (CLIPK_QGELU_DERIV)
+  TRY(gemm(act, act, CLIPK_EPI_BIAS_QGELU | (h && qgelu_deriv_on() ? CLIPK_QGELU_DERIV : 0), rows, 4 * W, W, xn, w[8], (const float*)w[9],
+           nullptr, g, h, nullptr, 0, st, text ? CLIPK_PROF_GEMM_FC : CLIPK_PROF_NONE, sk, skb, text ? "text.fc_fwd" : "vit.fc_fwd"));
   TRY(gemm(act, rd, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo,
            nullptr, nullptr, 0, st, pg, sk, skb, text ? "text.proj_fwd" : "vit.proj_fwd"));
   return CLIPK_OK;
@@ -501,7 +514,8 @@ static int block_post_fold(const clipk_encoder* e, const std::array<const void*,
   TRY(gemm_ln(act, CLIPK_EPI_BIAS_RES, rows, W, W, o, w[4], (const float*)w[5], X, Xm, nullptr, lnst, nullptr,
               nullptr, st, pg, text ? "text.out_fwd" : "vit.out_fwd"));
   TRY(ln_merge(rows, W, lnst, m2, r2, rnb, st, text));
-  TRY(gemm_ln(act, CLIPK_EPI_BIAS_QGELU, rows, 4 * W, W, Xm, f[3], (const float*)f[5], nullptr, g, h, nullptr,
+  TRY(gemm_ln(act, CLIPK_EPI_BIAS_QGELU | (h && qgelu_deriv_on() ? CLIPK_QGELU_DERIV : 0), rows, 4 * W, W, Xm, f[3], (const float*)f[5],
+              nullptr, g, h, nullptr,
               (const float*)f[4], rnb, st, text ? CLIPK_PROF_GEMM_FC : CLIPK_PROF_NONE,
               text ? "text.fc_fwd" : "vit.fc_fwd"));
   if (stats_next)
@@ -866,15 +880,20 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
     return clipk_layernorm_bwd_x2(rd, gd, n, W, b.dxn, W, x, W, nullptr, gamma, mean, rstd, b.dX_lp, gd, W,
                                   last ? dX : nullptr, b.dX_lp, gd, nullptr, W, st);
   };
+  // the forward saved quickgelu'(h) in t.h (CLIPK_QGELU_DERIV), except on the A-operand QuickGELU
+  // knob's path (block_post), whose c_proj reads the pre-activation h itself
+  const int dgelu_epi = (io.text && act != CLIPK_F32 && a_qgelu_on()) || !qgelu_deriv_on()
+                            ? CLIPK_EPI_DQGELU
+                            : (CLIPK_EPI_DQGELU | CLIPK_QGELU_DERIV);
   for (int l = e->layers - 1; l >= 0; --l) {
     const auto& w = e->lw[l];
     if (!w[12] || !w[13] || !w[14] || !w[15]) return CLIPK_EINVAL;
     const bool compact = eotl && l == e->layers - 1;
     const int n = compact ? nout : rows;  // rows of the post-attention half
-    // MLP: dg = dX . Wproj ; dh = dg * qgelu'(h)  (h saved in the act dtype: more precise
-    // than saving qgelu'(h), which rounds the saturated region)
-    TRY(gemm(gd, gd, CLIPK_EPI_DQGELU, n, 4 * W, W, b.dX_lp, w[15], nullptr, nullptr, b.dh, nullptr,
-             t.h[l], act, st, io.text ? CLIPK_PROF_GEMM_DGELU : CLIPK_PROF_NONE, nullptr, 0, SITE("proj_dx_dgelu")));
+    // MLP: dg = dX . Wproj ; dh = dg * qgelu'(h), qgelu'(h) saved by the forward's c_fc epilogue
+    // in the act dtype (16-bit: rms 1.8e-4 on the derivative vs 2.9e-5 when recomputing it from a
+    // 16-bit h -- under the 16-bit rounding of dh itself -- for no exp / rcp in this epilogue)
+    TRY(gemm(gd, gd, dgelu_epi, n, 4 * W, W, b.dX_lp, w[15], nullptr, nullptr, b.dh, nullptr, t.h[l], act, st, io.text ? CLIPK_PROF_GEMM_DGELU : CLIPK_PROF_NONE, nullptr, 0, SITE("proj_dx_dgelu")));
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, n, W, 4 * W, b.dh, w[14], nullptr, nullptr, b.dxn, nullptr,
              nullptr, 0, st, pg, nullptr, 0, SITE("fc_dx")));
     TRY(ln_bwd(n, t.Xm[l], (const float*)w[6], t.mean2[l], t.rstd2[l], false));

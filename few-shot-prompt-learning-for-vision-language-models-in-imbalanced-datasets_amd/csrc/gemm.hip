@@ -148,6 +148,12 @@ __device__ __forceinline__ f32x4 mma_split(u32x4 bh, u32x4 bl, u32x4 ah, u32x4 a
 }
 constexpr float kSplitAlpha = 1.0f / CLIPK_SPLIT_SCALE;  // the packed weights' scale, undone
 
+// Training's QuickGELU pair with the derivative saved (CLIPK_QGELU_DERIV, include/clipk.h):
+// internal epilogue ids next to the public CLIPK_EPI_* ones
+constexpr int EPI_QGELU_D = 5;  // out = quickgelu(acc + bias), out2 = quickgelu'(acc + bias)
+constexpr int EPI_DMUL = 6;     // out = acc * aux (aux: the saved quickgelu')
+constexpr bool epi_qgelu(int e) { return e == CLIPK_EPI_BIAS_QGELU || e == EPI_QGELU_D; }
+
 __device__ __forceinline__ void glds16(const char* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(
       (const __attribute__((address_space(1))) void*)src,
@@ -460,8 +466,8 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
   const int fr = lane & 15;         // fragment row within a 16-row sub-tile
   const int fq = lane >> 4;         // 16-B chunk within a 64-B k-window
   const int sw = swz(fr);           // row swizzle (sub-tile row base is a multiple of 16)
-  constexpr bool HAS_BIAS = EPI == CLIPK_EPI_BIAS || EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_BIAS_QGELU;
-  constexpr bool HAS_EXT = EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU;
+  constexpr bool HAS_BIAS = EPI == CLIPK_EPI_BIAS || EPI == CLIPK_EPI_BIAS_RES || epi_qgelu(EPI);
+  constexpr bool HAS_EXT = EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU || EPI == EPI_DMUL;
 
   set_tile(tile);
   // deep ring: wait until stage kt+1 has landed while `younger` later stages stay in flight
@@ -550,7 +556,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
     // row -- measured slower: qkv 86 -> 110 us, c_fc 129 -> 158 us per launch.)
     constexpr bool LN_IN = LNM == 2, LN_OUT = LNM == 1;
     static_assert(!LN_OUT || (EPI == CLIPK_EPI_BIAS_RES && sizeof(TO) == 2 && CW == 8), "LN statistics: 16-bit out");
-    static_assert(!LN_IN || ((EPI == CLIPK_EPI_BIAS || EPI == CLIPK_EPI_BIAS_QGELU) && sizeof(T) == 2 && CW == 8),
+    static_assert(!LN_IN || ((EPI == CLIPK_EPI_BIAS || epi_qgelu(EPI)) && sizeof(T) == 2 && CW == 8),
                   "LN fold");
     [[maybe_unused]] f32x2 lnp[LN_IN ? 2 : 1][NQ];
     auto load_ln = [&](int i, int slot) {
@@ -913,7 +919,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         tile_rsrc(LN_OUT ? g.lnstats + (size_t)m0 * lng * 2 : nullptr, LN_OUT ? rows_ok * lng * 8 : 0);
     const __amdgpu_buffer_rsrc_t ro = tile_rsrc(outb + (size_t)m0 * g.ldo, rows_ok * g.ldo * (long long)sizeof(TO));
     __amdgpu_buffer_rsrc_t ro2 = ro;
-    if constexpr (EPI == CLIPK_EPI_BIAS_QGELU)
+    if constexpr (epi_qgelu(EPI))
       ro2 = tile_rsrc(g.out2 ? (const TO*)g.out2 + (size_t)m0 * g.ldo : nullptr,
                       g.out2 ? rows_ok * g.ldo * (long long)sizeof(TO) : 0);
     [[maybe_unused]] __amdgpu_buffer_rsrc_t prs = tile_rsrc(nullptr, 0);
@@ -995,11 +1001,27 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
           buf_store16<TO>(ro2, off, v);  // no-op when out2 is null (zero-sized resource)
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] = quick_gelu(v[c]);
+        } else if constexpr (EPI == EPI_QGELU_D) {
+          // the derivative from the same sigmoid: 3 more VALU per element here, and the
+          // backward's epilogue (EPI_DMUL) is one multiply instead of exp + rcp + 6
+          float dq[CW];
+#pragma unroll
+          for (int c = 0; c < CW; ++c) {
+            const float sg = qgelu_sigmoid(v[c]);
+            dq[c] = sg * fmaf(1.702f * v[c], 1.0f - sg, 1.0f);
+            v[c] *= sg;
+          }
+          buf_store16<TO>(ro2, off, dq);
         } else if constexpr (EPI == CLIPK_EPI_DQGELU) {
           float h[CW];
           raw_f32<TX, CW>(ext[q], h);
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] *= quick_gelu_grad(h[c]);
+        } else if constexpr (EPI == EPI_DMUL) {
+          float dq[CW];
+          raw_f32<TX, CW>(ext[q], dq);
+#pragma unroll
+          for (int c = 0; c < CW; ++c) v[c] *= dq[c];
         }
         buf_store16<TO, LN_OUT ? CLIPK_GEMM_SPOL_LN : CLIPK_GEMM_SPOL>(ro, off, v);
       }
@@ -1150,7 +1172,7 @@ static int num_cus() {
 // with an fp32 residual / aux operand would spill: they keep the 2-slot loop)
 template <typename T, typename TO, typename TX, int EPI, int BM, int LNM = 0>
 static bool try_pp(const GemmArgs& g, int nwg, hipStream_t st) {
-  constexpr bool ext32 = (EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU) && sizeof(TX) == 4;
+  constexpr bool ext32 = (EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU || EPI == EPI_DMUL) && sizeof(TX) == 4;
   if constexpr (CLIPK_GEMM_PP && (sizeof(T) == 2 || __is_same(T, f32s)) && !(BM == 256 && ext32)) {
     if (g.K * (int)sizeof(T) < 2 * GEMM_ROWB) return false;
     hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, BM, 256, 2, 4, true, GEMM_ROWB, 2, false, true, LNM>),
@@ -1307,6 +1329,8 @@ static int dispatch_split(int out_dtype, int epi, int aux_dtype, const GemmArgs&
     case CLIPK_EPI_DQGELU:
       return aux_dtype == CLIPK_F32 ? launch_gemm_split<CLIPK_EPI_DQGELU>(g, st) : CLIPK_EDTYPE;
     case CLIPK_EPI_NONE: return launch_gemm_split<CLIPK_EPI_NONE>(g, st);
+    case EPI_QGELU_D: return launch_gemm_split<EPI_QGELU_D>(g, st);
+    case EPI_DMUL: return aux_dtype == CLIPK_F32 ? launch_gemm_split<EPI_DMUL>(g, st) : CLIPK_EDTYPE;
     default: return CLIPK_EINVAL;
   }
 }
@@ -1382,6 +1406,13 @@ static int dispatch_out(int out_dtype, int epi, int aux_dtype, const GemmArgs& g
     if (aux_dtype == CLIPK_F32) return launch_gemm<T, T, float, CLIPK_EPI_DQGELU>(g, st);
     return CLIPK_EDTYPE;
   }
+  if (epi == EPI_DMUL) {  // backward with the saved derivative: out (grad dtype) = acc * aux
+    if (out_dtype != DT<T>::id) return CLIPK_EDTYPE;
+    if (aux_dtype == CLIPK_F16) return launch_gemm<T, T, f16, EPI_DMUL>(g, st);
+    if (aux_dtype == CLIPK_BF16) return launch_gemm<T, T, bf16, EPI_DMUL>(g, st);
+    if (aux_dtype == CLIPK_F32) return launch_gemm<T, T, float, EPI_DMUL>(g, st);
+    return CLIPK_EDTYPE;
+  }
 #define CLIPK_OUTS(EPIV)                                                           \
   switch (out_dtype) {                                                             \
     case CLIPK_F32: return launch_gemm<T, float, float, EPIV>(g, st);              \
@@ -1393,6 +1424,10 @@ static int dispatch_out(int out_dtype, int epi, int aux_dtype, const GemmArgs& g
   if (epi == CLIPK_EPI_BIAS_QGELU) {
     if (out_dtype == CLIPK_F32 && sizeof(T) != 4) return CLIPK_EDTYPE;
     CLIPK_OUTS(CLIPK_EPI_BIAS_QGELU)
+  }
+  if (epi == EPI_QGELU_D) {
+    if (out_dtype == CLIPK_F32 && sizeof(T) != 4) return CLIPK_EDTYPE;
+    CLIPK_OUTS(EPI_QGELU_D)
   }
   if (epi == CLIPK_EPI_NONE) { CLIPK_OUTS(CLIPK_EPI_NONE) }
 #undef CLIPK_OUTS
@@ -1435,8 +1470,10 @@ static int gemm_entry(int in_dtype, int out_dtype, int epi, int M, int N, int K,
                       const void* aux, int aux_dtype, int ldaux, void* ws, void* stream) {
   if (!A || !B || !out) return CLIPK_EINVAL;
   const bool ag = (epi & CLIPK_A_QGELU) != 0;
-  epi &= ~CLIPK_A_QGELU;
+  const bool deriv = (epi & CLIPK_QGELU_DERIV) != 0;
+  epi &= ~(CLIPK_A_QGELU | CLIPK_QGELU_DERIV);
   if (ag && (in_dtype == CLIPK_F32 || in_dtype == CLIPK_F32S || epi != CLIPK_EPI_BIAS_RES)) return CLIPK_EINVAL;
+  if (deriv && epi != CLIPK_EPI_BIAS_QGELU && epi != CLIPK_EPI_DQGELU) return CLIPK_EINVAL;
   if (M <= 0) return M == 0 ? CLIPK_OK : CLIPK_ESHAPE;
   const int esz = (in_dtype == CLIPK_F32 || in_dtype == CLIPK_F32S) ? 4 : 2;
   if (N <= 0 || K <= 0 || N % GEMM_NMIN != 0 || (K * esz) % GEMM_ROWB != 0) return CLIPK_ESHAPE;
@@ -1453,6 +1490,7 @@ static int gemm_entry(int in_dtype, int out_dtype, int epi, int M, int N, int K,
     g.tail_flags = (unsigned*)((char*)ws + kTailPairs * kTailPairBytes);
   }
   hipStream_t st = (hipStream_t)stream;
+  if (deriv) epi = epi == CLIPK_EPI_BIAS_QGELU ? EPI_QGELU_D : EPI_DMUL;
   switch (in_dtype) {
     case CLIPK_F16: return dispatch_out<f16>(out_dtype, epi, aux_dtype, g, st, ag);
     case CLIPK_BF16: return dispatch_out<bf16>(out_dtype, epi, aux_dtype, g, st, ag);
@@ -1478,6 +1516,7 @@ template <typename T>
 static int dispatch_ln(int epi, const GemmArgs& g, hipStream_t st) {
   if (!g.colsum) return launch_gemm<T, T, T, CLIPK_EPI_BIAS_RES, 1>(g, st);
   if (epi == CLIPK_EPI_BIAS) return launch_gemm<T, T, float, CLIPK_EPI_BIAS, 2>(g, st);
+  if (epi == EPI_QGELU_D) return launch_gemm<T, T, float, EPI_QGELU_D, 2>(g, st);
   return launch_gemm<T, T, float, CLIPK_EPI_BIAS_QGELU, 2>(g, st);
 }
 }  // namespace clipk
@@ -1504,6 +1543,9 @@ extern "C" int clipk_gemm_ln_ws(int in_dtype, int epi, int M, int N, int K, cons
   if (!A || !B || !out || !bias) return CLIPK_EINVAL;
   if (ws && ws_bytes < tail_ws_bytes()) return CLIPK_EWORKSPACE;
   if (in_dtype != CLIPK_F16 && in_dtype != CLIPK_BF16) return CLIPK_EDTYPE;
+  const bool deriv = (epi & CLIPK_QGELU_DERIV) != 0;  // fold form of c_fc: out2 = quickgelu'
+  epi &= ~CLIPK_QGELU_DERIV;
+  if (deriv && (epi != CLIPK_EPI_BIAS_QGELU || !colsum)) return CLIPK_EINVAL;
   if (!colsum) {  // producer: the statistics partials of the output
     if (!stats || rnb || epi != CLIPK_EPI_BIAS_RES || !res || ldr < N || ldr % 8) return CLIPK_EINVAL;
   } else {        // fold: (rstd, -rstd * mean) of A's rows in
@@ -1519,6 +1561,7 @@ extern "C" int clipk_gemm_ln_ws(int in_dtype, int epi, int M, int N, int K, cons
     g.tail_flags = (unsigned*)((char*)ws + kTailPairs * kTailPairBytes);
   }
   hipStream_t st = (hipStream_t)stream;
+  if (deriv) epi = EPI_QGELU_D;
   return in_dtype == CLIPK_F16 ? dispatch_ln<f16>(epi, g, st) : dispatch_ln<bf16>(epi, g, st);
 }
 
@@ -1550,6 +1593,12 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(int S, int M, int N,
   if constexpr (EPI == CLIPK_EPI_BIAS_RES) v += *reinterpret_cast<const f32x4*>(res + (size_t)m * ldr + c);
   if constexpr (EPI == CLIPK_EPI_BIAS_QGELU) {
     if (out2) store4<TO>(out2 + (size_t)m * ldo + c, v[0], v[1], v[2], v[3]);
+    v = (f32x4){quick_gelu(v[0]), quick_gelu(v[1]), quick_gelu(v[2]), quick_gelu(v[3])};
+  }
+  if constexpr (EPI == EPI_QGELU_D) {
+    if (out2)
+      store4<TO>(out2 + (size_t)m * ldo + c, quick_gelu_grad(v[0]), quick_gelu_grad(v[1]), quick_gelu_grad(v[2]),
+                 quick_gelu_grad(v[3]));
     v = (f32x4){quick_gelu(v[0]), quick_gelu(v[1]), quick_gelu(v[2]), quick_gelu(v[3])};
   }
   store4<TO>(out + (size_t)m * ldo + c, v[0], v[1], v[2], v[3]);
@@ -1606,7 +1655,9 @@ extern "C" int clipk_gemm_splitk(int in_dtype, int out_dtype, int epi, int M, in
   if (N <= 0 || K <= 0 || N % GEMM_NMIN != 0 || (K * esz) % GEMM_ROWB != 0) return CLIPK_ESHAPE;
   if (lda < K || ldb < K || (lda * esz) % 16 || (ldb * esz) % 16 || ldo < N || ldo % 4) return CLIPK_ESHAPE;
   if (splits > K * esz / GEMM_ROWB) return CLIPK_ESHAPE;
-  if (epi == CLIPK_EPI_DQGELU) return CLIPK_EINVAL;
+  const bool deriv = (epi & CLIPK_QGELU_DERIV) != 0;
+  epi &= ~CLIPK_QGELU_DERIV;
+  if (epi == CLIPK_EPI_DQGELU || (deriv && epi != CLIPK_EPI_BIAS_QGELU)) return CLIPK_EINVAL;
   if ((epi == CLIPK_EPI_BIAS || epi == CLIPK_EPI_BIAS_RES || epi == CLIPK_EPI_BIAS_QGELU) && !bias)
     return CLIPK_EINVAL;
   if (epi == CLIPK_EPI_BIAS_RES && (!res || ldr < N || ldr % 4 || out_dtype != CLIPK_F32)) return CLIPK_EINVAL;
@@ -1648,6 +1699,7 @@ extern "C" int clipk_gemm_splitk(int in_dtype, int out_dtype, int epi, int M, in
   }
   if (epi == CLIPK_EPI_NONE) { CLIPK_FIN(CLIPK_EPI_NONE) }
   if (epi == CLIPK_EPI_BIAS) { CLIPK_FIN(CLIPK_EPI_BIAS) }
+  if (epi == CLIPK_EPI_BIAS_QGELU && deriv) { CLIPK_FIN(EPI_QGELU_D) }
   if (epi == CLIPK_EPI_BIAS_QGELU) { CLIPK_FIN(CLIPK_EPI_BIAS_QGELU) }
   if (epi == CLIPK_EPI_BIAS_RES) return splitk_finish<float, CLIPK_EPI_BIAS_RES>(splits, g, part, st);
 #undef CLIPK_FIN
@@ -1667,6 +1719,11 @@ extern "C" int clipk_gemm_stamps(void* host, size_t bytes) {
 }
 
 // Test / benchmark knob: the split tail of clipk_gemm_ws on (1) or off (0).
+// (encoder.hip: the pair flags need zeroing only while the split tail can run)
+namespace clipk {
+bool gemm_tail_enabled() { return tail_mode() != 0; }
+}  // namespace clipk
+
 extern "C" int clipk_gemm_set_tail(int on) {
   if (on != 0 && on != 1) return CLIPK_EINVAL;
   g_tail = on;

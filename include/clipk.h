@@ -64,6 +64,13 @@ enum {
  * (applied to each 16-B chunk of A as it is staged into LDS), so the producer of h need
  * not also write quickgelu(h) (the text c_proj forward). 16-bit in_dtype only. */
 enum { CLIPK_A_QGELU = 0x100 };
+/* Epilogue flag OR-ed into epi, training's QuickGELU pair (replaces keeping the pre-activation,
+ * PromptSRC/clip/model.py:162-164, 177): with CLIPK_EPI_BIAS_QGELU, out2 = quickgelu'(acc + bias)
+ * instead of acc + bias; with CLIPK_EPI_DQGELU, aux already holds quickgelu'(h) and
+ * out = acc * aux. The forward epilogue has sigmoid(1.702 h) in hand (three more VALU per element);
+ * the backward epilogue drops its exp + rcp per element. Also accepted by clipk_gemm_ln (fold
+ * form of EPI_BIAS_QGELU) and clipk_gemm_splitk (EPI_BIAS_QGELU). */
+enum { CLIPK_QGELU_DERIV = 0x200 };
 
 const char* clipk_version(void);
 const char* clipk_strerror(int status);

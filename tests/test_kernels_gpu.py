@@ -424,6 +424,45 @@ def test_gemm_split_fp32_class(dev, M, Nn, K):
     assert e_none * 50 < e16
 
 
+@pytest.mark.parametrize("prec", [torch.float16, torch.bfloat16, torch.float32, "fp32s"])
+@pytest.mark.parametrize("M", [300, 6000, 47160])
+def test_gemm_qgelu_deriv_pair(dev, prec, M):
+    """CLIPK_QGELU_DERIV (training's c_fc / dgelu pair): EPI_BIAS_QGELU writes out2 =
+    quickgelu'(acc + bias) beside out = quickgelu(acc + bias), and EPI_DQGELU with the flag is
+    out = acc * aux; vs torch fp32 of the same ops (tolerance per dtype; fp32s 4e-6), on the small-M,
+    128x128 and ping-pong tiles. The QuickGELU output is bitwise the plain epilogue's."""
+    Nn, K = 2048, 512
+    g = torch.Generator(device="cpu").manual_seed(M)
+    a = torch.randn(M, K, generator=g).to(dev)
+    w = (torch.randn(Nn, K, generator=g) / math.sqrt(K)).to(dev)
+    bias = (0.3 * torch.randn(Nn, generator=g)).to(dev)
+    dy = torch.randn(M, K, generator=g).to(dev)  # dgelu: dY [M, W] . Wproj^T [W -> 4W]
+    wproj = (torch.randn(Nn, K, generator=g) / math.sqrt(K)).to(dev)
+    if prec == "fp32s":
+        A, B, Dy, Wp, odt, tol = a, ops.split_pack(w), dy, ops.split_pack(wproj), torch.float32, 4e-6
+        ref = a.double() @ w.double().t() + bias.double()
+        acc = dy.double() @ wproj.double().t()
+    else:
+        A, B, Dy, Wp, odt, tol = a.to(prec), w.to(prec), dy.to(prec), wproj.to(prec), prec, TOL[prec]
+        ref = A.double() @ B.double().t() + bias.double()
+        acc = Dy.double() @ Wp.double().t()
+    sg = torch.sigmoid(1.702 * ref)
+    gq, dq = ops.gemm(A, B, N.EPI_BIAS_QGELU | N.QGELU_DERIV, odt, bias=bias, want_out2=True)
+    g0 = ops.gemm(A, B, N.EPI_BIAS_QGELU, odt, bias=bias)
+    assert torch.equal(gq, g0)
+    scale = lambda r: r.abs().max().item() + 1e-12
+    e_g = ((gq.double() - ref * sg).abs().max() / scale(ref * sg)).item()
+    dref = sg * (1 + 1.702 * ref * (1 - sg))
+    e_d = ((dq.double() - dref).abs().max() / scale(dref)).item()
+    assert e_g <= tol and e_d <= tol, f"qgelu {e_g:.3e} deriv {e_d:.3e} > {tol}"
+    out = ops.gemm(Dy, Wp, N.EPI_DQGELU | N.QGELU_DERIV, odt, aux=dq)
+    want = acc * dq.double()
+    e_o = ((out.double() - want).abs().max() / scale(want)).item()
+    assert e_o <= tol, f"dmul {e_o:.3e} > {tol}"
+    with pytest.raises(N.ClipkError):  # the flag means nothing to the other epilogues
+        ops.gemm(A, B, N.EPI_BIAS | N.QGELU_DERIV, odt, bias=bias)
+
+
 @pytest.mark.parametrize("M", [96, 1576, 47160])
 def test_gemm_split_parts_exact(dev, M):
     """The in-register split itself, bit for bit: with B = I (packed hi = 64, lo = 0) every output
@@ -553,6 +592,10 @@ def test_gemm_splitk(dev, dtype, M, Nn, K, splits):
     hr = ref + bias
     close(hq, hr, dtype, "splitk qgelu.h")
     close(gq, hr * torch.sigmoid(1.702 * hr), dtype, "splitk qgelu.g")
+    gd, dd = ops.gemm_splitk(A, B, N.EPI_BIAS_QGELU | N.QGELU_DERIV, odt, bias=bias, want_out2=True, splits=splits)
+    sg = torch.sigmoid(1.702 * hr)
+    assert torch.equal(gd, gq)
+    close(dd, sg * (1 + 1.702 * hr * (1 - sg)), dtype, "splitk qgelu deriv")
     close(ops.gemm_splitk(A, B, N.EPI_BIAS, odt, bias=bias, splits=splits), hr, dtype, "splitk bias")
 
 

@@ -93,6 +93,12 @@ def test_gemm_ln_fold(dev, dtype, epi, Mr, Wd, Nn):
     assert ((rstd.double() * torch.sqrt(var + 1e-5) - 1).abs().max().item()) <= 2e-5
     assert e_fold <= TOL[dtype], f"fold rel err {e_fold:.3e}"
     assert e_fold <= 1.5 * e_unf + 2e-3, f"fold {e_fold:.3e} vs un-fused {e_unf:.3e}"
+    if epi == N.EPI_BIAS_QGELU and Mr >= 8000:
+        # training's fold form (CLIPK_QGELU_DERIV): out2 = quickgelu'(pre-activation)
+        og, d = ops.gemm_ln(x, wp, epi | N.QGELU_DERIV, c, colsum=s, rnb=rnb, want_out2=True)
+        sg = torch.sigmoid(1.702 * ref)
+        assert torch.equal(og, out), "the QuickGELU output does not depend on what out2 holds"
+        assert _rel(d, sg * (1 + 1.702 * ref * (1 - sg))) <= TOL[dtype]
 
 
 def _encoder_pair(arch, prec, dev):
