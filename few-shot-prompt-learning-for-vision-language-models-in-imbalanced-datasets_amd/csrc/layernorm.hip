@@ -417,35 +417,53 @@ namespace clipk {
 // mean = sum_g sum_g / width; M2 = sum_g M2_g + 64 (sum_g / 64 - mean)^2; rstd = 1 / sqrt(M2 /
 // width + 1e-5) as model.py:153-159. Outputs (each optional): mean, rstd (the LayerNorm
 // backward's), and rnb = (rstd, -rstd * mean) pairs (the folding GEMM's one 8-B load per row).
-// 16 lanes per row, lane j holding partial j (one 8-B load; idle past width / 64), sums over the
-// 16 lanes by DPP in a fixed pattern (deterministic): the kernel is one memory round trip (the
-// first form, one thread per row reading 64 B, took 5 us at 47k rows).
+// LPR (8 or 16 >= width / 64) lanes per row, lane j holding partial j (8-B loads), sums over the
+// LPR lanes by DPP in a fixed pattern (deterministic; idle lanes add exact zeros, so the 8- and
+// 16-lane forms give the same bits). Each lane group merges RPG rows whose loads are all issued
+// before the first sum: one load per wave left the kernel latency-bound at 1.3 TB/s (37 us at
+// the eval's 590k rows); the first form, one thread per row reading 64 B, took 5 us at 47k rows.
 template <int CTRL>
 __device__ __forceinline__ float dpp_row(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
-__device__ __forceinline__ float sum16(float v) {
+template <int LPR>
+__device__ __forceinline__ float sum_lanes(float v) {
   v += dpp_row<0xB1>(v);   // quad: xor 1
   v += dpp_row<0x4E>(v);   // quad: xor 2
   v += dpp_row<0x141>(v);  // half-row mirror: quads 0 <-> 1
-  return v + dpp_row<0x140>(v);  // row mirror: halves 0 <-> 1
+  if constexpr (LPR == 16) v += dpp_row<0x140>(v);  // row mirror: halves 0 <-> 1
+  return v;
 }
+constexpr int kMergeRPG = 4;  // rows per lane group
+template <int LPR>
 __global__ __launch_bounds__(256) void ln_stats_merge_kernel(int rows, int ng, const f32x2* __restrict__ st,
                                                              float* __restrict__ mean, float* __restrict__ rstd,
                                                              f32x2* __restrict__ rnb) {
-  const int lane = threadIdx.x & 63, j = lane & 15;
-  const int r = (blockIdx.x * 256 + threadIdx.x) >> 4;
-  const bool ok = r < rows && j < ng;
-  const f32x2 p = ok ? st[(size_t)r * ng + j] : (f32x2){0.f, 0.f};
+  constexpr int RPW = 64 / LPR;  // rows per wave and load
+  const int lane = threadIdx.x & 63, j = lane % LPR;
+  const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int r0 = wave * RPW * kMergeRPG + lane / LPR;
+  f32x2 p[kMergeRPG];
+#pragma unroll
+  for (int k = 0; k < kMergeRPG; ++k) {
+    const int r = r0 + k * RPW;
+    p[k] = (r < rows && j < ng) ? st[(size_t)r * ng + j] : (f32x2){0.f, 0.f};
+  }
   const float inv_w = 1.0f / (64.0f * ng);
-  const float mu = sum16(p[0]) * inv_w;
-  const float d = p[0] * (1.0f / 64.0f) - mu;
-  const float m2 = sum16(ok ? fmaf(64.0f * d, d, p[1]) : 0.f);
-  if (r >= rows || j != 0) return;
-  const float rs = rsqrtf(m2 * inv_w + 1e-5f);
-  if (mean) mean[r] = mu;
-  if (rstd) rstd[r] = rs;
-  if (rnb) rnb[r] = (f32x2){rs, -rs * mu};
+#pragma unroll
+  for (int k = 0; k < kMergeRPG; ++k) {
+    const int r = r0 + k * RPW;
+    const bool ok = r < rows && j < ng;
+    const float mu = sum_lanes<LPR>(p[k][0]) * inv_w;
+    const float d = p[k][0] * (1.0f / 64.0f) - mu;
+    const float m2 = sum_lanes<LPR>(ok ? fmaf(64.0f * d, d, p[k][1]) : 0.f);
+    if (r < rows && j == 0) {
+      const float rs = rsqrtf(m2 * inv_w + 1e-5f);
+      if (mean) mean[r] = mu;
+      if (rstd) rstd[r] = rs;
+      if (rnb) rnb[r] = (f32x2){rs, -rs * mu};
+    }
+  }
 }
 }  // namespace clipk
 
@@ -454,9 +472,15 @@ extern "C" int clipk_ln_stats_merge(int rows, int width, const float* stats, flo
   if (!stats || (!mean && !rstd && !rnb)) return CLIPK_EINVAL;
   if (rows < 0 || width % 128 || width < 128 || width > 1024) return CLIPK_ESHAPE;
   if (rows == 0) return CLIPK_OK;
-  hipLaunchKernelGGL(ln_stats_merge_kernel, dim3((unsigned)(((long)rows * 16 + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, rows, width / 64, reinterpret_cast<const f32x2*>(stats), mean, rstd,
-                     reinterpret_cast<f32x2*>(rnb));
+  const int ng = width / 64, lpr = ng <= 8 ? 8 : 16;
+  const long waves = ((long)rows + (64 / lpr) * kMergeRPG - 1) / ((64 / lpr) * kMergeRPG);
+  const dim3 grid((unsigned)((waves + 3) / 4));
+  if (lpr == 8)
+    hipLaunchKernelGGL(ln_stats_merge_kernel<8>, grid, dim3(256), 0, (hipStream_t)stream, rows, ng,
+                       reinterpret_cast<const f32x2*>(stats), mean, rstd, reinterpret_cast<f32x2*>(rnb));
+  else
+    hipLaunchKernelGGL(ln_stats_merge_kernel<16>, grid, dim3(256), 0, (hipStream_t)stream, rows, ng,
+                       reinterpret_cast<const f32x2*>(stats), mean, rstd, reinterpret_cast<f32x2*>(rnb));
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
 }

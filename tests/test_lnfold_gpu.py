@@ -58,6 +58,26 @@ def test_gemm_ln_stats(dev, dtype, Mr, Nn, K):
     assert ((rstd.double() * torch.sqrt(var + 1e-5) - 1).abs().max().item()) <= 2e-5
 
 
+@pytest.mark.parametrize("Wd", [128, 512, 768, 1024])
+@pytest.mark.parametrize("Mr", [1, 31, 33, 4097, 150001])
+def test_ln_stats_merge_widths(dev, Wd, Mr):
+    """clipk_ln_stats_merge alone: 8-lane (width <= 512) and 16-lane row groups, 4 rows per lane
+    group, ragged row counts; vs the fp64 statistics of x, and
+    bitwise-equal reruns."""
+    g = torch.Generator(device="cpu").manual_seed(Mr + Wd)
+    x = torch.randn(Mr, Wd, generator=g) + 3.0 * torch.randn(Mr, 1, generator=g)
+    x[:, 3] *= 25.0
+    st = partials(x).to(dev)
+    mean, rstd, rnb = ops.ln_stats_merge(st, Wd)
+    m2, r2, n2 = ops.ln_stats_merge(st, Wd)
+    assert torch.equal(mean, m2) and torch.equal(rstd, r2) and torch.equal(rnb, n2)
+    assert torch.equal(rnb[:, 0], rstd) and torch.equal(rnb[:, 1], -rstd * mean)
+    xd = x.double().to(dev)
+    mu, var = xd.mean(1), xd.var(1, unbiased=False)
+    assert ((mean.double() - mu).abs() <= 1e-5 * (xd.abs().amax(1) + 1)).all()
+    assert ((rstd.double() * torch.sqrt(var + 1e-5) - 1).abs().max().item()) <= 2e-5
+
+
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("epi", [N.EPI_BIAS, N.EPI_BIAS_QGELU])
 @pytest.mark.parametrize("Mr,Wd,Nn", [(47160, 512, 1536), (47160, 512, 2048), (8000, 512, 2048), (300, 768, 2304),
