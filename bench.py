@@ -96,6 +96,9 @@ def reference_cpu(arch, classes):
 # include/clipk.h CLIPK_F32S), the ceiling for its algorithmic (fp32) FLOPs
 PEAK = {"fp16": 2500.0, "bf16": 2500.0, "amp": 2500.0, "fp32": 157.3, "fp32s": 2500.0 / 3}
 HBM_PEAK_GBS = 8000.0  # HBM3E, MI355X_MICROARCH.md
+# batch-1 lines: ~2.7 ms steps, so 50 timed steps (10 let one host hiccup move the mean ~20 %:
+# 3.32 ms in one round-4 run against 2.70 over 50 steps of tools/b1_time.py on the same build)
+B1_STEPS = 50
 # the latest round's PMC passes (tools/pmc_bench.sh), else the previous round's
 PMC_FILE = next((f for f in (os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r04_pmc", "r03_pmc"))
                  if os.path.exists(f)), os.path.join(ROOT, "profiles", "r04_pmc", "traffic.json"))
@@ -498,8 +501,9 @@ def main():
     if not args.no_extra and world > 1:
         # the reference's CoCoOp batch (1 image / step) with the classes sharded over the ranks
         tr1, dm1 = build_trainer(args, args.prec, 1, dev, 0, class_shard=True)
-        t1, _ = time_train(tr1, dm1, 10, 3)
-        out["batch1_class_shard"] = {"images_per_sec": round(10 / t1, 3), "ms_per_step": round(100 * t1, 3),
+        t1, _ = time_train(tr1, dm1, B1_STEPS, 5)
+        out["batch1_class_shard"] = {"images_per_sec": round(B1_STEPS / t1, 3),
+                                     "ms_per_step": round(1000 * t1 / B1_STEPS, 3), "steps": B1_STEPS,
                                      "global_batch": 1, "classes_per_rank": tr1.model.prompt_learner.layout.n_cls,
                                      "scaling": "strong"}
         del tr1, dm1
@@ -507,8 +511,9 @@ def main():
     if not args.no_extra and world == 1:  # the N > 1 scaling runs report the headline lines only
         # the reference's batch size for CoCoOp (configs/trainers/CoCoOp/*.yaml: 1 image/step)
         tr1, dm1 = build_trainer(args, args.prec, 1, dev, rank)
-        t1, _ = time_train(tr1, dm1, 10, 3)
-        out["batch1"] = {"images_per_sec": round(world * 10 / t1, 3), "ms_per_step": round(100 * t1, 3),
+        t1, _ = time_train(tr1, dm1, B1_STEPS, 5)
+        out["batch1"] = {"images_per_sec": round(world * B1_STEPS / t1, 3),
+                         "ms_per_step": round(1000 * t1 / B1_STEPS, 3), "steps": B1_STEPS,
                          "images_per_gpu_per_step": 1}
         del tr1, dm1
         torch.cuda.empty_cache()

@@ -419,9 +419,11 @@ namespace clipk {
 // backward's), and rnb = (rstd, -rstd * mean) pairs (the folding GEMM's one 8-B load per row).
 // LPR (8 or 16 >= width / 64) lanes per row, lane j holding partial j (8-B loads), sums over the
 // LPR lanes by DPP in a fixed pattern (deterministic; idle lanes add exact zeros, so the 8- and
-// 16-lane forms give the same bits). Each lane group merges RPG rows whose loads are all issued
-// before the first sum: one load per wave left the kernel latency-bound at 1.3 TB/s (37 us at
-// the eval's 590k rows); the first form, one thread per row reading 64 B, took 5 us at 47k rows.
+// 16-lane forms give the same bits). At >= 64k rows each lane group merges 4 rows whose loads are
+// all issued before the first sum: one load per wave left the kernel latency-bound at 1.3 TB/s
+// (26 us at the eval's 590k rows -> 13 us); below, one row per group keeps more blocks (the
+// batch-1 step's 5.9k rows: 185 vs 47). The first form, one thread per row reading 64 B, took
+// 5 us at 47k rows.
 template <int CTRL>
 __device__ __forceinline__ float dpp_row(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
@@ -434,24 +436,23 @@ __device__ __forceinline__ float sum_lanes(float v) {
   if constexpr (LPR == 16) v += dpp_row<0x140>(v);  // row mirror: halves 0 <-> 1
   return v;
 }
-constexpr int kMergeRPG = 4;  // rows per lane group
-template <int LPR>
+template <int LPR, int RPG>
 __global__ __launch_bounds__(256) void ln_stats_merge_kernel(int rows, int ng, const f32x2* __restrict__ st,
                                                              float* __restrict__ mean, float* __restrict__ rstd,
                                                              f32x2* __restrict__ rnb) {
   constexpr int RPW = 64 / LPR;  // rows per wave and load
   const int lane = threadIdx.x & 63, j = lane % LPR;
   const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
-  const int r0 = wave * RPW * kMergeRPG + lane / LPR;
-  f32x2 p[kMergeRPG];
+  const int r0 = wave * RPW * RPG + lane / LPR;
+  f32x2 p[RPG];
 #pragma unroll
-  for (int k = 0; k < kMergeRPG; ++k) {
+  for (int k = 0; k < RPG; ++k) {
     const int r = r0 + k * RPW;
     p[k] = (r < rows && j < ng) ? st[(size_t)r * ng + j] : (f32x2){0.f, 0.f};
   }
   const float inv_w = 1.0f / (64.0f * ng);
 #pragma unroll
-  for (int k = 0; k < kMergeRPG; ++k) {
+  for (int k = 0; k < RPG; ++k) {
     const int r = r0 + k * RPW;
     const bool ok = r < rows && j < ng;
     const float mu = sum_lanes<LPR>(p[k][0]) * inv_w;
@@ -472,15 +473,20 @@ extern "C" int clipk_ln_stats_merge(int rows, int width, const float* stats, flo
   if (!stats || (!mean && !rstd && !rnb)) return CLIPK_EINVAL;
   if (rows < 0 || width % 128 || width < 128 || width > 1024) return CLIPK_ESHAPE;
   if (rows == 0) return CLIPK_OK;
-  const int ng = width / 64, lpr = ng <= 8 ? 8 : 16;
-  const long waves = ((long)rows + (64 / lpr) * kMergeRPG - 1) / ((64 / lpr) * kMergeRPG);
+  const int ng = width / 64, lpr = ng <= 8 ? 8 : 16, rpg = rows >= 65536 ? 4 : 1;
+  const long waves = ((long)rows + (64 / lpr) * rpg - 1) / ((64 / lpr) * rpg);
   const dim3 grid((unsigned)((waves + 3) / 4));
-  if (lpr == 8)
-    hipLaunchKernelGGL(ln_stats_merge_kernel<8>, grid, dim3(256), 0, (hipStream_t)stream, rows, ng,
-                       reinterpret_cast<const f32x2*>(stats), mean, rstd, reinterpret_cast<f32x2*>(rnb));
-  else
-    hipLaunchKernelGGL(ln_stats_merge_kernel<16>, grid, dim3(256), 0, (hipStream_t)stream, rows, ng,
-                       reinterpret_cast<const f32x2*>(stats), mean, rstd, reinterpret_cast<f32x2*>(rnb));
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, (hipStream_t)stream, rows, ng, reinterpret_cast<const f32x2*>(stats),
+                       mean, rstd, reinterpret_cast<f32x2*>(rnb));
+  };
+  if (lpr == 8) {
+    if (rpg == 4) go(ln_stats_merge_kernel<8, 4>);
+    else go(ln_stats_merge_kernel<8, 1>);
+  } else {
+    if (rpg == 4) go(ln_stats_merge_kernel<16, 4>);
+    else go(ln_stats_merge_kernel<16, 1>);
+  }
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
 }
