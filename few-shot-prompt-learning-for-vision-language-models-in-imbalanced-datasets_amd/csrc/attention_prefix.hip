@@ -840,20 +840,28 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
   float* sk = sK[w];
   float* sv = sV[w];
   const int u_end = min((k + 1) * kValuChunk, ntiles + 1);
+  // the next unit's q / k / v rows are loaded into registers while this unit computes (one
+  // unit ahead: a wave otherwise waits out a full HBM latency per unit)
+  float qn[16], kn[16], vn[16];
+  int t0n, nn, pren, rrn, firstn;
+  auto fetch = [&](int u) {
+    f32_unit(tiles, row_first, P, u, r, t0n, nn, pren, rrn, firstn);
+    const float* qp = qkv + ((size_t)g * R + t0n + rrn) * ldq + h * 64 + 16 * s;
+    ld16(qp, qn);
+    ld16(qp + W, kn);
+    ld16(qp + 2 * W, vn);
+  };
+  if (k * kValuChunk < u_end) fetch(k * kValuChunk);
   for (int u = k * kValuChunk; u < u_end; ++u) {
-    int t0, n, pre, rr, first;
-    f32_unit(tiles, row_first, P, u, r, t0, n, pre, rr, first);
+    const int t0 = t0n, n = nn, pre = pren, rr = rrn, first = firstn;
     const size_t row = (size_t)g * R + t0 + rr;
-    const float* qp = qkv + row * ldq + h * 64 + 16 * s;
-    float q[16], t[16];
-    ld16(qp, q);
+    float q[16];
 #pragma unroll
-    for (int d = 0; d < 16; ++d) q[d] *= kScale;
-    ld16(qp + W, t);
-    st16(sk + r * 64 + 16 * s, t);
-    ld16(qp + 2 * W, t);
-    st16(sv + r * 64 + 16 * s, t);
+    for (int d = 0; d < 16; ++d) q[d] = qn[d] * kScale;
+    st16(sk + r * 64 + 16 * s, kn);
+    st16(sv + r * 64 + 16 * s, vn);
     lds_sync();
+    if (u + 1 < u_end) fetch(u + 1);
     float m = -INFINITY, l = 0.f, o[16];
 #pragma unroll
     for (int d = 0; d < 16; ++d) o[d] = 0.f;
@@ -896,7 +904,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
 // Phase 3 (lane = prefix key): the prefix rows' dK, dV partial of this unit, accumulated over
 // the chunk in registers and written once per chunk (prefix_kv_reduce sums the chunks).
 template <int WPB>
-__global__ __launch_bounds__(WPB * 64) void attn_prefix_bwd_f32(
+__global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 waves per SIMD (<= 256 VGPRs)
     int G, int P, int R, int ntiles, const int* __restrict__ tiles, const int* __restrict__ row_first, int H,
     int nchunk, const float* __restrict__ qkv, int ldq, const float* __restrict__ o_fwd, int ldof,
     const float* __restrict__ dout, int lddo, const float* __restrict__ lse, float* __restrict__ dqkv, int lddq,
@@ -919,25 +927,38 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_bwd_f32(
 #pragma unroll
   for (int d = 0; d < 16; ++d) { akp[d] = 0.f; avp[d] = 0.f; }
   const int u_end = min((k + 1) * kValuChunk, ntiles + 1);
+  // the next unit's rows (q, dO, o, k, v, lse) are loaded into registers while this unit
+  // computes (one unit ahead, as the forward)
+  float qn[16], dOn[16], on[16], kn[16], vn[16], lin = 0.f;
+  int t0n, nn, pren, rrn, firstn;
+  auto fetch = [&](int u) {
+    f32_unit(tiles, row_first, P, u, r, t0n, nn, pren, rrn, firstn);
+    const size_t rw = (size_t)g * R + t0n + rrn;
+    const float* qp = qkv + rw * ldq + h * 64 + 16 * s;
+    ld16(qp, qn);
+    ld16(dout + rw * lddo + h * 64 + 16 * s, dOn);
+    ld16(o_fwd + rw * ldof + h * 64 + 16 * s, on);
+    ld16(qp + W, kn);
+    ld16(qp + 2 * W, vn);
+    lin = lse[rw * H + h];
+  };
+  if (k * kValuChunk < u_end) fetch(k * kValuChunk);
   for (int u = k * kValuChunk; u < u_end; ++u) {
-    int t0, n, pre, rr, first;
-    f32_unit(tiles, row_first, P, u, r, t0, n, pre, rr, first);
+    const int t0 = t0n, n = nn, pre = pren, rr = rrn, first = firstn;
     const bool qok = r < n;
     const size_t row = (size_t)g * R + t0 + rr;
-    const float* qp = qkv + row * ldq + h * 64 + 16 * s;
-    float q[16], dO[16], t[16];
-    ld16(qp, q);
+    float q[16], dO[16];
 #pragma unroll
-    for (int d = 0; d < 16; ++d) q[d] *= kScale;
-    ld16(dout + row * lddo + h * 64 + 16 * s, dO);
-    ld16(o_fwd + row * ldof + h * 64 + 16 * s, t);
-    const float Di = quad_sum(dot16(dO, t));
-    const float li = lse[row * H + h];
-    ld16(qp + W, t);
-    st16(sa + r * 64 + 16 * s, t);
-    ld16(qp + 2 * W, t);
-    st16(sb + r * 64 + 16 * s, t);
+    for (int d = 0; d < 16; ++d) {
+      q[d] = qn[d] * kScale;
+      dO[d] = dOn[d];
+    }
+    const float Di = quad_sum(dot16(dO, on));
+    const float li = lin;
+    st16(sa + r * 64 + 16 * s, kn);
+    st16(sb + r * 64 + 16 * s, vn);
     lds_sync();
+    if (u + 1 < u_end) fetch(u + 1);
     // phase 1: lane = query row rr
     float dq[16];
 #pragma unroll
