@@ -29,7 +29,7 @@
 namespace clipk {
 
 // tiles whose loads are issued together (template parameter; env CLIPK_PREFIX_*_BATCH)
-constexpr int kValuChunk = 8;                 // units per wave, fp32 kernels (16: one round of ~7 waves per CU at the bench shape)
+constexpr int kValuChunkMin = 4;              // units per wave, fp32 kernels: at least (f32_uc)
 
 // Units per wave of the MFMA kernels (env CLIPK_PREFIX_FWD_CHUNK / _BWD_CHUNK, read once).
 static int chunk_env(const char* name, int def) {
@@ -60,6 +60,19 @@ static int bwd_uc(int G, int ntiles, int H) {
   while (uc > 4 && (long)G * H * ((ntiles + 1 + uc - 1) / uc) < 8L * prefix_num_cus()) uc /= 2;
   return uc;
 }
+// Units per wave of the fp32 kernels: the G * H * chunks waves sized to one round of `wpc`
+// resident waves per CU (4..16 units). A fixed 8 gave the headline forward 3,840 waves for 3,072
+// slots (1.25 rounds, the second a quarter full): forward 120 -> 101 us, backward 224 -> 208 us
+// isolated (profiles/r04s/).
+static int f32_uc(int G, int ntiles, int H, int wpc) {
+  const long slots = (long)wpc * prefix_num_cus();
+  const long uc = ((long)(ntiles + 1) * G * H + slots - 1) / slots;
+  // at most 16: many groups (the eval's 100 images) keep several rounds of shorter waves
+  return (int)(uc < kValuChunkMin ? kValuChunkMin : uc > 16 ? 16 : uc);
+}
+// resident waves per CU of the fp32 kernels at WPB = 2 (VGPRs: forward 146 -> 3 per SIMD,
+// backward <= 256 -> 2; LDS: forward 24 KB, backward 34 KB per 2-wave block)
+constexpr int kF32FwdWpc = 12, kF32BwdWpc = 8;
 static int fwd_batch() { static int c = chunk_env("CLIPK_PREFIX_FWD_BATCH", 1); return c; }
 static int bwd_batch() { static int c = chunk_env("CLIPK_PREFIX_BWD_BATCH", 2); return c; }
 // Waves per block (4 or 8; env CLIPK_PREFIX_WPB). Waves are head-fastest, so 8 waves (H = 8)
@@ -766,7 +779,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_bwd_lds(int G, int P, in
 }
 
 // ------------------------------------------------------------------ fp32 kernels (PREC fp32 / fp32s)
-// One wave per (group, chunk of kValuChunk units, head); blocks of WPB waves (f32_wpb) share one
+// One wave per (group, chunk of f32_uc units, head); blocks of WPB waves (f32_wpb) share one
 // (group, head), so the prefix K/V rows are staged into LDS once per block. Lane = 4 r + s: row
 // r of the unit (query in the forward and for dQ, key for dK / dV) and 16-column slice s of
 // the head; a dot product is 16 FMAs on the lane's slice plus a quad sum (2 DPP adds). K/V
@@ -827,7 +840,8 @@ __device__ __forceinline__ void f32_stage_prefix(const float* __restrict__ qkv, 
 template <int WPB>
 __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
     int G, int P, int R, int ntiles, const int* __restrict__ tiles, const int* __restrict__ row_first, int H,
-    int nchunk, const float* __restrict__ qkv, int ldq, float* __restrict__ out, int ldo, float* __restrict__ lse) {
+    int nchunk, int uc, const float* __restrict__ qkv, int ldq, float* __restrict__ out, int ldo,
+    float* __restrict__ lse) {
   __shared__ CLIPK_LDS_ALIGN float sKp[16 * 64], sVp[16 * 64];
   __shared__ CLIPK_LDS_ALIGN float sK[WPB][16 * 64], sV[WPB][16 * 64];
   int g, h, k, w;
@@ -839,7 +853,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
   const int lane = threadIdx.x & 63, r = lane >> 2, s = lane & 3;
   float* sk = sK[w];
   float* sv = sV[w];
-  const int u_end = min((k + 1) * kValuChunk, ntiles + 1);
+  const int u_end = min((k + 1) * uc, ntiles + 1);
   // the next unit's q / k / v rows are loaded into registers while this unit computes (one
   // unit ahead: a wave otherwise waits out a full HBM latency per unit)
   float qn[16], kn[16], vn[16];
@@ -851,8 +865,8 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
     ld16(qp + W, kn);
     ld16(qp + 2 * W, vn);
   };
-  if (k * kValuChunk < u_end) fetch(k * kValuChunk);
-  for (int u = k * kValuChunk; u < u_end; ++u) {
+  if (k * uc < u_end) fetch(k * uc);
+  for (int u = k * uc; u < u_end; ++u) {
     const int t0 = t0n, n = nn, pre = pren, rr = rrn, first = firstn;
     const size_t row = (size_t)g * R + t0 + rr;
     float q[16];
@@ -862,31 +876,54 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
     st16(sv + r * 64 + 16 * s, vn);
     lds_sync();
     if (u + 1 < u_end) fetch(u + 1);
-    float m = -INFINITY, l = 0.f, o[16];
+    // exact two-pass softmax over the prefix keys, then the row's own class keys first..rr: the
+    // scores stay in registers (key loops unrolled to 16 with wave-uniform bounds), so there is
+    // no per-key rescale branch (the online form diverged per row on every new maximum)
+    float sp[16], so[16], m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (j < pre) {
+        float kv[16];
+        ld16(sKp + j * 64 + 16 * s, kv);
+        sp[j] = quad_sum(dot16(q, kv));
+        m = fmaxf(m, sp[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (j < n) {
+        float kv[16];
+        ld16(sk + j * 64 + 16 * s, kv);
+        const float sc = quad_sum(dot16(q, kv));
+        so[j] = (j <= rr && j >= first) ? sc : -INFINITY;
+        m = fmaxf(m, so[j]);
+      }
+    }
+    float l = 0.f, o[16];
 #pragma unroll
     for (int d = 0; d < 16; ++d) o[d] = 0.f;
-    // online softmax over the prefix keys, then the row's own class keys first..rr
-    auto key = [&](const float* kr, const float* vr, bool ok) {
-      float kv[16];
-      ld16(kr + 16 * s, kv);
-      const float sc = quad_sum(dot16(q, kv));
-      if (ok) {
-        if (sc > m) {
-          const float a = __expf(m - sc);  // 0 for the first key (m = -inf)
-          l *= a;
 #pragma unroll
-          for (int d = 0; d < 16; ++d) o[d] *= a;
-          m = sc;
-        }
-        const float p = __expf(sc - m);
+    for (int j = 0; j < 16; ++j) {
+      if (j < pre) {
+        float vv[16];
+        ld16(sVp + j * 64 + 16 * s, vv);
+        const float p = __expf(sp[j] - m);
         l += p;
-        ld16(vr + 16 * s, kv);
 #pragma unroll
-        for (int d = 0; d < 16; ++d) o[d] = fmaf(p, kv[d], o[d]);
+        for (int d = 0; d < 16; ++d) o[d] = fmaf(p, vv[d], o[d]);
       }
-    };
-    for (int j = 0; j < pre; ++j) key(sKp + j * 64, sVp + j * 64, true);
-    for (int j = 0; j < n; ++j) key(sk + j * 64, sv + j * 64, j <= rr && j >= first);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (j < n) {
+        float vv[16];
+        ld16(sv + j * 64 + 16 * s, vv);
+        const float p = __expf(so[j] - m);  // 0 for the masked keys
+        l += p;
+#pragma unroll
+        for (int d = 0; d < 16; ++d) o[d] = fmaf(p, vv[d], o[d]);
+      }
+    }
     if (r < n) {
       const float inv = 1.0f / l;
 #pragma unroll
@@ -906,12 +943,15 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
 template <int WPB>
 __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 waves per SIMD (<= 256 VGPRs)
     int G, int P, int R, int ntiles, const int* __restrict__ tiles, const int* __restrict__ row_first, int H,
-    int nchunk, const float* __restrict__ qkv, int ldq, const float* __restrict__ o_fwd, int ldof,
+    int nchunk, int uc, const float* __restrict__ qkv, int ldq, const float* __restrict__ o_fwd, int ldof,
     const float* __restrict__ dout, int lddo, const float* __restrict__ lse, float* __restrict__ dqkv, int lddq,
     float* __restrict__ part) {
   __shared__ CLIPK_LDS_ALIGN float sKp[16 * 64], sVp[16 * 64];
-  __shared__ CLIPK_LDS_ALIGN float sA[WPB][16 * 64], sB[WPB][16 * 64];  // K|V, then Q|dO
-  __shared__ CLIPK_LDS_ALIGN float sP[WPB][16 * 32], sS[WPB][16 * 32];
+  // padded rows (bank-conflict-free stores): K|V then Q|dO rows at stride RS floats; P / dS at
+  // stride PS (a column of 16 query rows written by one lane per row hit 2 banks at stride 32)
+  constexpr int RS = 68, PS = 33;
+  __shared__ CLIPK_LDS_ALIGN float sA[WPB][16 * RS], sB[WPB][16 * RS];
+  __shared__ CLIPK_LDS_ALIGN float sP[WPB][16 * PS], sS[WPB][16 * PS];
   int g, h, k, w;
   f32_block<WPB>(H, nchunk, g, h, k, w);
   const int W = H * 64;
@@ -926,7 +966,7 @@ __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 wav
   float akp[16], avp[16];  // prefix row r's dK / dV slice, summed over the chunk
 #pragma unroll
   for (int d = 0; d < 16; ++d) { akp[d] = 0.f; avp[d] = 0.f; }
-  const int u_end = min((k + 1) * kValuChunk, ntiles + 1);
+  const int u_end = min((k + 1) * uc, ntiles + 1);
   // the next unit's rows (q, dO, o, k, v, lse) are loaded into registers while this unit
   // computes (one unit ahead, as the forward)
   float qn[16], dOn[16], on[16], kn[16], vn[16], lin = 0.f;
@@ -942,8 +982,8 @@ __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 wav
     ld16(qp + 2 * W, vn);
     lin = lse[rw * H + h];
   };
-  if (k * kValuChunk < u_end) fetch(k * kValuChunk);
-  for (int u = k * kValuChunk; u < u_end; ++u) {
+  if (k * uc < u_end) fetch(k * uc);
+  for (int u = k * uc; u < u_end; ++u) {
     const int t0 = t0n, n = nn, pre = pren, rr = rrn, first = firstn;
     const bool qok = r < n;
     const size_t row = (size_t)g * R + t0 + rr;
@@ -955,8 +995,8 @@ __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 wav
     }
     const float Di = quad_sum(dot16(dO, on));
     const float li = lin;
-    st16(sa + r * 64 + 16 * s, kn);
-    st16(sb + r * 64 + 16 * s, vn);
+    st16(sa + r * RS + 16 * s, kn);
+    st16(sb + r * RS + 16 * s, vn);
     lds_sync();
     if (u + 1 < u_end) fetch(u + 1);
     // phase 1: lane = query row rr
@@ -974,12 +1014,12 @@ __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 wav
 #pragma unroll
       for (int d = 0; d < 16; ++d) dq[d] = fmaf(ds, kv[d], dq[d]);
       if (s == 0) {
-        sp[r * 32 + col] = p;
-        ss[r * 32 + col] = ds;
+        sp[r * PS + col] = p;
+        ss[r * PS + col] = ds;
       }
     };
     for (int j = 0; j < pre; ++j) key(sKp + j * 64, sVp + j * 64, qok, j);
-    for (int j = 0; j < n; ++j) key(sa + j * 64, sb + j * 64, qok && j <= rr && j >= first, 16 + j);
+    for (int j = 0; j < n; ++j) key(sa + j * RS, sb + j * RS, qok && j <= rr && j >= first, 16 + j);
     if (qok) {
 #pragma unroll
       for (int d = 0; d < 16; ++d) dq[d] *= kScale;
@@ -987,16 +1027,16 @@ __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 wav
     }
     // sA / sB: the unit's scaled q and dO rows for the key phases (after every lane's phase-1
     // reads of K / V: program order)
-    st16(sa + r * 64 + 16 * s, q);
-    st16(sb + r * 64 + 16 * s, dO);
+    st16(sa + r * RS + 16 * s, q);
+    st16(sb + r * RS + 16 * s, dO);
     lds_sync();
     // phases 2 / 3: lane = key; sum over the unit's queries i of dS[i][key] q_i, P[i][key] dO_i
     auto keysum = [&](int col, float* dk, float* dv) {
       for (int i = 0; i < n; ++i) {
-        const float pv = sp[i * 32 + col], dsv = ss[i * 32 + col];
+        const float pv = sp[i * PS + col], dsv = ss[i * PS + col];
         float a[16], b[16];
-        ld16(sa + i * 64 + 16 * s, a);
-        ld16(sb + i * 64 + 16 * s, b);
+        ld16(sa + i * RS + 16 * s, a);
+        ld16(sb + i * RS + 16 * s, b);
 #pragma unroll
         for (int d = 0; d < 16; ++d) {
           dk[d] = fmaf(dsv, a[d], dk[d]);
@@ -1101,11 +1141,12 @@ static int prefix_fwd(int G, int P, int R, int ntiles, const int* tiles, const i
       else go(attn_prefix_fwd_mfma<T, 4>);
     }
   } else {
-    const int nchunk = n_chunks(ntiles, kValuChunk);
+    const int uc = f32_uc(G, ntiles, H, kF32FwdWpc);
+    const int nchunk = n_chunks(ntiles, uc);
     auto go = [&](auto kern, int wpb) {
       const long blocks = (long)G * ((nchunk + wpb - 1) / wpb) * H;
       hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * wpb), 0, st, G, P, R, ntiles, tiles, row_first, H, nchunk,
-                         (const float*)qkv, ldq, (float*)out, ldo, lse);
+                         uc, (const float*)qkv, ldq, (float*)out, ldo, lse);
     };
     const int wpb = f32_wpb();
     if (wpb == 2) go(attn_prefix_fwd_f32<2>, 2);
@@ -1121,7 +1162,7 @@ static int prefix_bwd(int G, int P, int R, int ntiles, const int* tiles, const i
                       const void* qkv, int ldq, const void* ofwd, int ldof, const void* dout, int lddo,
                       const float* lse, void* dqkv, int lddq, float* part, hipStream_t st) {
   constexpr bool mfma = sizeof(TG) == 2 && sizeof(T) == 2;
-  const int uc = mfma ? bwd_uc(G, ntiles, H) : kValuChunk;
+  const int uc = mfma ? bwd_uc(G, ntiles, H) : f32_uc(G, ntiles, H, kF32BwdWpc);
   const int nchunk = n_chunks(ntiles, uc);
   const long waves = (long)G * nchunk * H;
   if constexpr (mfma && __is_same(T, TG)) {
@@ -1160,7 +1201,7 @@ static int prefix_bwd(int G, int P, int R, int ntiles, const int* tiles, const i
     auto go = [&](auto kern, int wpb) {
       const long blocks = (long)G * ((nchunk + wpb - 1) / wpb) * H;
       hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * wpb), 0, st, G, P, R, ntiles, tiles, row_first, H, nchunk,
-                         (const float*)qkv, ldq, (const float*)ofwd, ldof, (const float*)dout, lddo, lse,
+                         uc, (const float*)qkv, ldq, (const float*)ofwd, ldof, (const float*)dout, lddo, lse,
                          (float*)dqkv, lddq, part);
     };
     const int wpb = f32_wpb();
@@ -1187,8 +1228,8 @@ static int prefix_shape_ok(int G, int P, int R, int ntiles, int heads, int ldq) 
 
 extern "C" size_t clipk_attention_prefix_ws_bytes(int G, int ntiles, int heads) {
   if (G <= 0 || ntiles <= 0 || heads <= 0) return 0;
-  const int ub = bwd_uc(G, ntiles, heads);
-  const int uc = ub < kValuChunk ? ub : kValuChunk;  // the larger chunk count
+  const int ub = bwd_uc(G, ntiles, heads), uf = f32_uc(G, ntiles, heads, kF32BwdWpc);
+  const int uc = ub < uf ? ub : uf;  // the larger chunk count (16-bit or fp32 backward)
   return (size_t)G * n_chunks(ntiles, uc) * 16 * 2 * heads * 64 * sizeof(float);
 }
 

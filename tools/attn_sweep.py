@@ -30,9 +30,12 @@ def one(iters=30):
     tiles = torch.from_numpy(tl.reshape(-1).copy()).to(dev)
     row_first = torch.from_numpy(rf).to(dev)
     nt = tiles.numel() // 2
-    qkv = (torch.randn(G * R, 3 * W, device=dev) * 0.5).to(torch.float16)
-    dout = (torch.randn(G * R, W, device=dev) * 0.5).to(torch.float16)
-    dq = torch.empty(G * R, 3 * W, device=dev, dtype=torch.float16)
+    # SWEEP_DTYPE=fp32: the fp32 kernels (PREC fp32 / fp32s), which also read the forward output
+    f32 = os.environ.get("SWEEP_DTYPE", "fp16") == "fp32"
+    dt, did, esz = (torch.float32, N.F32, 4) if f32 else (torch.float16, N.F16, 2)
+    qkv = (torch.randn(G * R, 3 * W, device=dev) * 0.5).to(dt)
+    dout = (torch.randn(G * R, W, device=dev) * 0.5).to(dt)
+    dq = torch.empty(G * R, 3 * W, device=dev, dtype=dt)
     nb = N.load().clipk_attention_prefix_ws_bytes(G, nt, H)
     ws = torch.empty(nb, dtype=torch.uint8, device=dev)
     # clean-cache flush: READ 1 GiB (a write flush would leave the 256-MB Infinity Cache full
@@ -45,17 +48,17 @@ def one(iters=30):
     o, lse = ops.attention_prefix(qkv, G, P, R, tiles, row_first, H, lse=True)
 
     def bwd():
-        N.call("clipk_attention_prefix_bwd", N.F16, N.F16, G, P, R, nt, p(tiles), p(row_first), H, p(qkv),
+        N.call("clipk_attention_prefix_bwd", did, did, G, P, R, nt, p(tiles), p(row_first), H, p(qkv),
                3 * W, p(o), W, p(dout), W, p(lse), p(dq), 3 * W, p(ws), nb, sp)
 
     def fwd():
-        N.call("clipk_attention_prefix_fwd", N.F16, G, P, R, nt, p(tiles), p(row_first), H, p(qkv), 3 * W,
+        N.call("clipk_attention_prefix_fwd", did, G, P, R, nt, p(tiles), p(row_first), H, p(qkv), 3 * W,
                p(o), W, p(lse), sp)
 
     rows = G * R
     res = {"rows": rows, "tiles_per_group": nt}
-    for name, fn, by in (("fwd", fwd, rows * W * 4 * 2 + 4 * rows * H),
-                         ("bwd", bwd, rows * W * 8 * 2 + 4 * rows * H)):
+    for name, fn, by in (("fwd", fwd, rows * W * 4 * esz + 4 * rows * H),
+                         ("bwd", bwd, rows * W * (9 if f32 else 8) * esz + 4 * rows * H)):
         ts = []
         for i in range(iters + 3):
             if mode == "clean":
