@@ -250,11 +250,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int width, const 
 
 using namespace clipk;
 
-template <typename TI>
-static int ln_fwd_launch(int out_dtype, int rows, int width, const TI* x, int ldx, const int* in_rows,
-                         const float* gamma, const float* beta, void* out, int ldo, float* mean, float* rstd,
-                         hipStream_t st) {
-  constexpr int RPW = CLIPK_LN_RPW;
+template <typename TI, int RPW>
+static int ln_fwd_launch_rpw(int out_dtype, int rows, int width, const TI* x, int ldx, const int* in_rows,
+                             const float* gamma, const float* beta, void* out, int ldo, float* mean, float* rstd,
+                             hipStream_t st) {
   dim3 grid((rows + 4 * RPW - 1) / (4 * RPW)), block(256);
   const bool v8 = width % 512 == 0 && ldx % 8 == 0 && ldo % 8 == 0;
   const bool one = v8 && width == 512;  // one 64-lane chunk of 8 elements per row
@@ -277,6 +276,29 @@ static int ln_fwd_launch(int out_dtype, int rows, int width, const TI* x, int ld
 #undef CLIPK_LNF
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
+}
+// Rows per wave: CLIPK_LN_RPW (2) for the 16-bit residual stream; for an fp32 one (PREC fp32 /
+// fp32s: twice the bytes per row) knob CLIPK_LN_RPW32 = 1, 2 or 4 (default 2)
+static int ln_rpw32() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLIPK_LN_RPW32");
+    v = e ? atoi(e) : 2;
+    if (v != 1 && v != 4) v = 2;
+  }
+  return v;
+}
+template <typename TI>
+static int ln_fwd_launch(int out_dtype, int rows, int width, const TI* x, int ldx, const int* in_rows,
+                         const float* gamma, const float* beta, void* out, int ldo, float* mean, float* rstd,
+                         hipStream_t st) {
+  if constexpr (sizeof(TI) == 4) {
+    const int r = ln_rpw32();
+    if (r == 1) return ln_fwd_launch_rpw<TI, 1>(out_dtype, rows, width, x, ldx, in_rows, gamma, beta, out, ldo, mean, rstd, st);
+    if (r == 4) return ln_fwd_launch_rpw<TI, 4>(out_dtype, rows, width, x, ldx, in_rows, gamma, beta, out, ldo, mean, rstd, st);
+  }
+  return ln_fwd_launch_rpw<TI, CLIPK_LN_RPW>(out_dtype, rows, width, x, ldx, in_rows, gamma, beta, out, ldo, mean,
+                                            rstd, st);
 }
 
 extern "C" int clipk_layernorm_fwd_x(int x_dtype, int out_dtype, int rows, int width, const void* x, int ldx,
