@@ -68,6 +68,7 @@ SIGNATURES = {
     "clipk_meta_net_fwd": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "clipk_meta_net_bwd": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "clipk_sgd_step": (_I, [_L, _P, _P, _P, _F, _F, _F, _I, _P]),
+    "clipk_sgd_step_multi": (_I, [_I, _P, _P, _P, _P, _P, _F, _F, _F, _P]),
     "clipk_cast": (_I, [_I, _L, _P, _P, _P]),
     "clipk_rows_copy": (_I, [_I, _I, _P, _P, _P, _P, _P]),
     "clipk_vit_embed_ln_vpt": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),

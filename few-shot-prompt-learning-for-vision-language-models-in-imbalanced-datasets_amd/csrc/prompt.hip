@@ -310,12 +310,71 @@ __global__ __launch_bounds__(64) void ce_loss_kernel(int B, int C, const float* 
 }
 
 // ---------------------------------------------------------------- Meta-Net (cocoop.py:139-143)
+// Block (image b, 64-output block ob): every block of an image recomputes the Hd hidden units
+// (W1 stays in L2). Lane l of a wave holds x[b, 4 l .. 4 l + 3 (+ 256 i)] and the matching W1
+// columns of up to 16 hidden units, all loaded before the first sum, so the wave pays one load
+// round trip instead of one per hidden unit (the first form, a dependent load + wave sum per
+// unit, took 23-24 us at any batch: a latency chain on the step's critical path). Then 4 lanes
+// per output split the Hd-long second dot product (fixed order: 4 interleaved partial sums, then
+// the quad sum). V % 256 == 0, V <= 1024, Hd <= 64, 16-B aligned x / W1 (the CLIP widths);
+// other shapes run meta_net_fwd_generic_kernel.
 __global__ __launch_bounds__(256) void meta_net_fwd_kernel(int V, int Hd, int Wd, const float* __restrict__ x,
                                                            const float* __restrict__ w1,
                                                            const float* __restrict__ b1,
                                                            const float* __restrict__ w2,
                                                            const float* __restrict__ b2,
                                                            float* __restrict__ h, float* __restrict__ y) {
+  extern __shared__ float sh[];  // Hd floats
+  const int b = blockIdx.x, ob = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nc = V / 256;  // float4 chunks per lane (1..4)
+  const float* xb = x + (size_t)b * V;
+  f32x4 xv[4], wk[16][4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    if (c < nc) xv[c] = *reinterpret_cast<const f32x4*>(xb + 4 * lane + 256 * c);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int k = wv + 4 * j;
+    if (k < Hd) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (c < nc) wk[j][c] = *reinterpret_cast<const f32x4*>(w1 + (size_t)k * V + 4 * lane + 256 * c);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int k = wv + 4 * j;
+    if (k < Hd) {
+      float a = 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (c < nc)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a = fmaf(wk[j][c][e], xv[c][e], a);
+      a = fmaxf(wave_sum(a) + b1[k], 0.f);
+      if (lane == 0) { sh[k] = a; if (h && ob == 0) h[(size_t)b * Hd + k] = a; }
+    }
+  }
+  __syncthreads();
+  const int o = ob * 64 + (tid >> 2), part = tid & 3;
+  const bool ok = o < Wd;
+  float a = 0.f;
+  if (ok) {
+#pragma unroll 16
+    for (int k = part; k < Hd; k += 4) a += w2[(size_t)o * Hd + k] * sh[k];
+  }
+  a += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, a), 0xB1, 0xF, 0xF, false));
+  a += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, a), 0x4E, 0xF, 0xF, false));
+  if (ok && part == 0) y[(size_t)b * Wd + o] = a + b2[o];
+}
+
+// any V / Hd (tiny test models): one block per image, a dependent load + wave sum per hidden unit
+__global__ __launch_bounds__(256) void meta_net_fwd_generic_kernel(int V, int Hd, int Wd, const float* __restrict__ x,
+                                                                   const float* __restrict__ w1,
+                                                                   const float* __restrict__ b1,
+                                                                   const float* __restrict__ w2,
+                                                                   const float* __restrict__ b2,
+                                                                   float* __restrict__ h, float* __restrict__ y) {
   extern __shared__ float sh[];  // Hd floats
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const float* xb = x + (size_t)b * V;
@@ -390,6 +449,32 @@ __global__ __launch_bounds__(256) void meta_net_bwd_b_kernel(int B, int V, int H
 __global__ __launch_bounds__(256) void sgd_kernel(long n, float* __restrict__ p, const float* __restrict__ g,
                                                   float* __restrict__ buf, float lr, float mom, float wd,
                                                   int has_buf) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float d = g[i] + wd * p[i];
+    const float bb = has_buf ? mom * buf[i] + d : d;
+    buf[i] = bb;
+    p[i] -= lr * bb;
+  }
+}
+
+// One launch for every parameter of a group (the prompt learner's ctx + Meta-Net: five launches
+// at the reference's batch of 1, each a kernel boundary on the step's critical path): tensor
+// blockIdx.y, the per-element arithmetic of sgd_kernel (bitwise the same update)
+constexpr int kSgdMaxTensors = 16;
+struct SgdTensors {
+  float* p[kSgdMaxTensors];
+  const float* g[kSgdMaxTensors];
+  float* buf[kSgdMaxTensors];
+  long n[kSgdMaxTensors];
+  int has[kSgdMaxTensors];
+};
+__global__ __launch_bounds__(256) void sgd_multi_kernel(SgdTensors t, float lr, float mom, float wd) {
+  const int k = blockIdx.y;
+  const long n = t.n[k];
+  float* __restrict__ p = t.p[k];
+  const float* __restrict__ g = t.g[k];
+  float* __restrict__ buf = t.buf[k];
+  const int has_buf = t.has[k];
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
     const float d = g[i] + wd * p[i];
     const float bb = has_buf ? mom * buf[i] + d : d;
@@ -599,7 +684,13 @@ extern "C" int clipk_meta_net_fwd(int B, int V, int Hd, int Wd, const float* x, 
   if (!x || !w1 || !b1 || !w2 || !b2 || !y) return CLIPK_EINVAL;
   if (B < 0 || V <= 0 || Hd <= 0 || Wd <= 0) return CLIPK_ESHAPE;
   if (B == 0) return CLIPK_OK;
-  hipLaunchKernelGGL(meta_net_fwd_kernel, dim3(B), dim3(256), Hd * sizeof(float), (hipStream_t)stream,
+  if (V % 256 || V > 1024 || Hd > 64 || ((uintptr_t)x | (uintptr_t)w1) % 16) {
+    hipLaunchKernelGGL(meta_net_fwd_generic_kernel, dim3(B), dim3(256), Hd * sizeof(float), (hipStream_t)stream, V,
+                       Hd, Wd, x, w1, b1, w2, b2, h, y);
+    CLIPK_CHECK_LAUNCH();
+    return CLIPK_OK;
+  }
+  hipLaunchKernelGGL(meta_net_fwd_kernel, dim3(B, (Wd + 63) / 64), dim3(256), Hd * sizeof(float), (hipStream_t)stream,
                      V, Hd, Wd, x, w1, b1, w2, b2, h, y);
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
@@ -618,6 +709,29 @@ extern "C" int clipk_meta_net_bwd(int B, int V, int Hd, int Wd, const float* x, 
   CLIPK_CHECK_LAUNCH();
   hipLaunchKernelGGL(meta_net_bwd_b_kernel, dim3((nw1 + 255) / 256), dim3(256), 0, st, B, V, Hd, x, dh_ws, dw1,
                      db1);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_sgd_step_multi(int count, float* const* p, const float* const* g, float* const* buf,
+                                    const long* n, const int* has_buf, float lr, float momentum,
+                                    float weight_decay, void* stream) {
+  if (count < 0 || count > kSgdMaxTensors || (count && (!p || !g || !buf || !n || !has_buf))) return CLIPK_EINVAL;
+  SgdTensors t{};
+  long nmax = 0;
+  for (int k = 0; k < count; ++k) {
+    if (!p[k] || !g[k] || !buf[k]) return CLIPK_EINVAL;
+    if (n[k] < 0) return CLIPK_ESHAPE;
+    t.p[k] = p[k];
+    t.g[k] = g[k];
+    t.buf[k] = buf[k];
+    t.n[k] = n[k];
+    t.has[k] = has_buf[k];
+    nmax = n[k] > nmax ? n[k] : nmax;
+  }
+  if (nmax == 0) return CLIPK_OK;
+  hipLaunchKernelGGL(sgd_multi_kernel, dim3(grid_for(nmax), count), dim3(256), 0, (hipStream_t)stream, t, lr,
+                     momentum, weight_decay);
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
 }

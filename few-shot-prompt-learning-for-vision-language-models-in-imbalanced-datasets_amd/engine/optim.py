@@ -32,6 +32,9 @@ class FusedSGD(torch.optim.Optimizer):
     def step(self, closure=None):
         loss = closure() if closure is not None else None
         for grp in self.param_groups:
+            # the group's tensors in one launch per 16 (clipk_sgd_step_multi): at the reference's
+            # batch of 1 the five per-tensor launches were kernel boundaries on the critical path
+            ps, gs, bufs, has = [], [], [], []
             for p in grp["params"]:
                 if p.grad is None:
                     continue
@@ -39,16 +42,22 @@ class FusedSGD(torch.optim.Optimizer):
                     raise RuntimeError("FusedSGD runs on the GPU only (HIP kernel); no CPU path")
                 if grp.get("dampening", 0) != 0 or grp.get("nesterov", False) or grp.get("maximize", False):
                     raise ValueError("FusedSGD implements dampening=0, nesterov=False, maximize=False")
+                if p.dtype != torch.float32 or not p.is_contiguous():
+                    raise ValueError("FusedSGD: fp32 contiguous parameters")
                 st = self.state[p]
                 buf = st.get("momentum_buffer")
-                has = buf is not None
-                if not has:
+                h = buf is not None
+                if not h:
                     buf = st["momentum_buffer"] = torch.empty_like(p)
                 elif buf.device != p.device or not buf.is_contiguous():
                     buf = st["momentum_buffer"] = buf.to(p.device).contiguous()
-                ops.sgd_step(p.data, p.grad.contiguous(), buf, grp["lr"], grp["momentum"],
-                             grp["weight_decay"], has)
+                ps.append(p.data)
+                gs.append(p.grad if p.grad.is_contiguous() else p.grad.contiguous())
+                bufs.append(buf)
+                has.append(h)
                 p._clipk_gen = getattr(p, "_clipk_gen", 0) + 1  # invalidates cached text features
+            if ps:
+                ops.sgd_step_multi(ps, gs, bufs, grp["lr"], grp["momentum"], grp["weight_decay"], has)
         return loss
 
 

@@ -322,6 +322,19 @@ def sgd_step(p, g, buf, lr, momentum, weight_decay, has_buf):
            float(weight_decay), int(has_buf), _stream())
 
 
+def sgd_step_multi(ps, gs, bufs, lr, momentum, weight_decay, has_bufs):
+    """clipk_sgd_step_multi: one launch per 16 tensors (fp32, contiguous, on one device)."""
+    import ctypes
+    for i in range(0, len(ps), 16):
+        P_, G_, B_ = ps[i:i + 16], gs[i:i + 16], bufs[i:i + 16]
+        c = len(P_)
+        VP = ctypes.c_void_p * c
+        N.call("clipk_sgd_step_multi", c, VP(*[t.data_ptr() for t in P_]), VP(*[t.data_ptr() for t in G_]),
+               VP(*[t.data_ptr() for t in B_]), (ctypes.c_long * c)(*[t.numel() for t in P_]),
+               (ctypes.c_int * c)(*[int(h) for h in has_bufs[i:i + 16]]), float(lr), float(momentum),
+               float(weight_decay), _stream())
+
+
 def cast(x, dtype):
     y = torch.empty(x.shape, device=x.device, dtype=dtype)
     N.call("clipk_cast", DT[dtype], x.numel(), _p(x.contiguous()), _p(y), _stream())

@@ -25,6 +25,7 @@
  *                         (coop.py:131-163,324; cocoop.py:66-101,233)
  *   clipk_meta_net_*      CoCoOp Meta-Net Linear-ReLU-Linear (cocoop.py:139-143,182-185)
  *   clipk_sgd_step        torch.optim.SGD momentum/wd step (dassl optim/optimizer.py:105-113)
+ *   clipk_sgd_step_multi  the same over a param group's tensors in one launch
  *   clipk_text_*          TextEncoder.forward + its input-grad backward (coop.py:195-205)
  *   clipk_vit_forward     VisionTransformer.forward (model.py:401-431), frozen, fwd only
  */
@@ -304,7 +305,9 @@ int clipk_ce_loss(int B, int C, const float* logits, const int64_t* labels, cons
                   float gamma, int focal, float grad_scale, float* row_loss, float* dlogits,
                   void* stream);
 
-/* CoCoOp Meta-Net: h = relu(x W1^T + b1); y = h W2^T + b2. x [B,V], W1 [Hd,V], W2 [Wd,Hd]. */
+/* CoCoOp Meta-Net: h = relu(x W1^T + b1); y = h W2^T + b2. x [B,V], W1 [Hd,V], W2 [Wd,Hd].
+ * The CLIP widths (V % 256 == 0, V <= 1024, Hd <= 64, x / W1 16-B aligned) take the
+ * many-block form; other shapes one block per image. */
 int clipk_meta_net_fwd(int B, int V, int Hd, int Wd, const float* x, const float* w1,
                        const float* b1, const float* w2, const float* b2, float* h, float* y,
                        void* stream);
@@ -316,6 +319,11 @@ int clipk_meta_net_bwd(int B, int V, int Hd, int Wd, const float* x, const float
 /* p -= lr * (buf = momentum*buf + (g + wd*p)); first step (has_buf==0): buf = g + wd*p. */
 int clipk_sgd_step(long n, float* p, const float* g, float* buf, float lr, float momentum,
                    float weight_decay, int has_buf, void* stream);
+/* clipk_sgd_step over up to 16 tensors of one param group in one launch (p[k], g[k], buf[k] of
+ * n[k] floats, has_buf[k] per tensor; host arrays): the same per-element update. */
+int clipk_sgd_step_multi(int count, float* const* p, const float* const* g, float* const* buf,
+                         const long* n, const int* has_buf, float lr, float momentum,
+                         float weight_decay, void* stream);
 
 /* Row gather / scatter: dst row (dst_rows ? dst_rows[i] : i) = src row (src_rows ? src_rows[i] : i)
  * for i < n; rows of row_bytes (multiple of 16) bytes, 16-B aligned. The text encoder's last

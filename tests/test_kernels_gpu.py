@@ -296,9 +296,9 @@ def test_cosine_logits_ce_focal(dev):
         close(dtxt, txt.grad, torch.float32, "dtxt")
 
 
-def test_meta_net_and_sgd(dev):
+@pytest.mark.parametrize("B,V,Wd", [(4, 512, 512), (1, 768, 768), (3, 1024, 640), (2, 96, 80)])
+def test_meta_net_and_sgd(dev, B, V, Wd):
     g = torch.Generator().manual_seed(3)
-    B, V, Wd = 4, 512, 512
     Hd = V // 16
     x = torch.randn(B, V, generator=g).to(dev)
     w1 = (torch.randn(Hd, V, generator=g) * 0.05).to(dev).requires_grad_(True)
@@ -323,6 +323,18 @@ def test_meta_net_and_sgd(dev):
         opt.step()
         ops.sgd_step(p, gr, buf, 0.002, 0.9, 5e-4, step > 0)
     close(p, pr.detach(), torch.float32, "sgd")
+    # the multi-tensor launch (FusedSGD's path): bitwise the per-tensor update, ragged sizes
+    sizes = [1000, 17, 4096, 1, 2048]
+    ps = [torch.randn(n, generator=g).to(dev) for n in sizes]
+    gs = [torch.randn(n, generator=g).to(dev) for n in sizes]
+    pa, ba = [t.clone() for t in ps], [torch.zeros_like(t) for t in ps]
+    pb, bb = [t.clone() for t in ps], [torch.zeros_like(t) for t in ps]
+    for step in range(3):
+        for t, gt, mt in zip(pa, gs, ba):
+            ops.sgd_step(t, gt, mt, 0.002, 0.9, 5e-4, step > 0)
+        ops.sgd_step_multi(pb, gs, bb, 0.002, 0.9, 5e-4, [step > 0] * len(sizes))
+    for t1, t2, m1, m2 in zip(pa, pb, ba, bb):
+        assert torch.equal(t1, t2) and torch.equal(m1, m2)
 
 
 @pytest.mark.parametrize("cfg", [0, 1, 2, 3, 6])
@@ -638,7 +650,10 @@ def attn_prefix_ref(qkv, G, C, P, R, off, qlen, H):
 @pytest.mark.parametrize("dtype,gdtype", [(torch.float16, torch.bfloat16), (torch.bfloat16, torch.bfloat16),
                                           (torch.float16, torch.float16), (torch.float32, torch.float32)])
 @pytest.mark.parametrize("G,C,P,H,max_q", [(2, 37, 5, 8, 6), (1, 19, 16, 2, 7), (3, 16, 2, 4, 16), (2, 3, 9, 2, 1),
-                                           (2, 53, 5, 2, 3), (1, 40, 3, 2, 9)])
+                                           (2, 53, 5, 2, 3), (1, 40, 3, 2, 9),
+                                           # enough waves for the fp32 kernels' units per wave
+                                           # (f32_uc) to leave their 4-unit floor
+                                           (24, 300, 5, 8, 7)])
 def test_attention_prefix_fwd_bwd(dev, dtype, gdtype, G, C, P, H, max_q):
     R, tiles, row_first, off, qlen, g = prefix_case(G, C, P, H, max_q, seed=G * 100 + C + P)
     W = H * 64
