@@ -687,7 +687,7 @@ def test_attention_prefix_kernel_variants(knobs):
                         "-k", "test_attention_prefix_fwd_bwd"], env=env, capture_output=True, text=True, timeout=300,
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-    assert "24 passed" in r.stdout, r.stdout[-500:]
+    assert "28 passed" in r.stdout, r.stdout[-500:]  # 4 dtype pairs x 7 shapes
 
 
 def test_prompt_rows_and_ctx_grad_rows(dev):
