@@ -10,10 +10,12 @@ def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     steps = int(sys.argv[2])
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    sgd = [i for i, r in enumerate(rows) if "sgd_kernel" in r["Kernel_Name"]]
+    # the optimizer step closes each train step: sgd_multi_kernel (one per param group, round 4)
+    # or the per-tensor sgd_kernel launches of earlier builds
+    sgd = [i for i, r in enumerate(rows) if "sgd_kernel" in r["Kernel_Name"] or "sgd_multi_kernel" in r["Kernel_Name"]]
     per = len(sgd) // (steps + 3) if len(sgd) % (steps + 3) == 0 else None
     # the timed region: after the warmup steps' last sgd launch, up to the last sgd launch
-    k = per or 5
+    k = per or 1
     beg = sgd[-steps * k - 1] + 1
     end = sgd[-1] + 1
     agg = defaultdict(lambda: [0, 0.0])
