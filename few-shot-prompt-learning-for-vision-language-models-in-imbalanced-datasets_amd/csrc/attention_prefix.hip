@@ -779,6 +779,27 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_bwd_lds(int G, int P, in
 }
 
 // ------------------------------------------------------------------ fp32 kernels (PREC fp32 / fp32s)
+// lane slice s of a 64-float head row: columns {kCs c + kSl s + e : c, e < 4}. Interleaved
+// (CLIPK_F32_IL=1, default): each f32x4 load of the 4 lanes of a row covers 64 contiguous
+// bytes; contiguous (0): lane s holds columns 16 s .. 16 s + 15. Every global and LDS row
+// access of the fp32 kernels uses this one map, so q / k / v / dO / o slices pair up.
+#ifndef CLIPK_F32_IL
+#define CLIPK_F32_IL 1
+#endif
+constexpr int kSl = CLIPK_F32_IL ? 4 : 16, kCs = CLIPK_F32_IL ? 16 : 4;
+__device__ __forceinline__ void ld16x(const float* __restrict__ p, float* v) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const f32x4 t = *reinterpret_cast<const f32x4*>(p + kCs * c);
+    v[4 * c] = t[0]; v[4 * c + 1] = t[1]; v[4 * c + 2] = t[2]; v[4 * c + 3] = t[3];
+  }
+}
+__device__ __forceinline__ void st16x(float* __restrict__ p, const float* v) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    *reinterpret_cast<f32x4*>(p + kCs * c) = (f32x4){v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]};
+}
+
 // One wave per (group, chunk of f32_uc units, head); blocks of WPB waves (f32_wpb) share one
 // (group, head), so the prefix K/V rows are staged into LDS once per block. Lane = 4 r + s: row
 // r of the unit (query in the forward and for dQ, key for dK / dV) and 16-column slice s of
@@ -860,10 +881,10 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
   int t0n, nn, pren, rrn, firstn;
   auto fetch = [&](int u) {
     f32_unit(tiles, row_first, P, u, r, t0n, nn, pren, rrn, firstn);
-    const float* qp = qkv + ((size_t)g * R + t0n + rrn) * ldq + h * 64 + 16 * s;
-    ld16(qp, qn);
-    ld16(qp + W, kn);
-    ld16(qp + 2 * W, vn);
+    const float* qp = qkv + ((size_t)g * R + t0n + rrn) * ldq + h * 64 + kSl * s;
+    ld16x(qp, qn);
+    ld16x(qp + W, kn);
+    ld16x(qp + 2 * W, vn);
   };
   if (k * uc < u_end) fetch(k * uc);
   for (int u = k * uc; u < u_end; ++u) {
@@ -872,8 +893,8 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
     float q[16];
 #pragma unroll
     for (int d = 0; d < 16; ++d) q[d] = qn[d] * kScale;
-    st16(sk + r * 64 + 16 * s, kn);
-    st16(sv + r * 64 + 16 * s, vn);
+    st16x(sk + r * 64 + kSl * s, kn);
+    st16x(sv + r * 64 + kSl * s, vn);
     lds_sync();
     if (u + 1 < u_end) fetch(u + 1);
     // exact two-pass softmax over the prefix keys, then the row's own class keys first..rr: the
@@ -884,7 +905,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
     for (int j = 0; j < 16; ++j) {
       if (j < pre) {
         float kv[16];
-        ld16(sKp + j * 64 + 16 * s, kv);
+        ld16x(sKp + j * 64 + kSl * s, kv);
         sp[j] = quad_sum(dot16(q, kv));
         m = fmaxf(m, sp[j]);
       }
@@ -893,7 +914,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
     for (int j = 0; j < 16; ++j) {
       if (j < n) {
         float kv[16];
-        ld16(sk + j * 64 + 16 * s, kv);
+        ld16x(sk + j * 64 + kSl * s, kv);
         const float sc = quad_sum(dot16(q, kv));
         so[j] = (j <= rr && j >= first) ? sc : -INFINITY;
         m = fmaxf(m, so[j]);
@@ -906,7 +927,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
     for (int j = 0; j < 16; ++j) {
       if (j < pre) {
         float vv[16];
-        ld16(sVp + j * 64 + 16 * s, vv);
+        ld16x(sVp + j * 64 + kSl * s, vv);
         const float p = __expf(sp[j] - m);
         l += p;
 #pragma unroll
@@ -917,7 +938,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
     for (int j = 0; j < 16; ++j) {
       if (j < n) {
         float vv[16];
-        ld16(sv + j * 64 + 16 * s, vv);
+        ld16x(sv + j * 64 + kSl * s, vv);
         const float p = __expf(so[j] - m);  // 0 for the masked keys
         l += p;
 #pragma unroll
@@ -928,7 +949,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
       const float inv = 1.0f / l;
 #pragma unroll
       for (int d = 0; d < 16; ++d) o[d] *= inv;
-      st16(out + row * ldo + h * 64 + 16 * s, o);
+      st16x(out + row * ldo + h * 64 + kSl * s, o);
       if (lse && s == 0) lse[row * H + h] = m + __logf(l);
     }
     lds_sync();  // this unit's sK / sV reads done before the next unit's writes (program order)
@@ -974,12 +995,12 @@ __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 wav
   auto fetch = [&](int u) {
     f32_unit(tiles, row_first, P, u, r, t0n, nn, pren, rrn, firstn);
     const size_t rw = (size_t)g * R + t0n + rrn;
-    const float* qp = qkv + rw * ldq + h * 64 + 16 * s;
-    ld16(qp, qn);
-    ld16(dout + rw * lddo + h * 64 + 16 * s, dOn);
-    ld16(o_fwd + rw * ldof + h * 64 + 16 * s, on);
-    ld16(qp + W, kn);
-    ld16(qp + 2 * W, vn);
+    const float* qp = qkv + rw * ldq + h * 64 + kSl * s;
+    ld16x(qp, qn);
+    ld16x(dout + rw * lddo + h * 64 + kSl * s, dOn);
+    ld16x(o_fwd + rw * ldof + h * 64 + kSl * s, on);
+    ld16x(qp + W, kn);
+    ld16x(qp + 2 * W, vn);
     lin = lse[rw * H + h];
   };
   if (k * uc < u_end) fetch(k * uc);
@@ -995,8 +1016,8 @@ __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 wav
     }
     const float Di = quad_sum(dot16(dO, on));
     const float li = lin;
-    st16(sa + r * RS + 16 * s, kn);
-    st16(sb + r * RS + 16 * s, vn);
+    st16x(sa + r * RS + kSl * s, kn);
+    st16x(sb + r * RS + kSl * s, vn);
     lds_sync();
     if (u + 1 < u_end) fetch(u + 1);
     // phase 1: lane = query row rr
@@ -1005,8 +1026,8 @@ __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 wav
     for (int d = 0; d < 16; ++d) dq[d] = 0.f;
     auto key = [&](const float* kr, const float* vr, bool ok, int col) {
       float kv[16], vv[16];
-      ld16(kr + 16 * s, kv);
-      ld16(vr + 16 * s, vv);
+      ld16x(kr + kSl * s, kv);
+      ld16x(vr + kSl * s, vv);
       const float sc = quad_sum(dot16(q, kv));
       const float dp = quad_sum(dot16(dO, vv));
       const float p = ok ? __expf(sc - li) : 0.f;
@@ -1023,20 +1044,20 @@ __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 wav
     if (qok) {
 #pragma unroll
       for (int d = 0; d < 16; ++d) dq[d] *= kScale;
-      st16(dqkv + row * lddq + h * 64 + 16 * s, dq);
+      st16x(dqkv + row * lddq + h * 64 + kSl * s, dq);
     }
     // sA / sB: the unit's scaled q and dO rows for the key phases (after every lane's phase-1
     // reads of K / V: program order)
-    st16(sa + r * RS + 16 * s, q);
-    st16(sb + r * RS + 16 * s, dO);
+    st16x(sa + r * RS + kSl * s, q);
+    st16x(sb + r * RS + kSl * s, dO);
     lds_sync();
     // phases 2 / 3: lane = key; sum over the unit's queries i of dS[i][key] q_i, P[i][key] dO_i
     auto keysum = [&](int col, float* dk, float* dv) {
       for (int i = 0; i < n; ++i) {
         const float pv = sp[i * PS + col], dsv = ss[i * PS + col];
         float a[16], b[16];
-        ld16(sa + i * RS + 16 * s, a);
-        ld16(sb + i * RS + 16 * s, b);
+        ld16x(sa + i * RS + kSl * s, a);
+        ld16x(sb + i * RS + kSl * s, b);
 #pragma unroll
         for (int d = 0; d < 16; ++d) {
           dk[d] = fmaf(dsv, a[d], dk[d]);
@@ -1052,8 +1073,8 @@ __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 wav
       for (int d = 0; d < 16; ++d) { dk[d] = 0.f; dv[d] = 0.f; }
       keysum(16 + r, dk, dv);
       if (qok) {
-        st16(dqkv + row * lddq + W + h * 64 + 16 * s, dk);
-        st16(dqkv + row * lddq + 2 * W + h * 64 + 16 * s, dv);
+        st16x(dqkv + row * lddq + W + h * 64 + kSl * s, dk);
+        st16x(dqkv + row * lddq + 2 * W + h * 64 + kSl * s, dv);
       }
       keysum(r, akp, avp);  // prefix key r (zero columns past pre)
     }
@@ -1061,9 +1082,9 @@ __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 wav
   }
   if (r < P) {
     // (dK = sum dS q with q already scaled: no further factor)
-    float* pb = part + (((size_t)g * nchunk + k) * 16 + r) * (2 * W) + h * 64 + 16 * s;
-    st16(pb, akp);
-    st16(pb + W, avp);
+    float* pb = part + (((size_t)g * nchunk + k) * 16 + r) * (2 * W) + h * 64 + kSl * s;
+    st16x(pb, akp);
+    st16x(pb + W, avp);
   }
 }
 
