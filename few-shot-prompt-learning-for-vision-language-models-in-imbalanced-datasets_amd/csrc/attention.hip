@@ -99,7 +99,8 @@ __global__ __launch_bounds__(256) void attn_fwd_short(int nseq, int L, int H, in
 // ------------------------------------------------------------------ forward, any L, fp32
 // (PREC fp32 / fp32s: the ViT's L = 50..577, plain text 64 < L <= 77). Block = 64 query rows of
 // one (sequence, head), 4 waves of 16 rows; lane = 4 r + s holds row r's 16-column slice s of q
-// and o; K / V in 64-key LDS chunks, a score is 16 FMAs + a quad sum, exact online softmax.
+// and o (the interleaved map of attn_common.h); K / V in 64-key LDS chunks, a score is 16 FMAs
+// + a quad sum, exact online softmax.
 __global__ __launch_bounds__(256) void attn_fwd_f32(int nseq, int L, int H, int causal, const float* __restrict__ qkv,
                                                     int ldq, float* __restrict__ out, int ldo,
                                                     float* __restrict__ lse) {
@@ -112,7 +113,7 @@ __global__ __launch_bounds__(256) void attn_fwd_f32(int nseq, int L, int H, int 
   const bool row_ok = i < L;
   const size_t row = (size_t)sq * L + (row_ok ? i : L - 1);
   float q[16], o[16];
-  ld16(qkv + row * ldq + h * 64 + 16 * s, q);
+  ld16x(qkv + row * ldq + h * 64 + kSl * s, q);
 #pragma unroll
   for (int d = 0; d < 16; ++d) {
     q[d] *= kScale;
@@ -127,18 +128,18 @@ __global__ __launch_bounds__(256) void attn_fwd_f32(int nseq, int L, int H, int 
       const int jr = j0 + (tid >> 2), part = tid & 3;
       float t[16];
       if (jr < L) {
-        const float* base = qkv + ((size_t)sq * L + jr) * ldq + h * 64 + part * 16;
-        ld16(base + W, t);
-        st16(&sk[(tid >> 2) * 64 + part * 16], t);
-        ld16(base + 2 * W, t);
-        st16(&sv[(tid >> 2) * 64 + part * 16], t);
+        const float* base = qkv + ((size_t)sq * L + jr) * ldq + h * 64 + part * kSl;
+        ld16x(base + W, t);
+        st16x(&sk[(tid >> 2) * 64 + part * kSl], t);
+        ld16x(base + 2 * W, t);
+        st16x(&sv[(tid >> 2) * 64 + part * kSl], t);
       }
     }
     __syncthreads();
     const int nj = min(64, jend - j0);
     for (int j = 0; j < nj; ++j) {
       float kv[16];
-      ld16(&sk[j * 64 + 16 * s], kv);
+      ld16x(&sk[j * 64 + kSl * s], kv);
       const float sc = quad_sum(dot16(q, kv));
       if (!causal || j0 + j <= i) {
         if (sc > m) {
@@ -150,7 +151,7 @@ __global__ __launch_bounds__(256) void attn_fwd_f32(int nseq, int L, int H, int 
         }
         const float p = __expf(sc - m);
         l += p;
-        ld16(&sv[j * 64 + 16 * s], kv);
+        ld16x(&sv[j * 64 + kSl * s], kv);
 #pragma unroll
         for (int d = 0; d < 16; ++d) o[d] = fmaf(p, kv[d], o[d]);
       }
@@ -160,7 +161,7 @@ __global__ __launch_bounds__(256) void attn_fwd_f32(int nseq, int L, int H, int 
     const float inv = 1.0f / l;
 #pragma unroll
     for (int d = 0; d < 16; ++d) o[d] *= inv;
-    st16(out + row * ldo + h * 64 + 16 * s, o);
+    st16x(out + row * ldo + h * 64 + kSl * s, o);
     if (lse && s == 0) lse[row * H + h] = m + __logf(l);
   }
 }

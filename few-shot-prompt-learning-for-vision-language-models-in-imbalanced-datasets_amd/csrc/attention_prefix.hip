@@ -779,27 +779,6 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_bwd_lds(int G, int P, in
 }
 
 // ------------------------------------------------------------------ fp32 kernels (PREC fp32 / fp32s)
-// lane slice s of a 64-float head row: columns {kCs c + kSl s + e : c, e < 4}. Interleaved
-// (CLIPK_F32_IL=1, default): each f32x4 load of the 4 lanes of a row covers 64 contiguous
-// bytes; contiguous (0): lane s holds columns 16 s .. 16 s + 15. Every global and LDS row
-// access of the fp32 kernels uses this one map, so q / k / v / dO / o slices pair up.
-#ifndef CLIPK_F32_IL
-#define CLIPK_F32_IL 1
-#endif
-constexpr int kSl = CLIPK_F32_IL ? 4 : 16, kCs = CLIPK_F32_IL ? 16 : 4;
-__device__ __forceinline__ void ld16x(const float* __restrict__ p, float* v) {
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const f32x4 t = *reinterpret_cast<const f32x4*>(p + kCs * c);
-    v[4 * c] = t[0]; v[4 * c + 1] = t[1]; v[4 * c + 2] = t[2]; v[4 * c + 3] = t[3];
-  }
-}
-__device__ __forceinline__ void st16x(float* __restrict__ p, const float* v) {
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-    *reinterpret_cast<f32x4*>(p + kCs * c) = (f32x4){v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]};
-}
-
 // One wave per (group, chunk of f32_uc units, head); blocks of WPB waves (f32_wpb) share one
 // (group, head), so the prefix K/V rows are staged into LDS once per block. Lane = 4 r + s: row
 // r of the unit (query in the forward and for dQ, key for dK / dV) and 16-column slice s of

@@ -4,6 +4,8 @@ setting (the CLIPK_PREFIX_* knobs are read once per process).
 
     python tools/attn_sweep.py            # sweep (spawns one child per setting)
     python tools/attn_sweep.py --one      # time the current environment's setting
+    python tools/attn_sweep.py --anyl     # the fp32 any-L forward (attn_fwd_f32): ViT-B/16
+                                          # L = 197 (100 images) and plain text L = 77 (causal)
 """
 import ctypes
 import json
@@ -92,7 +94,39 @@ SWEEP = [
 ]
 
 
+def anyl(iters=30):
+    import torch
+    from fsp_amd import _native as N
+    dev = torch.device("cuda")
+    st = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(st.cuda_stream)
+    flush = torch.ones(1 << 28, dtype=torch.float32, device=dev)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    res = {}
+    for name, nseq, L, H, causal in (("vit_L197", 100, 197, 12, 0), ("text_L77", 1000, 77, 8, 1)):
+        W = H * 64
+        qkv = torch.randn(nseq * L, 3 * W, device=dev) * 0.5
+        o = torch.empty(nseq * L, W, device=dev)
+        lse = torch.empty(nseq * L, H, device=dev)
+        ts = []
+        for i in range(iters + 3):
+            flush.max()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(st)
+            N.call("clipk_attention_fwd", N.F32, nseq, L, H, causal, p(qkv), 3 * W, p(o), W, p(lse), sp)
+            b.record(st)
+            torch.cuda.synchronize()
+            if i >= 3:
+                ts.append(a.elapsed_time(b))
+        ts.sort()
+        res[name] = {"us": round(ts[len(ts) // 2] * 1e3, 1)}
+    print(json.dumps(res), flush=True)
+
+
 def main():
+    if "--anyl" in sys.argv:
+        anyl()
+        return
     if "--one" in sys.argv:
         one()
         return
