@@ -128,18 +128,30 @@ def ln_fold_enabled() -> bool:
     return os.environ.get("FSP_LN_FOLD", "1") != "0"
 
 
-def ln_fold_weights(w, b, gamma, beta, act, device):
+def ln_fold_weights(w, b, gamma, beta, act, device, split=False):
     """LayerNorm folded into the Linear that consumes it (include/clipk.h, clipk_gemm_ln):
     LN(x) W^T + b = rstd * (x W'^T - mean * s) + c with W' = W diag(gamma) in the operand dtype,
     s = W' summed over its input dimension (of the rounded W'), c = b + W beta.
+    ``split`` (PREC fp32s): W' fp32, split-packed (ops.split_pack), and s summed over the value
+    the split GEMM multiplies by, (hi + lo) / SPLIT_SCALE, so the mean term cancels against it.
     Returns (W', s, c) on ``device``, or None when W' does not fit the operand dtype."""
     wd = w.double()
     wp = (wd * gamma.double()[None, :]).to(act)
     if not bool(torch.isfinite(wp.float()).all()):
         return None
-    s = wp.double().sum(1).float()
+    if split:
+        x = wp.float() * N.SPLIT_SCALE
+        if not float(x.abs().max()) < 65504.0:
+            return None
+        hi = x.half().float()
+        lo = (x - hi).half().float()  # x - hi is exact in fp32, as in clipk_split_pack
+        s = ((hi.double() + lo.double()) / N.SPLIT_SCALE).sum(1).float()
+        wdev = ops.split_pack(wp.float().to(device).contiguous())
+    else:
+        s = wp.double().sum(1).float()
+        wdev = wp.to(device).contiguous()
     c = (b.double() + wd @ beta.double()).float()
-    return (wp.to(device).contiguous(), s.to(device).contiguous(), c.to(device).contiguous())
+    return (wdev, s.to(device).contiguous(), c.to(device).contiguous())
 
 
 class _Encoder:
@@ -166,8 +178,9 @@ class TextEncoderCore(_Encoder):
         self.W, self.E, self.layers, self.heads = W, arch.embed_dim, nl, W // 64
         keep = []
         table = []
-        # LayerNorm fold of ln_1 / ln_2 into in_proj / c_fc (16-bit encoders; clipk_encoder_set_ln_fold)
-        fold = [] if act != torch.float32 and ln_fold_enabled() else None
+        # LayerNorm fold of ln_1 / ln_2 into in_proj / c_fc (16-bit encoders and PREC fp32s;
+        # clipk_encoder_set_ln_fold)
+        fold = [] if (act != torch.float32 or split) and ln_fold_enabled() else None
         for i in range(nl):
             p = {k: _t(sd[f"transformer.resblocks.{i}.{k}"]).float() for k in _LAYER_KEYS}
             f32 = lambda x: x.to(self.device, torch.float32).contiguous()
@@ -183,9 +196,9 @@ class TextEncoderCore(_Encoder):
             table += row
             if fold is not None:
                 f_in = ln_fold_weights(p["attn.in_proj_weight"], p["attn.in_proj_bias"], p["ln_1.weight"],
-                                       p["ln_1.bias"], act, self.device)
+                                       p["ln_1.bias"], act, self.device, split)
                 f_fc = ln_fold_weights(p["mlp.c_fc.weight"], p["mlp.c_fc.bias"], p["ln_2.weight"],
-                                       p["ln_2.bias"], act, self.device)
+                                       p["ln_2.bias"], act, self.device, split)
                 fold = fold + list(f_in) + list(f_fc) if f_in and f_fc else None
         P = _t(sd["text_projection"]).float()
         head = [_t(sd["ln_final.weight"]).float().to(self.device).contiguous(),

@@ -481,6 +481,7 @@ static int gemm_ln(int act, int epi, int M, int N, int K, const void* A, const v
   const double b = gemm_bytes(act, act, epi, M, N, K, o2 != nullptr, act) + (stats ? (double)M * (N / 64) * 8 : 0.0) +
                    (rnb ? 8.0 * M : 0.0);
   ProfScope ps(prof_cls, st, 2.0 * M * N * K, site, b);
+  if (t_split && act == CLIPK_F32) act = CLIPK_F32S;  // PREC fp32s: the split-packed weights
   return clipk_gemm_ln_ws(act, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, stats, colsum, rnb, t_gemm_ws,
                           t_gemm_ws ? clipk_gemm_ws_bytes() : 0, st);
 }
@@ -633,7 +634,7 @@ static EncIO text_io(const clipk_encoder* e) {
 #define SITE(n) (io.text ? "text." n : "vit." n)
 
 // LN fold in this call: set on the encoder, 16-bit residual stream (the text encoder's, or the
-// ViT's forward, clipk_vit_forward), no deep prompts (they rewrite rows between a producer's
+// ViT's forward, clipk_vit_forward) or PREC fp32s (fp32 stream, split GEMMs), no deep prompts (they rewrite rows between a producer's
 // statistics and their use) and not the A-operand QuickGELU knob. Knob CLIPK_TEXT_LNFOLD=0 runs
 // the LayerNorm passes.
 static bool ln_fold_on(const clipk_encoder* e, const EncIO& io) {
@@ -644,7 +645,7 @@ static bool ln_fold_on(const clipk_encoder* e, const EncIO& io) {
   }
   // clipk_ln_stats_merge covers widths that are multiples of 128 up to 1024; wider encoders run
   // the LayerNorm passes
-  return v != 0 && (int)e->fold.size() == e->layers && e->act != CLIPK_F32 && io.rd == e->act &&
+  return v != 0 && (int)e->fold.size() == e->layers && (e->act != CLIPK_F32 || e->split) && io.rd == e->act &&
          e->W % 128 == 0 && e->W <= 1024 && !(e->deep.n_deep > 0 && e->deep.prompts) && !a_qgelu_on();
 }
 
@@ -1258,7 +1259,7 @@ extern "C" int clipk_encoder_set_ln_fold(clipk_encoder* e, const void* const* fo
     e->fold.clear();
     return CLIPK_OK;
   }
-  if (e->act == CLIPK_F32) return CLIPK_EDTYPE;
+  if (e->act == CLIPK_F32 && !e->split) return CLIPK_EDTYPE;  // fp32s: call after set_split
   std::vector<std::array<const void*, 6>> f(e->layers);
   for (int l = 0; l < e->layers; ++l)
     for (int i = 0; i < 6; ++i) {

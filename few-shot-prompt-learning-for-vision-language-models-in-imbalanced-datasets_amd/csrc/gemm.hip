@@ -75,6 +75,13 @@ __device__ __forceinline__ float sum8(float v) {
   v += dpp_f<0x4E>(v);
   return v + dpp_f<0x141>(v);
 }
+// Sum over the aligned 8- or 16-lane group (16: + the row mirror i <-> 15 - i, the other half)
+template <int L>
+__device__ __forceinline__ float sum_group(float v) {
+  v = sum8(v);
+  if constexpr (L == 16) v += dpp_f<0x140>(v);
+  return v;
+}
 constexpr int STAMP_TILES = 8, STAMP_BLOCKS = 2048;
 
 template <typename T>
@@ -555,9 +562,9 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
     // producer's partials here instead of in clipk_ln_stats_merge -- 2 loads + 2 8-lane sums per
     // row -- measured slower: qkv 86 -> 110 us, c_fc 129 -> 158 us per launch.)
     constexpr bool LN_IN = LNM == 2, LN_OUT = LNM == 1;
-    static_assert(!LN_OUT || (EPI == CLIPK_EPI_BIAS_RES && sizeof(TO) == 2 && CW == 8), "LN statistics: 16-bit out");
-    static_assert(!LN_IN || ((EPI == CLIPK_EPI_BIAS || epi_qgelu(EPI)) && sizeof(T) == 2 && CW == 8),
-                  "LN fold");
+    // (16-bit out: 8 lanes per row of 64 columns; PREC fp32s, fp32 out: 16)
+    static_assert(!LN_OUT || (EPI == CLIPK_EPI_BIAS_RES && (sizeof(TO) == 2 || SPLIT)), "LN statistics");
+    static_assert(!LN_IN || ((EPI == CLIPK_EPI_BIAS || epi_qgelu(EPI)) && (sizeof(T) == 2 || SPLIT)), "LN fold");
     [[maybe_unused]] f32x2 lnp[LN_IN ? 2 : 1][NQ];
     auto load_ln = [&](int i, int slot) {
       if constexpr (LN_IN) {
@@ -985,14 +992,14 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
               vr[c] = to_f32((TO)v[c]);  // the stored value
               s += vr[c];
             }
-            s = sum8(s);
+            s = sum_group<LPR>(s);
             const float mu = s * (1.0f / 64.0f);
 #pragma unroll
             for (int c = 0; c < CW; ++c) {
               const float d = vr[c] - mu;
               s2 = fmaf(d, d, s2);
             }
-            s2 = sum8(s2);
+            s2 = sum_group<LPR>(s2);
             typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
             const int so = ec == 0 ? ((m - m0) * lng + nbase / 64) * 8 : 0x40000000;
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, (f32x2){s, s2}), rst, so, 0, 0);
@@ -1286,7 +1293,7 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
 // picks the 192- or 256-row tiles): the ping-pong loop on 192x256 tiles (256-row ones spill at
 // 256 VGPRs with the split's temporaries); otherwise 128x128 tiles (a 4-slot ring when the grid
 // is at most one tile per CU).
-template <int EPI>
+template <int EPI, int LNM = 0>
 static int launch_gemm_split(const GemmArgs& g, hipStream_t st) {
   const int cus = num_cus();
   const_cast<GemmArgs&>(g).stamp = gemm_stamp_buf();
@@ -1295,26 +1302,26 @@ static int launch_gemm_split(const GemmArgs& g, hipStream_t st) {
   if (cfg == 7) {  // small M (the ViT): 64x128 tiles, twice the 128x128 grid
     const int nwg = ((g.M + 63) / 64) * (g.N / 128);
     if (nwg <= cus && deep_small())
-      hipLaunchKernelGGL((gemm_nt_kernel<f32s, float, float, EPI, 64, 128, 2, 2, false, GEMM_ROWB, 4>), dim3(nwg),
+      hipLaunchKernelGGL((gemm_nt_kernel<f32s, float, float, EPI, 64, 128, 2, 2, false, GEMM_ROWB, 4, false, false, LNM>), dim3(nwg),
                          dim3(256), 0, st, g);
     else
-      hipLaunchKernelGGL((gemm_nt_kernel<f32s, float, float, EPI, 64, 128, 2, 2, false, GEMM_ROWB, 2>), dim3(nwg),
+      hipLaunchKernelGGL((gemm_nt_kernel<f32s, float, float, EPI, 64, 128, 2, 2, false, GEMM_ROWB, 2, false, false, LNM>), dim3(nwg),
                          dim3(256), 0, st, g);
     CLIPK_CHECK_LAUNCH();
     return CLIPK_OK;
   }
   if (cfg == 1 || cfg == 6) {
-    if (try_pp<f32s, float, float, EPI, 192>(g, ((g.M + 191) / 192) * (g.N / 256), st)) {
+    if (try_pp<f32s, float, float, EPI, 192, LNM>(g, ((g.M + 191) / 192) * (g.N / 256), st)) {
       CLIPK_CHECK_LAUNCH();
       return CLIPK_OK;
     }
   }
   const int nwg = ((g.M + 127) / 128) * (g.N / 128);
   if (nwg <= cus && deep_small())
-    hipLaunchKernelGGL((gemm_nt_kernel<f32s, float, float, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 4>), dim3(nwg),
+    hipLaunchKernelGGL((gemm_nt_kernel<f32s, float, float, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 4, false, false, LNM>), dim3(nwg),
                        dim3(256), 0, st, g);
   else
-    hipLaunchKernelGGL((gemm_nt_kernel<f32s, float, float, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 2>), dim3(nwg),
+    hipLaunchKernelGGL((gemm_nt_kernel<f32s, float, float, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 2, false, false, LNM>), dim3(nwg),
                        dim3(256), 0, st, g);
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
@@ -1519,10 +1526,18 @@ static int dispatch_ln(int epi, const GemmArgs& g, hipStream_t st) {
   if (epi == EPI_QGELU_D) return launch_gemm<T, T, float, EPI_QGELU_D, 2>(g, st);
   return launch_gemm<T, T, float, CLIPK_EPI_BIAS_QGELU, 2>(g, st);
 }
+// PREC fp32s (A fp32, B split-packed, fp32 out / residual / quickgelu')
+static int dispatch_ln_split(int epi, const GemmArgs& g, hipStream_t st) {
+  if (!g.colsum) return launch_gemm_split<CLIPK_EPI_BIAS_RES, 1>(g, st);
+  if (epi == CLIPK_EPI_BIAS) return launch_gemm_split<CLIPK_EPI_BIAS, 2>(g, st);
+  if (epi == EPI_QGELU_D) return launch_gemm_split<EPI_QGELU_D, 2>(g, st);
+  return launch_gemm_split<CLIPK_EPI_BIAS_QGELU, 2>(g, st);
+}
 }  // namespace clipk
 
 // LayerNorm folded into the text GEMMs (include/clipk.h): statistics partials out (EPI_BIAS_RES)
-// or colsum + per-row (rstd, -rstd * mean) in (EPI_BIAS / EPI_BIAS_QGELU); 16-bit in and out.
+// or colsum + per-row (rstd, -rstd * mean) in (EPI_BIAS / EPI_BIAS_QGELU); 16-bit in and out, or
+// CLIPK_F32S (fp32 A / out / residual, B split-packed).
 extern "C" int clipk_gemm_ln_ws(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B,
                                 int ldb, const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
                                 float* stats, const float* colsum, const float* rnb, void* ws, size_t ws_bytes,
@@ -1542,7 +1557,7 @@ extern "C" int clipk_gemm_ln_ws(int in_dtype, int epi, int M, int N, int K, cons
                                 void* stream) {
   if (!A || !B || !out || !bias) return CLIPK_EINVAL;
   if (ws && ws_bytes < tail_ws_bytes()) return CLIPK_EWORKSPACE;
-  if (in_dtype != CLIPK_F16 && in_dtype != CLIPK_BF16) return CLIPK_EDTYPE;
+  if (in_dtype != CLIPK_F16 && in_dtype != CLIPK_BF16 && in_dtype != CLIPK_F32S) return CLIPK_EDTYPE;
   const bool deriv = (epi & CLIPK_QGELU_DERIV) != 0;  // fold form of c_fc: out2 = quickgelu'
   epi &= ~CLIPK_QGELU_DERIV;
   if (deriv && (epi != CLIPK_EPI_BIAS_QGELU || !colsum)) return CLIPK_EINVAL;
@@ -1552,7 +1567,8 @@ extern "C" int clipk_gemm_ln_ws(int in_dtype, int epi, int M, int N, int K, cons
     if (stats || !rnb || (epi != CLIPK_EPI_BIAS && epi != CLIPK_EPI_BIAS_QGELU)) return CLIPK_EINVAL;
   }
   if (M <= 0) return M == 0 ? CLIPK_OK : CLIPK_ESHAPE;
-  if (N <= 0 || K <= 0 || N % GEMM_NMIN != 0 || (K * 2) % GEMM_ROWB != 0) return CLIPK_ESHAPE;
+  const int esz = in_dtype == CLIPK_F32S ? 4 : 2;
+  if (N <= 0 || K <= 0 || N % GEMM_NMIN != 0 || (K * esz) % GEMM_ROWB != 0) return CLIPK_ESHAPE;
   if (lda < K || ldb < K || lda % 8 || ldb % 8 || ldo < N || ldo % 8) return CLIPK_ESHAPE;
   GemmArgs g{(const char*)A, (const char*)B, M, N, K, lda, ldb, bias, res, ldr, out, ldo, out2, nullptr,
              0, nullptr, 1, 0, 0, stats, colsum, reinterpret_cast<const f32x2*>(rnb)};
@@ -1562,6 +1578,7 @@ extern "C" int clipk_gemm_ln_ws(int in_dtype, int epi, int M, int N, int K, cons
   }
   hipStream_t st = (hipStream_t)stream;
   if (deriv) epi = EPI_QGELU_D;
+  if (in_dtype == CLIPK_F32S) return dispatch_ln_split(epi, g, st);
   return in_dtype == CLIPK_F16 ? dispatch_ln<f16>(epi, g, st) : dispatch_ln<bf16>(epi, g, st);
 }
 

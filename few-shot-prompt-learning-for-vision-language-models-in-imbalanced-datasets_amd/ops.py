@@ -89,9 +89,12 @@ def gemm_ln(a, b, epi, bias, stats=None, res=None, colsum=None, rnb=None, want_o
     Producer (EPI_BIAS_RES, colsum None): the statistics partials of the output are written to
     stats (fp32 [M, N/64, 2]). Fold (EPI_BIAS / EPI_BIAS_QGELU): a is the LayerNorm input x with
     per-row rnb = (rstd, -rstd * mean) (ln_stats_merge of its partials), b = W diag(gamma),
-    bias = b + W beta, colsum = row sums of b. Output in a's dtype."""
+    bias = b + W beta, colsum = row sums of b. Output in a's dtype. PREC fp32s: a fp32 and b an
+    int32 split_pack(...) weight (CLIPK_F32S; colsum summed over the packed value, see
+    clip.model.ln_fold_weights)."""
     _need(a, "A")
-    _need(b, "B", a.dtype)
+    split = a.dtype == torch.float32 and b.dtype == torch.int32
+    _need(b, "B", torch.int32 if split else a.dtype)
     M, K = a.shape
     Nn = b.shape[0]
     out = torch.empty(M, Nn, device=a.device, dtype=a.dtype)
@@ -102,7 +105,7 @@ def gemm_ln(a, b, epi, bias, stats=None, res=None, colsum=None, rnb=None, want_o
             _need(t, nm, torch.float32)
     if res is not None:
         _need(res, "res", a.dtype)
-    N.call("clipk_gemm_ln", DT[a.dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias), _p(res), Nn, _p(out), Nn,
+    N.call("clipk_gemm_ln", N.F32S if split else DT[a.dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias), _p(res), Nn, _p(out), Nn,
            _p(out2), _p(stats), _p(colsum), _p(rnb), _stream())
     return (out, out2) if want_out2 else out
 

@@ -134,7 +134,8 @@ int clipk_gemm_splitk(int in_dtype, int out_dtype, int epi, int M, int N, int K,
  *   LN(x) W^T + b = rstd * (x W'^T - mean * s) + c,  W' = W diag(gamma) (in_dtype),
  *   s_j = sum_k W'[j,k], c_j = b_j + sum_k beta_k W[j,k] (fp32),
  * so the GEMM reads the residual stream x itself and no normalised copy is written.
- * Two modes, 16-bit in_dtype == out dtype:
+ * Two modes, 16-bit in_dtype == out dtype, or in_dtype CLIPK_F32S (A, out, res fp32; B = W'
+ * split-packed by clipk_split_pack; s summed over the packed value, (hi + lo) / 64):
  *  - colsum == NULL: EPI_BIAS_RES (the residual-stream producer); in addition, per row m and
  *    64-column group g of the ROUNDED output, stats[(m * N/64 + g) * 2 + {0, 1}] = (sum, sum of
  *    squared deviations from the group's mean) (fp32);
@@ -376,7 +377,8 @@ int clipk_encoder_set_input_rows(clipk_encoder* e, int mode);
  * built from the layer's ln_1 / ln_2 and in_proj / c_fc weights. When set, layers >= 1 take
  * ln_1 from the previous layer's c_proj epilogue statistics and every layer takes ln_2 from its
  * out_proj epilogue (layer 0's ln_1 and ln_final stay LayerNorm passes; not used with deep
- * prompts or an fp32 encoder). The saved mean / rstd are the same quantities the LayerNorm pass
+ * prompts or an fp32 encoder; a PREC fp32s encoder (clipk_encoder_set_split first) takes W_in' /
+ * W_fc' split-packed). The saved mean / rstd are the same quantities the LayerNorm pass
  * writes, so the backward is unchanged. fold_ptrs == NULL clears. Pointers must stay valid. A ViT
  * handle (clipk_vision_create) takes the same table for its ln_1 / ln_2: its forward with a
  * 16-bit act dtype (clipk_vit_forward) runs the residual stream in that dtype through the text

@@ -6,7 +6,8 @@ as rstd * (x W'^T - mean * s) + c, W' = W diag(gamma): the producer GEMM writes 
 statistics partials of the residual stream it stores, and the consumer GEMM reads x itself.
 Bars: the statistics match torch on the stored (rounded) values to fp32 rounding; the folded
 GEMM is within the dtype's tolerance of the fp64 reference and no further from it than the
-un-fused path (LayerNorm pass -> 16-bit -> GEMM) by more than a small margin."""
+un-fused path (LayerNorm pass -> 16-bit -> GEMM) by more than a small margin. PREC fp32s (fp32
+stream, split-packed W'): the same at fp32-class bars."""
 import math
 import os
 
@@ -121,6 +122,70 @@ def test_gemm_ln_fold(dev, dtype, epi, Mr, Wd, Nn):
         assert _rel(d, sg * (1 + 1.702 * ref * (1 - sg))) <= TOL[dtype]
 
 
+@pytest.mark.parametrize("Mr,Nn,K", [(47160, 512, 2048), (8000, 512, 512), (300, 512, 2048), (1, 512, 512)])
+def test_gemm_ln_stats_split(dev, Mr, Nn, K):
+    """PREC fp32s statistics producer (fp32 out, 16 lanes per 64-column group): the stored output
+    is bitwise the plain split GEMM's, the partials merge to the fp64 statistics of it."""
+    g = torch.Generator(device="cpu").manual_seed(Mr + Nn + K + 1)
+    a = torch.randn(Mr, K, generator=g).to(dev)
+    b = ops.split_pack((torch.randn(Nn, K, generator=g) / math.sqrt(K)).to(dev))
+    bias = (0.1 * torch.randn(Nn, generator=g)).to(dev)
+    res = torch.randn(Mr, Nn, generator=g) + 3.0 * torch.randn(Mr, 1, generator=g)
+    res[:, 7] *= 40.0
+    res = res.to(dev)
+    stats = torch.full((Mr, Nn // 64, 2), float("nan"), device=dev)
+    out = ops.gemm_ln(a, b, N.EPI_BIAS_RES, bias, stats, res=res)
+    plain = ops.gemm(a, b, N.EPI_BIAS_RES, torch.float32, bias=bias, res=res)
+    assert torch.equal(out, plain), "stats epilogue changed the stored output"
+    ref = partials(out)
+    assert torch.allclose(stats[..., 0], ref[..., 0], rtol=0, atol=1e-4 * float(out.abs().max()))
+    assert ((stats[..., 1] - ref[..., 1]).abs() <= 1e-5 * ref[..., 1] + 1e-3).all()
+    mean, rstd, _ = ops.ln_stats_merge(stats, Nn)
+    x = out.double()
+    assert ((mean.double() - x.mean(1)).abs() <= 1e-6 * (x.abs().amax(1) + 1)).all()
+    assert ((rstd.double() * torch.sqrt(x.var(1, unbiased=False) + 1e-5) - 1).abs().max().item()) <= 2e-6
+
+
+@pytest.mark.parametrize("epi", [N.EPI_BIAS, N.EPI_BIAS_QGELU])
+@pytest.mark.parametrize("Mr,Wd,Nn", [(47160, 512, 1536), (8000, 512, 2048), (300, 512, 2048), (3, 512, 1536)])
+def test_gemm_ln_fold_split(dev, epi, Mr, Wd, Nn):
+    """PREC fp32s fold (fp32 x, split-packed W'): within fp32-class tolerance of the fp64
+    LayerNorm -> Linear, and no further from it than the un-fused fp32s path (fp32 LayerNorm
+    pass -> split GEMM with W) by more than fp32 rounding."""
+    g = torch.Generator(device="cpu").manual_seed(Mr * 5 + Wd + Nn + epi)
+    x = torch.randn(Mr, Wd, generator=g) + 2.0 * torch.randn(Mr, 1, generator=g)
+    x[:, 5] *= 30.0
+    x = x.to(dev)
+    gamma = (1.0 + 0.2 * torch.randn(Wd, generator=g)).to(dev)
+    beta = (0.1 * torch.randn(Wd, generator=g)).to(dev)
+    w = (torch.randn(Nn, Wd, generator=g) / math.sqrt(Wd)).to(dev)
+    bias = (0.05 * torch.randn(Nn, generator=g)).to(dev)
+    wp, s, c = M.ln_fold_weights(w.cpu(), bias.cpu(), gamma.cpu(), beta.cpu(), torch.float32, dev, split=True)
+    xd = x.double()
+    ref = F.layer_norm(xd, (Wd,), gamma.double(), beta.double(), eps=1e-5) @ w.double().t() + bias.double()
+    xn = ops.layernorm(x, gamma, beta, out_dtype=torch.float32)
+    wq = ops.split_pack(w)
+    _, _, rnb = ops.ln_stats_merge(partials(x), Wd)
+    if epi == N.EPI_BIAS:
+        out = ops.gemm_ln(x, wp, epi, c, colsum=s, rnb=rnb)
+        unf = ops.gemm(xn, wq, N.EPI_BIAS, torch.float32, bias=bias)
+        e_fold, e_unf = _rel(out, ref), _rel(unf, ref)
+    else:
+        ref_g = ref * torch.sigmoid(1.702 * ref)
+        out, d = ops.gemm_ln(x, wp, epi | N.QGELU_DERIV, c, colsum=s, rnb=rnb, want_out2=True)
+        unf = ops.gemm(xn, wq, N.EPI_BIAS_QGELU, torch.float32, bias=bias)
+        sg = torch.sigmoid(1.702 * ref)
+        e_fold = max(_rel(out, ref_g), _rel(d, sg * (1 + 1.702 * ref * (1 - sg))))
+        e_unf = _rel(unf, ref_g)
+    # the fold's rstd * (x W'^T) - rstd * mean * s cancels: its rounding scales with the row's
+    # rms / std = sqrt(1 + mean^2 / var) (up to ~5 for these rows: offsets 2 N(0, 1), std ~1.7),
+    # the un-fused path's (which rounds the normalised row) does not
+    mu, var = xd.mean(1), xd.var(1, unbiased=False)
+    amp = float(torch.sqrt(1 + mu * mu / var).max())
+    assert e_fold <= 2e-5, f"fold rel err {e_fold:.3e}"
+    assert e_fold <= 2.0 * amp * e_unf + 2e-6, f"fold {e_fold:.3e} vs un-fused {e_unf:.3e} (amp {amp:.2f})"
+
+
 def _encoder_pair(arch, prec, dev):
     sd = synth.make_state_dict(arch, seed=0)
     a = synth.ARCHS[arch]
@@ -134,7 +199,7 @@ def _encoder_pair(arch, prec, dev):
     return a, on, off, ref
 
 
-@pytest.mark.parametrize("prec", ["fp16", "bf16", "amp"])
+@pytest.mark.parametrize("prec", ["fp16", "bf16", "amp", "fp32s"])
 def test_text_encoder_fold_on_off(dev, prec):
     """Whole text encoder (12 layers, plain layout, EOT-last layer): the folded encoder's
     features and input gradient against the fp32 encoder, no worse than the un-fused one."""
@@ -160,6 +225,10 @@ def test_text_encoder_fold_on_off(dev, prec):
         r = res["ref"][i] if i == 0 else res["ref"][i][live]
         e_on = cos((res["on"][i] if i == 0 else res["on"][i][live]).flatten(), r.flatten())
         e_off = cos((res["off"][i] if i == 0 else res["off"][i][live]).flatten(), r.flatten())
-        bar = 5e-3 if prec == "bf16" else 1e-3
+        bar = {"bf16": 5e-3, "fp32s": 1e-9}.get(prec, 1e-3)
         assert e_on <= bar, f"{nm}: fold 1-cos {e_on:.3e}"
-        assert e_on <= 2.0 * e_off + 1e-5, f"{nm}: fold {e_on:.3e} vs un-fused {e_off:.3e}"
+        assert e_on <= 2.0 * e_off + (1e-11 if prec == "fp32s" else 1e-5), \
+            f"{nm}: fold {e_on:.3e} vs un-fused {e_off:.3e}"
+        if prec == "fp32s":  # fp32-class: the features themselves, not only their direction
+            ro = (res["on"][i] if i == 0 else res["on"][i][live])
+            assert _rel(ro, r) <= 1e-4, f"{nm}: fold rel err {_rel(ro, r):.3e}"
