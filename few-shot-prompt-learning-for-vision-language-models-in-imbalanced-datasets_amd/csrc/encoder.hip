@@ -855,6 +855,10 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
            nullptr, nullptr, 0, st, pg));
   // the ViT's residual stream is fp32: its gradient stays fp32 too
   const bool r16 = io.rd != CLIPK_F32 && text_dres16(e);
+  // fp32 gradients with the fp32 stream (PREC fp32 / fp32s): the input-grad GEMMs read dX itself
+  // (a second fp32 copy in dX_lp would be 4 B/element more per LayerNorm backward, unread)
+  const bool lp_alias = !r16 && gd == CLIPK_F32;
+  void* const dA = lp_alias ? (void*)dX : b.dX_lp;  // the A operand of proj_dx / out_dx
   const bool eotl = text_eot_last(sh);
   auto zero = [&](void* p, size_t bytes) {
     return hipMemsetAsync(p, 0, bytes, st) == hipSuccess ? CLIPK_OK : (int)hipGetLastError();
@@ -862,12 +866,13 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
   if (!eotl) {
     // ln_final's gradient lands on the EOT rows of zeroed full-row streams
     if (!r16) TRY(zero(dX, (size_t)rows * W * 4));
-    TRY(zero(b.dX_lp, (size_t)rows * W * esize(gd)));
+    if (!lp_alias) TRY(zero(b.dX_lp, (size_t)rows * W * esize(gd)));
   }
   const int rd = io.rd;
   const int* frows = eotl ? nullptr : eot_rows;  // EOT-last: the last layer's rows are compact
   TRY(clipk_layernorm_bwd_x2(rd, CLIPK_F32, nout, W, b.dlnf, W, t.Xf, W, frows, io.lnf_w, t.meanf,
-                             t.rstdf, nullptr, CLIPK_F32, W, r16 ? nullptr : dX, b.dX_lp, gd, frows, W, st));
+                             t.rstdf, nullptr, CLIPK_F32, W, r16 ? nullptr : dX, lp_alias ? nullptr : b.dX_lp, gd,
+                             frows, W, st));
   // residual-gradient update of one LayerNorm backward over n rows: dres (fp32 dX or the
   // 16-bit dX_lp, in place) + LN'(dxn); last: the encoder input's gradient, always fp32 into dX
   // algorithmic LN-backward bytes per row: dy (grad), x (residual dtype), residual gradient
@@ -877,7 +882,7 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
     ProfScope ps(CLIPK_PROF_NONE, st, 0.0, SITE("ln_bwd"), lnbb);
     if (!r16)
       return clipk_layernorm_bwd_x(rd, gd, n, W, b.dxn, W, x, W, nullptr, gamma, mean, rstd, dX, W, dX,
-                                   last ? nullptr : b.dX_lp, gd, nullptr, W, st);
+                                   last || lp_alias ? nullptr : b.dX_lp, gd, nullptr, W, st);
     return clipk_layernorm_bwd_x2(rd, gd, n, W, b.dxn, W, x, W, nullptr, gamma, mean, rstd, b.dX_lp, gd, W,
                                   last ? dX : nullptr, b.dX_lp, gd, nullptr, W, st);
   };
@@ -894,12 +899,12 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
     // MLP: dg = dX . Wproj ; dh = dg * qgelu'(h), qgelu'(h) saved by the forward's c_fc epilogue
     // in the act dtype (16-bit: rms 1.8e-4 on the derivative vs 2.9e-5 when recomputing it from a
     // 16-bit h -- under the 16-bit rounding of dh itself -- for no exp / rcp in this epilogue)
-    TRY(gemm(gd, gd, dgelu_epi, n, 4 * W, W, b.dX_lp, w[15], nullptr, nullptr, b.dh, nullptr, t.h[l], act, st, io.text ? CLIPK_PROF_GEMM_DGELU : CLIPK_PROF_NONE, nullptr, 0, SITE("proj_dx_dgelu")));
+    TRY(gemm(gd, gd, dgelu_epi, n, 4 * W, W, dA, w[15], nullptr, nullptr, b.dh, nullptr, t.h[l], act, st, io.text ? CLIPK_PROF_GEMM_DGELU : CLIPK_PROF_NONE, nullptr, 0, SITE("proj_dx_dgelu")));
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, n, W, 4 * W, b.dh, w[14], nullptr, nullptr, b.dxn, nullptr,
              nullptr, 0, st, pg, nullptr, 0, SITE("fc_dx")));
     TRY(ln_bwd(n, t.Xm[l], (const float*)w[6], t.mean2[l], t.rstd2[l], false));
     // attention: do = dXm . Wout ; dqkv ; dxn1 = dqkv . Win
-    TRY(gemm(gd, gd, CLIPK_EPI_NONE, n, W, W, b.dX_lp, w[13], nullptr, nullptr, compact ? b.dh : b.do_,
+    TRY(gemm(gd, gd, CLIPK_EPI_NONE, n, W, W, dA, w[13], nullptr, nullptr, compact ? b.dh : b.do_,
              nullptr, nullptr, 0, st, pg, nullptr, 0, SITE("out_dx")));
     if (compact) {
       // back to the full row layout: do and the residual gradient (the one LN1's backward
@@ -952,7 +957,7 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
         TRY(clipk_rows_collect(gd, d.n_ctx, d.n_per, W, b.dX_lp, W, nullptr, 0, 0, d.rows,
                                d.grads + (size_t)(l - 1) * d.n_ctx * W, 0, 1, st));
       else
-        TRY(clipk_rows_collect(CLIPK_F32, d.n_ctx, d.n_per, W, dX, W, b.dX_lp, gd, W, d.rows,
+        TRY(clipk_rows_collect(CLIPK_F32, d.n_ctx, d.n_per, W, dX, W, lp_alias ? nullptr : b.dX_lp, gd, W, d.rows,
                                d.grads + (size_t)(l - 1) * d.n_ctx * W, 0, 1, st));
     }
   }
