@@ -1,6 +1,6 @@
 """CPU: host-side logic (no GPU compute): the C-ABI library loads and exports every
 symbol include/clipk.h declares, prompt slot tables reproduce the reference prompt
-layouts, tokenizer, config, registry, losses' alpha, metrics."""
+layouts, tokenizer, config, registry, losses' alpha, metrics, the fp32s LN-fold table contract."""
 import json
 import os
 import re
@@ -461,3 +461,34 @@ def test_resume_keeps_the_modules_own_keys(tmp_path):
                       str(tmp_path / "ck2" / "prompt_learner"))
     with pytest.raises(RuntimeError, match="Missing key"):
         t.resume_model_if_exist(str(tmp_path / "ck2"))
+
+
+def test_ln_fold_weights_split_contract(monkeypatch):
+    """PREC fp32s LayerNorm fold tables (clip/model.py ln_fold_weights(split=True)): W' goes to
+    clipk_split_pack as fp32 W diag(gamma), and s sums the value the split GEMM multiplies by,
+    (hi + lo) / SPLIT_SCALE with hi = fp16(64 W'), lo = fp16(64 W' - hi) (clipk_split_pack), so the
+    fold's mean term cancels against the operand actually used; c = b + W beta as the 16-bit form."""
+    from fsp_amd import ops, _native as N
+    from fsp_amd.clip import model as M
+    seen = {}
+    monkeypatch.setattr(ops, "split_pack", lambda w: seen.setdefault("w", w.clone()))
+    g = torch.Generator().manual_seed(3)
+    w = torch.randn(24, 64, generator=g) / 8
+    w[0, :5] = torch.tensor([1e-9, -3e-7, 2.5e-5, 0.7, -1.3])  # tiny, subnormal-lo and large parts
+    gamma = 1 + 0.2 * torch.randn(64, generator=g)
+    beta = 0.1 * torch.randn(64, generator=g)
+    b = 0.05 * torch.randn(24, generator=g)
+    wp, s, c = M.ln_fold_weights(w, b, gamma, beta, torch.float32, "cpu", split=True)
+    ref_wp = (w.double() * gamma.double()[None, :]).float()
+    assert torch.equal(seen["w"], ref_wp) and wp is not None
+    x = ref_wp * N.SPLIT_SCALE
+    hi = x.half().float()
+    lo = (x - hi).half().float()
+    assert torch.equal(s, ((hi.double() + lo.double()) / N.SPLIT_SCALE).sum(1).float())
+    assert torch.equal(c, (b.double() + w.double() @ beta.double()).float())
+    # the packed value is W' to ~2^-22 relative: s is the fp32 row sum up to that
+    assert torch.allclose(s.double(), ref_wp.double().sum(1), rtol=0, atol=1e-6 * float(ref_wp.abs().sum(1).max()))
+    # out of the fp16 range at the split scale: no fold table (the encoder runs the LN passes)
+    big = torch.full((2, 64), 2000.0)
+    assert M.ln_fold_weights(big, torch.zeros(2), torch.ones(64), torch.zeros(64), torch.float32, "cpu",
+                             split=True) is None
