@@ -106,10 +106,12 @@ PMC_FILE = next((f for f in (os.path.join(ROOT, "profiles", r, "traffic.json") f
 # kernel classes of the step: launch sites that run the same kernel instantiation (rocprofv3
 # kernel-name key, for the PMC traffic lookup) -- the text GEMMs by role, attention, LN. Each
 # class's bound is decided from its own algorithmic FLOPs and bytes per launch (kernel_table).
+DX_SITES = ["text.fc_dx", "text.qkv_dx", "text.out_dx", "text.fc_dx_eot", "text.out_dx_eot"]
 KERNELS = {
-    "gemm_dx_n512": (["text.fc_dx", "text.qkv_dx", "text.out_dx"], "EPI_NONE 192x256"),
+    "gemm_dx_n512": (DX_SITES, "EPI_NONE 192x256"),
     "gemm_proj_fwd": (["text.proj_fwd"], "EPI_BIAS_RES N=512 K=2048"),
-    "gemm_dgelu": (["text.proj_dx_dgelu"], "EPI_DQGELU | QGELU_DERIV (acc x the saved quickgelu')"),
+    "gemm_dgelu": (["text.proj_dx_dgelu", "text.proj_dx_dgelu_eot"],
+                   "EPI_DQGELU | QGELU_DERIV (acc x the saved quickgelu')"),
     "gemm_fc_fwd": (["text.fc_fwd"], "EPI_BIAS_QGELU | QGELU_DERIV N=2048 (QuickGELU(h) and quickgelu'(h); ln_2 folded)"),
     "gemm_qkv_fwd": (["text.qkv_fwd"], "EPI_BIAS N=1536 (ln_1 folded)"),
     "gemm_out_fwd": (["text.out_fwd"], "EPI_BIAS_RES N=512"),
@@ -121,6 +123,10 @@ KERNELS = {
     "vit": (["vit.patch_embed", "vit.qkv_fwd", "vit.attn_fwd", "vit.out_fwd", "vit.fc_fwd", "vit.proj_fwd",
              "vit.ln_fwd", "vit.ln_stats", "vit.eot_gather", "vit.head"], "ViT forward (all sites)"),
 }
+# the dominant class split by GEMM shape (M rows x N 512 x K): the 11 full-row launches of each
+# input-grad GEMM, and the last layer's compact EOT-row launches (M = B*C)
+DX_SHAPES = {"fc_dx K=2048": ["text.fc_dx"], "qkv_dx K=1536": ["text.qkv_dx"], "out_dx K=512": ["text.out_dx"],
+             "eot fc_dx+out_dx": ["text.fc_dx_eot", "text.out_dx_eot"]}
 ROOF_PMC_KEY = {"gemm_dx_n512": "gemm_nt_kernelIDF16_DF16_fLi4ELi192ELi256",
                 "gemm_dgelu": "gemm_nt_kernelIDF16_DF16_DF16_Li6E",
                 "gemm_proj_fwd": "gemm_nt_kernelIDF16_DF16_DF16_Li1ELi192ELi256ELi2ELi4ELb1ELi128ELi2ELb0ELb1E",
@@ -186,9 +192,8 @@ def cpu_baseline(arch_name, n_ctx_init, n_cls_full, sample_cls, threads):
               else "the full class set, unscaled")
     return {"value": round(1.0 / per_img, 6), "unit": "images/sec", "cores": threads, "kind": "port",
             "nproc": os.cpu_count(),
-            "sample": f"oracle/clip_oracle.py fp32 CPU, CoCoOp {arch_name} 1 image x {sample_cls} classes "
-                      f"fwd+bwd at 77 tokens ({t_all:.2f}s) on {threads} threads (host nproc {os.cpu_count()}), "
-                      f"{scaled}"}
+            "sample": f"oracle fp32 CPU, CoCoOp {arch_name} 1 image x {sample_cls} classes fwd+bwd at 77 tokens "
+                      f"({t_all:.1f}s) on {threads} threads (nproc {os.cpu_count()}), {scaled}"}
 
 
 def kernel_table(sites, steps, prec):
@@ -215,6 +220,28 @@ def kernel_table(sites, steps, prec):
                      "flop_per_byte": round(fl / by, 1) if by else None,
                      "flops_per_launch": fl / n, "bytes_per_launch": by / n}
     return out
+
+
+def dx_by_shape(sites, steps, prec):
+    """The N = 512 input-grad class per GEMM shape: launches per step, avg us per launch, TF/s and
+    the fraction of the MFMA peak (names the worst shape of the roofline kernel)."""
+    out = {}
+    for name, members in DX_SHAPES.items():
+        ms = sum(sites[x][0] for x in members if x in sites)
+        n = sum(sites[x][1] for x in members if x in sites)
+        fl = sum(sites[x][2] for x in members if x in sites)
+        if n:
+            tf = fl / (ms * 1e-3) / 1e12
+            out[name] = {"launches": round(n / steps, 1), "avg_us": round(1000 * ms / n, 1), "tflops": round(tf, 1),
+                         "mfma_frac": round(tf / PEAK[prec], 4)}
+    return out
+
+
+def executed_gemm_tflops(sites, steps, step_s):
+    """GEMM FLOPs the step actually launches (every text + ViT GEMM site: shared-prefix packed
+    rows, EOT-only last layer) per second of step time."""
+    fl = sum(v[2] for v in sites.values()) / steps
+    return round(fl / step_s / 1e12, 2)
 
 
 def roofline_of(table, prec):
@@ -371,14 +398,17 @@ def precision_line(args, prec, dev, rank, world, steps=10, warmup=2, n_eval=5000
     t, sites = time_train(tr, dm, steps, warmup, prof_steps=2)
     table = kernel_table(sites, 2, prec) if sites else None
     e, n = time_eval(tr, dm, n_eval)
+    roof = roofline_of(table, prec) if table else None
+    if roof:  # the bench line carries the headline's full roofline record; here the essentials
+        roof = {k: roof[k] for k in ("bound", "achieved", "peak", "unit", "frac", "kernel_class", "avg_launch_ms")}
     line = {"images_per_sec": round(world * args.batch * steps / t, 3), "ms_per_step": round(1000 * t / steps, 3),
             "steps": steps, "eval_images_per_sec": round(e, 3), "eval_images": int(dist.sum_over_ranks(n)),
-            "roofline": roofline_of(table, prec) if table else None,
-            "kernels": ({k: {kk: v[kk] for kk in ("launches_per_step", "ms_per_step", "bound", "roof_frac", "tflops",
-                                                  "gbs")} for k, v in table.items()} if table else None)}
+            "roofline": roof,
+            # the classes over 0.5 ms/step: [ms/step, bound, fraction of that roof]
+            "kernels": ({k: [v["ms_per_step"], v["bound"], v["roof_frac"]] for k, v in table.items()
+                         if v["ms_per_step"] >= 0.5} if table else None)}
     if prec == "fp32s":
-        line["peak_note"] = ("fp32s roofline peak = dense fp16 MFMA peak / 3 (three fp16 MFMAs per fp32-class "
-                             "product); achieved counts the algorithmic fp32 FLOPs")
+        line["peak_note"] = "peak = fp16 MFMA peak / 3 (3 fp16 MFMAs per fp32-class product)"
     del tr, dm
     torch.cuda.empty_cache()
     return line
@@ -437,6 +467,7 @@ def main():
 
     import torch
     from fsp_amd import dist
+    from fsp_amd import _native as N
     from fsp_amd.clip import synth
 
     local = dist.init_from_env()
@@ -460,6 +491,8 @@ def main():
 
     f_img, f_txt, b_txt = flops(arch, args.classes, L)
     step_flops = args.batch * (f_img + args.classes * (f_txt + b_txt))
+    _, f77, b77 = flops(arch, args.classes, 77)
+    step_flops_77 = args.batch * (f_img + args.classes * (f77 + b77))
     value = world * args.batch * args.steps / t
     out = {
         "metric": metric_name(args.arch), "value": round(value, 3), "unit": "images/sec", "n_gpus": world,
@@ -474,19 +507,23 @@ def main():
                    "text_layout": ("shared-prefix packed, %d text rows/image (plain: %d)"
                                    % (lay.rows_per_group, args.classes * L)) if lay.pack is not None
                                   else f"plain [B*C, {L}]",
-                   "vision": ("each step starts the NEXT batch's (frozen) image encoder on a side stream at its "
-                              "top (NATIVE.PREFETCH_VISION, as TrainerX.run_epoch does with its one-batch "
-                              "lookahead): one ViT forward and one text fwd+bwd per timed step"
+                   "vision": ("the NEXT batch's frozen ViT forward on a side stream (NATIVE.PREFETCH_VISION, "
+                              "TrainerX.run_epoch's lookahead): one ViT fwd + one text fwd+bwd per step"
                               if trainer.cfg.NATIVE.get("PREFETCH_VISION", False) else "in line")},
         "eval_images_per_sec": round(eval_ips, 3),
         "eval_images": int(dist.sum_over_ranks(n_eval)),
         "eval_note": "forward only, test batch 100, distinct resident images sharded over the ranks",
-        # reference-equivalent FLOPs (plain [B*C, L_eff] layout) per second, not executed FLOPs
+        "source_digest": N.library_digest()[:16],
+        # SURVEY §8(d) algorithmic FLOPs per second: the plain [B*C, L_eff] layout (L_eff = max EOT
+        # + 1), the same at the reference's 77 tokens, and the GEMM FLOPs the step executes
+        # (shared-prefix packed rows, EOT-only last layer; attention not counted)
         "model_tflops_per_gpu": round(step_flops * args.steps / t / 1e12, 2),
+        "model_tflops_per_gpu_l77": round(step_flops_77 * args.steps / t / 1e12, 2),
+        "executed_gemm_tflops_per_gpu": executed_gemm_tflops(sites, n_prof, t / args.steps) if sites else None,
         "roofline": roof,
-        "kernels": ({k: {kk: v[kk] for kk in ("kernel", "launches_per_step", "ms_per_step", "avg_launch_ms",
-                                               "tflops", "mfma_frac", "gbs", "hbm_frac", "bound", "roof_frac",
-                                               "flop_per_byte")}
+        "dx_by_shape": dx_by_shape(sites, n_prof, args.prec) if sites else None,
+        # per kernel class: [launches/step, ms/step, bound, fraction of that roof, TF/s, GB/s]
+        "kernels": ({k: [v["launches_per_step"], v["ms_per_step"], v["bound"], v["roof_frac"], v["tflops"], v["gbs"]]
                      for k, v in table.items()} if table else None),
     }
     del trainer, dm
@@ -517,6 +554,18 @@ def main():
                          "images_per_gpu_per_step": 1}
         del tr1, dm1
         torch.cuda.empty_cache()
+        # single-GPU proxy of batch-1 class sharding at N = 2 / 4 / 8: one rank's work
+        # -- B = 1 at C / N classes -- timed alone, a lower bound on the N-GPU step (the logit
+        # all-gather and the gradient all-reduce come on top)
+        proxy = {}
+        for n in (2, 4, 8):
+            cls = args.classes // n
+            trp, dmp = build_trainer(argparse.Namespace(**{**vars(args), "classes": cls}), args.prec, 1, dev, rank)
+            tp, _ = time_train(trp, dmp, B1_STEPS, 5)
+            proxy[f"n{n}"] = {"classes": cls, "ms_per_step": round(1000 * tp / B1_STEPS, 3)}
+            del trp, dmp
+            torch.cuda.empty_cache()
+        out["batch1_class_shard_proxy"] = proxy
         # BASELINE config 2: CoOp n_ctx 16, ViT-B/16 fp16, 1000 classes, batch 32
         trc, dmc = build_coop_trainer(args, args.prec, 32, dev, rank, n_test_device=args.eval_images)
         tc, _ = time_train(trc, dmc, 10, 3)
@@ -535,11 +584,15 @@ def main():
             out[p] = precision_line(args, p, dev, rank, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            threads = min(16, os.cpu_count() or 1)
-            # the whole workload unit (1 image x all classes, fwd + bwd): ~25 s on 16 threads, no
-            # extrapolation (the 50-class sample scaled linearly overstated the rate ~3x: the
-            # text activations of 1,000 x 77 tokens do not stay in cache)
-            cb = cpu_baseline(args.arch, "a photo of a", args.classes, args.cpu_classes or args.classes, threads)
+            # the whole workload unit (1 image x all classes, fwd + bwd), no extrapolation (a
+            # 50-class sample scaled linearly overstated the rate ~3x: the text activations of
+            # 1,000 x 77 tokens do not stay in cache). SURVEY §8(d): the full host (every CPU this
+            # process may run on) and an 8-thread run (the build container's reference timing)
+            host = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+            cb = cpu_baseline(args.arch, "a photo of a", args.classes, args.cpu_classes or args.classes, host)
+            cb["affinity_cpus"] = host
+            c8 = cpu_baseline(args.arch, "a photo of a", args.classes, args.cpu_classes or args.classes, 8)
+            cb["eight_threads"] = {"value": c8["value"], "cores": 8}
             cb["reference"] = reference_cpu(args.arch, args.classes)
             out["cpu_baseline"] = cb
         except Exception as e:  # report, never fake

@@ -7,10 +7,32 @@ GPU, every op raises. Build with ``python __graft_entry__.py`` (``build()``) or
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
+import sys
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CLIPK_LIB") or os.path.join(_PKG, "libclipk.so")  # override: A/B builds
+_ROOT = os.path.dirname(_PKG)
+
+
+def source_files():
+    """The sources libclipk.so is built from, as (path relative to the repo root, absolute path):
+    csrc/{*.hip, *.h, Makefile} and include/clipk.h, in name order."""
+    csrc = os.path.join(_PKG, "csrc")
+    names = sorted(n for n in os.listdir(csrc) if n.endswith((".hip", ".h")) or n == "Makefile")
+    rel = [("csrc/" + n, os.path.join(csrc, n)) for n in names]
+    return rel + [("include/clipk.h", os.path.join(_ROOT, "include", "clipk.h"))]
+
+
+def source_digest():
+    """sha256 (hex) of "<sha256 of content>  <relative path>\n" over source_files(): the value
+    the Makefile compiles into the library (clipk_source_digest, include/clipk.h)."""
+    h = hashlib.sha256()
+    for rel, path in source_files():
+        with open(path, "rb") as f:
+            h.update(f"{hashlib.sha256(f.read()).hexdigest()}  {rel}\n".encode())
+    return h.hexdigest()
 
 F32, F16, BF16, F32S = 0, 1, 2, 3  # F32S: fp32 activations x split-packed weights (PREC fp32s)
 SPLIT_SCALE = 64.0  # CLIPK_SPLIT_SCALE: clipk_split_pack stores SPLIT_SCALE * W
@@ -29,20 +51,17 @@ _D = ctypes.c_double
 # name -> (restype, argtypes); must match include/clipk.h exactly
 SIGNATURES = {
     "clipk_version": (ctypes.c_char_p, []),
+    "clipk_source_digest": (ctypes.c_char_p, []),
     "clipk_strerror": (ctypes.c_char_p, [_I]),
     "clipk_device_arch_ok": (_I, []),
     "clipk_gemm": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P, _I, _I, _P]),
-    "clipk_gemm_ws_bytes": (_S, []),
-    "clipk_gemm_ws": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P, _I, _I, _P, _S, _P]),
     "clipk_gemm_auto_splits": (_I, [_I, _I, _I, _I]),
     "clipk_gemm_splitk_ws_bytes": (_S, [_I, _I, _I]),
     "clipk_gemm_splitk": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P, _S, _P]),
     "clipk_gemm_set_config": (_I, [_I]),
-    "clipk_gemm_set_tail": (_I, [_I]),
     "clipk_split_pack": (_I, [_I, _I, _P, _I, _P, _P]),
     "clipk_gemm_ln": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P]),
     "clipk_ln_stats_merge": (_I, [_I, _I, _P, _P, _P, _P, _P]),
-    "clipk_gemm_ln_ws": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _S, _P]),
     "clipk_image_resample": (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P]),
     "clipk_gemm_stamps": (_I, [_P, _S]),
     "clipk_layernorm_fwd": (_I, [_I, _I, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P]),
@@ -78,6 +97,8 @@ SIGNATURES = {
     "clipk_encoder_set_input_rows": (_I, [_P, _I]),
     "clipk_encoder_set_ln_fold": (_I, [_P, _P]),
     "clipk_encoder_set_split": (_I, [_P, _I]),
+    "clipk_encoder_set_split_target": (_I, [_P, _I]),
+    "clipk_encoder_set_status": (_I, [_P, _P]),
     "clipk_vit_prompted_saved_bytes": (_S, [_P, _I, _I]),
     "clipk_vit_prompted_ws_bytes": (_S, [_P, _I, _I]),
     "clipk_vit_forward_prompted": (_I, [_P, _I, _P, _I, _P, _P, _P, _S, _P, _S, _P]),
@@ -143,8 +164,18 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    built = lib.clipk_source_digest().decode()
+    tree = source_digest()
+    if built != tree:
+        raise ClipkError(f"{LIB_PATH} was built from other sources than this tree (library digest {built[:16]}, "
+                         f"tree {tree[:16]}): rebuild it (`python __graft_entry__.py` or `make -C csrc`)")
     _lib = lib
     return lib
+
+
+def library_digest():
+    """clipk_source_digest() of the loaded library (== source_digest(): load() checks it)."""
+    return load().clipk_source_digest().decode()
 
 
 def strerror(rc: int) -> str:
@@ -160,3 +191,8 @@ def call(name: str, *args):
     rc = getattr(load(), name)(*args)
     check(rc, name)
     return rc
+
+
+if __name__ == "__main__" and sys.argv[1:] == ["--digest-header"]:
+    # csrc/Makefile: the digest compiled into the library
+    print(f'#define CLIPK_SOURCE_DIGEST "{source_digest()}"')

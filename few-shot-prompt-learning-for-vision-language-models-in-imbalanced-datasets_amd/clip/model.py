@@ -212,8 +212,14 @@ class TextEncoderCore(_Encoder):
                                               _ptrs(table), _ptrs(head), ctypes.byref(h)),
                 "clipk_encoder_create(text)")
         self.handle = h
+        self._status = None
         if split:
             N.check(N.load().clipk_encoder_set_split(h, 1), "clipk_encoder_set_split(text)")
+            # overflow flags of the split calls (clipk_encoder_set_status): 1 = a forward's
+            # features, 2 = a backward's gradients came out non-finite
+            self._status = torch.zeros(1, dtype=torch.int32, device=self.device)
+            N.check(N.load().clipk_encoder_set_status(h, ops._p(self._status)), "clipk_encoder_set_status")
+            N.check(N.load().clipk_encoder_set_split_target(h, self.SPLIT_TARGET), "clipk_encoder_set_split_target")
         if fold:
             self._keep += fold
             N.check(N.load().clipk_encoder_set_ln_fold(h, _ptrs(fold)), "clipk_encoder_set_ln_fold")
@@ -258,7 +264,23 @@ class TextEncoderCore(_Encoder):
                     "clipk_text_forward_packed")
         else:
             N.check(lib.clipk_text_forward(h, shape.nseq, shape.L, *tail), "clipk_text_forward")
+        if self._status is not None and not save:
+            self._check_status(forward_only=True)  # inference: no backward will look
         return txt, saved
+
+    # PREC fp32s: an overflowed backward is re-run once with this much lower scale target (10 more
+    # bits of headroom below fp16's 65504 for gradient growth through the layers)
+    SPLIT_TARGET, SPLIT_RETRY_TARGET = 7, -3
+
+    def _check_status(self, forward_only=False):
+        """Read and clear the split overflow flags (one host synchronisation); a non-finite
+        forward raises. Returns the backward flag."""
+        st = int(self._status.item())
+        self._status.zero_()
+        if st & 1:
+            raise N.ClipkError("PREC fp32s text encoder: non-finite features -- an activation exceeded fp16's "
+                               "range (65504) in the split-fp16 GEMM operands; use PREC fp32")
+        return bool(st & 2) and not forward_only
 
     def backward(self, dtxt, shape, saved):
         lib = N.load()
@@ -272,13 +294,31 @@ class TextEncoderCore(_Encoder):
         tail = (ops._p(shape.eot_rows), ops._p(dtxt.contiguous()), ops._p(saved), saved.numel(), ops._p(dx0),
                 ops._p(ws), ws.numel(), ops._stream())
         self._input_rows(lib, shape)
-        if shape.packed:
-            N.check(lib.clipk_text_backward_packed(h, shape.G, shape.C, shape.P, shape.R, shape.ntiles,
-                                                   ops._p(shape.tiles), ops._p(shape.row_first), *tail),
-                    "clipk_text_backward_packed")
-        else:
-            N.check(lib.clipk_text_backward(h, shape.nseq, shape.L, *tail), "clipk_text_backward")
+
+        def run():
+            if shape.packed:
+                N.check(lib.clipk_text_backward_packed(h, shape.G, shape.C, shape.P, shape.R, shape.ntiles,
+                                                       ops._p(shape.tiles), ops._p(shape.row_first), *tail),
+                        "clipk_text_backward_packed")
+            else:
+                N.check(lib.clipk_text_backward(h, shape.nseq, shape.L, *tail), "clipk_text_backward")
+
+        run()
+        if self._status is not None and self._check_status():
+            # the gradients overflowed the split operands' fp16 range: once more at a lower scale
+            # target (exact: the backward is linear in dtxt and the scale a power of two)
+            type(self).split_retries += 1
+            N.check(lib.clipk_encoder_set_split_target(h, self.SPLIT_RETRY_TARGET), "clipk_encoder_set_split_target")
+            try:
+                run()
+            finally:
+                lib.clipk_encoder_set_split_target(h, self.SPLIT_TARGET)
+            if self._check_status():
+                raise N.ClipkError("PREC fp32s text encoder backward: non-finite gradients even at the lowered "
+                                   "scale target (gradient growth beyond fp16's range); use PREC fp32")
         return dx0
+
+    split_retries = 0  # PREC fp32s backwards re-run at the lower scale target (overflow), all instances
 
 
 class TextEncodeFn(torch.autograd.Function):

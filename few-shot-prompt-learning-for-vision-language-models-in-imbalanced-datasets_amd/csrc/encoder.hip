@@ -42,6 +42,8 @@ struct clipk_encoder {
   // clipk_encoder_set_split: PREC fp32s -- fp32 activations, every GEMM weight split-packed
   // (clipk_split_pack) and every GEMM on the split-fp16 MFMA path (CLIPK_F32S)
   int split = 0;
+  int split_target = 7;     // the backward's gradient scale puts max |s dtxt| in [2^(t-1), 2^t)
+  int* status = nullptr;    // clipk_encoder_set_status: overflow flags of split calls (device)
 };
 
 namespace clipk {
@@ -56,23 +58,6 @@ struct SplitScope {
   int prev;
   explicit SplitScope(const clipk_encoder* e) : prev(t_split) { t_split = e->split; }
   ~SplitScope() { t_split = prev; }
-};
-// The GEMMs of an encoder call get the call's split-tail workspace (clipk_gemm_ws: the N = 512
-// text GEMMs' tiles past the first round run as K halves on paired blocks); its pair flags are
-// zeroed once per call.
-static thread_local void* t_gemm_ws = nullptr;
-bool gemm_tail_enabled();  // gemm.hip
-struct GemmWsScope {
-  void* prev;
-  int rc = CLIPK_OK;
-  GemmWsScope(void* ws, hipStream_t st) : prev(t_gemm_ws) {
-    t_gemm_ws = ws;
-    if (ws && gemm_tail_enabled()) {  // no split tail (the default): no flags to clear, no launch
-      const size_t fb = 128 * sizeof(unsigned);  // the flags at the end of clipk_gemm_ws_bytes()
-      if (hipMemsetAsync((char*)ws + clipk_gemm_ws_bytes() - fb, 0, fb, st) != hipSuccess) rc = (int)hipGetLastError();
-    }
-  }
-  ~GemmWsScope() { t_gemm_ws = prev; }
 };
 static inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -176,8 +161,7 @@ static int gemm(int in, int out, int epi, int M, int N, int K, const void* A, co
                site ? gemm_bytes(in, out, epi, M, N, K, o2 != nullptr, auxdt) : 0.0);
   if (sk && (epi & ~CLIPK_QGELU_DERIV) != CLIPK_EPI_DQGELU)
     return clipk_gemm_splitk(in, out, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, 0, sk, skb, st);
-  return clipk_gemm_ws(in, out, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, aux, auxdt, N, t_gemm_ws,
-                       t_gemm_ws ? clipk_gemm_ws_bytes() : 0, st);
+  return clipk_gemm(in, out, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, aux, auxdt, N, st);
 }
 
 // split-K workspace for the block GEMMs of a vision forward at `rows` rows (0 when none splits)
@@ -206,7 +190,6 @@ struct TextBufs {
   // LN fold: per (row, 64-column group) statistics partials of the residual stream; mean /
   // rstd of the un-saved (inference) forward
   float *lnst = nullptr, *tm = nullptr, *tr = nullptr, *rnb = nullptr;
-  void* gemm_ws = nullptr;  // clipk_gemm_ws split-tail workspace
   size_t saved_bytes = 0, ws_bytes = 0;
 };
 
@@ -257,7 +240,6 @@ static TextBufs text_layout(const clipk_encoder* e, size_t rows, int nout, void*
   t.tm = (float*)wk.take(rows * 4);
   t.tr = (float*)wk.take(rows * 4);
   t.rnb = (float*)wk.take(rows * 8);
-  t.gemm_ws = wk.take(clipk_gemm_ws_bytes());
   t.saved_bytes = save ? sv.off : 0;
   t.ws_bytes = wk.off;
   return t;
@@ -269,7 +251,6 @@ struct TextBwdBufs {
   void *dtg, *dX_lp, *dh, *do_, *dqkv, *dxn;  // dxn: LN-output grads in the grad dtype
   float* dlnf;
   float* gscale;  // PREC fp32s: the backward's gradient scale s and 1 / s (+ amax partials)
-  void* gemm_ws;  // clipk_gemm_ws split-tail workspace
   void* part;  // shared-prefix attention: per-chunk prefix dK/dV partials
   size_t bytes;
 };
@@ -288,7 +269,6 @@ static TextBwdBufs text_bwd_layout(const clipk_encoder* e, size_t rows, int nout
   b.dqkv = c.take(rows * 3 * W * g);
   b.part = part_bytes ? c.take(part_bytes) : nullptr;
   b.gscale = (float*)c.take((2 + kAmaxBlocks) * sizeof(float));
-  b.gemm_ws = c.take(clipk_gemm_ws_bytes());
   b.bytes = c.off;
   return b;
 }
@@ -308,15 +288,15 @@ __global__ __launch_bounds__(256) void amax_partial_kernel(long n, const float* 
   __syncthreads();
   if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
 }
-// sc[0] = s, sc[1] = 1 / s from the partial maxima sc[2 ..]
-__global__ __launch_bounds__(64) void grad_scale_pick_kernel(int nparts, float* __restrict__ sc) {
+// sc[0] = s, sc[1] = 1 / s from the partial maxima sc[2 ..]: m s in [2^(target-1), 2^target)
+__global__ __launch_bounds__(64) void grad_scale_pick_kernel(int nparts, int target, float* __restrict__ sc) {
   float m = 0.f;
   for (int i = threadIdx.x; i < nparts; i += 64) m = fmaxf(m, sc[2 + i]);
   m = wave_max(m);
   if (threadIdx.x == 0) {
     int ex = 0;
     if (m > 0.f && m < INFINITY) (void)frexpf(m, &ex);  // m = f 2^ex, f in [0.5, 1)
-    const int k = min(max(7 - ex, -120), 120);           // m * 2^k in [64, 128)
+    const int k = min(max(target - ex, -120), 120);      // m * 2^k in [2^(target-1), 2^target)
     sc[0] = ldexpf(1.0f, k);
     sc[1] = ldexpf(1.0f, -k);
   }
@@ -326,9 +306,9 @@ __global__ __launch_bounds__(256) void scale_by_kernel(long n, const float* __re
   const float s = sc[which];
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) y[i] = x[i] * s;
 }
-static int grad_scale_in(const clipk_encoder*, long n, const float* x, float* y, float* sc, hipStream_t st) {
+static int grad_scale_in(const clipk_encoder* e, long n, const float* x, float* y, float* sc, hipStream_t st) {
   hipLaunchKernelGGL(amax_partial_kernel, dim3(kAmaxBlocks), dim3(256), 0, st, n, x, sc + 2);
-  hipLaunchKernelGGL(grad_scale_pick_kernel, dim3(1), dim3(64), 0, st, kAmaxBlocks, sc);
+  hipLaunchKernelGGL(grad_scale_pick_kernel, dim3(1), dim3(64), 0, st, kAmaxBlocks, e->split_target, sc);
   hipLaunchKernelGGL(scale_by_kernel, dim3((unsigned)std::min<long>((n + 255) / 256, 4096)), dim3(256), 0, st, n, x, y,
                      (const float*)sc, 0);
   CLIPK_CHECK_LAUNCH();
@@ -337,6 +317,28 @@ static int grad_scale_in(const clipk_encoder*, long n, const float* x, float* y,
 static int grad_scale_out(long n, float* x, const float* sc, hipStream_t st) {
   hipLaunchKernelGGL(scale_by_kernel, dim3((unsigned)std::min<long>((n + 255) / 256, 8192)), dim3(256), 0, st, n, x, x,
                      sc, 1);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+// Overflow check of a split (PREC fp32s) call's results (clipk_encoder_set_status): status |= bit
+// when any of nseg segments of seg_len floats (seg_stride apart) holds a non-finite value -- the
+// fp16 parts of an operand past 65504 give inf, and inf - inf NaN, which reaches the outputs.
+__global__ __launch_bounds__(256) void finite_check_kernel(int nseg, long seg_len, long seg_stride,
+                                                           const float* __restrict__ x, int* __restrict__ status,
+                                                           int bit) {
+  const long n = (long)nseg * seg_len;
+  bool bad = false;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    bad |= !__builtin_isfinite(x[(i / seg_len) * seg_stride + i % seg_len]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(status, bit);
+}
+static int split_check(const clipk_encoder* e, int nseg, long seg_len, long seg_stride, const float* x, int bit,
+                       hipStream_t st) {
+  if (!e->split || !e->status || nseg <= 0 || seg_len <= 0) return CLIPK_OK;
+  const long nb = ((long)nseg * seg_len + 255) / 256;
+  hipLaunchKernelGGL(finite_check_kernel, dim3((unsigned)std::min<long>(nb, 2048)), dim3(256), 0, st, nseg, seg_len,
+                     seg_stride, x, e->status, bit);
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
 }
@@ -482,8 +484,7 @@ static int gemm_ln(int act, int epi, int M, int N, int K, const void* A, const v
                    (rnb ? 8.0 * M : 0.0);
   ProfScope ps(prof_cls, st, 2.0 * M * N * K, site, b);
   if (t_split && act == CLIPK_F32) act = CLIPK_F32S;  // PREC fp32s: the split-packed weights
-  return clipk_gemm_ln_ws(act, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, stats, colsum, rnb, t_gemm_ws,
-                          t_gemm_ws ? clipk_gemm_ws_bytes() : 0, st);
+  return clipk_gemm_ln(act, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, stats, colsum, rnb, st);
 }
 // mean / rstd (kept for the LayerNorm backward) and the folding GEMM's (rstd, -rstd mean) pairs
 static int ln_merge(int rows, int W, const float* lnst, float* m, float* r, float* rnb, hipStream_t st, bool text) {
@@ -530,8 +531,6 @@ static int block_post_fold(const clipk_encoder* e, const std::array<const void*,
 
 using namespace clipk;
 
-extern "C" const char* clipk_version(void) { return "clipk 0.1.0 gfx950"; }
-
 extern "C" const char* clipk_strerror(int status) {
   switch (status) {
     case CLIPK_OK: return "ok";
@@ -539,6 +538,7 @@ extern "C" const char* clipk_strerror(int status) {
     case CLIPK_ESHAPE: return "shape violates a kernel constraint";
     case CLIPK_EDTYPE: return "unsupported dtype combination";
     case CLIPK_EWORKSPACE: return "workspace too small";
+    case CLIPK_ERANGE: return "input outside the supported range (clipk_split_pack: |W| >= 65504 / 64 or not finite)";
     default: return status > 0 ? hipGetErrorString((hipError_t)status) : "unknown error";
   }
 }
@@ -747,8 +747,6 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
   const bool save = saved != nullptr;
   TextBufs t = text_layout(e, sh.rows, sh.nout, saved, ws, save, io.rd);
   if (ws_bytes < t.ws_bytes || (save && saved_bytes < t.saved_bytes)) return CLIPK_EWORKSPACE;
-  GemmWsScope gemm_ws_scope(t.gemm_ws, st);
-  TRY(gemm_ws_scope.rc);
   const int W = e->W, rows = sh.rows, rd = io.rd;
   const int pg = io.text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE;
   // layer-0 input: x0 (fp32) into X[0] (the residual dtype) when saving (LN1 backward reads
@@ -813,7 +811,7 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
                             t.meanf, t.rstdf, st));
   TRY(gemm(e->act, CLIPK_F32, CLIPK_EPI_NONE, sh.nout, e->E, W, t.lnf, io.proj_f, nullptr, nullptr, txt,
            nullptr, nullptr, 0, st, pg, nullptr, 0, SITE("head")));
-  return CLIPK_OK;
+  return split_check(e, 1, (long)sh.nout * e->E, 0, txt, 1, st);
 }
 
 // Residual-gradient stream of the text backward: fp32, or the grad dtype when that is fp16
@@ -839,8 +837,6 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
   TextBufs t = text_layout(e, sh.rows, sh.nout, const_cast<void*>(saved), nullptr, true, io.rd);
   TextBwdBufs b = text_bwd_layout(e, sh.rows, sh.nout, sh.part_bytes(e->heads), ws);
   if (saved_bytes < t.saved_bytes || ws_bytes < b.bytes) return CLIPK_EWORKSPACE;
-  GemmWsScope gemm_ws_scope(b.gemm_ws, st);
-  TRY(gemm_ws_scope.rc);
   const int W = e->W, rows = sh.rows, nout = sh.nout, gd = e->grad, act = e->act;
   const int pg = io.text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE;
   float* dX = dx0;
@@ -899,13 +895,16 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
     // MLP: dg = dX . Wproj ; dh = dg * qgelu'(h), qgelu'(h) saved by the forward's c_fc epilogue
     // in the act dtype (16-bit: rms 1.8e-4 on the derivative vs 2.9e-5 when recomputing it from a
     // 16-bit h -- under the 16-bit rounding of dh itself -- for no exp / rcp in this epilogue)
-    TRY(gemm(gd, gd, dgelu_epi, n, 4 * W, W, dA, w[15], nullptr, nullptr, b.dh, nullptr, t.h[l], act, st, io.text ? CLIPK_PROF_GEMM_DGELU : CLIPK_PROF_NONE, nullptr, 0, SITE("proj_dx_dgelu")));
+    // (the last layer's compact EOT-row launches are sites of their own: a different GEMM grid)
+    TRY(gemm(gd, gd, dgelu_epi, n, 4 * W, W, dA, w[15], nullptr, nullptr, b.dh, nullptr, t.h[l], act, st,
+             io.text ? CLIPK_PROF_GEMM_DGELU : CLIPK_PROF_NONE, nullptr, 0,
+             compact ? SITE("proj_dx_dgelu_eot") : SITE("proj_dx_dgelu")));
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, n, W, 4 * W, b.dh, w[14], nullptr, nullptr, b.dxn, nullptr,
-             nullptr, 0, st, pg, nullptr, 0, SITE("fc_dx")));
+             nullptr, 0, st, pg, nullptr, 0, compact ? SITE("fc_dx_eot") : SITE("fc_dx")));
     TRY(ln_bwd(n, t.Xm[l], (const float*)w[6], t.mean2[l], t.rstd2[l], false));
     // attention: do = dXm . Wout ; dqkv ; dxn1 = dqkv . Win
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, n, W, W, dA, w[13], nullptr, nullptr, compact ? b.dh : b.do_,
-             nullptr, nullptr, 0, st, pg, nullptr, 0, SITE("out_dx")));
+             nullptr, nullptr, 0, st, pg, nullptr, 0, compact ? SITE("out_dx_eot") : SITE("out_dx")));
     if (compact) {
       // back to the full row layout: do and the residual gradient (the one LN1's backward
       // reads: the 16-bit stream, or fp32 dX) scattered to the EOT rows of zeroed buffers
@@ -966,6 +965,13 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
     TRY(grad_scale_out((long)rows * W, dX, b.gscale, st));
     const DeepPrompts& d = e->deep;
     if (d.n_deep > 0 && d.grads) TRY(grad_scale_out((long)d.n_deep * d.n_ctx * W, d.grads, b.gscale, st));
+    // the returned gradients must be finite (prefix-input mode: only the prefix rows of dx0 are
+    // specified)
+    if (io.text && prefix_mode(e, sh))
+      TRY(split_check(e, sh.G, (long)sh.P * W, (long)sh.R * W, dX, 2, st));
+    else
+      TRY(split_check(e, 1, (long)rows * W, 0, dX, 2, st));
+    if (d.n_deep > 0 && d.grads) TRY(split_check(e, 1, (long)d.n_deep * d.n_ctx * W, 0, d.grads, 2, st));
   }
   return CLIPK_OK;
 }
@@ -1130,7 +1136,7 @@ extern "C" int clipk_vit_forward(const clipk_encoder* e, int B, const float* img
                           (const float*)e->head[3], v.cls, D, nullptr, nullptr, st));
   TRY(gemm(act, CLIPK_F32, CLIPK_EPI_NONE, B, e->E, D, v.cls, e->head[4], nullptr, nullptr, feat,
            nullptr, nullptr, 0, st, CLIPK_PROF_NONE, nullptr, 0, "vit.head"));
-  return CLIPK_OK;
+  return split_check(e, 1, (long)B * e->E, 0, feat, 1, st);
 }
 
 // ---------------------------------------------------------------- prompted ViT (training)
@@ -1279,6 +1285,18 @@ extern "C" int clipk_encoder_set_split(clipk_encoder* e, int on) {
   if (!e || (on != 0 && on != 1)) return CLIPK_EINVAL;
   if (on && (e->act != CLIPK_F32 || e->grad != CLIPK_F32)) return CLIPK_EDTYPE;
   e->split = on;
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_encoder_set_split_target(clipk_encoder* e, int target) {
+  if (!e || target < -24 || target > 30) return CLIPK_EINVAL;
+  e->split_target = target;
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_encoder_set_status(clipk_encoder* e, int* status) {
+  if (!e) return CLIPK_EINVAL;
+  e->status = status;
   return CLIPK_OK;
 }
 

@@ -57,12 +57,6 @@ struct GemmArgs {
   float* lnstats;
   const float* colsum;
   const f32x2* lnrnb;
-  // split tail (TAIL launches, clipk_gemm_ws): the grid's G blocks take tiles 0..G-1 one each,
-  // then the remaining tiles as two K halves on blocks 8 apart (one XCD); the first half's
-  // fp32 accumulators go to tail_ws, published by tail_flags[pair] (release / acquire, agent
-  // scope), and the second half adds them before the epilogue and clears the flag
-  float* tail_ws;
-  unsigned* tail_flags;
 };
 
 // Sum over the aligned 8-lane group (DPP: quad xor 1, quad xor 2, half-row mirror i <-> 7 - i).
@@ -342,7 +336,7 @@ __device__ __forceinline__ void skew_start(int us, int bid) {
 // LNM (clipk_gemm_ln): 1 = per-row LayerNorm statistics of the output, 2 = LayerNorm of A
 // folded into the epilogue (see GemmArgs).
 template <typename T, typename TO, typename TX, int EPI, int BM, int BN, int WM, int WN, bool PERSIST,
-          int ROWB = GEMM_ROWB, int DEPTH = 2, bool AG = false, bool PP = false, int LNM = 0, bool TAIL = false>
+          int ROWB = GEMM_ROWB, int DEPTH = 2, bool AG = false, bool PP = false, int LNM = 0>
 __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
   static_assert(DEPTH == 2 || !PERSIST, "deep ring: non-persistent launches only");
   static_assert(!AG || (!PERSIST && DEPTH == 2 && sizeof(T) == 2 && ROWB == 128), "A-operand QuickGELU path");
@@ -352,7 +346,6 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
   static_assert(!SPLIT || (ROWB == 128 && !AG), "split-fp16 GEMM: 128-B staged rows");
   static_assert(!PP || (PERSIST && !AG && DEPTH == 2 && ROWB == 128 && WM == 2 && WN == 4 && BN == 256 &&
                         (sizeof(T) == 2 || SPLIT) && BM % 64 == 0), "ping-pong main loop (K >= 128)");
-  static_assert(!TAIL || PP, "split tail: ping-pong launches");
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int OPA = BM * ROWB, OPB = BN * ROWB, STAGE = OPA + OPB;
@@ -389,22 +382,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
   const int t_end = t_beg + (xcd < r ? q + 1 : q);
   const int t_step = PERSIST ? (int)(gridDim.x >> 3) : 1;
   int tile = t_beg + (bid >> 3);
-  // TAIL: work item 0 = data-parallel tile xcd * G/8 + slot (the launcher guarantees G < ntiles
-  // <= 1.5 G), item 1 = tail pair p = xcd * G/16 + slot / 2 (tile G + p), K half slot & 1; the
-  // second half runs on the block 8 ids later (same XCD, dispatched after the first: no wait
-  // on a block that cannot be resident)
-  const int tail_g = TAIL ? (int)gridDim.x : 0;
-  auto tail_item = [&](int& t, int& k0, int& n, int& role, int nk_total) {
-    const int slot = bid >> 3, pr = xcd * (tail_g >> 4) + (slot >> 1);
-    t = tail_g + pr;
-    const int h = slot & 1;
-    k0 = h ? nk_total / 2 : 0;
-    n = h ? nk_total - nk_total / 2 : nk_total / 2;
-    role = h ? 2 : 1;
-    return t < ntiles;
-  };
-  if constexpr (TAIL) tile = xcd * (tail_g >> 3) + (bid >> 3);
-  else if (tile >= t_end) return;  // block-uniform
+  if (tile >= t_end) return;  // block-uniform
   if constexpr (PERSIST) skew_start(g.skew, bid);
   const int ks = PERSIST ? 0 : tile / ntiles;
   if (!PERSIST) tile -= ks * ntiles;
@@ -514,12 +492,11 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
                                 ? g.stamp + (size_t)bid * (STAMP_TILES * 3 + 4) : nullptr;
   if (stp) { stp[0] = __builtin_amdgcn_s_memtime(); stp[1] = __builtin_amdgcn_s_memrealtime(); }
 
-  int kt0c = kt0, nkc = nk, role = 0;  // this item's K range and role (TAIL: 1 publish, 2 combine)
+  const int kt0c = kt0, nkc = nk, kt0n = 0;  // this tile's K range, the next tile's first K step
   while (true) {
     const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
-    int next = tile + t_step, kt0n = 0, nkn = nk, role_n = 0;
-    bool has_next = PERSIST && next < t_end;
-    if constexpr (TAIL) has_next = role == 0 && tail_item(next, kt0n, nkn, role_n, nk_all);
+    const int next = tile + t_step;
+    const bool has_next = PERSIST && next < t_end;
     f32x4 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -794,37 +771,6 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         G8_BAR();
       }
       if (!lag) G8_BAR();  // both wave rows level again: the epilogues run side by side
-      if constexpr (TAIL) {
-        // The pair's fp32 accumulators, lane-major per (wave, sub-tile) (1 KB per instruction),
-        // and its flag travel with sc1 (write-through past the XCD's L2; loads sc0 | sc1, from the
-        // coherent point): correct whichever XCDs the two blocks run on, with no L2 write-back.
-        // A store is counted by vmcnt until it is acknowledged, so the data is out before the
-        // flag. The wait is bounded (~0.1 s): a lost flag gives wrong numbers, never a hang.
-        const int pr = tile - tail_g;
-        const __amdgpu_buffer_rsrc_t frs = tile_rsrc(pr >= 0 ? (const void*)(g.tail_flags + pr) : nullptr, 4);
-        if (role == 1) {
-          const __amdgpu_buffer_rsrc_t wrs =
-              tile_rsrc(reinterpret_cast<f32x4*>(g.tail_ws) + (size_t)pr * (NW * TM * TN * 64),
-                        (long long)NW * TM * TN * 64 * 16);
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), wrs,
-                                                     (((w * TM + i) * TN + j) * 64 + lane) * 16, 0, 16);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          G8_BAR();
-          if (threadIdx.x == 0) __builtin_amdgcn_raw_buffer_store_b32(1u, frs, 0, 0, 16);
-        } else if (role == 2) {
-          if (threadIdx.x == 0) {
-            for (int spin = 0; spin < (1 << 22); ++spin) {
-              if (__builtin_amdgcn_raw_buffer_load_b32(frs, 0, 0, 17) != 0u) break;
-              __builtin_amdgcn_s_sleep(2);
-            }
-          }
-          G8_BAR();
-        }
-      }
     } else
     // group 0's operands are loaded at the top of the last K step (its MFMAs hide them)
     for (int kt = 0; kt < nk; ++kt, ++it) {
@@ -897,7 +843,6 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
     // on both the write and the read-back side).
     if (stp && ti < STAMP_TILES) stp[3 + 3 * ti] = __builtin_amdgcn_s_memrealtime();
     static_assert(TN == 4, "epilogue assumes 64 columns per wave");
-    if (!TAIL || role != 1) {
     float bia[CW];
 #pragma unroll
     for (int c = 0; c < CW; ++c) bia[c] = 0.f;
@@ -929,12 +874,6 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
     if constexpr (epi_qgelu(EPI))
       ro2 = tile_rsrc(g.out2 ? (const TO*)g.out2 + (size_t)m0 * g.ldo : nullptr,
                       g.out2 ? rows_ok * g.ldo * (long long)sizeof(TO) : 0);
-    [[maybe_unused]] __amdgpu_buffer_rsrc_t prs = tile_rsrc(nullptr, 0);
-    if constexpr (TAIL) {
-      const int pr = tile - tail_g;
-      if (role == 2) prs = tile_rsrc(reinterpret_cast<f32x4*>(g.tail_ws) + (size_t)pr * (NW * TM * TN * 64),
-                                     (long long)NW * TM * TN * 64 * 16);
-    }
 #pragma unroll
     for (int d = 1; d < XD; ++d) load_ext(d, extq[d]);
 #pragma unroll
@@ -944,15 +883,6 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
 #pragma unroll
       for (int q = 0; q < NQ; ++q) ext[q] = extq[i % XD][q];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous group's read-back done
-      if constexpr (TAIL) {
-        // a split tail's second half: + the first half's accumulators (a resource that is empty
-        // unless this tile combines: out-of-range loads return 0, no branch around acc -- a
-        // branch there made hipcc keep two copies of the accumulators and spill)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                     prs, (((w * TM + i) * TN + j) * 64 + lane) * 16, 0, 17));
-      }
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         *reinterpret_cast<f32x4*>(scr + fr * 64 + (((4 * j + fq) ^ fr) << 2)) = acc[i][j];
@@ -1035,15 +965,6 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       if (i + XD < TM) load_ext(i + XD, extq[i % XD]);  // this group's slot is free again
       if (i + 2 < TM) load_ln(i + 2, i & 1);
     }
-    }  // epilogue (skipped by a split tail's first half)
-    if constexpr (TAIL) {
-      if (role == 2) {  // every wave has read the partial (its epilogue consumed it): clear the flag
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        G8_BAR();
-        if (threadIdx.x == 0)
-          __builtin_amdgcn_raw_buffer_store_b32(0u, tile_rsrc(g.tail_flags + (tile - tail_g), 4), 0, 0, 16);
-      }
-    }
     if (stp && ti < STAMP_TILES) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       stp[4 + 3 * ti] = __builtin_amdgcn_s_memrealtime();
@@ -1054,9 +975,6 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       break;
     }
     tile = next;
-    kt0c = kt0n;
-    nkc = nkn;
-    role = role_n;
     if constexpr (!PP) {
       // the K loop left `it` one past this tile's last step: buffer it & 1 holds the
       // next tile's prefetched first stage
@@ -1189,49 +1107,13 @@ static bool try_pp(const GemmArgs& g, int nwg, hipStream_t st) {
   return false;
 }
 
-// Split tail (caller workspace, clipk_gemm_ws): 256x256 ping-pong tiles when the grid of G = 256
-// blocks would run 1 < rounds <= 1.5 -- the N = 512 text GEMMs at 47k rows: 370 tiles, where
-// the 192-row tiles take 2 rounds -- with the tiles past the first round cut in two K halves
-// on paired blocks (GemmArgs::tail_ws). EPI_NONE and the 16-bit residual epilogue (the N = 512
-// producers / input-grad GEMMs of the text encoder).
-constexpr int kTailPairs = 128;  // max pairs (G / 2)
-constexpr size_t kTailPairBytes = 8 * 64 * 64 * 16;  // 8 waves x 32 sub-tiles x 64 lanes x 16 B
-static size_t tail_ws_bytes() { return kTailPairs * kTailPairBytes + kTailPairs * sizeof(unsigned); }
-// Off by default: measured slower on the headline step than the 192x256 tiles it replaces
-// (profiles/r04e/ab_split_tail.txt: 10.67 -> 11.39 ms/step; the N = 512 input-grad class 2.28 ->
-// 2.46 ms, the K = 512 out_proj 0.52 -> 0.85 ms -- the 256x256 tile does not run the predicted
-// 1.2x the 192-row tile's rate at N = 512, and the halves' partial exchange sits in the epilogue).
-// Knob CLIPK_GEMM_TAIL=1 (or clipk_gemm_set_tail(1)) turns it on.
-static int g_tail = -1;
-static int tail_mode() {
-  if (g_tail < 0) {
-    const char* e = getenv("CLIPK_GEMM_TAIL");
-    g_tail = e ? atoi(e) : 0;
-  }
-  return g_tail;
-}
-template <typename T, typename TO, typename TX, int EPI, int LNM>
-static bool try_tail(const GemmArgs& g, hipStream_t st) {
-  constexpr bool ok_epi = EPI == CLIPK_EPI_NONE || (EPI == CLIPK_EPI_BIAS_RES && sizeof(TX) == 2);
-  if constexpr (!CLIPK_GEMM_PP || sizeof(T) != 2 || sizeof(TO) != 2 || !ok_epi) {
-    return false;
-  } else {
-    if (!g.tail_ws || !tail_mode() || g.N % 256 || g.K * (int)sizeof(T) < 4 * GEMM_ROWB) return false;
-    const int G = (num_cus() / 16) * 16;
-    const int nt = ((g.M + 255) / 256) * (g.N / 256);
-    if (G < 16 || G / 2 > kTailPairs || !(nt > G && nt - G <= G / 2)) return false;
-    hipLaunchKernelGGL((gemm_nt_kernel<T, TO, TX, EPI, 256, 256, 2, 4, true, GEMM_ROWB, 2, false, true, LNM, true>),
-                       dim3(G), dim3(512), 0, st, g);
-    return true;
-  }
-}
+// (Round 4 built a "split tail" for the N = 512 GEMMs -- 256x256 tiles with the tiles past the
+// first round cut in two K halves on paired blocks, the first half's fp32 partial handed over
+// through a caller workspace -- and measured it slower on the headline step, 10.67 -> 11.39
+// ms/step, profiles/r04e/ab_split_tail.txt; removed in round 5.)
 
 template <typename T, typename TO, typename TX, int EPI, int LNM = 0>
 static int launch_gemm(const GemmArgs& g, hipStream_t st) {
-  if (try_tail<T, TO, TX, EPI, LNM>(g, st)) {
-    CLIPK_CHECK_LAUNCH();
-    return CLIPK_OK;
-  }
   const int cfg = pick_cfg(g.M, g.N, (int)sizeof(T));
   const_cast<GemmArgs&>(g).stamp = gemm_stamp_buf();
   if (g_skew < 0) {
@@ -1445,36 +1327,11 @@ static int dispatch_out(int out_dtype, int epi, int aux_dtype, const GemmArgs& g
 
 using namespace clipk;
 
-namespace clipk {
-static int gemm_entry(int in_dtype, int out_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B,
-                      int ldb, const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
-                      const void* aux, int aux_dtype, int ldaux, void* ws, void* stream);
-}
-
 extern "C" int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, int K,
                           const void* A, int lda, const void* B, int ldb,
                           const float* bias, const void* res, int ldr,
                           void* out, int ldo, void* out2, const void* aux, int aux_dtype,
                           int ldaux, void* stream) {
-  return gemm_entry(in_dtype, out_dtype, epi, M, N, K, A, lda, B, ldb, bias, res, ldr, out, ldo, out2, aux,
-                    aux_dtype, ldaux, nullptr, stream);
-}
-
-extern "C" size_t clipk_gemm_ws_bytes(void) { return tail_ws_bytes(); }
-
-extern "C" int clipk_gemm_ws(int in_dtype, int out_dtype, int epi, int M, int N, int K, const void* A, int lda,
-                             const void* B, int ldb, const float* bias, const void* res, int ldr, void* out, int ldo,
-                             void* out2, const void* aux, int aux_dtype, int ldaux, void* ws, size_t ws_bytes,
-                             void* stream) {
-  if (ws && ws_bytes < tail_ws_bytes()) return CLIPK_EWORKSPACE;
-  return gemm_entry(in_dtype, out_dtype, epi, M, N, K, A, lda, B, ldb, bias, res, ldr, out, ldo, out2, aux,
-                    aux_dtype, ldaux, ws, stream);
-}
-
-namespace clipk {
-static int gemm_entry(int in_dtype, int out_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B,
-                      int ldb, const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
-                      const void* aux, int aux_dtype, int ldaux, void* ws, void* stream) {
   if (!A || !B || !out) return CLIPK_EINVAL;
   const bool ag = (epi & CLIPK_A_QGELU) != 0;
   const bool deriv = (epi & CLIPK_QGELU_DERIV) != 0;
@@ -1486,16 +1343,14 @@ static int gemm_entry(int in_dtype, int out_dtype, int epi, int M, int N, int K,
   if (N <= 0 || K <= 0 || N % GEMM_NMIN != 0 || (K * esz) % GEMM_ROWB != 0) return CLIPK_ESHAPE;
   if (lda < K || ldb < K || (lda * esz) % 16 || (ldb * esz) % 16 || ldo < N || ldo % 4)
     return CLIPK_ESHAPE;
+  // CLIPK_F32S: B is clipk_split_pack's output, whose rows are exactly K split elements apart
+  if (in_dtype == CLIPK_F32S && ldb != K) return CLIPK_ESHAPE;
   if ((epi == CLIPK_EPI_BIAS || epi == CLIPK_EPI_BIAS_RES || epi == CLIPK_EPI_BIAS_QGELU) && !bias)
     return CLIPK_EINVAL;
   if (epi == CLIPK_EPI_BIAS_RES && (!res || ldr < N || ldr % 4)) return CLIPK_EINVAL;
   if (epi == CLIPK_EPI_DQGELU && (!aux || ldaux < N || ldaux % 4)) return CLIPK_EINVAL;
   GemmArgs g{(const char*)A, (const char*)B, M, N, K, lda, ldb, bias, res, ldr, out, ldo, out2, aux,
              ldaux, nullptr, 1, 0};
-  if (ws) {  // split-tail workspace: partials, then the pair flags (zero between launches)
-    g.tail_ws = (float*)ws;
-    g.tail_flags = (unsigned*)((char*)ws + kTailPairs * kTailPairBytes);
-  }
   hipStream_t st = (hipStream_t)stream;
   if (deriv) epi = epi == CLIPK_EPI_BIAS_QGELU ? EPI_QGELU_D : EPI_DMUL;
   switch (in_dtype) {
@@ -1506,11 +1361,50 @@ static int gemm_entry(int in_dtype, int out_dtype, int epi, int M, int N, int K,
     default: return CLIPK_EDTYPE;
   }
 }
-}  // namespace clipk
+
+// |W| limit of clipk_split_pack (include/clipk.h): the packed hi part CLIPK_SPLIT_SCALE * W must
+// stay a finite fp16 (below 65504, which it then cannot round past)
+constexpr float kSplitPackMax = 65504.0f / CLIPK_SPLIT_SCALE;
+
+// one pass: *flag = 1 when any |W| >= kSplitPackMax or W is not finite (the pack's output
+// would hold an inf / NaN part)
+__device__ int g_split_range_flag;
+__global__ __launch_bounds__(256) void split_range_kernel(int N, int K, const float* __restrict__ W, int ldw,
+                                                          int* __restrict__ flag) {
+  const long n = (long)N * K;
+  bool bad = false;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float x = W[(i / K) * ldw + i % K];
+    bad |= !(fabsf(x) < kSplitPackMax);  // NaN compares false
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) *flag = 1;
+}
 
 extern "C" int clipk_split_pack(int N, int K, const float* W, int ldw, void* out, void* stream) {
   if (!W || !out) return CLIPK_EINVAL;
   if (N <= 0 || K <= 0 || K % 32 != 0 || ldw < K) return CLIPK_ESHAPE;
+  // the range precondition is enforced here, not left to the caller: one synchronous check
+  // (packing runs once per model, at construction) through a module-scope flag
+  {
+    const hipStream_t st = (hipStream_t)stream;
+    int h = 0;
+    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_split_range_flag), &h, sizeof(int), 0, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) {
+      int* flag = nullptr;
+      e = hipGetSymbolAddress((void**)&flag, HIP_SYMBOL(g_split_range_flag));
+      if (e == hipSuccess) {
+        const long n = (long)N * K, nb = (n + 255) / 256;
+        hipLaunchKernelGGL(split_range_kernel, dim3((unsigned)(nb < 1024 ? nb : 1024)), dim3(256), 0, st, N, K, W, ldw,
+                           flag);
+        e = hipGetLastError();
+      }
+    }
+    if (e == hipSuccess)
+      e = hipMemcpyFromSymbolAsync(&h, HIP_SYMBOL(g_split_range_flag), sizeof(int), 0, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return (int)e;
+    if (h) return CLIPK_ERANGE;
+  }
   const long n = (long)N * (K / 8);
   hipLaunchKernelGGL(split_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, N, K, W,
                      ldw, (f16*)out);
@@ -1538,25 +1432,10 @@ static int dispatch_ln_split(int epi, const GemmArgs& g, hipStream_t st) {
 // LayerNorm folded into the text GEMMs (include/clipk.h): statistics partials out (EPI_BIAS_RES)
 // or colsum + per-row (rstd, -rstd * mean) in (EPI_BIAS / EPI_BIAS_QGELU); 16-bit in and out, or
 // CLIPK_F32S (fp32 A / out / residual, B split-packed).
-extern "C" int clipk_gemm_ln_ws(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B,
-                                int ldb, const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
-                                float* stats, const float* colsum, const float* rnb, void* ws, size_t ws_bytes,
-                                void* stream);
-
 extern "C" int clipk_gemm_ln(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B,
                              int ldb, const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
                              float* stats, const float* colsum, const float* rnb, void* stream) {
-  return clipk_gemm_ln_ws(in_dtype, epi, M, N, K, A, lda, B, ldb, bias, res, ldr, out, ldo, out2, stats, colsum, rnb,
-                          nullptr, 0, stream);
-}
-
-// clipk_gemm_ln with the split-tail workspace of clipk_gemm_ws (the LN-statistics producers)
-extern "C" int clipk_gemm_ln_ws(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B,
-                                int ldb, const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
-                                float* stats, const float* colsum, const float* rnb, void* ws, size_t ws_bytes,
-                                void* stream) {
   if (!A || !B || !out || !bias) return CLIPK_EINVAL;
-  if (ws && ws_bytes < tail_ws_bytes()) return CLIPK_EWORKSPACE;
   if (in_dtype != CLIPK_F16 && in_dtype != CLIPK_BF16 && in_dtype != CLIPK_F32S) return CLIPK_EDTYPE;
   const bool deriv = (epi & CLIPK_QGELU_DERIV) != 0;  // fold form of c_fc: out2 = quickgelu'
   epi &= ~CLIPK_QGELU_DERIV;
@@ -1570,12 +1449,9 @@ extern "C" int clipk_gemm_ln_ws(int in_dtype, int epi, int M, int N, int K, cons
   const int esz = in_dtype == CLIPK_F32S ? 4 : 2;
   if (N <= 0 || K <= 0 || N % GEMM_NMIN != 0 || (K * esz) % GEMM_ROWB != 0) return CLIPK_ESHAPE;
   if (lda < K || ldb < K || lda % 8 || ldb % 8 || ldo < N || ldo % 8) return CLIPK_ESHAPE;
+  if (in_dtype == CLIPK_F32S && ldb != K) return CLIPK_ESHAPE;  // clipk_split_pack's row stride
   GemmArgs g{(const char*)A, (const char*)B, M, N, K, lda, ldb, bias, res, ldr, out, ldo, out2, nullptr,
              0, nullptr, 1, 0, 0, stats, colsum, reinterpret_cast<const f32x2*>(rnb)};
-  if (ws) {
-    g.tail_ws = (float*)ws;
-    g.tail_flags = (unsigned*)((char*)ws + kTailPairs * kTailPairBytes);
-  }
   hipStream_t st = (hipStream_t)stream;
   if (deriv) epi = EPI_QGELU_D;
   if (in_dtype == CLIPK_F32S) return dispatch_ln_split(epi, g, st);
@@ -1672,6 +1548,7 @@ extern "C" int clipk_gemm_splitk(int in_dtype, int out_dtype, int epi, int M, in
   if (N <= 0 || K <= 0 || N % GEMM_NMIN != 0 || (K * esz) % GEMM_ROWB != 0) return CLIPK_ESHAPE;
   if (lda < K || ldb < K || (lda * esz) % 16 || (ldb * esz) % 16 || ldo < N || ldo % 4) return CLIPK_ESHAPE;
   if (splits > K * esz / GEMM_ROWB) return CLIPK_ESHAPE;
+  if (in_dtype == CLIPK_F32S && ldb != K) return CLIPK_ESHAPE;  // clipk_split_pack's row stride
   const bool deriv = (epi & CLIPK_QGELU_DERIV) != 0;
   epi &= ~CLIPK_QGELU_DERIV;
   if (epi == CLIPK_EPI_DQGELU || (deriv && epi != CLIPK_EPI_BIAS_QGELU)) return CLIPK_EINVAL;
@@ -1732,18 +1609,6 @@ extern "C" int clipk_gemm_stamps(void* host, size_t bytes) {
   if (!g_stamp || !host || bytes < need) return CLIPK_EINVAL;
   if (hipDeviceSynchronize() != hipSuccess) return (int)hipGetLastError();
   if (hipMemcpy(host, g_stamp, need, hipMemcpyDeviceToHost) != hipSuccess) return (int)hipGetLastError();
-  return CLIPK_OK;
-}
-
-// Test / benchmark knob: the split tail of clipk_gemm_ws on (1) or off (0).
-// (encoder.hip: the pair flags need zeroing only while the split tail can run)
-namespace clipk {
-bool gemm_tail_enabled() { return tail_mode() != 0; }
-}  // namespace clipk
-
-extern "C" int clipk_gemm_set_tail(int on) {
-  if (on != 0 && on != 1) return CLIPK_EINVAL;
-  g_tail = on;
   return CLIPK_OK;
 }
 

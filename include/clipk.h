@@ -49,7 +49,8 @@ enum {
   CLIPK_EINVAL = -1,     /* null pointer / bad enum */
   CLIPK_ESHAPE = -2,     /* shape violates a kernel constraint */
   CLIPK_EDTYPE = -3,     /* unsupported dtype combination */
-  CLIPK_EWORKSPACE = -4  /* workspace too small */
+  CLIPK_EWORKSPACE = -4, /* workspace too small */
+  CLIPK_ERANGE = -5      /* an input outside the range the kernel supports (clipk_split_pack) */
 };
 
 /* GEMM epilogues:  acc = A[M,K] . B[N,K]^T  (fp32 accumulate)                         */
@@ -74,6 +75,10 @@ enum { CLIPK_A_QGELU = 0x100 };
 enum { CLIPK_QGELU_DERIV = 0x200 };
 
 const char* clipk_version(void);
+/* sha256 (hex) over the sources this library was built from: csrc/{*.hip,*.h,Makefile} and
+ * include/clipk.h, in file-name order, each as "<sha256 of content>  <relative path>\n"
+ * (fsp_amd/_native.py source_digest; the loader refuses a library built from another tree). */
+const char* clipk_source_digest(void);
 const char* clipk_strerror(int status);
 int clipk_device_arch_ok(void); /* 1 if device 0 is gfx950 */
 
@@ -86,29 +91,14 @@ int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, int K,
                void* out, int ldo, void* out2, const void* aux, int aux_dtype, int ldaux,
                void* stream);
 
-/* clipk_gemm with a caller workspace (ws_bytes >= clipk_gemm_ws_bytes(); ws NULL: clipk_gemm).
- * With the split tail on (clipk_gemm_set_tail / CLIPK_GEMM_TAIL=1; off by default): when a
- * 256x256 grid would take between 1 and 1.5 rounds of the CUs (the N = 512 text GEMMs
- * at ~47k rows), its tiles past the first round run as two K halves on paired blocks of one XCD
- * (the first half's fp32 partial through ws, a release / acquire flag pair), so the second
- * round takes half a tile instead of a whole one. 16-bit in / out, EPI_NONE or the 16-bit
- * residual epilogue; other calls behave as clipk_gemm. The flags at the end of ws must be zero
- * before a call (each call leaves them zero); the two K halves are summed in a fixed order
- * (deterministic), which differs from the single-tile order in the last bits. */
-size_t clipk_gemm_ws_bytes(void);
-int clipk_gemm_ws(int in_dtype, int out_dtype, int epi, int M, int N, int K,
-                  const void* A, int lda, const void* B, int ldb,
-                  const float* bias, const void* res, int ldr,
-                  void* out, int ldo, void* out2, const void* aux, int aux_dtype, int ldaux,
-                  void* ws, size_t ws_bytes, void* stream);
-
 /* fp32-class GEMM on the 16-bit MFMA (PREC "fp32s"; the reference runs these Linear layers in
  * fp32, PromptSRC/clip/model.py:171-177, 699). clipk_split_pack stores W [N, K] (fp32, row
  * stride ldw) as CLIPK_SPLIT_SCALE * W split into fp16 parts hi = fp16(x), lo = fp16(x - hi):
  * per 8 consecutive k, 16 B of hi then 16 B of lo (4 B per element, the out buffer holds
- * N * K * 4 bytes; K % 32 == 0). |W| must stay below 65504 / CLIPK_SPLIT_SCALE (the caller
- * checks). clipk_gemm(in_dtype = CLIPK_F32S, ...) then takes A fp32 [M, K] and B = the packed
- * weight (ldb = K) and forms every product as hi(a) hi(b) + hi(a) lo(b) + lo(a) hi(b) with
+ * N * K * 4 bytes; K % 32 == 0). |W| must stay below 65504 / CLIPK_SPLIT_SCALE: the call
+ * checks it (one pass over W, then a stream synchronisation: packing runs once per model) and
+ * returns CLIPK_ERANGE for a larger or non-finite value. clipk_gemm(in_dtype = CLIPK_F32S, ...)
+ * then takes A fp32 [M, K] and B = the packed weight (ldb must equal K) and forms every product as hi(a) hi(b) + hi(a) lo(b) + lo(a) hi(b) with
  * v_mfma_f32_16x16x32_f16 (fp32 accumulate; A split in registers as its fragments are read),
  * scaled by 1 / CLIPK_SPLIT_SCALE before the epilogue: ~22 significant bits per operand, the
  * fp32 result to ~1e-6 relative. out / res / aux fp32 (epilogues as above). */
@@ -149,18 +139,10 @@ int clipk_gemm_ln(int in_dtype, int epi, int M, int N, int K, const void* A, int
                   float* stats, const float* colsum, const float* rnb, void* stream);
 int clipk_ln_stats_merge(int rows, int width, const float* stats, float* mean, float* rstd, float* rnb,
                          void* stream);
-/* clipk_gemm_ln with the split-tail workspace of clipk_gemm_ws (same ws contract). */
-int clipk_gemm_ln_ws(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B, int ldb,
-                     const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
-                     float* stats, const float* colsum, const float* rnb, void* ws, size_t ws_bytes, void* stream);
-
 /* Benchmark knob: force the 16-bit GEMM tile configuration (0: 128x128, 1: 256x256
  * (persistent above 2 x CUs tiles), 2: 256x128, 3: 256x256 non-persistent, 6: 192x256;
  * -1 = automatic by shape; other values: CLIPK_EINVAL). Not needed for normal use. */
 int clipk_gemm_set_config(int cfg);
-/* Test / benchmark knob: clipk_gemm_ws's split tail on (1) or off (0, default: measured slower
- * than the 192x256 tiles on the headline step). */
-int clipk_gemm_set_tail(int on);
 
 /* Image preprocessing (Dassl/torchvision Resize+CenterCrop / RandomResizedCrop+flip,
  * ToTensor, Normalize; transforms.py:206-354): Pillow-exact bicubic resampling of a crop
@@ -393,6 +375,18 @@ int clipk_encoder_set_ln_fold(clipk_encoder* e, const void* const* fold_ptrs);
  * from max |dtxt| (exact, undone on dx0 and the deep-prompt gradients), so the gradient operands
  * sit in fp16's normal range. Reference semantics: PromptSRC/clip/model.py:699 (fp32 model). */
 int clipk_encoder_set_split(clipk_encoder* e, int on);
+/* The split backward's scale target t (default 7): s puts max |s dtxt| in [2^(t-1), 2^t). A lower
+ * target leaves more headroom below fp16's 65504 for gradient growth through the layers, at
+ * fewer significant bits for the smallest gradients. -24 <= t <= 30 (t > 16 overflows by design:
+ * a test of the overflow status). */
+int clipk_encoder_set_split_target(clipk_encoder* e, int target);
+/* Overflow status of a PREC fp32s (split) encoder's calls: status = a device int the encoder
+ * ORs flags into -- 1 when a text / ViT forward produced a non-finite feature, 2 when a backward's
+ * returned gradients (dx0, deep-prompt and visual-prompt gradients) hold a non-finite value (the
+ * split operands' fp16 range was exceeded: an activation or gradient past 65504). The caller zeroes
+ * it and reads it when it synchronises (fsp_amd/clip/model.py re-runs an overflowed backward at a
+ * lower scale target). NULL detaches. The pointer must stay valid for the calls that follow. */
+int clipk_encoder_set_status(clipk_encoder* e, int* status);
 
 /* ViT with visual prompts, forward with saved activations and input-grad backward (the
  * prompted VisionTransformer of IVLP / PromptSRC, model.py:401-431, and MaPLe, 434-485):

@@ -233,8 +233,40 @@ def tokenizer_table():
     table = {w: tok.encode(w) for w in words}
     probes = ["X X X X class7.", "a photo of a class123.", "a photo of a dog.",
               "Hello, World! it's 2 o'clock", "X " * 16 + "class999."]
+    probes += template_probes()
     enc = {s: tok.encode(s) for s in probes}
     return table, enc
+
+
+# class names for the template probes: punctuation inside words (hyphen, apostrophe), several
+# words, digits, capitals, and long words the BPE merge loop builds from many merges
+PROBE_NAMES = ["dog", "golden retriever", "jack-o'-lantern", "potter's wheel", "T-shirt", "hen-of-the-woods",
+               "Granny Smith", "class123", "African elephant", "internationalization", "photographs",
+               "unbelievably embroidered", "3D printer", "rock beauty", "Yorkshire terrier", "spider web",
+               "crossword puzzle", "car mirror", "Band Aid", "water ouzel"]
+EXTRA_PROBES = ["  multiple   spaces  and\ttabs  ", "semicolons; colons: dashes -- and (parens)",
+                "&amp; html escapes &lt;b&gt;", "a photo of a {}, a type of pet.", "ALL CAPS SHOUTING!!!",
+                "mixed123digits456and789words", "it's they're we've I'm you'll he'd", "e.g. i.e. etc.",
+                "comma,separated,values", "question? exclamation! period."]
+
+
+def template_probes():
+    """Every prompt template the reference ships (trainers/imagenet_templates.py
+    IMAGENET_TEMPLATES + IMAGENET_TEMPLATES_SELECT, trainers/zsclip.py CUSTOM_TEMPLATES), each
+    filled with one of PROBE_NAMES in turn, plus EXTRA_PROBES."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_imagenet_templates",
+                                                  os.path.join(REF, "trainers", "imagenet_templates.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    import trainers.zsclip as zs
+    temps = list(m.IMAGENET_TEMPLATES) + list(m.IMAGENET_TEMPLATES_SELECT) + sorted(set(zs.CUSTOM_TEMPLATES.values()))
+    out = []
+    for i, t in enumerate(temps):
+        s = t.format(PROBE_NAMES[i % len(PROBE_NAMES)])
+        if s not in out:
+            out.append(s)
+    return out + EXTRA_PROBES
 
 
 def save(name, meta, arrays):
@@ -242,19 +274,103 @@ def save(name, meta, arrays):
     print("wrote", name, {k: v.shape for k, v in arrays.items()})
 
 
+def run_cocoop_headline(arch, n_cls, batch, ctx_init, n_ctx, chunk=100):
+    """run_cocoop at the benchmark's size (ViT-B/16, C = 1,000, B = 8), where the reference's
+    one-shot autograd graph would hold ~40 GB of text activations per image: the same
+    reference modules and the same arithmetic as CustomCLIP.forward (cocoop.py:235-260) --
+    image_encoder, prompt_learner (meta_net, ctx_shifted, construct_prompts), text_encoder,
+    normalize, logit_scale.exp() * imf @ txt^T, criterion -- with the text encoder evaluated
+    over class chunks: the logits without a graph, then dlogits = d loss / d logits, then per
+    (image, chunk) the text encoder re-run with a graph and back-propagated from its dlogits
+    slice into the prompts, and finally prompts.backward(d prompts) into ctx and meta_net.
+    Mathematically the reference's backward; only the fp32 summation order of the per-chunk
+    gradient accumulation differs."""
+    from clip.model import build_model
+    import trainers.cocoop as cocoop
+    tsd, digest = build_clip(arch)
+    a = synth.ARCHS[arch]
+    design = dict(DESIGN, trainer="CoCoOp")
+    model = build_model(dict(tsd), design).float()
+    cfg = make_cfg(a.image_resolution, cocoop=dict(N_CTX=n_ctx, CTX_INIT=ctx_init, PREC="fp32", USE_FOCAL_LOSS=False))
+    names = synth.synthetic_classnames(n_cls)
+    cc = cocoop.CustomCLIP(cfg, names, model)
+    for n, p in cc.named_parameters():
+        if "prompt_learner" not in n:
+            p.requires_grad_(False)
+    pl = cc.prompt_learner
+    mn = synth.make_meta_net(a.embed_dim, a.transformer_width, seed=4)
+    with torch.no_grad():
+        for k, v in mn.items():
+            dict(pl.named_parameters())[k].copy_(torch.from_numpy(v))
+    ctx0 = pl.ctx.detach().clone().numpy()
+    img = torch.from_numpy(synth.make_images(batch, a.image_resolution, seed=1))
+    lbl = torch.from_numpy(synth.make_labels(batch, n_cls, seed=2))
+    tok = cc.tokenized_prompts
+    out = dict(arch=arch, digest=digest, n_cls=n_cls, batch=batch, n_ctx=pl.n_ctx, ctx_init=ctx_init, focal=0,
+               chunked=chunk)
+    cc.train()
+    imf = cc.image_encoder(img.type(cc.dtype))
+    imf = imf / imf.norm(dim=-1, keepdim=True)
+    prompts = cc.prompt_learner(imf)  # (batch, n_cls, n_tkn, dim), graph to ctx / meta_net
+    scale = cc.logit_scale.exp()
+
+    def chunk_logits(b, c0, c1, p):
+        tf = cc.text_encoder(p, tok[c0:c1])
+        tf = tf / tf.norm(dim=-1, keepdim=True)
+        return scale * imf[b].detach() @ tf.t()
+
+    logits = torch.zeros(batch, n_cls)
+    with torch.no_grad():
+        for b in range(batch):
+            for c0 in range(0, n_cls, chunk):
+                c1 = min(c0 + chunk, n_cls)
+                logits[b, c0:c1] = chunk_logits(b, c0, c1, prompts[b, c0:c1])
+            print("logits image", b, flush=True)
+    lg = logits.clone().requires_grad_(True)
+    loss = cc.criterion(lg, lbl)
+    (dlogits,) = torch.autograd.grad(loss, lg)
+    dprompts = torch.zeros_like(prompts)
+    for b in range(batch):
+        for c0 in range(0, n_cls, chunk):
+            c1 = min(c0 + chunk, n_cls)
+            p = prompts[b, c0:c1].detach().requires_grad_(True)
+            chunk_logits(b, c0, c1, p).backward(dlogits[b, c0:c1])
+            dprompts[b, c0:c1] = p.grad
+        print("backward image", b, flush=True)
+    prompts.backward(dprompts)
+    grads = {"grad_ctx": pl.ctx.grad.detach().clone().numpy()}
+    for k, p in pl.named_parameters():
+        if k.startswith("meta_net"):
+            grads["grad_" + k] = p.grad.detach().clone().numpy()
+    sgd_after_step(pl)
+    arrays = dict(ctx0=ctx0, image_features=imf.detach().numpy(), logits=logits.numpy(),
+                  loss=np.asarray(loss.item(), np.float32), ctx_after_step=pl.ctx.detach().numpy(),
+                  tokenized=tok.numpy().astype(np.int32), **grads)
+    return out, arrays
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also full-size ViT-B/L sets (slow)")
+    ap.add_argument("--only", choices=["tokenizer", "headline"],
+                    help="tokenizer: the BPE probes alone; headline: the benchmark-size CoCoOp set alone "
+                         "(ViT-B/16, C 1000, B 8: ~15 min on 8 threads)")
     args = ap.parse_args()
     torch.set_num_threads(8)
     _install_stubs()
 
+    if args.only == "headline":
+        m, a = run_cocoop_headline("ViT-B/16", 1000, 8, "a photo of a", 4)
+        save("cocoop_vitb16_c1000_b8", m, a)
+        return
     table, enc = tokenizer_table()
     pkg = os.path.join(REPO, "few-shot-prompt-learning-for-vision-language-models-in-imbalanced-datasets_amd")
     with open(os.path.join(pkg, "clip", "bpe_fallback.json"), "w") as f:
         json.dump(table, f, indent=0, sort_keys=True)
     with open(os.path.join(HERE, "tokenizer_probes.json"), "w") as f:
         json.dump(enc, f, indent=0, sort_keys=True)
+    if args.only == "tokenizer":
+        return
 
     lrs = lr_sequences()
     np.savez(os.path.join(HERE, "lr_schedule.npz"), ep10=lrs[10], ep50=lrs[50])

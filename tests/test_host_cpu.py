@@ -30,6 +30,33 @@ def test_library_exports_every_header_symbol():
     assert "shape" in _native.strerror(-2)
 
 
+def test_library_is_built_from_this_tree():
+    """libclipk.so embeds the digest of the sources it was built from (clipk_source_digest); the
+    loader compares it with the tree it ships with."""
+    from fsp_amd import _native
+    _native.load()
+    assert _native.library_digest() == _native.source_digest()
+    rels = [r for r, _ in _native.source_files()]
+    assert "csrc/gemm.hip" in rels and "csrc/Makefile" in rels and rels[-1] == "include/clipk.h"
+
+
+def test_stale_library_is_refused(monkeypatch, tmp_path):
+    """A library whose embedded digest differs from the tree (a stale build) does not load."""
+    from fsp_amd import _native
+    monkeypatch.setattr(_native, "_lib", None)
+    monkeypatch.setattr(_native, "source_digest", lambda: "0" * 64)
+    with pytest.raises(_native.ClipkError, match="built from other sources"):
+        _native.load()
+    # and the digest really follows the sources: one byte changed in a copy changes it
+    src = tmp_path / "gemm.hip"
+    orig = dict(_native.source_files())["csrc/gemm.hip"]
+    src.write_bytes(open(orig, "rb").read() + b"\n")
+    monkeypatch.undo()
+    files = [(r, str(src) if r == "csrc/gemm.hip" else p) for r, p in _native.source_files()]
+    monkeypatch.setattr(_native, "source_files", lambda: files)
+    assert _native.source_digest() != _native.library_digest()
+
+
 def test_gemm_config_knob_range():
     """The GEMM tile knob accepts the shipped configurations only (7 = the round-3 64x128
     small-M tile); the variants measured slower (4 / 5: 64-B rows, 8 / 9: deep-A ring; round 2's

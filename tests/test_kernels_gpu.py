@@ -496,40 +496,45 @@ def test_gemm_split_parts_exact(dev, M):
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("K", [256, 512, 1536, 2048])
 @pytest.mark.parametrize("M", [47160, 33000, 45000])
-def test_gemm_split_tail(dev, dtype, K, M):
-    """clipk_gemm_ws (split tail: 256x256 tiles, the tiles past the first round as two K halves on
-    paired blocks, partial + flag through the workspace) vs a torch fp32 reference and vs plain
-    clipk_gemm: EPI_NONE and the 16-bit residual epilogue at the N = 512 text shapes (47,160 rows:
-    370 tiles on 256 CUs). Reruns are bitwise equal and the pair flags are left zero."""
-    lib = N.load()
-    N.check(lib.clipk_gemm_set_tail(1), "clipk_gemm_set_tail")  # off by default (DESIGN §5)
-    try:
-        _split_tail_case(dev, dtype, K, M)
-    finally:
-        lib.clipk_gemm_set_tail(0)
-
-
-def _split_tail_case(dev, dtype, K, M):
+def test_gemm_n512_large_m(dev, dtype, K, M):
+    """The N = 512 text GEMMs at the headline's row counts (47,160 rows: the 192x256 ping-pong
+    tiles, 492 tiles on 256 CUs) vs a torch fp32 reference: EPI_NONE (the input-grad GEMMs) and
+    the 16-bit residual epilogue (out_proj / c_proj forward); reruns bitwise equal."""
     Nn = 512
     g = torch.Generator(device="cpu").manual_seed(M + K)
     A = torch.randn(M, K, generator=g).to(dev).to(dtype)
     B = (torch.randn(Nn, K, generator=g) / math.sqrt(K)).to(dev).to(dtype)
     bias = torch.randn(Nn, generator=g).to(dev)
     res = torch.randn(M, Nn, generator=g).to(dev).to(dtype)
-    ws = ops.gemm_ws(dev)
-    nflag = 128 * 4
     ref = A.float() @ B.float().t()
-    o1 = ops.gemm(A, B, N.EPI_NONE, dtype, ws=ws)
-    o2 = ops.gemm(A, B, N.EPI_NONE, dtype, ws=ws)
+    o1 = ops.gemm(A, B, N.EPI_NONE, dtype)
+    o2 = ops.gemm(A, B, N.EPI_NONE, dtype)
     torch.cuda.synchronize()
     assert torch.equal(o1, o2)
-    assert int(ws[-nflag:].sum()) == 0
-    close(o1, ref, dtype, f"tail none K{K}")
-    plain = ops.gemm(A, B, N.EPI_NONE, dtype)
-    close(o1, plain, dtype, f"tail vs plain K{K}")
-    r1 = ops.gemm(A, B, N.EPI_BIAS_RES, dtype, bias=bias, res=res, ws=ws)
-    close(r1, ref + bias + res.float(), dtype, f"tail res K{K}")
-    assert int(ws[-nflag:].sum()) == 0
+    close(o1, ref, dtype, f"n512 none K{K}")
+    r1 = ops.gemm(A, B, N.EPI_BIAS_RES, dtype, bias=bias, res=res)
+    close(r1, ref + bias + res.float(), dtype, f"n512 res K{K}")
+
+
+def test_split_pack_range_and_stride(dev):
+    """clipk_split_pack enforces |W| < 65504 / SPLIT_SCALE itself (CLIPK_ERANGE for a larger or a
+    non-finite value), and the CLIPK_F32S GEMMs refuse a B row stride other than K (the packed
+    weight's rows are exactly K elements apart)."""
+    lib = N.load()
+    K, Nn = 64, 128
+    ok = torch.full((Nn, K), 65504.0 / N.SPLIT_SCALE * 0.999, device=dev)
+    out = torch.empty(Nn, K, dtype=torch.int32, device=dev)
+    assert lib.clipk_split_pack(Nn, K, ops._p(ok), K, ops._p(out), ops._stream()) == 0
+    for bad in (65504.0 / N.SPLIT_SCALE, float("inf"), float("nan")):
+        w = torch.zeros(Nn, K, device=dev)
+        w[Nn - 1, K - 1] = bad
+        assert lib.clipk_split_pack(Nn, K, ops._p(w), K, ops._p(out), ops._stream()) == -5, bad
+    a = torch.randn(16, K, device=dev)
+    o = torch.empty(16, Nn, device=dev)
+    common = (N.F32S, N.F32, N.EPI_NONE, 16, Nn, K, ops._p(a), K, ops._p(out))
+    assert lib.clipk_gemm(*common, 2 * K, None, None, Nn, ops._p(o), Nn, None, None, 0, Nn, ops._stream()) == -2
+    assert lib.clipk_gemm(*common, K, None, None, Nn, ops._p(o), Nn, None, None, 0, Nn, ops._stream()) == 0
+    torch.cuda.synchronize()
 
 
 @pytest.mark.parametrize("reduction", ["mean", "sum", "none"])

@@ -101,9 +101,13 @@ def cocoop_oracle(meta, ref, truncate=True):
     return logits.detach().numpy(), float(loss), grads
 
 
-@pytest.mark.parametrize("name", ["cocoop_tiny_ctxinit_ce", "cocoop_tiny_focal", "cocoop_vitb16_c4"])
+@pytest.mark.parametrize("name", ["cocoop_tiny_ctxinit_ce", "cocoop_tiny_focal", "cocoop_vitb16_c4",
+                                  "cocoop_vitl14_336_c3"])
 def test_oracle_cocoop(name):
+    """Also at ViT-L/14@336px (577 image tokens, W = 768 text): the only reference output at the
+    config-5 architecture, which pins the oracle that gates config 5 at C = 1,000."""
     meta, ref = load_fixture(name)
+    torch.set_num_threads(8)
     logits, loss, grads = cocoop_oracle(meta, ref)
     assert np.abs(logits - ref["logits"]).max() <= 1e-4
     assert rel_err(loss, ref["loss"]) <= 1e-5
