@@ -59,6 +59,15 @@ def metric_name(arch):
 REF_CPU_FILE = os.path.join(ROOT, "profiles", "r03_ref_cpu_timing.jsonl")
 
 
+_T0 = time.time()
+
+
+def log(msg):
+    """Progress on stderr (the JSON line alone goes to stdout): a long default run keeps
+    writing, so a watchdog on silent commands does not take it for hung."""
+    print(f"[bench {time.time() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def launcher_cmd(argv, n, port):
     """The torchrun command bench.py --gpus N (N > 1) starts as its child: one rank per GPU
     of this node, rendezvous on 127.0.0.1, the same bench arguments."""
@@ -480,6 +489,7 @@ def main():
     arch = synth.ARCHS[args.arch]
     n_eval_rank = dist.shard_range(args.eval_images)[1] - dist.shard_range(args.eval_images)[0]
 
+    log(f"headline: {args.arch} B={args.batch} C={args.classes} {args.prec}")
     trainer, dm = build_trainer(args, args.prec, args.batch, dev, rank, n_test_device=n_eval_rank)
     lay = trainer.model.prompt_learner.layout
     L = lay.L
@@ -487,7 +497,9 @@ def main():
     t, sites = time_train(trainer, dm, args.steps, args.warmup, prof_steps=n_prof)
     table = kernel_table(sites, n_prof, args.prec) if sites else None
     roof = roofline_of(table, args.prec) if table else None
+    log(f"headline train {1000 * t / args.steps:.3f} ms/step; eval")
     eval_ips, n_eval = time_eval(trainer, dm, n_eval_rank)
+    log(f"eval {eval_ips:.1f} img/s")
 
     f_img, f_txt, b_txt = flops(arch, args.classes, L)
     step_flops = args.batch * (f_img + args.classes * (f_txt + b_txt))
@@ -533,6 +545,7 @@ def main():
     elif not args.no_extra and not args.no_configs and world == 1:
         # BASELINE configs 4 and 5 per GPU beside the headline (their own archs, bf16)
         for key, arch in (("config4", "ViT-L/14"), ("config5", "ViT-L/14@336px")):
+            log(key)
             out[key] = baseline_config_line(argparse.Namespace(**{**vars(args), "arch": arch}), dev, rank, world,
                                             n_eval=2000)
     if not args.no_extra and world > 1:
@@ -547,6 +560,7 @@ def main():
         torch.cuda.empty_cache()
     if not args.no_extra and world == 1:  # the N > 1 scaling runs report the headline lines only
         # the reference's batch size for CoCoOp (configs/trainers/CoCoOp/*.yaml: 1 image/step)
+        log("batch1")
         tr1, dm1 = build_trainer(args, args.prec, 1, dev, rank)
         t1, _ = time_train(tr1, dm1, B1_STEPS, 5)
         out["batch1"] = {"images_per_sec": round(world * B1_STEPS / t1, 3),
@@ -560,6 +574,7 @@ def main():
         proxy = {}
         for n in (2, 4, 8):
             cls = args.classes // n
+            log(f"batch1 class-shard proxy n{n}")
             trp, dmp = build_trainer(argparse.Namespace(**{**vars(args), "classes": cls}), args.prec, 1, dev, rank)
             tp, _ = time_train(trp, dmp, B1_STEPS, 5)
             proxy[f"n{n}"] = {"classes": cls, "ms_per_step": round(1000 * tp / B1_STEPS, 3)}
@@ -567,6 +582,7 @@ def main():
             torch.cuda.empty_cache()
         out["batch1_class_shard_proxy"] = proxy
         # BASELINE config 2: CoOp n_ctx 16, ViT-B/16 fp16, 1000 classes, batch 32
+        log("coop config 2")
         trc, dmc = build_coop_trainer(args, args.prec, 32, dev, rank, n_test_device=args.eval_images)
         tc, _ = time_train(trc, dmc, 10, 3)
         ec, nc = time_eval(trc, dmc, args.eval_images)
@@ -581,6 +597,7 @@ def main():
         # the fp32-class precisions, the paths that meet the north-star |d logit| <= 1e-3:
         # PREC fp32s (split-fp16 MFMA GEMMs, fp32 elsewhere) and PREC fp32 (f32-input MFMA)
         for p in ("fp32s", "fp32"):
+            log(p)
             out[p] = precision_line(args, p, dev, rank, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -588,9 +605,17 @@ def main():
             # 50-class sample scaled linearly overstated the rate ~3x: the text activations of
             # 1,000 x 77 tokens do not stay in cache). SURVEY §8(d): the full host (every CPU this
             # process may run on) and an 8-thread run (the build container's reference timing)
-            host = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+            # "full host" = the CPU share this process is given: OMP_NUM_THREADS where the
+            # launcher sets it (the GPU box: 16 of its nproc), else every CPU of the affinity set
+            # (threads beyond the share oversubscribe it: 256 threads on a 16-CPU share ran
+            # for minutes)
+            aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+            host = int(os.environ.get("OMP_NUM_THREADS") or 0) or aff
+            log(f"cpu baseline, {host} threads")
             cb = cpu_baseline(args.arch, "a photo of a", args.classes, args.cpu_classes or args.classes, host)
-            cb["affinity_cpus"] = host
+            cb["affinity_cpus"] = aff
+            cb["share_note"] = "cores = OMP_NUM_THREADS (the process's CPU share) or the affinity set"
+            log("cpu baseline, 8 threads")
             c8 = cpu_baseline(args.arch, "a photo of a", args.classes, args.cpu_classes or args.classes, 8)
             cb["eight_threads"] = {"value": c8["value"], "cores": 8}
             cb["reference"] = reference_cpu(args.arch, args.classes)

@@ -309,8 +309,8 @@ def run_cocoop_headline(arch, n_cls, batch, ctx_init, n_ctx, chunk=100):
     out = dict(arch=arch, digest=digest, n_cls=n_cls, batch=batch, n_ctx=pl.n_ctx, ctx_init=ctx_init, focal=0,
                chunked=chunk)
     cc.train()
-    imf = cc.image_encoder(img.type(cc.dtype))
-    imf = imf / imf.norm(dim=-1, keepdim=True)
+    imf_raw = cc.image_encoder(img.type(cc.dtype))
+    imf = imf_raw / imf_raw.norm(dim=-1, keepdim=True)
     prompts = cc.prompt_learner(imf)  # (batch, n_cls, n_tkn, dim), graph to ctx / meta_net
     scale = cc.logit_scale.exp()
 
@@ -343,7 +343,7 @@ def run_cocoop_headline(arch, n_cls, batch, ctx_init, n_ctx, chunk=100):
         if k.startswith("meta_net"):
             grads["grad_" + k] = p.grad.detach().clone().numpy()
     sgd_after_step(pl)
-    arrays = dict(ctx0=ctx0, image_features=imf.detach().numpy(), logits=logits.numpy(),
+    arrays = dict(ctx0=ctx0, image_features=imf_raw.detach().numpy(), logits=logits.numpy(),
                   loss=np.asarray(loss.item(), np.float32), ctx_after_step=pl.ctx.detach().numpy(),
                   tokenized=tok.numpy().astype(np.int32), **grads)
     return out, arrays
