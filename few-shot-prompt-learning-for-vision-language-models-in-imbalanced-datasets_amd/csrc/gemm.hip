@@ -141,9 +141,21 @@ __device__ __forceinline__ void split8(u32x4 a0, u32x4 a1, u32x4& hi, u32x4& lo)
 }
 // a . b ~= hi(a) hi(b) + hi(a) lo(b) + lo(a) hi(b) (lo . lo ~ 2^-22 relative is dropped); the
 // weight's parts (packed, clipk_split_pack) are the instruction's A operand (swapped operands)
+// Precision experiment (build-time, A/B only): CLIPK_SPLIT_TERMS 2 drops the
+// lo(a) hi(b) term -- the activation operand rounded to fp16, the weight kept at ~22 bits -- in
+// the GEMMs of epilogue class `CLIPK_SPLIT_TERMS_EPI` (0: every GEMM, 1: the backward's input-grad
+// GEMMs, EPI_NONE / EPI_DMUL / EPI_DQGELU).
+#ifndef CLIPK_SPLIT_TERMS
+#define CLIPK_SPLIT_TERMS 3
+#endif
+#ifndef CLIPK_SPLIT_TERMS_EPI
+#define CLIPK_SPLIT_TERMS_EPI 0
+#endif
+template <bool TWO = false>
 __device__ __forceinline__ f32x4 mma_split(u32x4 bh, u32x4 bl, u32x4 ah, u32x4 al, f32x4 c) {
   c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, bl), __builtin_bit_cast(f16x8, ah), c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, bh), __builtin_bit_cast(f16x8, al), c, 0, 0, 0);
+  if constexpr (!TWO)
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, bh), __builtin_bit_cast(f16x8, al), c, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, bh), __builtin_bit_cast(f16x8, ah), c, 0,
                                                 0, 0);
 }
@@ -187,6 +199,12 @@ template <> struct Raw<32> { uint4 v[2]; };
 // the LayerNorm-pass c_fc; with plain stores 0.04 ms.
 #ifndef CLIPK_GEMM_SPOL_LN
 #define CLIPK_GEMM_SPOL_LN 0
+#endif
+// Store policy of the outputs the NEXT GEMM reads as its A operand: c_fc's QuickGELU(h) (c_proj,
+// forward) and dgelu's dh (fc_dx, backward). c_fc's second output (the saved QuickGELU', read a
+// whole forward + backward later) keeps CLIPK_GEMM_SPOL.
+#ifndef CLIPK_GEMM_SPOL_CHAIN
+#define CLIPK_GEMM_SPOL_CHAIN 2
 #endif
 // CLIPK_GEMM_PP: 192x256 / 256x256 launches with >= 2 K tiles run the ping-pong main loop
 // (1, persistent; 2 = one tile per block, A/B; 0 = the 2-slot loop). Same-box A/B
@@ -343,6 +361,9 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
   // PREC fp32s: 4-byte elements (A fp32, B split-packed), staged as fp32; a 128-B K step is
   // one 32-deep k-window read as two 16-B chunks per fragment (2 fq, 2 fq + 1), 3 MFMAs each
   constexpr bool SPLIT = __is_same(T, f32s);
+  [[maybe_unused]] constexpr bool TWO_TERMS =
+      CLIPK_SPLIT_TERMS == 2 && (CLIPK_SPLIT_TERMS_EPI == 0 || EPI == CLIPK_EPI_NONE || EPI == CLIPK_EPI_DQGELU ||
+                                 EPI == EPI_DMUL);
   static_assert(!SPLIT || (ROWB == 128 && !AG), "split-fp16 GEMM: 128-B staged rows");
   static_assert(!PP || (PERSIST && !AG && DEPTH == 2 && ROWB == 128 && WM == 2 && WN == 4 && BN == 256 &&
                         (sizeof(T) == 2 || SPLIT) && BM % 64 == 0), "ping-pong main loop (K >= 128)");
@@ -639,7 +660,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
           for (int i = 0; i < TM2; ++i)
 #pragma unroll
             for (int j = 0; j < TN2; ++j)
-              acc[h * TM2 + i][q * TN2 + j] = mma_split(fbs[NFB == 2 ? q : 0][0][j], fbs[NFB == 2 ? q : 0][1][j],
+              acc[h * TM2 + i][q * TN2 + j] = mma_split<TWO_TERMS>(fbs[NFB == 2 ? q : 0][0][j], fbs[NFB == 2 ? q : 0][1][j],
                                                         fa[0][i], fa[1][i], acc[h * TM2 + i][q * TN2 + j]);
         } else {
 #pragma unroll
@@ -806,7 +827,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
           split8(*reinterpret_cast<const u32x4*>(As + i * 16 * ROWB + p0),
                  *reinterpret_cast<const u32x4*>(As + i * 16 * ROWB + p1), ah, al);
 #pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mma_split(bh[j], bl[j], ah, al, acc[i][j]);
+          for (int j = 0; j < TN; ++j) acc[i][j] = mma_split<TWO_TERMS>(bh[j], bl[j], ah, al, acc[i][j]);
         }
       } else
 #pragma unroll
@@ -960,7 +981,8 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] *= dq[c];
         }
-        buf_store16<TO, LN_OUT ? CLIPK_GEMM_SPOL_LN : CLIPK_GEMM_SPOL>(ro, off, v);
+        constexpr bool CHAIN = epi_qgelu(EPI) || EPI == CLIPK_EPI_DQGELU || EPI == EPI_DMUL;
+        buf_store16<TO, LN_OUT ? CLIPK_GEMM_SPOL_LN : (CHAIN ? CLIPK_GEMM_SPOL_CHAIN : CLIPK_GEMM_SPOL)>(ro, off, v);
       }
       if (i + XD < TM) load_ext(i + XD, extq[i % XD]);  // this group's slot is free again
       if (i + 2 < TM) load_ln(i + 2, i & 1);

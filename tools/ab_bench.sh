@@ -19,7 +19,7 @@ for round in 1 2; do
     tail -1 $f | python3 -c "
 import json,sys
 d=json.loads(sys.stdin.read()); k=d['kernels']
-print('$t', $round, 'ms', d['ms_per_step'], 'eval', round(d['eval_images_per_sec']), ' '.join(f'{n}={v[\"ms_per_step\"]:.3f}' for n,v in k.items()))
+print('$t', $round, 'ms', d['ms_per_step'], 'eval', round(d['eval_images_per_sec']), ' '.join(f'{n}={v[1]:.3f}' for n,v in k.items()))
 " | tee -a gpurun_out/ab.log
   done
 done

@@ -58,7 +58,11 @@ constexpr int GPS = SLOT / 1024;                         // LDS-DMA instructions
 constexpr int LPW = GPS / 4;                             // per loader wave: 7 (A: 3, B: 4)
 static_assert(GPS % 4 == 0 && OPA / 1024 == 12 && (BN * ROWB) / 1024 == 16, "slot split");
 
-template <int NS, int MODE, int WARM>
+// ABLK: A in the K-blocked layout [M / BM][K / 32][BM][32] (each ring slot's A part one contiguous
+// 12 KB, each LDS-DMA instruction 1 KB contiguous) instead of row-major [M][K] (8 or 16 rows of
+// 64-128 B per instruction, rows K * 2 bytes apart): whether the load path is limited by the
+// scattered row pieces rather than by bytes.
+template <int NS, int MODE, int WARM, bool ABLK = false>
 __global__ __launch_bounds__(512, 1) void ring(const f16* __restrict__ A, const f16* __restrict__ B, f16* C, int M,
                                                int N, int K) {
   constexpr int D = NS - 1;
@@ -94,7 +98,7 @@ __global__ __launch_bounds__(512, 1) void ring(const f16* __restrict__ A, const 
       const int row = (isa[i] ? u : u - 12) * 16 + lane / 4;
       urow[i] = row;
       const int c = (lane % 4) ^ swz(row);
-      poff[i] = row * K * 2 + c * 16;
+      poff[i] = (ABLK && isa[i] ? row * ROWB : row * K * 2) + c * 16;
     }
     auto issue = [&](int g) {
       if (g >= nsteps) return;
@@ -107,9 +111,11 @@ __global__ __launch_bounds__(512, 1) void ring(const f16* __restrict__ A, const 
 #pragma unroll
       for (int i = 0; i < LPW; ++i) {
         const int u = lw * LPW + i;
+        // blocked A: the panel's K step kt is the contiguous BM x 64 B block kt
+        const int soff = (ABLK && isa[i]) ? kt * BM * ROWB : kt * ROWB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(isa[i] ? ra : rb,
                                                  (__attribute__((address_space(3))) void*)(base + u * 1024), 16,
-                                                 poff[i], kt * ROWB, 0, 0);
+                                                 poff[i], soff, 0, 0);
       }
       (void)urow;
     };
@@ -226,10 +232,11 @@ __global__ __launch_bounds__(512, 1) void ring(const f16* __restrict__ A, const 
   }
 }
 
-template <int NS, int MODE, int WARM>
+template <int NS, int MODE, int WARM, bool ABLK = false>
 static int launch(const void* A, const void* B, void* C, int M, int N, int K, int grid, hipStream_t st) {
   if (N % BN || (K * 2) % (2 * ROWB)) return -2;  // an even number of 32-deep K steps
-  hipLaunchKernelGGL((ring<NS, MODE, WARM>), dim3(grid), dim3(512), 0, st, (const f16*)A, (const f16*)B, (f16*)C, M, N,
+  if (ABLK && M % BM) return -4;
+  hipLaunchKernelGGL((ring<NS, MODE, WARM, ABLK>), dim3(grid), dim3(512), 0, st, (const f16*)A, (const f16*)B, (f16*)C, M, N,
                      K);
   return (int)hipGetLastError();
 }
@@ -251,5 +258,10 @@ extern "C" int ring_gemm(int ns, int warm, int mode, const void* A, const void* 
   V(5, 8)
   V(4, 8)
 #undef V
+  if (ns == 5 && warm == 100) {  // blocked A (the caller passes A in the [M/192][K/32][192][32] layout)
+    if (mode == 0) return launch<5, 0, 0, true>(A, B, C, M, N, K, grid, st);
+    if (mode == 1) return launch<5, 1, 0, true>(A, B, C, M, N, K, grid, st);
+    if (mode == 2) return launch<5, 2, 0, true>(A, B, C, M, N, K, grid, st);
+  }
   return -1;
 }

@@ -34,7 +34,7 @@ def timeit(fn, iters=12, warm=3, rounds=3):
 def main():
     nss = [tuple(int(x) for x in v.split("w")) for v in (sys.argv[1] if len(sys.argv) > 1 else "4w0,5w0").split(",")]
     modes = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "0,1,2").split(",")]
-    M = int(os.environ.get("RING_M", 47160))
+    M = int(os.environ.get("RING_M", 47232))  # 246 x 192 (the blocked-A variant needs M % 192 == 0)
     grid = int(os.environ.get("RING_GRID", 256))
     lib = ctypes.CDLL(os.path.join(HERE, "libringlab.so"))
     lib.ring_gemm.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_int] * 4 + \
@@ -49,6 +49,9 @@ def main():
         C = torch.empty(M, n, device=dev, dtype=torch.float16)
         fl = 2.0 * M * n * k
         ref = (As[0].float() @ B.float().t())
+        # blocked copies of A for the ABLK variant (ns 5, warm 100): [M/192][K/32][192][32]
+        Ab = [a.view(M // 192, 192, k // 32, 32).permute(0, 2, 1, 3).contiguous() if any(w == 100 for _, w in nss)
+              else None for a in As]
         ms = timeit(lambda i: ops.gemm(As[i % nbuf], B, N.EPI_NONE, torch.float16, out=C))
         print(f"N{n} K{k}: ours(prod auto) {ms*1e3:7.1f} us {fl/ms/1e9:7.1f} TF/s", flush=True)
         ms = timeit(lambda i: torch.matmul(As[i % nbuf], B.t(), out=C))
@@ -56,7 +59,8 @@ def main():
         for ns, wm in nss:
             for md in modes:
                 C.zero_()
-                rc = lib.ring_gemm(ns, wm, md, As[0].data_ptr(), B.data_ptr(), C.data_ptr(), M, n, k, grid, st())
+                AA = Ab if wm == 100 else As
+                rc = lib.ring_gemm(ns, wm, md, AA[0].data_ptr(), B.data_ptr(), C.data_ptr(), M, n, k, grid, st())
                 if rc:
                     print(f"  ring ns{ns}w{wm} mode {md}: rc {rc}")
                     continue
@@ -65,10 +69,10 @@ def main():
                     torch.cuda.synchronize()
                     e = ((C.float() - ref).abs().max() / ref.abs().max()).item()
                     err = f" relerr {e:.1e}" + ("  <-- WRONG" if e > 1e-2 else "")
-                ms = timeit(lambda i: lib.ring_gemm(ns, wm, md, As[i % nbuf].data_ptr(), B.data_ptr(), C.data_ptr(), M,
+                ms = timeit(lambda i: lib.ring_gemm(ns, wm, md, AA[i % nbuf].data_ptr(), B.data_ptr(), C.data_ptr(), M,
                                                     n, k, grid, st()))
                 print(f"  ring ns{ns}w{wm} {MODES[md]:17s} {ms*1e3:7.1f} us {fl/ms/1e9:7.1f} TF/s{err}", flush=True)
-        del As, B, C, ref
+        del As, Ab, B, C, ref
         torch.cuda.empty_cache()
 
 
