@@ -576,8 +576,11 @@ def main():
             cls = args.classes // n
             log(f"batch1 class-shard proxy n{n}")
             trp, dmp = build_trainer(argparse.Namespace(**{**vars(args), "classes": cls}), args.prec, 1, dev, rank)
-            tp, _ = time_train(trp, dmp, B1_STEPS, 5)
-            proxy[f"n{n}"] = {"classes": cls, "ms_per_step": round(1000 * tp / B1_STEPS, 3)}
+            # two timed rounds, the faster reported (one round of r05f read 2.31 ms at 125 classes,
+            # 1.69 ms when run alone, profiles/r05k/)
+            rounds = [time_train(trp, dmp, B1_STEPS, 5)[0] for _ in range(2)]
+            proxy[f"n{n}"] = {"classes": cls, "ms_per_step": round(1000 * min(rounds) / B1_STEPS, 3),
+                              "rounds_ms": [round(1000 * t / B1_STEPS, 3) for t in rounds]}
             del trp, dmp
             torch.cuda.empty_cache()
         out["batch1_class_shard_proxy"] = proxy

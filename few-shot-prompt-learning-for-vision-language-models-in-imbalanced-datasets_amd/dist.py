@@ -71,22 +71,43 @@ def _all_reduce(t, op=td.ReduceOp.SUM):
     return t
 
 
+def _grad_bucket(ps):
+    """The persistent flat buffer of a fixed parameter list and one view of it per parameter,
+    kept on the first parameter (its lifetime) and rebuilt when the list or a shape changes."""
+    sig = tuple((id(p), tuple(p.shape)) for p in ps) + (ps[0].grad.dtype, ps[0].grad.device)
+    b = getattr(ps[0], "_clipk_grad_bucket", None)
+    if b is None or b[0] != sig:
+        flat = torch.empty(sum(p.numel() for p in ps), dtype=ps[0].grad.dtype, device=ps[0].grad.device)
+        views, off = [], 0
+        for p in ps:
+            views.append(flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+        b = (sig, flat, views)
+        ps[0]._clipk_grad_bucket = b
+    return b[1], b[2]
+
+
 def allreduce_grads(params, average: bool = True):
-    """Sum (mean) the gradients of ``params`` across ranks in ONE fused bucket."""
+    """Sum (mean) the gradients of ``params`` across ranks in ONE fused bucket: the gradients are
+    copied into a persistent flat buffer (one multi-tensor copy, or none when they already are its
+    views), reduced in place, and each ``p.grad`` is rebound to its view of the result (no
+    per-step concatenation, no copy back)."""
     if not is_dist():
         return
-    grads = [p.grad for p in params if p.grad is not None]
-    if not grads:
+    ps = [p for p in params if p.grad is not None]
+    if not ps:
         return
-    flat = torch.cat([g.reshape(-1) for g in grads])
+    if len({(p.grad.dtype, p.grad.device) for p in ps}) != 1:
+        raise ValueError("allreduce_grads: the gradients of one bucket must share dtype and device")
+    flat, views = _grad_bucket(ps)
+    todo = [(v, p.grad) for p, v in zip(ps, views) if p.grad.data_ptr() != v.data_ptr()]
+    if todo:
+        torch._foreach_copy_([v for v, _ in todo], [g for _, g in todo])
     _all_reduce(flat)
-    if average:
+    if average and world_size() > 1:
         flat.div_(world_size())
-    off = 0
-    for g in grads:
-        n = g.numel()
-        g.copy_(flat[off:off + n].view_as(g))
-        off += n
+    for p, v in zip(ps, views):
+        p.grad = v
 
 
 def broadcast_params(params, src: int = 0):

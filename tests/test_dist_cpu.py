@@ -74,6 +74,32 @@ def test_collectives_gloo_ws2():
     assert out[0]["shard"] == (0, 5) and out[1]["shard"] == (5, 10)
 
 
+def _bucket_steps(rank, world):
+    """Three steps through one persistent gradient bucket: fresh grads (zero_grad to None), then
+    grads accumulated in place into the bucket's views (zero_grad(set_to_none=False))."""
+    from fsp_amd import dist
+    p1 = torch.nn.Parameter(torch.zeros(3, 4))
+    p2 = torch.nn.Parameter(torch.zeros(5))
+    opt = torch.optim.SGD([p1, p2], lr=0.1)
+    out = []
+    for step, none in enumerate((True, True, False)):
+        opt.zero_grad(set_to_none=none)
+        ((p1 * (rank + 1 + step)).sum() + (p2 * torch.arange(5.0) * (rank + 1)).sum()).backward()
+        dist.allreduce_grads([p1, p2])
+        out.append((p1.grad.clone().numpy(), p2.grad.clone().numpy(),
+                    p1.grad.data_ptr() == p1._clipk_grad_bucket[1].data_ptr()))
+    return out
+
+
+def test_grad_bucket_persists_across_steps():
+    out = _run(_bucket_steps)
+    for r in (0, 1):
+        for step, (g1, g2, rebound) in enumerate(out[r]):
+            np.testing.assert_allclose(g1, np.full((3, 4), 1.5 + step))  # mean of rank+1+step
+            np.testing.assert_allclose(g2, np.arange(5) * 1.5)
+            assert rebound
+
+
 def _cocoop_dp(rank, world):
     """Per-rank CoCoOp grads on its half of the batch (oracle math), then dist.allreduce."""
     from oracle import clip_oracle as O
