@@ -109,8 +109,8 @@ HBM_PEAK_GBS = 8000.0  # HBM3E, MI355X_MICROARCH.md
 # 3.32 ms in one round-4 run against 2.70 over 50 steps of tools/b1_time.py on the same build)
 B1_STEPS = 50
 # the latest round's PMC passes (tools/pmc_bench.sh), else the previous round's
-PMC_FILE = next((f for f in (os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r04_pmc", "r03_pmc"))
-                 if os.path.exists(f)), os.path.join(ROOT, "profiles", "r04_pmc", "traffic.json"))
+PMC_FILE = next((f for f in (os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r05_pmc", "r04_pmc", "r03_pmc"))
+                 if os.path.exists(f)), os.path.join(ROOT, "profiles", "r05_pmc", "traffic.json"))
 
 # kernel classes of the step: launch sites that run the same kernel instantiation (rocprofv3
 # kernel-name key, for the PMC traffic lookup) -- the text GEMMs by role, attention, LN. Each

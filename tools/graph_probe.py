@@ -4,7 +4,7 @@ Warm-up steps run eagerly, one forward_backward is captured (static batch), then
 graph steps are timed in the same process (interleaved). Diagnostic only: the graph bakes the
 step's host-side scalars (the SGD learning rate) into its kernel arguments.
 
-    python tools/graph_probe.py [--batch 8]
+    python tools/graph_probe.py [--batch 8] [--classes 1000]
 """
 import argparse
 import os
@@ -18,12 +18,13 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--classes", type=int, default=1000)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--no-graph", action="store_true", help="eager only: same batch vs alternating batches")
     a = ap.parse_args()
     import torch
     import bench
-    args = argparse.Namespace(arch="ViT-B/16", classes=1000)
+    args = argparse.Namespace(arch="ViT-B/16", classes=a.classes)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     trainer, dm = bench.build_trainer(args, "fp16", a.batch, dev, 0)
