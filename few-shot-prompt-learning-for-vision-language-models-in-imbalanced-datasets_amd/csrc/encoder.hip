@@ -491,16 +491,28 @@ static int ln_merge(int rows, int W, const float* lnst, float* m, float* r, floa
   ProfScope ps(CLIPK_PROF_NONE, st, 0.0, text ? "text.ln_stats" : "vit.ln_stats", (double)rows * (W / 64) * 8 + 16.0 * rows);
   return clipk_ln_stats_merge(rows, W, lnst, m, r, rnb, st);
 }
+// the merge + fold pair as one clipk_gemm_ln_merge launch where the library runs it in-kernel
+// (16-bit, the batch-1 text shapes), else the two launches under their own profiling sites
+static int gemm_ln_merged(int act, int epi, int M, int N, int K, const void* A, const void* B, const float* bias,
+                          void* o, void* o2, const float* lnst, const float* colsum, float* m, float* r,
+                          float* rnb, hipStream_t st, int prof_cls, const char* site, bool text) {
+  if (t_split || act == CLIPK_F32 || !clipk_gemm_ln_merge_fused(act, M, N, K)) {
+    TRY(ln_merge(M, K, lnst, m, r, rnb, st, text));
+    return gemm_ln(act, epi, M, N, K, A, B, bias, nullptr, o, o2, nullptr, colsum, rnb, st, prof_cls, site);
+  }
+  const double b = gemm_bytes(act, act, epi, M, N, K, o2 != nullptr, act) + (double)M * (K / 64) * 8 + 16.0 * M;
+  ProfScope ps(prof_cls, st, 2.0 * M * N * K, site, b);
+  return clipk_gemm_ln_merge(act, epi, M, N, K, A, K, B, K, bias, o, N, o2, lnst, colsum, m, r, rnb, st);
+}
 // attention half: ln_1 statistics of X merged from the partials the previous layer's c_proj
 // epilogue wrote (lnst); the qkv projection reads X itself through the fold
 static int block_attn_fold(const clipk_encoder* e, const std::array<const void*, 6>& f, const SeqShape& sh,
                            const void* X, void* qkv, void* o, float* lse, float* m1, float* r1, const float* lnst,
                            float* rnb, hipStream_t st, bool text) {
   const int W = e->W, rows = sh.rows, act = e->act;
-  TRY(ln_merge(rows, W, lnst, m1, r1, rnb, st, text));
-  TRY(gemm_ln(act, CLIPK_EPI_BIAS, rows, 3 * W, W, X, f[0], (const float*)f[2], nullptr, qkv, nullptr,
-              nullptr, (const float*)f[1], rnb, st, text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE,
-              text ? "text.qkv_fwd" : "vit.qkv_fwd"));
+  TRY(gemm_ln_merged(act, CLIPK_EPI_BIAS, rows, 3 * W, W, X, f[0], (const float*)f[2], qkv, nullptr, lnst,
+                     (const float*)f[1], m1, r1, rnb, st, text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE,
+                     text ? "text.qkv_fwd" : "vit.qkv_fwd", text));
   const double ab = (double)rows * 4 * W * esize(act) + (lse ? 4.0 * rows * e->heads : 0.0);
   ProfScope ps(text ? CLIPK_PROF_ATTN : CLIPK_PROF_NONE, st, 0.0, text ? "text.attn_fwd" : "vit.attn_fwd", ab);
   return attn_fwd(e, sh, qkv, o, lse, st);
@@ -515,11 +527,9 @@ static int block_post_fold(const clipk_encoder* e, const std::array<const void*,
   const int pg = text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE;
   TRY(gemm_ln(act, CLIPK_EPI_BIAS_RES, rows, W, W, o, w[4], (const float*)w[5], X, Xm, nullptr, lnst, nullptr,
               nullptr, st, pg, text ? "text.out_fwd" : "vit.out_fwd"));
-  TRY(ln_merge(rows, W, lnst, m2, r2, rnb, st, text));
-  TRY(gemm_ln(act, CLIPK_EPI_BIAS_QGELU | (h && qgelu_deriv_on() ? CLIPK_QGELU_DERIV : 0), rows, 4 * W, W, Xm, f[3], (const float*)f[5],
-              nullptr, g, h, nullptr,
-              (const float*)f[4], rnb, st, text ? CLIPK_PROF_GEMM_FC : CLIPK_PROF_NONE,
-              text ? "text.fc_fwd" : "vit.fc_fwd"));
+  TRY(gemm_ln_merged(act, CLIPK_EPI_BIAS_QGELU | (h && qgelu_deriv_on() ? CLIPK_QGELU_DERIV : 0), rows, 4 * W, W, Xm,
+                     f[3], (const float*)f[5], g, h, lnst, (const float*)f[4], m2, r2, rnb, st,
+                     text ? CLIPK_PROF_GEMM_FC : CLIPK_PROF_NONE, text ? "text.fc_fwd" : "vit.fc_fwd", text));
   if (stats_next)
     return gemm_ln(act, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo, nullptr, lnst,
                    nullptr, nullptr, st, pg, text ? "text.proj_fwd" : "vit.proj_fwd");

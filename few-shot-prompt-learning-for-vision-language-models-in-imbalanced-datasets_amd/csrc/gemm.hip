@@ -57,6 +57,9 @@ struct GemmArgs {
   float* lnstats;
   const float* colsum;
   const f32x2* lnrnb;
+  // LNM 3 (clipk_gemm_ln_merge): the fold reads the producer's partials (lnstats) and merges each
+  // row's itself, exactly as clipk_ln_stats_merge; the column-0 tiles write mean / rstd / rnb
+  float* lnmean; float* lnrstd; f32x2* lnrnb_out;
 };
 
 // Sum over the aligned 8-lane group (DPP: quad xor 1, quad xor 2, half-row mirror i <-> 7 - i).
@@ -351,7 +354,8 @@ __device__ __forceinline__ void skew_start(int us, int bid) {
 // the other's LDS reads. A region is restaged (for K tile t+2, or t+1 for B0) one phase after
 // its last read; the K tile t+1 wait is a counted vmcnt at phase 4 of tile t that leaves the
 // three regions already issued for t+2 in flight -- the ring never drains in the loop.
-// LNM (clipk_gemm_ln): 1 = per-row LayerNorm statistics of the output, 2 = LayerNorm of A
+// LNM (clipk_gemm_ln): 1 = per-row LayerNorm statistics of the output, 2 = LayerNorm of A,
+// 3 = LNM 2 with the statistics merge of clipk_ln_stats_merge inside (clipk_gemm_ln_merge)
 // folded into the epilogue (see GemmArgs).
 template <typename T, typename TO, typename TX, int EPI, int BM, int BN, int WM, int WN, bool PERSIST,
           int ROWB = GEMM_ROWB, int DEPTH = 2, bool AG = false, bool PP = false, int LNM = 0>
@@ -559,13 +563,18 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
     // LN fold: mean / rstd of the lane's rows, two 16-row groups ahead of their use. (Merging the
     // producer's partials here instead of in clipk_ln_stats_merge -- 2 loads + 2 8-lane sums per
     // row -- measured slower: qkv 86 -> 110 us, c_fc 129 -> 158 us per launch.)
-    constexpr bool LN_IN = LNM == 2, LN_OUT = LNM == 1;
+    constexpr bool LN_IN = LNM == 2 || LNM == 3, LN_OUT = LNM == 1, LN_MERGE = LNM == 3;
+    // LN_MERGE: 16-bit out (8 lanes per row = the 8 partials of W = 512: lane ec merges partial
+    // ec, the merge kernel's lane map and DPP order, so the same bits) on the 192-row ping-pong
+    // tiles, whose free residual ring holds the tile's partials (loaded at the tile's start)
+    static_assert(!LN_MERGE || (PP && BM == 192 && sizeof(TO) == 2), "in-kernel LN statistics merge");
     // (16-bit out: 8 lanes per row of 64 columns; PREC fp32s, fp32 out: 16)
     static_assert(!LN_OUT || (EPI == CLIPK_EPI_BIAS_RES && (sizeof(TO) == 2 || SPLIT)), "LN statistics");
     static_assert(!LN_IN || ((EPI == CLIPK_EPI_BIAS || epi_qgelu(EPI)) && (sizeof(T) == 2 || SPLIT)), "LN fold");
     [[maybe_unused]] f32x2 lnp[LN_IN ? 2 : 1][NQ];
+    [[maybe_unused]] f32x2 lnpart[LN_MERGE ? TM : 1][NQ];
     auto load_ln = [&](int i, int slot) {
-      if constexpr (LN_IN) {
+      if constexpr (LN_IN && !LN_MERGE) {
         const int mg = m0 + wm * (BM / WM) + i * 16;
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
@@ -692,6 +701,16 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       // during this tile's last phases and epilogue (nk >= 2).
       const bool lag = wm == 1;
       const TRes cra = rsrc_a(m0), crb = rsrc_b(n0);
+      if constexpr (LN_MERGE) {  // this tile's rows' partials, in flight through the K loop
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) {
+            int mc = m0 + wm * (BM / WM) + i * 16 + RPQ * q + er;
+            mc = mc < g.M ? mc : g.M - 1;
+            lnpart[i][q] = reinterpret_cast<const f32x2*>(g.lnstats)[(size_t)mc * LPR + ec];
+          }
+      }
       // PP2: K tile t+1 landed; the A0 + B0 regions just issued for t+2 stay in flight
       auto wait_ahead2 = [&]() {
         if (two_a) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -923,7 +942,21 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] *= kSplitAlpha;  // exact (power of 2)
         }
-        if constexpr (LN_IN) {
+        if constexpr (LN_MERGE) {
+          // clipk_ln_stats_merge's arithmetic on the row's 8 partials (ln_stats_merge_kernel)
+          const f32x2 pp = lnpart[i][q];
+          const float mu = sum8(pp[0]) * (1.0f / 512.0f);
+          const float d = pp[0] * (1.0f / 64.0f) - mu;
+          const float rs = rsqrtf(sum8(fmaf(64.0f * d, d, pp[1])) * (1.0f / 512.0f) + 1e-5f);
+          const float nb = -rs * mu;
+          if (n0 == 0 && ec == 0 && m < g.M) {
+            if (g.lnmean) g.lnmean[m] = mu;
+            if (g.lnrstd) g.lnrstd[m] = rs;
+            g.lnrnb_out[m] = (f32x2){rs, nb};
+          }
+#pragma unroll
+          for (int c = 0; c < CW; ++c) v[c] = fmaf(rs, v[c], fmaf(nb, csum[c], bia[c]));
+        } else if constexpr (LN_IN) {
           const float rs = lnp[i & 1][q][0], nb = lnp[i & 1][q][1];
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] = fmaf(rs, v[c], fmaf(nb, csum[c], bia[c]));
@@ -1478,6 +1511,71 @@ extern "C" int clipk_gemm_ln(int in_dtype, int epi, int M, int N, int K, const v
   if (deriv) epi = EPI_QGELU_D;
   if (in_dtype == CLIPK_F32S) return dispatch_ln_split(epi, g, st);
   return in_dtype == CLIPK_F16 ? dispatch_ln<f16>(epi, g, st) : dispatch_ln<bf16>(epi, g, st);
+}
+
+namespace clipk {
+// clipk_gemm_ln_merge's in-kernel form: 16-bit, W = K = 512 (8 partials per row), the shape on the
+// 192-row ping-pong tiles (the batch-1 text encoder's qkv / c_fc at 5.9k rows). Knob
+// CLIPK_LN_MERGE_FUSED=0 (A/B): always the merge launch + clipk_gemm_ln.
+static bool ln_merge_fused_ok(int in_dtype, int M, int N, int K) {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("CLIPK_LN_MERGE_FUSED");
+    on = e ? atoi(e) : 1;
+  }
+  return on && CLIPK_GEMM_PP && (in_dtype == CLIPK_F16 || in_dtype == CLIPK_BF16) && K == 512 && N % 256 == 0 &&
+         pick_cfg(M, N, 2) == 6;
+}
+template <typename T, int EPI>
+static int launch_ln_merge(GemmArgs g, hipStream_t st) {
+  g.stamp = gemm_stamp_buf();
+  if (g_skew < 0) {
+    const char* e = getenv("CLIPK_GEMM_SKEW");
+    g_skew = e ? atoi(e) : 0;
+  }
+  g.skew = g_skew;
+  const int nwg = ((g.M + 191) / 192) * (g.N / 256);
+  hipLaunchKernelGGL((gemm_nt_kernel<T, T, float, EPI, 192, 256, 2, 4, true, GEMM_ROWB, 2, false, true, 3>),
+                     dim3(pp_grid(nwg, num_cus())), dim3(512), 0, st, g);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+template <typename T>
+static int dispatch_ln_merge(int epi, const GemmArgs& g, hipStream_t st) {
+  if (epi == CLIPK_EPI_BIAS) return launch_ln_merge<T, CLIPK_EPI_BIAS>(g, st);
+  if (epi == EPI_QGELU_D) return launch_ln_merge<T, EPI_QGELU_D>(g, st);
+  return launch_ln_merge<T, CLIPK_EPI_BIAS_QGELU>(g, st);
+}
+}  // namespace clipk
+
+extern "C" int clipk_gemm_ln_merge_fused(int in_dtype, int M, int N, int K) {
+  return ln_merge_fused_ok(in_dtype, M, N, K) ? 1 : 0;
+}
+
+// LayerNorm fold with the statistics merge (include/clipk.h): what clipk_ln_stats_merge +
+// clipk_gemm_ln compute, in one launch where the shape allows (ln_merge_fused_ok), else those two.
+extern "C" int clipk_gemm_ln_merge(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B,
+                                   int ldb, const float* bias, void* out, int ldo, void* out2, const float* stats,
+                                   const float* colsum, float* mean, float* rstd, float* rnb, void* stream) {
+  if (!stats || !colsum || !rnb) return CLIPK_EINVAL;
+  const int e0 = epi & ~CLIPK_QGELU_DERIV;
+  if (!ln_merge_fused_ok(in_dtype, M, N, K) || lda < K || ldb < K || lda % 8 || ldb % 8 || ldo < N || ldo % 8 ||
+      !A || !B || !out || !bias || (e0 != CLIPK_EPI_BIAS && e0 != CLIPK_EPI_BIAS_QGELU) ||
+      ((epi & CLIPK_QGELU_DERIV) && e0 != CLIPK_EPI_BIAS_QGELU)) {
+    // the two-launch form (it also reports every argument error)
+    if (M > 0) {
+      const int rc = clipk_ln_stats_merge(M, K, stats, mean, rstd, rnb, stream);
+      if (rc != CLIPK_OK) return rc;
+    }
+    return clipk_gemm_ln(in_dtype, epi, M, N, K, A, lda, B, ldb, bias, nullptr, 0, out, ldo, out2, nullptr, colsum, rnb,
+                         stream);
+  }
+  GemmArgs g{(const char*)A, (const char*)B, M, N, K, lda, ldb, bias, nullptr, 0, out, ldo, out2, nullptr,
+             0, nullptr, 1, 0, 0, const_cast<float*>(stats), colsum, nullptr, mean, rstd,
+             reinterpret_cast<f32x2*>(rnb)};
+  hipStream_t st = (hipStream_t)stream;
+  const int ee = (epi & CLIPK_QGELU_DERIV) ? EPI_QGELU_D : e0;
+  return in_dtype == CLIPK_F16 ? dispatch_ln_merge<f16>(ee, g, st) : dispatch_ln_merge<bf16>(ee, g, st);
 }
 
 namespace clipk {

@@ -100,6 +100,27 @@ def gemm_ln(a, b, epi, bias, stats=None, res=None, colsum=None, rnb=None, want_o
     return (out, out2) if want_out2 else out
 
 
+def gemm_ln_merge(a, b, epi, bias, stats, colsum, want_out2=False):
+    """clipk_gemm_ln_merge: ln_stats_merge(stats, K) then the fold gemm_ln(a, b, epi, bias,
+    colsum=colsum, rnb=...), as one launch where the library covers the shape. Returns
+    (out[, out2], mean, rstd, rnb); 16-bit a."""
+    _need(a, "A")
+    _need(b, "B", a.dtype)
+    _need(stats, "stats", torch.float32)
+    _need(colsum, "colsum", torch.float32)
+    _need(bias, "bias", torch.float32)
+    M, K = a.shape
+    Nn = b.shape[0]
+    out = torch.empty(M, Nn, device=a.device, dtype=a.dtype)
+    out2 = torch.empty_like(out) if want_out2 else None
+    mean = torch.empty(M, device=a.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    rnb = torch.empty(M, 2, device=a.device, dtype=torch.float32)
+    N.call("clipk_gemm_ln_merge", DT[a.dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias), _p(out), Nn, _p(out2),
+           _p(stats), _p(colsum), _p(mean), _p(rstd), _p(rnb), _stream())
+    return ((out, out2) if want_out2 else (out,)) + (mean, rstd, rnb)
+
+
 def ln_stats_merge(stats, width):
     """clipk_ln_stats_merge: [M, width/64, 2] partials -> (mean, rstd, rnb): fp32 [M], [M], [M, 2]
     with rnb = (rstd, -rstd * mean)."""

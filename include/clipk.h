@@ -139,6 +139,17 @@ int clipk_gemm_ln(int in_dtype, int epi, int M, int N, int K, const void* A, int
                   float* stats, const float* colsum, const float* rnb, void* stream);
 int clipk_ln_stats_merge(int rows, int width, const float* stats, float* mean, float* rstd, float* rnb,
                          void* stream);
+/* clipk_ln_stats_merge(M, K, stats, mean, rstd, rnb) followed by the fold clipk_gemm_ln(...,
+ * colsum, rnb) (res NULL), as ONE launch where the library covers the shape in-kernel (16-bit,
+ * K = 512, the 192-row tile configuration: the batch-1 text encoder's LN-fold GEMMs), else as
+ * those two calls. Outputs are bitwise those of the two calls: out / out2, mean and rstd
+ * (optional) and rnb (required). Replaces the merge launch between a producer and its fold
+ * (PromptSRC/clip/model.py:153-159, 185-188: ln_1 / ln_2 of each residual block). */
+int clipk_gemm_ln_merge(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B,
+                        int ldb, const float* bias, void* out, int ldo, void* out2, const float* stats,
+                        const float* colsum, float* mean, float* rstd, float* rnb, void* stream);
+/* 1 when clipk_gemm_ln_merge runs the shape as one launch, 0 when as the two calls. */
+int clipk_gemm_ln_merge_fused(int in_dtype, int M, int N, int K);
 /* Benchmark knob: force the 16-bit GEMM tile configuration (0: 128x128, 1: 256x256
  * (persistent above 2 x CUs tiles), 2: 256x128, 3: 256x256 non-persistent, 6: 192x256;
  * -1 = automatic by shape; other values: CLIPK_EINVAL). Not needed for normal use. */

@@ -122,6 +122,37 @@ def test_gemm_ln_fold(dev, dtype, epi, Mr, Wd, Nn):
         assert _rel(d, sg * (1 + 1.702 * ref * (1 - sg))) <= TOL[dtype]
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("epi", [N.EPI_BIAS, N.EPI_BIAS_QGELU, N.EPI_BIAS_QGELU | N.QGELU_DERIV])
+@pytest.mark.parametrize("Mr,Nn,fused", [(5895, 1536, True), (5895, 2048, True), (5000, 2048, True),
+                                         (47160, 1536, False), (3000, 2048, False), (1, 1536, False)])
+def test_gemm_ln_merge_equals_two_launches(dev, dtype, epi, Mr, Nn, fused):
+    """clipk_gemm_ln_merge (the statistics merge inside the folding GEMM: the batch-1 text shapes,
+    5.9k rows on 192-row tiles) against clipk_ln_stats_merge + clipk_gemm_ln: every output
+    bitwise equal (out, out2, mean, rstd, rnb), ragged last row block included; the shapes the
+    library does not fuse take the two launches themselves."""
+    Wd = 512
+    assert N.load().clipk_gemm_ln_merge_fused(N.F16 if dtype == torch.float16 else N.BF16, Mr, Nn, Wd) == int(fused)
+    g = torch.Generator(device="cpu").manual_seed(Mr + Nn + epi)
+    x = torch.randn(Mr, Wd, generator=g) + 2.0 * torch.randn(Mr, 1, generator=g)
+    x[:, 5] *= 30.0
+    x = x.to(dev, dtype)
+    gamma = (1.0 + 0.2 * torch.randn(Wd, generator=g)).to(dev)
+    beta = (0.1 * torch.randn(Wd, generator=g)).to(dev)
+    w = (torch.randn(Nn, Wd, generator=g) / math.sqrt(Wd)).to(dev)
+    bias = (0.05 * torch.randn(Nn, generator=g)).to(dev)
+    wp, s, c = M.ln_fold_weights(w, bias, gamma, beta, dtype, dev)
+    st = partials(x)
+    two = epi != N.EPI_BIAS
+    mean, rstd, rnb = ops.ln_stats_merge(st, Wd)
+    ref = ops.gemm_ln(x, wp, epi, c, colsum=s, rnb=rnb, want_out2=two)
+    ref = ref if two else (ref,)
+    got = ops.gemm_ln_merge(x, wp, epi, c, st, s, want_out2=two)
+    for nm, u, v in zip(("out", "out2", "mean", "rstd", "rnb") if two else ("out", "mean", "rstd", "rnb"),
+                        got, tuple(ref) + (mean, rstd, rnb)):
+        assert torch.equal(u, v), f"{nm} differs from the two-launch form"
+
+
 @pytest.mark.parametrize("Mr,Nn,K", [(47160, 512, 2048), (8000, 512, 512), (300, 512, 2048), (1, 512, 512)])
 def test_gemm_ln_stats_split(dev, Mr, Nn, K):
     """PREC fp32s statistics producer (fp32 out, 16 lanes per 64-column group): the stored output
