@@ -194,7 +194,9 @@ def reduce_scatter_rows(g, counts):
     padded blocks all-reduced on the host, then this rank's block."""
     r = rank()
     m = max(counts)
-    padded = pad_rank_blocks(g, counts)
+    if g.shape[0] != sum(counts):
+        raise ValueError(f"{g.shape[0]} rows for shard counts {counts}")
+    padded = g.contiguous() if min(counts) == m else pad_rank_blocks(g, counts)
     if td.get_backend() == "nccl":
         out = torch.empty((m,) + tuple(g.shape[1:]), dtype=g.dtype, device=g.device)
         td.reduce_scatter_tensor(out, padded, op=td.ReduceOp.SUM)
@@ -205,9 +207,20 @@ def reduce_scatter_rows(g, counts):
 
 def all_gather_rows(x, counts):
     """Every rank's row block [counts[r], ...] -> [sum(counts), ...] on every rank (rank
-    order), through equal-size padded blocks (all_gather_into_tensor on RCCL)."""
+    order), through equal-size padded blocks (all_gather_into_tensor on RCCL); equal shards
+    (C divisible by the world size) skip the padding and unpadding copies."""
     w, m = len(counts), max(counts)
     xc = x.contiguous()
+    if min(counts) == m:
+        h = _host(xc)
+        if td.get_backend() == "nccl":
+            full = torch.empty((w * m,) + tuple(h.shape[1:]), dtype=h.dtype, device=h.device)
+            td.all_gather_into_tensor(full, h)
+        else:
+            parts = [torch.empty_like(h) for _ in range(w)]
+            td.all_gather(parts, h)
+            full = torch.cat(parts, 0)
+        return full.to(x.device)
     pad = torch.zeros((m,) + tuple(xc.shape[1:]), dtype=xc.dtype, device=xc.device)
     pad[:xc.shape[0]] = xc
     h = _host(pad)
@@ -251,6 +264,14 @@ class GatherClassColumns(torch.autograd.Function):
     def forward(ctx, x, counts):
         ctx.counts = counts
         ctx.r = rank()
+        w = len(counts)
+        if min(counts) == max(counts) and td.get_backend() == "nccl":
+            # equal shards: gather the [B, C_r] blocks as they are and interleave them into
+            # [B, C] with one copy (no transposes, no padding)
+            xc = x.contiguous()
+            buf = torch.empty((w,) + tuple(xc.shape), dtype=xc.dtype, device=xc.device)
+            td.all_gather_into_tensor(buf, xc)
+            return buf.permute(1, 0, 2).reshape(xc.shape[0], w * xc.shape[1])
         full_t = all_gather_rows(x.t(), counts)  # [C, B]
         return full_t.t().contiguous()
 

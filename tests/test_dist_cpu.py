@@ -299,8 +299,12 @@ def _rank_blocks(rank, world):
     padded = dist.pad_rank_blocks(g, counts)
     back = dist.unpad_rank_blocks(padded, counts)
     mine = torch.full((counts[rank], 2), float(rank + 1))
+    # equal shards take the no-padding path
+    g4 = torch.arange(4 * 2, dtype=torch.float32).reshape(4, 2) * (rank + 1)
+    mine2 = torch.full((2, 2), float(rank + 1))
     return {"padded": padded.numpy(), "back": back.numpy(), "rs": dist.reduce_scatter_rows(g, counts).numpy(),
-            "ag": dist.all_gather_rows(mine, counts).numpy()}
+            "ag": dist.all_gather_rows(mine, counts).numpy(),
+            "rs_eq": dist.reduce_scatter_rows(g4, [2, 2]).numpy(), "ag_eq": dist.all_gather_rows(mine2, [2, 2]).numpy()}
 
 
 def test_pad_reduce_scatter_all_gather_rows():
@@ -315,6 +319,9 @@ def test_pad_reduce_scatter_all_gather_rows():
         np.testing.assert_array_equal(o["back"], g * (r + 1))
         np.testing.assert_array_equal(o["rs"], (g * 3)[:3] if r == 0 else (g * 3)[3:])
         np.testing.assert_array_equal(o["ag"], np.array([[1, 1]] * 3 + [[2, 2]] * 2, np.float32))
+        g4 = np.arange(8, dtype=np.float32).reshape(4, 2)
+        np.testing.assert_array_equal(o["rs_eq"], (g4 * 3)[2 * r:2 * r + 2])
+        np.testing.assert_array_equal(o["ag_eq"], np.array([[1, 1]] * 2 + [[2, 2]] * 2, np.float32))
 
 
 def _augment_streams(rank, world):
