@@ -347,6 +347,10 @@ def time_train(trainer, dm, steps, warmup, batch=None, prof_steps=0):
 
     for i in range(warmup):
         step(i)
+    if os.environ.get("BENCH_GC"):  # A/B knob (lab): collect, then freeze the long-lived objects
+        import gc
+        gc.collect()
+        gc.freeze()
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
@@ -403,8 +407,11 @@ def precision_line(args, prec, dev, rank, world, steps=10, warmup=2, n_eval=5000
     (site events in 2 extra steps)."""
     import torch
     from fsp_amd import dist
+    from fsp_amd.clip.model import TextEncoderCore
     tr, dm = build_trainer(args, prec, args.batch, dev, rank, n_test_device=n_eval)
+    retries0 = TextEncoderCore.split_retries
     t, sites = time_train(tr, dm, steps, warmup, prof_steps=2)
+    retries = TextEncoderCore.split_retries - retries0
     table = kernel_table(sites, 2, prec) if sites else None
     e, n = time_eval(tr, dm, n_eval)
     roof = roofline_of(table, prec) if table else None
@@ -418,6 +425,9 @@ def precision_line(args, prec, dev, rank, world, steps=10, warmup=2, n_eval=5000
                          if v["ms_per_step"] >= 0.5} if table else None)}
     if prec == "fp32s":
         line["peak_note"] = "peak = fp16 MFMA peak / 3 (3 fp16 MFMAs per fp32-class product)"
+        # backward passes re-run at the lower gradient scale after a range overflow (warm-up,
+        # timed and profiled steps; each one doubles that step's backward)
+        line["split_retries"] = retries
     del tr, dm
     torch.cuda.empty_cache()
     return line
