@@ -347,10 +347,6 @@ def time_train(trainer, dm, steps, warmup, batch=None, prof_steps=0):
 
     for i in range(warmup):
         step(i)
-    if os.environ.get("BENCH_GC"):  # A/B knob (lab): collect, then freeze the long-lived objects
-        import gc
-        gc.collect()
-        gc.freeze()
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
@@ -550,14 +546,6 @@ def main():
     }
     del trainer, dm
     torch.cuda.empty_cache()
-    if not args.no_extra and args.arch in ("ViT-L/14", "ViT-L/14@336px"):
-        out["config4" if args.arch == "ViT-L/14" else "config5"] = baseline_config_line(args, dev, rank, world)
-    elif not args.no_extra and not args.no_configs and world == 1:
-        # BASELINE configs 4 and 5 per GPU beside the headline (their own archs, bf16)
-        for key, arch in (("config4", "ViT-L/14"), ("config5", "ViT-L/14@336px")):
-            log(key)
-            out[key] = baseline_config_line(argparse.Namespace(**{**vars(args), "arch": arch}), dev, rank, world,
-                                            n_eval=2000)
     if not args.no_extra and world > 1:
         # the reference's CoCoOp batch (1 image / step) with the classes sharded over the ranks
         tr1, dm1 = build_trainer(args, args.prec, 1, dev, 0, class_shard=True)
@@ -586,8 +574,7 @@ def main():
             cls = args.classes // n
             log(f"batch1 class-shard proxy n{n}")
             trp, dmp = build_trainer(argparse.Namespace(**{**vars(args), "classes": cls}), args.prec, 1, dev, rank)
-            # two timed rounds, the faster reported (one round of r05f read 2.31 ms at 125 classes,
-            # 1.69 ms when run alone, profiles/r05k/)
+            # two timed rounds, the faster reported
             rounds = [time_train(trp, dmp, B1_STEPS, 5)[0] for _ in range(2)]
             proxy[f"n{n}"] = {"classes": cls, "ms_per_step": round(1000 * min(rounds) / B1_STEPS, 3),
                               "rounds_ms": [round(1000 * t / B1_STEPS, 3) for t in rounds]}
@@ -612,6 +599,16 @@ def main():
         for p in ("fp32s", "fp32"):
             log(p)
             out[p] = precision_line(args, p, dev, rank, world)
+    # after the ViT-B/16 lines: run before them, the ViT-L trainers left the launch-bound
+    # 125-class proxy at 2.31 instead of 1.66-1.68 ms/step (same kernel durations; profiles/r05n)
+    if not args.no_extra and args.arch in ("ViT-L/14", "ViT-L/14@336px"):
+        out["config4" if args.arch == "ViT-L/14" else "config5"] = baseline_config_line(args, dev, rank, world)
+    elif not args.no_extra and not args.no_configs and world == 1:
+        # BASELINE configs 4 and 5 per GPU beside the headline (their own archs, bf16)
+        for key, arch in (("config4", "ViT-L/14"), ("config5", "ViT-L/14@336px")):
+            log(key)
+            out[key] = baseline_config_line(argparse.Namespace(**{**vars(args), "arch": arch}), dev, rank, world,
+                                            n_eval=2000)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             # the whole workload unit (1 image x all classes, fwd + bwd), no extrapolation (a
