@@ -17,14 +17,64 @@ prefetch completes; the caller must not write it in place before then (consume t
 (``_version``) and the stale result is not used."""
 from __future__ import annotations
 
+import time
+
 import torch
+
+# Side streams by device index, shared by every model of the process (they run one at a time).
+_SIDE = {}
+
+
+def runs_beside(main, side, device, timeout_s=2.0) -> bool:
+    """Whether work queued on ``side`` runs while ``main`` is busy. HIP places each stream on one
+    of a few hardware queues (GPU_MAX_HW_QUEUES, 4); a stream that shares the main stream's queue
+    executes behind it in submission order, and a ViT "prefetched" there serialises with the
+    text encoder (+0.5 ms at B = 8, +0.6 ms at B = 1: tools/lab/side_stream_ab.py,
+    profiles/r05zb). Probe: ~4 ms of GEMMs on main, then a tiny op on side; on separate
+    queues the tiny op completes first."""
+    torch.cuda.synchronize(device)
+    a = torch.randn(8192, 8192, device=device, dtype=torch.float16)
+    x = torch.zeros(1, device=device)
+    with torch.cuda.stream(main):
+        for _ in range(4):
+            torch.mm(a, a)
+        ev_main = torch.cuda.Event()
+        ev_main.record(main)
+    with torch.cuda.stream(side):
+        x.add_(1)
+        ev_side = torch.cuda.Event()
+        ev_side.record(side)
+    t0 = time.perf_counter()
+    while not ev_side.query():
+        if time.perf_counter() - t0 > timeout_s:
+            break
+    beside = ev_side.query() and not ev_main.query()
+    torch.cuda.synchronize(device)
+    return beside
+
+
+def side_stream(device):
+    """A pool stream that runs beside the current (main) stream, probed once per device (up to
+    8 candidates; the last one if none passes)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    side = _SIDE.get(idx)
+    if side is None:
+        main = torch.cuda.current_stream(device)
+        held = []  # keep rejected candidates referenced while probing the next ones
+        for _ in range(8):
+            side = torch.cuda.Stream(device)
+            if runs_beside(main, side, device):
+                break
+            held.append(side)
+        _SIDE[idx] = side
+    return side
 
 
 class ImageFeatureSchedule:
     def _side(self, device):
         side = getattr(self, "_side_stream", None)
         if side is None or side.device != device:
-            side = self._side_stream = torch.cuda.Stream(device)
+            side = self._side_stream = side_stream(device)
         return side
 
     def prefetch_image_features(self, image):

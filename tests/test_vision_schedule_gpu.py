@@ -74,3 +74,12 @@ def test_features_only_for_the_same_unmodified_tensor(dev, tmp_path):
     m.prefetch_image_features(b)
     assert torch.equal(m.cached_image_features(a), m.image_encoder(a))
     assert torch.equal(m.cached_image_features(b), m.image_encoder(b))
+
+
+def test_side_stream_runs_beside_main(dev):
+    """The ViT prefetch's side stream is one whose work runs while the main stream is busy (a
+    pool stream on the main stream's hardware queue would serialise the two: profiles/r05zb)."""
+    from fsp_amd.trainers._vision import runs_beside, side_stream
+    s = side_stream(dev)
+    assert s is side_stream(dev), "one side stream per device"
+    assert runs_beside(torch.cuda.current_stream(dev), s, dev)
