@@ -32,9 +32,11 @@ def runs_beside(main, side, device, timeout_s=2.0) -> bool:
     text encoder (+0.5 ms at B = 8, +0.6 ms at B = 1: tools/lab/side_stream_ab.py,
     profiles/r05zb). Probe: ~4 ms of GEMMs on main, then a tiny op on side; on separate
     queues the tiny op completes first."""
+    x = torch.zeros(1, device=device)
+    with torch.cuda.stream(side):  # the stream's first use (its queue may be created lazily)
+        x.add_(1)
     torch.cuda.synchronize(device)
     a = torch.randn(8192, 8192, device=device, dtype=torch.float16)
-    x = torch.zeros(1, device=device)
     with torch.cuda.stream(main):
         for _ in range(4):
             torch.mm(a, a)

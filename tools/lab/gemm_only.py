@@ -1,7 +1,7 @@
 """The production GEMM alone on one text shape (default: fc_dx, M = 47,160 packed rows, N = 512,
 K = 2048, EPI_NONE, fp16), A rotated over >600 MB, for PMC passes
 (`rocprofv3 --pmc ... -- python3 tools/lab/gemm_only.py`): 20 launches after 3 warm-ups.
-    python tools/lab/gemm_only.py [N K]"""
+    python tools/lab/gemm_only.py [N K]      (BLASLT=1: torch.matmul instead)"""
 import os
 import sys
 
@@ -21,8 +21,12 @@ def main():
     As = [(torch.randn(M, k, device=dev, generator=g) * 0.5).half() for _ in range(nbuf)]
     B = (torch.randn(n, k, device=dev, generator=g) * 0.5).half()
     C = torch.empty(M, n, device=dev, dtype=torch.float16)
+    blaslt = os.environ.get("BLASLT")
     for i in range(23):
-        ops.gemm(As[i % nbuf], B, N.EPI_NONE, torch.float16, out=C)
+        if blaslt:  # the same product through hipBLASLt (torch.matmul)
+            torch.matmul(As[i % nbuf], B.t(), out=C)
+        else:
+            ops.gemm(As[i % nbuf], B, N.EPI_NONE, torch.float16, out=C)
     torch.cuda.synchronize()
     print("done", flush=True)
 
