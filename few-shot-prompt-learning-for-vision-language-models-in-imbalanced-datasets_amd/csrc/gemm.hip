@@ -248,6 +248,14 @@ template <> struct Raw<32> { uint4 v[2]; };
 #ifndef CLIPK_GEMM_PRIO
 #define CLIPK_GEMM_PRIO 1
 #endif
+// CLIPK_GEMM_WARM (A/B, build-time; 0 = off): the 192-row ping-pong loop (16-bit) touches one
+// dword of every 128-B line of the A panel CLIPK_GEMM_WARM K steps ahead (waves 0-2, one line per
+// lane), so the first read of each activation line is in flight before its LDS-DMA. The staging
+// lab measured 100 -> 94 us for this tile's operand stream at 2 steps ahead
+// (tools/lab/stage_lab.hip, profiles/r05zh/).
+#ifndef CLIPK_GEMM_WARM
+#define CLIPK_GEMM_WARM 0
+#endif
 // Diagnostic builds only (wrong results; tools/gemm_diag.sh): NOLOAD = stage no K step past
 // the first (the loop's compute + LDS + barrier ceiling), NOBAR = no barrier / vmcnt wait per
 // K step either.
@@ -389,7 +397,9 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
   static_assert(ROWB == 128 || (ROWB == 64 && sizeof(T) == 2), "staged row is 128 B (or 64 B for 16-bit)");
   static_assert(BM % RPI == 0 && BN % RPI == 0 && NG >= NW, "tile/wave mismatch");
   static_assert(!AG || BLOCKED, "A-operand QuickGELU path: blocked unit split");
-  __shared__ CLIPK_LDS_ALIGN char smem[DEPTH * STAGE + NW * EPI_SCRATCH];  // one array (see header)
+  // (+ 1 KiB: the CLIPK_GEMM_WARM junk area of the 192-row ping-pong loop)
+  __shared__ CLIPK_LDS_ALIGN char smem[DEPTH * STAGE + NW * EPI_SCRATCH +
+                                       (CLIPK_GEMM_WARM > 0 && PP && BM == 192 ? 1024 : 0)];  // one array (see header)
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
@@ -638,9 +648,23 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
           }
       };
       // K step s+1 landed; the three regions already issued for s+2 (A0, B1, A1) stay in flight
+      // (+ the warm-up load issued between B1 and A1, CLIPK_GEMM_WARM)
+      constexpr bool WARM = CLIPK_GEMM_WARM > 0 && BM == 192 && !SPLIT;
+      const bool warm_w = WARM && w < BM / 64;
       auto wait_ahead = [&]() {
-        if (two_a) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        if (warm_w) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+        else if (two_a) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      };
+      // one dword of A row (w * 64 + lane) of the tile at K tile kw: its 128-B line into L2, by an
+      // LDS-DMA into a junk area (no register result, so no compiler wait; wait_ahead counts it)
+      auto warm = [&](__amdgpu_buffer_rsrc_t ra_, int kw) {
+        if constexpr (WARM) {
+          if (warm_w)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                ra_, (__attribute__((address_space(3))) void*)(smem + DEPTH * STAGE + NW * EPI_SCRATCH + w * 256), 4,
+                (w * 64 + lane) * g.lda * (int)esz, kw * ROWB, 0, 0);
+        }
       };
       constexpr int NFB = CLIPK_GEMM_PPB0 ? 2 : 1;
       u32x4 fa[KK][TM2], fbs[NFB][KK][TN2];
@@ -794,7 +818,12 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         G8_BAR();
         if (CLIPK_GEMM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         rd_a(b, 1);                             // phase 3: A1 x B1
-        if (h2) pst(b, cra, in2 ? crb : xrb, k2, 3);
+        if (h2) {
+          pst(b, cra, in2 ? crb : xrb, k2, 3);
+          // the warm-up rides between B1 and A1 of s+2 (wait_ahead counts it): this tile's A
+          // CLIPK_GEMM_WARM steps ahead, clamped to its last K tile
+          warm(cra, kt0c + min(kt + CLIPK_GEMM_WARM, nkc - 1));
+        }
         seg_end(true);
         mm(1, 1);
         G8_BAR();

@@ -9,7 +9,8 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 NAMES = {0: "LDS-DMA (buffer_load ... lds)", 1: "registers + ds_write_b128", 2: "registers only (no LDS)",
-         10: "LDS-DMA, pre-blocked operands", 11: "registers + ds_write, pre-blocked"}
+         10: "LDS-DMA, pre-blocked operands", 11: "registers + ds_write, pre-blocked",
+         12: "LDS-DMA + A lines warmed 2 ahead", 13: "LDS-DMA + A lines warmed 4 ahead", 14: "LDS-DMA + A lines warmed 8 ahead"}
 
 
 def main():
@@ -25,7 +26,7 @@ def main():
     ntiles = (M // 192) * 2
     staged = ntiles * (K * 2 // 128) * (192 + 256) * 128  # bytes into LDS per launch
     for grid in (256, 512):
-        for mode, depth in ((0, 2), (1, 2), (2, 2), (2, 3), (10, 2), (11, 2)):
+        for mode, depth in ((0, 2), (10, 2), (12, 2), (13, 2), (14, 2)):
             rc = lib.stage_lab(mode, depth, As[0].data_ptr(), B.data_ptr(), M, K, grid, sink.data_ptr(), st)
             if rc:
                 print(f"mode {mode} depth {depth}: rc {rc}")
