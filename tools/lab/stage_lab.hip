@@ -22,7 +22,8 @@ constexpr int UNITS = STAGE / 1024;  // 1-KiB pieces (8 rows x 128 B) per stage:
 // contiguous run (as a packed layout would hold them) instead of 128-B row pieces 2K bytes apart.
 // PF > 0 (LDS-DMA only): one 4-B load per 128-B line of the A panel PF K steps ahead, issued
 // after the next stage's DMA and left in flight (an L2 warm-up of the first-touch activations)
-template <int MODE, int DEPTH, bool BLK = false, int PF = 0>
+// AA / AB: cache-policy bits of the A / B LDS-DMA loads (1 sc0, 2 nt, 16 sc1)
+template <int MODE, int DEPTH, bool BLK = false, int PF = 0, int AA = 0, int AB = 0>
 __global__ __launch_bounds__(512, 1) void stage_kernel(const char* __restrict__ A, const char* __restrict__ B, int M,
                                                        int K, int ntiles, int* sink) {
   __shared__ __attribute__((aligned(16))) char smem[MODE == 2 ? 1024 : DEPTH * STAGE];
@@ -45,9 +46,12 @@ __global__ __launch_bounds__(512, 1) void stage_kernel(const char* __restrict__ 
         const int off = BLK ? row * ROWB + (lane % 8) * 16 : row * K * 2 + (lane % 8) * 16;
         const int koff = BLK ? kt * (ua ? BM : BN) * ROWB : kt * ROWB;
         if constexpr (MODE == 0) {
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(ua ? ra : rb,
-                                                   (__attribute__((address_space(3))) void*)(smem + slot * STAGE + u * 1024),
-                                                   16, off, koff, 0, 0);
+          if (ua)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(smem + slot * STAGE + u * 1024),
+                                                     16, off, koff, 0, AA);
+          else
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (__attribute__((address_space(3))) void*)(smem + slot * STAGE + u * 1024),
+                                                     16, off, koff, 0, AB);
         } else {
           reg[slot][i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ua ? ra : rb, off + koff, 0, 0));
         }
@@ -106,6 +110,13 @@ extern "C" int stage_lab(int mode, int depth, const void* A, const void* B, int 
     const int ntiles = ((M + BM - 1) / BM) * 2;
     hipStream_t st = (hipStream_t)stream;
     if (depth != 2) return -1;
+    if (mode >= 30) {
+#define P(AAV, ABV) hipLaunchKernelGGL((stage_kernel<0, 2, false, 0, AAV, ABV>), dim3(grid), dim3(512), 0, st, (const char*)A, (const char*)B, M, K, ntiles, (int*)sink)
+      if (mode == 30) P(2, 0); else if (mode == 31) P(1, 0); else if (mode == 32) P(2, 2); else if (mode == 33) P(16, 0);
+      else if (mode == 34) P(0, 2); else P(3, 0);
+#undef P
+      return (int)hipGetLastError();
+    }
     if (mode == 12)
       hipLaunchKernelGGL((stage_kernel<0, 2, false, 2>), dim3(grid), dim3(512), 0, st, (const char*)A, (const char*)B, M, K, ntiles, (int*)sink);
     else if (mode == 13)

@@ -10,7 +10,9 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 NAMES = {0: "LDS-DMA (buffer_load ... lds)", 1: "registers + ds_write_b128", 2: "registers only (no LDS)",
          10: "LDS-DMA, pre-blocked operands", 11: "registers + ds_write, pre-blocked",
-         12: "LDS-DMA + A lines warmed 2 ahead", 13: "LDS-DMA + A lines warmed 4 ahead", 14: "LDS-DMA + A lines warmed 8 ahead"}
+         12: "LDS-DMA + A lines warmed 2 ahead", 13: "LDS-DMA + A lines warmed 4 ahead", 14: "LDS-DMA + A lines warmed 8 ahead",
+         30: "LDS-DMA, A nt", 31: "LDS-DMA, A sc0", 32: "LDS-DMA, A nt + B nt", 33: "LDS-DMA, A sc1",
+         34: "LDS-DMA, B nt", 35: "LDS-DMA, A sc0 nt"}
 
 
 def main():
@@ -26,7 +28,7 @@ def main():
     ntiles = (M // 192) * 2
     staged = ntiles * (K * 2 // 128) * (192 + 256) * 128  # bytes into LDS per launch
     for grid in (256, 512):
-        for mode, depth in ((0, 2), (10, 2), (12, 2), (13, 2), (14, 2)):
+        for mode, depth in ((0, 2), (30, 2), (31, 2), (32, 2), (33, 2), (34, 2), (35, 2)):
             rc = lib.stage_lab(mode, depth, As[0].data_ptr(), B.data_ptr(), M, K, grid, sink.data_ptr(), st)
             if rc:
                 print(f"mode {mode} depth {depth}: rc {rc}")
