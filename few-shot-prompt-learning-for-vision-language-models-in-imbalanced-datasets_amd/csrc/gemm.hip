@@ -248,6 +248,11 @@ template <> struct Raw<32> { uint4 v[2]; };
 #ifndef CLIPK_GEMM_PRIO
 #define CLIPK_GEMM_PRIO 1
 #endif
+// CLIPK_GEMM_APOL (A/B, build-time): cache-policy bits of the ping-pong loop's A-operand LDS-DMA
+// (0 default; the staging lab read 100 -> 96.5 us with sc0 (1) or sc1 (16), profiles/r05zh/)
+#ifndef CLIPK_GEMM_APOL
+#define CLIPK_GEMM_APOL 0
+#endif
 // CLIPK_GEMM_WARM (A/B, build-time; 0 = off): the 192-row ping-pong loop (16-bit) touches one
 // dword of every 128-B line of the A panel CLIPK_GEMM_WARM K steps ahead (waves 0-2, one line per
 // lane), so the first read of each activation line is in flight before its LDS-DMA. The staging
@@ -642,9 +647,14 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
         for (int i = 0; i < 2; ++i)
           if (r >= 2 || i == 0 || two_a) {
             const int row0 = unit_row0(r, i);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                r < 2 ? ra_ : rb_, (__attribute__((address_space(3))) void*)(smem + base + (r < 2 ? 0 : OPA) + row0 * ROWB),
-                16, poff[r][i], koff, 0, 0);
+            if (CLIPK_GEMM_APOL != 0 && r < 2)
+              __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                  ra_, (__attribute__((address_space(3))) void*)(smem + base + row0 * ROWB), 16, poff[r][i], koff, 0,
+                  CLIPK_GEMM_APOL);
+            else
+              __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                  r < 2 ? ra_ : rb_, (__attribute__((address_space(3))) void*)(smem + base + (r < 2 ? 0 : OPA) + row0 * ROWB),
+                  16, poff[r][i], koff, 0, 0);
           }
       };
       // K step s+1 landed; the three regions already issued for s+2 (A0, B1, A1) stay in flight
