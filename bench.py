@@ -103,7 +103,10 @@ def reference_cpu(arch, classes):
     return None
 # dense TFLOP/s (MI355X guide); fp32s: the fp16 MFMA peak / 3 (3 fp16 MFMAs per fp32-class product,
 # include/clipk.h CLIPK_F32S), the ceiling for its algorithmic (fp32) FLOPs
-PEAK = {"fp16": 2500.0, "bf16": 2500.0, "amp": 2500.0, "fp32": 157.3, "fp32s": 2500.0 / 3}
+PEAK = {"fp16": 2500.0, "bf16": 2500.0, "amp": 2500.0, "fp32": 157.3, "fp32s": 2500.0 / 3,
+        # PREC fp32s on fp16-valued weights (split mode 2, CLIPK_F32S16): 2 MFMAs per product
+        # (the LayerNorm-folded qkv / c_fc forward keep 3: their fraction is understated here)
+        "fp32s16": 2500.0 / 2}
 HBM_PEAK_GBS = 8000.0  # HBM3E, MI355X_MICROARCH.md
 # batch-1 lines: ~2.7 ms steps, so 50 timed steps (10 let one host hiccup move the mean ~20 %:
 # 3.32 ms in one round-4 run against 2.70 over 50 steps of tools/b1_time.py on the same build)
@@ -293,6 +296,7 @@ def build_coop_trainer(args, prec, batch, dev, rank, n_test=0, n_test_device=0):
     cfg.DATASET.NUM_SHOTS = 16
     cfg.OPTIM.MAX_EPOCH = 10
     cfg.TEST.NO_TEST = True
+    cfg.MODEL.SYNTH_FP16 = getattr(args, "weights", "fp16") == "fp16"
     dm = SyntheticDataManager(args.classes, arch.image_resolution, batch, n_batches=2, test_batch=100,
                               n_test=n_test, device=dev, rank=rank, n_test_device=n_test_device)
     with contextlib.redirect_stdout(io.StringIO()):
@@ -321,6 +325,7 @@ def build_trainer(args, prec, batch, dev, rank, n_test=0, n_test_device=0, class
     cfg.OPTIM.WARMUP_TYPE = "constant"
     cfg.TEST.NO_TEST = True
     cfg.NATIVE.COCOOP_SHARD = "class" if class_shard else "image"
+    cfg.MODEL.SYNTH_FP16 = getattr(args, "weights", "fp16") == "fp16"
     dm = SyntheticDataManager(args.classes, arch.image_resolution, batch, n_batches=2, test_batch=100,
                               n_test=n_test, device=dev, rank=rank, n_test_device=n_test_device)
     with contextlib.redirect_stdout(io.StringIO()):
@@ -397,7 +402,7 @@ def time_eval(trainer, dm, n_images):
     return dist.sum_over_ranks(n) / te, n
 
 
-def precision_line(args, prec, dev, rank, world, steps=10, warmup=2, n_eval=5000):
+def precision_line(args, prec, dev, rank, world, steps=10, warmup=2, n_eval=5000, prof=True):
     """The headline workload at another PREC: train img/s over `steps` timed steps, eval img/s
     over n_eval distinct resident images, and the roofline of its dominant kernel class
     (site events in 2 extra steps)."""
@@ -406,11 +411,13 @@ def precision_line(args, prec, dev, rank, world, steps=10, warmup=2, n_eval=5000
     from fsp_amd.clip.model import TextEncoderCore
     tr, dm = build_trainer(args, prec, args.batch, dev, rank, n_test_device=n_eval)
     retries0 = TextEncoderCore.split_retries
-    t, sites = time_train(tr, dm, steps, warmup, prof_steps=2)
+    t, sites = time_train(tr, dm, steps, warmup, prof_steps=2 if prof else 0)
     retries = TextEncoderCore.split_retries - retries0
-    table = kernel_table(sites, 2, prec) if sites else None
+    # the MFMA peak the dominant class is priced against: 3 or 2 fp16 MFMAs per product
+    pk = "fp32s16" if prec == "fp32s" and tr.model.text_core.split_mode == 2 else prec
+    table = kernel_table(sites, 2, pk) if sites else None
     e, n = time_eval(tr, dm, n_eval)
-    roof = roofline_of(table, prec) if table else None
+    roof = roofline_of(table, pk) if table else None
     if roof:  # the bench line carries the headline's full roofline record; here the essentials
         roof = {k: roof[k] for k in ("bound", "achieved", "peak", "unit", "frac", "kernel_class", "avg_launch_ms")}
     line = {"images_per_sec": round(world * args.batch * steps / t, 3), "ms_per_step": round(1000 * t / steps, 3),
@@ -420,7 +427,11 @@ def precision_line(args, prec, dev, rank, world, steps=10, warmup=2, n_eval=5000
             "kernels": ({k: [v["ms_per_step"], v["bound"], v["roof_frac"]] for k, v in table.items()
                          if v["ms_per_step"] >= 0.5} if table else None)}
     if prec == "fp32s":
-        line["peak_note"] = "peak = fp16 MFMA peak / 3 (3 fp16 MFMAs per fp32-class product)"
+        line["peak_note"] = ("peak = fp16 MFMA peak / %d (%d fp16 MFMAs per fp32-class product)"
+                             % ((2, 2) if pk == "fp32s16" else (3, 3)))
+        # 2: fp16-valued weights, the GEMMs but the LayerNorm-folded ones skip the weight-lo
+        # product (CLIPK_F32S16, bitwise the same results); 1: every GEMM 3 MFMAs per product
+        line["split_mode"] = {"text": tr.model.text_core.split_mode, "vision": tr.model.image_encoder.split_mode}
         # backward passes re-run at the lower gradient scale after a range overflow (warm-up,
         # timed and profiled steps; each one doubles that step's backward)
         line["split_retries"] = retries
@@ -470,6 +481,8 @@ def main():
     ap.add_argument("--no-prof", action="store_true", help="no per-site profiling steps")
     ap.add_argument("--no-extra", action="store_true", help="skip the fp32 / batch-1 lines")
     ap.add_argument("--no-configs", action="store_true", help="skip the BASELINE config 4 / 5 lines")
+    ap.add_argument("--weights", choices=("fp16", "fp32"), default="fp16",
+                    help="synthetic CLIP weights rounded to fp16 (as the released checkpoints) or fp32")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -517,7 +530,8 @@ def main():
         "rccl_world": world, "backend": torch.distributed.get_backend() if dist.is_dist() else None,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * t / args.steps, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.prec,
-        "data": "synthetic (seeded U[0,1) CLIP-normalised images, random-init CLIP weights)",
+        "data": "synthetic (seeded U[0,1) CLIP-normalised images, random-init CLIP weights%s)"
+                % (" rounded to fp16, as the released CLIP checkpoints hold them" if args.weights == "fp16" else ""),
         "config": {"workload": f"CoCoOp {args.arch} n_ctx=4 ctx_init='a photo of a', {args.classes} classes, "
                                f"{args.batch} images/GPU/step, train step fwd+bwd+SGD",
                    "model": f"CLIP {args.arch}", "global_batch": world * args.batch, "classes": args.classes,
@@ -599,6 +613,12 @@ def main():
         for p in ("fp32s", "fp32"):
             log(p)
             out[p] = precision_line(args, p, dev, rank, world)
+        if args.weights == "fp16":
+            # PREC fp32s on weights with fp32 mantissas (not a CLIP checkpoint: every GEMM keeps
+            # the weight-lo product, split mode 1)
+            log("fp32s, fp32-valued weights")
+            out["fp32s_fp32_weights"] = precision_line(argparse.Namespace(**{**vars(args), "weights": "fp32"}),
+                                                       "fp32s", dev, rank, world, n_eval=2000, prof=False)
     # after the ViT-B/16 lines: run before them, the ViT-L trainers left the launch-bound
     # 125-class proxy at 2.31 instead of 1.66-1.68 ms/step (same kernel durations; profiles/r05n)
     if not args.no_extra and args.arch in ("ViT-L/14", "ViT-L/14@336px"):

@@ -35,6 +35,7 @@ def source_digest():
     return h.hexdigest()
 
 F32, F16, BF16, F32S = 0, 1, 2, 3  # F32S: fp32 activations x split-packed weights (PREC fp32s)
+F32S16 = 4  # F32S with fp16-valued weights (every lo part zero): the weight-lo product skipped
 SPLIT_SCALE = 64.0  # CLIPK_SPLIT_SCALE: clipk_split_pack stores SPLIT_SCALE * W
 EPI_BIAS, EPI_BIAS_RES, EPI_BIAS_QGELU, EPI_DQGELU, EPI_NONE = 0, 1, 2, 3, 4
 A_QGELU = 0x100  # OR-ed into epi: the GEMM consumes quickgelu(A) (include/clipk.h)
@@ -60,6 +61,7 @@ SIGNATURES = {
     "clipk_gemm_splitk": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P, _S, _P]),
     "clipk_gemm_set_config": (_I, [_I]),
     "clipk_split_pack": (_I, [_I, _I, _P, _I, _P, _P]),
+    "clipk_split_lo_zero": (_I, [_I, _I, _P, _P]),
     "clipk_gemm_ln": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P]),
     "clipk_ln_stats_merge": (_I, [_I, _I, _P, _P, _P, _P, _P]),
     "clipk_gemm_ln_merge_fused": (_I, [_I, _I, _I, _I]),

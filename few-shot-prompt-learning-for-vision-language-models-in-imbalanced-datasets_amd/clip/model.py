@@ -72,6 +72,17 @@ def _mm_weight(x, device, act, split):
     return ops.split_pack(x) if split else x
 
 
+def split_mode(weights) -> int:
+    """clipk_encoder_set_split mode of a PREC fp32s encoder: 2 when every split-packed GEMM weight
+    it was created with is fp16-valued (ops.split_lo_zero; the released CLIP checkpoints are fp16,
+    PromptSRC/clip/clip.py:154-180), so those GEMMs skip the weight-lo product (CLIPK_F32S16, the
+    same results); else 1. Knob FSP_SPLIT_W16=0 keeps 1 (A/B)."""
+    if os.environ.get("FSP_SPLIT_W16", "1") == "0":
+        return 1
+    packed = [t for t in weights if isinstance(t, torch.Tensor) and t.dtype == torch.int32]
+    return 2 if packed and all(ops.split_lo_zero(t) for t in packed) else 1
+
+
 def _t(v):
     return torch.as_tensor(np.asarray(v)) if not isinstance(v, torch.Tensor) else v.detach()
 
@@ -213,8 +224,9 @@ class TextEncoderCore(_Encoder):
                 "clipk_encoder_create(text)")
         self.handle = h
         self._status = None
+        self.split_mode = split_mode(keep) if split else 0
         if split:
-            N.check(N.load().clipk_encoder_set_split(h, 1), "clipk_encoder_set_split(text)")
+            N.check(N.load().clipk_encoder_set_split(h, self.split_mode), "clipk_encoder_set_split(text)")
             # overflow flags of the split calls (clipk_encoder_set_status): 1 = a forward's
             # features, 2 = a backward's gradients came out non-finite
             self._status = torch.zeros(1, dtype=torch.int32, device=self.device)
@@ -438,8 +450,9 @@ class VisionEncoder(nn.Module, _Encoder):
                                              ops.DT[act], _ptrs(table), _ptrs(head), ctypes.byref(h)),
                 "clipk_vision_create")
         self.handle = h
+        self.split_mode = split_mode(self._keep + [self.proj_bwd]) if split else 0
         if split:
-            N.check(N.load().clipk_encoder_set_split(h, 1), "clipk_encoder_set_split(vision)")
+            N.check(N.load().clipk_encoder_set_split(h, self.split_mode), "clipk_encoder_set_split(vision)")
         if fold:
             self._keep += fold
             N.check(N.load().clipk_encoder_set_ln_fold(h, _ptrs(fold)), "clipk_encoder_set_ln_fold")

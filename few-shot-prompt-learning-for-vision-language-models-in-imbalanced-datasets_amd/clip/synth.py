@@ -122,8 +122,12 @@ def _param_specs(a: ClipArch):
     return specs
 
 
-def make_state_dict(arch: str | ClipArch, seed: int = 0, logit_scale: float = float(np.log(100.0))):
-    """Return {key: float32 ndarray} for a CLIP model of the given architecture."""
+def make_state_dict(arch: str | ClipArch, seed: int = 0, logit_scale: float = float(np.log(100.0)),
+                    fp16_values: bool = False):
+    """Return {key: float32 ndarray} for a CLIP model of the given architecture. fp16_values:
+    every parameter rounded to fp16 (then stored as float32), as the released CLIP checkpoints
+    hold them (fp16 archives, PromptSRC/clip/clip.py:154-180; build_model copies them into the
+    fp32 model, model.py:699-701): the weights a real fp32 run multiplies."""
     a = ARCHS[arch] if isinstance(arch, str) else arch
     rs = np.random.RandomState(seed)
     sd = {}
@@ -139,6 +143,8 @@ def make_state_dict(arch: str | ClipArch, seed: int = 0, logit_scale: float = fl
             v = 0.02 * z
         else:
             raise AssertionError(kind)
+        if fp16_values:
+            v = v.astype(np.float16)
         sd[key] = np.ascontiguousarray(v, dtype=np.float32)
     sd["logit_scale"] = np.asarray(logit_scale, dtype=np.float32)
     return sd

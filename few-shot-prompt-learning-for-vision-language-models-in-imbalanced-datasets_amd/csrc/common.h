@@ -23,12 +23,16 @@ constexpr int kWave = 64;
 // GEMM input tag of the split-fp16 fp32-class path (CLIPK_F32S): A fp32, B split-packed
 // (clipk_split_pack); 4 bytes per element on both operands.
 struct f32s { float v; };
+// ... and CLIPK_F32S16: the same operands, B's lo parts all zero (the weight-lo product skipped)
+struct f32h { float v; };
+template <typename T> constexpr bool is_split_v = __is_same(T, f32s) || __is_same(T, f32h);
 
 template <typename T> struct DT;
 template <> struct DT<float> { static constexpr int id = CLIPK_F32; };
 template <> struct DT<f16>   { static constexpr int id = CLIPK_F16; };
 template <> struct DT<bf16>  { static constexpr int id = CLIPK_BF16; };
 template <> struct DT<f32s>  { static constexpr int id = CLIPK_F32S; };
+template <> struct DT<f32h>  { static constexpr int id = CLIPK_F32S16; };
 
 __device__ __forceinline__ float to_f32(float x) { return x; }
 __device__ __forceinline__ float to_f32(f16 x) { return (float)x; }

@@ -40,7 +40,9 @@ struct clipk_encoder {
   // clipk_encoder_set_ln_fold: per layer {W_in', s_in, c_in, W_fc', s_fc, c_fc} (empty: off)
   std::vector<std::array<const void*, 6>> fold;
   // clipk_encoder_set_split: PREC fp32s -- fp32 activations, every GEMM weight split-packed
-  // (clipk_split_pack) and every GEMM on the split-fp16 MFMA path (CLIPK_F32S)
+  // (clipk_split_pack) and every GEMM on the split-fp16 MFMA path (CLIPK_F32S); 2: the weights
+  // given at creation are fp16-valued (clipk_split_lo_zero), their GEMMs run CLIPK_F32S16 (the
+  // LayerNorm-folded W' of clipk_encoder_set_ln_fold stay CLIPK_F32S)
   int split = 0;
   int split_target = 7;     // the backward's gradient scale puts max |s dtxt| in [2^(t-1), 2^t)
   int* status = nullptr;    // clipk_encoder_set_status: overflow flags of split calls (device)
@@ -48,7 +50,7 @@ struct clipk_encoder {
 
 namespace clipk {
 
-static inline size_t esize(int dt) { return (dt == CLIPK_F32 || dt == CLIPK_F32S) ? 4 : 2; }
+static inline size_t esize(int dt) { return (dt == CLIPK_F32 || dt == CLIPK_F32S || dt == CLIPK_F32S16) ? 4 : 2; }
 
 // PREC fp32s: while an encoder call of a split encoder runs, its fp32 GEMMs take the split-packed
 // weights (CLIPK_F32S). Set per call (RAII, per host thread) by the entry points below, so the
@@ -156,7 +158,7 @@ static double gemm_bytes(int in, int out, int epi, int M, int N, int K, bool has
 static int gemm(int in, int out, int epi, int M, int N, int K, const void* A, const void* B,
                 const float* bias, const void* res, void* o, void* o2, const void* aux, int auxdt,
                 hipStream_t st, int prof_cls, void* sk = nullptr, size_t skb = 0, const char* site = nullptr) {
-  if (t_split && in == CLIPK_F32) in = CLIPK_F32S;
+  if (t_split && in == CLIPK_F32) in = t_split == 2 ? CLIPK_F32S16 : CLIPK_F32S;
   ProfScope ps(prof_cls, st, 2.0 * M * N * K, site,
                site ? gemm_bytes(in, out, epi, M, N, K, o2 != nullptr, auxdt) : 0.0);
   if (sk && (epi & ~CLIPK_QGELU_DERIV) != CLIPK_EPI_DQGELU)
@@ -483,7 +485,9 @@ static int gemm_ln(int act, int epi, int M, int N, int K, const void* A, const v
   const double b = gemm_bytes(act, act, epi, M, N, K, o2 != nullptr, act) + (stats ? (double)M * (N / 64) * 8 : 0.0) +
                    (rnb ? 8.0 * M : 0.0);
   ProfScope ps(prof_cls, st, 2.0 * M * N * K, site, b);
-  if (t_split && act == CLIPK_F32) act = CLIPK_F32S;  // PREC fp32s: the split-packed weights
+  // PREC fp32s: the split-packed weights; a fold (colsum) multiplies W' = W diag(gamma), which
+  // is not fp16-valued even when W is
+  if (t_split && act == CLIPK_F32) act = t_split == 2 && !colsum ? CLIPK_F32S16 : CLIPK_F32S;
   return clipk_gemm_ln(act, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, stats, colsum, rnb, st);
 }
 // mean / rstd (kept for the LayerNorm backward) and the folding GEMM's (rstd, -rstd mean) pairs
@@ -1292,7 +1296,7 @@ extern "C" int clipk_encoder_set_ln_fold(clipk_encoder* e, const void* const* fo
 }
 
 extern "C" int clipk_encoder_set_split(clipk_encoder* e, int on) {
-  if (!e || (on != 0 && on != 1)) return CLIPK_EINVAL;
+  if (!e || on < 0 || on > 2) return CLIPK_EINVAL;
   if (on && (e->act != CLIPK_F32 || e->grad != CLIPK_F32)) return CLIPK_EDTYPE;
   e->split = on;
   return CLIPK_OK;

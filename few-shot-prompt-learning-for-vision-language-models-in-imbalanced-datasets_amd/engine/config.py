@@ -105,7 +105,8 @@ def get_cfg_default() -> CfgNode:
                     "SUBSAMPLE_CLASSES": "all"},
         "DATALOADER": {"NUM_WORKERS": 8, "TRAIN_X": {"SAMPLER": "RandomSampler", "BATCH_SIZE": 32},
                        "TEST": {"SAMPLER": "SequentialSampler", "BATCH_SIZE": 100}},
-        "MODEL": {"INIT_WEIGHTS": "", "BACKBONE": {"NAME": "ViT-B/16"}, "WEIGHTS_PATH": ""},
+        "MODEL": {"INIT_WEIGHTS": "", "BACKBONE": {"NAME": "ViT-B/16"}, "WEIGHTS_PATH": "",
+                  "SYNTH_FP16": False},
         "OPTIM": {"NAME": "sgd", "LR": 0.002, "WEIGHT_DECAY": 5e-4, "MOMENTUM": 0.9,
                   "SGD_DAMPNING": 0, "SGD_NESTEROV": False, "LR_SCHEDULER": "cosine",
                   "MAX_EPOCH": 10, "WARMUP_EPOCH": -1, "WARMUP_TYPE": "linear",

@@ -42,7 +42,8 @@ def load_clip(cfg, prec, device, text_grad=True, vision_grad=False):
     MODEL.BACKBONE.NAME (no network on this path). text_grad=False packs no backward
     weights (forward-only text encoder, e.g. zero-shot)."""
     path = cfg.MODEL.get("WEIGHTS_PATH", "")
-    sd = load_state_dict(path) if path else synth.make_state_dict(cfg.MODEL.BACKBONE.NAME, seed=0)
+    sd = load_state_dict(path) if path else synth.make_state_dict(
+        cfg.MODEL.BACKBONE.NAME, seed=0, fp16_values=bool(cfg.MODEL.get("SYNTH_FP16", False)))
     return build_model(sd, prec=prec, device=device, text_grad=text_grad, vision_grad=vision_grad)
 
 

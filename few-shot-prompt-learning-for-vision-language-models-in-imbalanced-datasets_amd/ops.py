@@ -48,10 +48,22 @@ def split_pack(w):
     return out
 
 
+def split_lo_zero(packed) -> bool:
+    """clipk_split_lo_zero: whether every lo part of a split_pack(...) weight is zero (the weight
+    is fp16-valued, so the GEMMs may run CLIPK_F32S16). Synchronises the stream."""
+    _need(packed, "packed", torch.int32)
+    n, k = packed.shape
+    rc = N.load().clipk_split_lo_zero(n, k, _p(packed), _stream())
+    if rc < 0 or rc > 1:
+        N.check(rc, "clipk_split_lo_zero")
+    return rc == 1
+
+
 def gemm(a, b, epi=N.EPI_NONE, out_dtype=torch.float32, bias=None, res=None, aux=None,
-         want_out2=False, out=None):
+         want_out2=False, out=None, w16=False):
     """out[M,N] = epi(a[M,K] @ b[N,K]^T); returns out (and out2 for EPI_BIAS_QGELU). With a
-    fp32 and b an int32 split_pack(...) weight: the fp32-class split-fp16 GEMM (CLIPK_F32S)."""
+    fp32 and b an int32 split_pack(...) weight: the fp32-class split-fp16 GEMM (CLIPK_F32S;
+    ``w16``: CLIPK_F32S16, b's lo parts all zero, see split_lo_zero)."""
     _need(a, "A")
     split = a.dtype == torch.float32 and b.dtype == torch.int32
     _need(b, "B", torch.int32 if split else a.dtype)
@@ -68,20 +80,20 @@ def gemm(a, b, epi=N.EPI_NONE, out_dtype=torch.float32, bias=None, res=None, aux
         _need(res, "res", torch.float32 if out.dtype == torch.float32 else out.dtype)
     if aux is not None:
         _need(aux, "aux")
-    args = (N.F32S if split else DT[a.dtype], DT[out.dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias),
+    args = ((N.F32S16 if w16 else N.F32S) if split else DT[a.dtype], DT[out.dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias),
             _p(res), Nn, _p(out), Nn, _p(out2), _p(aux), DT[aux.dtype] if aux is not None else 0, Nn)
     N.call("clipk_gemm", *args, _stream())
     return (out, out2) if want_out2 else out
 
 
-def gemm_ln(a, b, epi, bias, stats=None, res=None, colsum=None, rnb=None, want_out2=False):
+def gemm_ln(a, b, epi, bias, stats=None, res=None, colsum=None, rnb=None, want_out2=False, w16=False):
     """clipk_gemm_ln (include/clipk.h): 16-bit a[M,K] @ b[N,K]^T with the LayerNorm fold.
     Producer (EPI_BIAS_RES, colsum None): the statistics partials of the output are written to
     stats (fp32 [M, N/64, 2]). Fold (EPI_BIAS / EPI_BIAS_QGELU): a is the LayerNorm input x with
     per-row rnb = (rstd, -rstd * mean) (ln_stats_merge of its partials), b = W diag(gamma),
     bias = b + W beta, colsum = row sums of b. Output in a's dtype. PREC fp32s: a fp32 and b an
     int32 split_pack(...) weight (CLIPK_F32S; colsum summed over the packed value, see
-    clip.model.ln_fold_weights)."""
+    clip.model.ln_fold_weights; ``w16``: CLIPK_F32S16)."""
     _need(a, "A")
     split = a.dtype == torch.float32 and b.dtype == torch.int32
     _need(b, "B", torch.int32 if split else a.dtype)
@@ -95,7 +107,7 @@ def gemm_ln(a, b, epi, bias, stats=None, res=None, colsum=None, rnb=None, want_o
             _need(t, nm, torch.float32)
     if res is not None:
         _need(res, "res", a.dtype)
-    N.call("clipk_gemm_ln", N.F32S if split else DT[a.dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias), _p(res), Nn, _p(out), Nn,
+    N.call("clipk_gemm_ln", (N.F32S16 if w16 else N.F32S) if split else DT[a.dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias), _p(res), Nn, _p(out), Nn,
            _p(out2), _p(stats), _p(colsum), _p(rnb), _stream())
     return (out, out2) if want_out2 else out
 

@@ -40,8 +40,14 @@ extern "C" {
 #endif
 
 /* element types. CLIPK_F32S (GEMM input type only): fp32 activations times a weight packed by
- * clipk_split_pack -- the fp32-class GEMM on 16-bit MFMA of PREC "fp32s" (clipk_gemm) */
-enum { CLIPK_F32 = 0, CLIPK_F16 = 1, CLIPK_BF16 = 2, CLIPK_F32S = 3 };
+ * clipk_split_pack -- the fp32-class GEMM on 16-bit MFMA of PREC "fp32s" (clipk_gemm).
+ * CLIPK_F32S16 (GEMM input type only): CLIPK_F32S for a packed weight whose lo parts are all
+ * zero (clipk_split_lo_zero: W fp16-valued, as every released CLIP checkpoint's weights are --
+ * the reference loads them from the fp16 archive, PromptSRC/clip/clip.py:154-180); the
+ * hi(a) lo(b) product, exactly zero, is skipped: 2 MFMAs per product instead of 3, results
+ * bitwise those of CLIPK_F32S (on the 128x128 tiles, where the 2-MFMA kernel measured not
+ * bit-identical, the 3-MFMA kernel runs). */
+enum { CLIPK_F32 = 0, CLIPK_F16 = 1, CLIPK_BF16 = 2, CLIPK_F32S = 3, CLIPK_F32S16 = 4 };
 
 /* status codes (hipError_t values > 0 pass through) */
 enum {
@@ -104,6 +110,10 @@ int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, int K,
  * fp32 result to ~1e-6 relative. out / res / aux fp32 (epilogues as above). */
 #define CLIPK_SPLIT_SCALE 64.0f
 int clipk_split_pack(int N, int K, const float* W, int ldw, void* out, void* stream);
+/* 1 when every lo part of clipk_split_pack's output `packed` ([N, K] split elements) is zero
+ * (the weight is fp16-valued: CLIPK_F32S16 may multiply it), 0 when not, < 0 on error. One
+ * pass, then a stream synchronisation (checked once per weight, at model construction). */
+int clipk_split_lo_zero(int N, int K, const void* packed, void* stream);
 
 /* Split-K form of clipk_gemm for small M (the ViT at training batch sizes, whose 128x128
  * tile grid would leave most CUs idle): the K range is cut into `splits` slices whose fp32
@@ -384,7 +394,10 @@ int clipk_encoder_set_ln_fold(clipk_encoder* e, const void* const* fold_ptrs);
  * of its calls as CLIPK_F32S (the fp32-class split-fp16 MFMA product). LayerNorm, attention and
  * the residual stream stay fp32. The text backward then runs on s * dtxt with s a power of two
  * from max |dtxt| (exact, undone on dx0 and the deep-prompt gradients), so the gradient operands
- * sit in fp16's normal range. Reference semantics: PromptSRC/clip/model.py:699 (fp32 model). */
+ * sit in fp16's normal range. Reference semantics: PromptSRC/clip/model.py:699 (fp32 model).
+ * on = 2: as 1, and those weights are fp16-valued (clipk_split_lo_zero returned 1 for each; the
+ * released CLIP checkpoints): their GEMMs run CLIPK_F32S16, 2 MFMAs per product, the same results.
+ * The LayerNorm-folded W' (clipk_encoder_set_ln_fold) keep CLIPK_F32S. */
 int clipk_encoder_set_split(clipk_encoder* e, int on);
 /* The split backward's scale target t (default 7): s puts max |s dtxt| in [2^(t-1), 2^t). A lower
  * target leaves more headroom below fp16's 65504 for gradient growth through the layers, at

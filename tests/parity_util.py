@@ -20,12 +20,14 @@ def load_fixture(name):
     return meta, arrays
 
 
-def state_dict(arch):
+def state_dict(arch, fp16_values=False):
+    """The seeded synthetic CLIP (fp16_values: rounded to fp16 as the released checkpoints)."""
     from fsp_amd.clip import synth
-    if arch not in _SD_CACHE:
+    key = (arch, fp16_values)
+    if key not in _SD_CACHE:
         _SD_CACHE.clear()
-        _SD_CACHE[arch] = synth.make_state_dict(arch, seed=0)
-    return _SD_CACHE[arch]
+        _SD_CACHE[key] = synth.make_state_dict(arch, seed=0, fp16_values=fp16_values)
+    return _SD_CACHE[key]
 
 
 def make_cfg(meta, prec, cocoop=False, truncate=True, shared=True):
@@ -56,7 +58,7 @@ def make_cfg(meta, prec, cocoop=False, truncate=True, shared=True):
     return cfg
 
 
-def run_native(meta, arrays, prec, cocoop=False, dev="cuda", truncate=True, shared=True):
+def run_native(meta, arrays, prec, cocoop=False, dev="cuda", truncate=True, shared=True, fp16_values=False):
     """Returns dict with image_features, logits, loss, grads, ctx_after_step (numpy)."""
     from fsp_amd.clip import synth
     from fsp_amd.clip.model import build_model
@@ -64,12 +66,13 @@ def run_native(meta, arrays, prec, cocoop=False, dev="cuda", truncate=True, shar
     from fsp_amd.trainers import coop as C, cocoop as CC
     a = synth.ARCHS[meta["arch"]]
     cfg = make_cfg(meta, prec, cocoop, truncate, shared)
-    clip = build_model(state_dict(meta["arch"]), prec=prec, device=dev)
+    clip = build_model(state_dict(meta["arch"], fp16_values), prec=prec, device=dev)
     names = synth.synthetic_classnames(meta["n_cls"])
     mod = CC if cocoop else C
     model = mod.CustomCLIP(cfg, names, clip)
     pl = model.prompt_learner
-    out = {"packed": pl.layout.pack is not None, "P": getattr(pl.layout, "P", 0),
+    out = {"split_modes": (getattr(clip.text, "split_mode", None), getattr(clip.visual, "split_mode", None)),
+           "packed": pl.layout.pack is not None, "P": getattr(pl.layout, "P", 0),
            "prefix_input": pl.layout.shape(meta["batch"] if cocoop else 1).prefix_input}
     with torch.no_grad():
         if arrays.get("ctx0") is not None:

@@ -122,11 +122,11 @@ def test_cocoop_full(dev, name, prec, layout):
 _ORACLE_CACHE = {}
 
 
-def _cocoop_oracle(arch, n_cls, batch, seed_img=1):
+def _cocoop_oracle(arch, n_cls, batch, seed_img=1, fp16_values=False):
     """CPU oracle (pinned by the golden vectors) for a CoCoOp configuration too large for
     a committed fixture ("a photo of a" context, CE): logits, loss, d ctx, d meta_net.
     Cached per configuration (the ViT-B/16 C = 1000 case costs ~5 TFLOP on the host)."""
-    key = (arch, n_cls, batch, seed_img)
+    key = (arch, n_cls, batch, seed_img, fp16_values)
     if key in _ORACLE_CACHE:
         return _ORACLE_CACHE[key]
     import torch
@@ -134,7 +134,7 @@ def _cocoop_oracle(arch, n_cls, batch, seed_img=1):
     from fsp_amd.clip import synth
     from fsp_amd.clip.tokenizer import tokenize
     a = synth.ARCHS[arch]
-    p = O.as_torch_sd(synth.make_state_dict(arch, seed=0))
+    p = O.as_torch_sd(synth.make_state_dict(arch, seed=0, fp16_values=fp16_values))
     mp = {k: torch.from_numpy(v).requires_grad_(True)
           for k, v in synth.make_meta_net(a.embed_dim, a.transformer_width, seed=4).items()}
     names = synth.synthetic_classnames(n_cls)
