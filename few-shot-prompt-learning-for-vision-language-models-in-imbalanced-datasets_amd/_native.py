@@ -65,6 +65,7 @@ SIGNATURES = {
     "clipk_gemm_ln": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P]),
     "clipk_ln_stats_merge": (_I, [_I, _I, _P, _P, _P, _P, _P]),
     "clipk_gemm_ln_merge_fused": (_I, [_I, _I, _I, _I]),
+    "clipk_gemm_ln_gamma": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P]),
     "clipk_gemm_ln_merge": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P]),
     "clipk_image_resample": (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P]),
     "clipk_gemm_stamps": (_I, [_P, _S]),

@@ -139,14 +139,24 @@ def ln_fold_enabled() -> bool:
     return os.environ.get("FSP_LN_FOLD", "1") != "0"
 
 
-def ln_fold_weights(w, b, gamma, beta, act, device, split=False):
+def ln_fold_weights(w, b, gamma, beta, act, device, split=False, gamma_on_a=False):
     """LayerNorm folded into the Linear that consumes it (include/clipk.h, clipk_gemm_ln):
     LN(x) W^T + b = rstd * (x W'^T - mean * s) + c with W' = W diag(gamma) in the operand dtype,
     s = W' summed over its input dimension (of the rounded W'), c = b + W beta.
     ``split`` (PREC fp32s): W' fp32, split-packed (ops.split_pack), and s summed over the value
     the split GEMM multiplies by, (hi + lo) / SPLIT_SCALE, so the mean term cancels against it.
+    ``gamma_on_a`` (split mode 2, clipk_gemm_ln_gamma): B = W itself, split-packed, gamma applied
+    to A in the kernel; s = rowsums of W diag(gamma) over W's packed value.
     Returns (W', s, c) on ``device``, or None when W' does not fit the operand dtype."""
     wd = w.double()
+    if gamma_on_a:
+        x = w.float() * N.SPLIT_SCALE
+        hi = x.half().float()
+        lo = (x - hi).half().float()
+        s = (((hi.double() + lo.double()) / N.SPLIT_SCALE) * gamma.double()[None, :]).sum(1).float()
+        c = (b.double() + wd @ beta.double()).float()
+        wdev = ops.split_pack(w.float().to(device).contiguous())
+        return (wdev, s.to(device).contiguous(), c.to(device).contiguous())
     wp = (wd * gamma.double()[None, :]).to(act)
     if not bool(torch.isfinite(wp.float()).all()):
         return None
@@ -192,8 +202,10 @@ class TextEncoderCore(_Encoder):
         # LayerNorm fold of ln_1 / ln_2 into in_proj / c_fc (16-bit encoders and PREC fp32s;
         # clipk_encoder_set_ln_fold)
         fold = [] if (act != torch.float32 or split) and ln_fold_enabled() else None
+        params = []
         for i in range(nl):
             p = {k: _t(sd[f"transformer.resblocks.{i}.{k}"]).float() for k in _LAYER_KEYS}
+            params.append(p)
             f32 = lambda x: x.to(self.device, torch.float32).contiguous()
             A = lambda x: _mm_weight(x, self.device, act, split)
             G = lambda x: _mm_weight(x.t(), self.device, grad, split) if with_grad else None
@@ -205,12 +217,6 @@ class TextEncoderCore(_Encoder):
                    G(p["mlp.c_proj.weight"])]
             keep += row
             table += row
-            if fold is not None:
-                f_in = ln_fold_weights(p["attn.in_proj_weight"], p["attn.in_proj_bias"], p["ln_1.weight"],
-                                       p["ln_1.bias"], act, self.device, split)
-                f_fc = ln_fold_weights(p["mlp.c_fc.weight"], p["mlp.c_fc.bias"], p["ln_2.weight"],
-                                       p["ln_2.bias"], act, self.device, split)
-                fold = fold + list(f_in) + list(f_fc) if f_in and f_fc else None
         P = _t(sd["text_projection"]).float()
         head = [_t(sd["ln_final.weight"]).float().to(self.device).contiguous(),
                 _t(sd["ln_final.bias"]).float().to(self.device).contiguous(),
@@ -218,13 +224,24 @@ class TextEncoderCore(_Encoder):
                 _mm_weight(P, self.device, grad, split) if with_grad else None]
         keep += head
         self._keep = keep
+        # PREC fp32s split mode (2: fp16-valued weights, CLIPK_F32S16), decided before the fold:
+        # mode 2 folds gamma into A (clipk_gemm_ln_gamma) so B stays the fp16-valued W
+        self.split_mode = split_mode(keep) if split else 0
+        for p in params:
+            if fold is None:
+                break
+            ga = self.split_mode == 2
+            f_in = ln_fold_weights(p["attn.in_proj_weight"], p["attn.in_proj_bias"], p["ln_1.weight"],
+                                   p["ln_1.bias"], act, self.device, split, gamma_on_a=ga)
+            f_fc = ln_fold_weights(p["mlp.c_fc.weight"], p["mlp.c_fc.bias"], p["ln_2.weight"],
+                                   p["ln_2.bias"], act, self.device, split, gamma_on_a=ga)
+            fold = fold + list(f_in) + list(f_fc) if f_in and f_fc else None
         h = ctypes.c_void_p()
         N.check(N.load().clipk_encoder_create(W, nl, self.heads, self.E, ops.DT[act], ops.DT[grad],
                                               _ptrs(table), _ptrs(head), ctypes.byref(h)),
                 "clipk_encoder_create(text)")
         self.handle = h
         self._status = None
-        self.split_mode = split_mode(keep) if split else 0
         if split:
             N.check(N.load().clipk_encoder_set_split(h, self.split_mode), "clipk_encoder_set_split(text)")
             # overflow flags of the split calls (clipk_encoder_set_status): 1 = a forward's

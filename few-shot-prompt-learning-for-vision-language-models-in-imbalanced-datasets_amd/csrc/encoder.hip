@@ -41,8 +41,9 @@ struct clipk_encoder {
   std::vector<std::array<const void*, 6>> fold;
   // clipk_encoder_set_split: PREC fp32s -- fp32 activations, every GEMM weight split-packed
   // (clipk_split_pack) and every GEMM on the split-fp16 MFMA path (CLIPK_F32S); 2: the weights
-  // given at creation are fp16-valued (clipk_split_lo_zero), their GEMMs run CLIPK_F32S16 (the
-  // LayerNorm-folded W' of clipk_encoder_set_ln_fold stay CLIPK_F32S)
+  // given at creation are fp16-valued (clipk_split_lo_zero), their GEMMs run CLIPK_F32S16; the
+  // LayerNorm fold then takes W itself and applies gamma to A (clipk_gemm_ln_gamma), so it runs
+  // CLIPK_F32S16 too
   int split = 0;
   int split_target = 7;     // the backward's gradient scale puts max |s dtxt| in [2^(t-1), 2^t)
   int* status = nullptr;    // clipk_encoder_set_status: overflow flags of split calls (device)
@@ -481,13 +482,14 @@ static int block_fwd(const clipk_encoder* e, const std::array<const void*, 16>& 
 // ---- LayerNorm fold (clipk_encoder_set_ln_fold; text encoder, 16-bit residual stream)
 static int gemm_ln(int act, int epi, int M, int N, int K, const void* A, const void* B, const float* bias,
                    const void* res, void* o, void* o2, float* stats, const float* colsum, const float* rnb,
-                   hipStream_t st, int prof_cls, const char* site) {
+                   hipStream_t st, int prof_cls, const char* site, const float* gamma = nullptr) {
   const double b = gemm_bytes(act, act, epi, M, N, K, o2 != nullptr, act) + (stats ? (double)M * (N / 64) * 8 : 0.0) +
-                   (rnb ? 8.0 * M : 0.0);
+                   (rnb ? 8.0 * M : 0.0) + (gamma ? 4.0 * K : 0.0);
   ProfScope ps(prof_cls, st, 2.0 * M * N * K, site, b);
-  // PREC fp32s: the split-packed weights; a fold (colsum) multiplies W' = W diag(gamma), which
-  // is not fp16-valued even when W is
-  if (t_split && act == CLIPK_F32) act = t_split == 2 && !colsum ? CLIPK_F32S16 : CLIPK_F32S;
+  // PREC fp32s: the split-packed weights. Split mode 2: every weight fp16-valued (CLIPK_F32S16),
+  // the fold with gamma on A (B = W); mode 1 folds W' = W diag(gamma) into B (CLIPK_F32S)
+  if (t_split && act == CLIPK_F32) act = t_split == 2 ? CLIPK_F32S16 : CLIPK_F32S;
+  if (gamma) return clipk_gemm_ln_gamma(act, epi, M, N, K, A, K, B, K, bias, o, N, o2, colsum, rnb, gamma, st);
   return clipk_gemm_ln(act, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, stats, colsum, rnb, st);
 }
 // mean / rstd (kept for the LayerNorm backward) and the folding GEMM's (rstd, -rstd mean) pairs
@@ -499,10 +501,11 @@ static int ln_merge(int rows, int W, const float* lnst, float* m, float* r, floa
 // (16-bit, the batch-1 text shapes), else the two launches under their own profiling sites
 static int gemm_ln_merged(int act, int epi, int M, int N, int K, const void* A, const void* B, const float* bias,
                           void* o, void* o2, const float* lnst, const float* colsum, float* m, float* r,
-                          float* rnb, hipStream_t st, int prof_cls, const char* site, bool text) {
+                          float* rnb, hipStream_t st, int prof_cls, const char* site, bool text,
+                          const float* gamma = nullptr) {
   if (t_split || act == CLIPK_F32 || !clipk_gemm_ln_merge_fused(act, M, N, K)) {
     TRY(ln_merge(M, K, lnst, m, r, rnb, st, text));
-    return gemm_ln(act, epi, M, N, K, A, B, bias, nullptr, o, o2, nullptr, colsum, rnb, st, prof_cls, site);
+    return gemm_ln(act, epi, M, N, K, A, B, bias, nullptr, o, o2, nullptr, colsum, rnb, st, prof_cls, site, gamma);
   }
   const double b = gemm_bytes(act, act, epi, M, N, K, o2 != nullptr, act) + (double)M * (K / 64) * 8 + 16.0 * M;
   ProfScope ps(prof_cls, st, 2.0 * M * N * K, site, b);
@@ -510,13 +513,14 @@ static int gemm_ln_merged(int act, int epi, int M, int N, int K, const void* A, 
 }
 // attention half: ln_1 statistics of X merged from the partials the previous layer's c_proj
 // epilogue wrote (lnst); the qkv projection reads X itself through the fold
+// (gamma: split mode 2, the fold's LayerNorm weight applied to A, f[0] = W itself)
 static int block_attn_fold(const clipk_encoder* e, const std::array<const void*, 6>& f, const SeqShape& sh,
                            const void* X, void* qkv, void* o, float* lse, float* m1, float* r1, const float* lnst,
-                           float* rnb, hipStream_t st, bool text) {
+                           float* rnb, hipStream_t st, bool text, const float* gamma = nullptr) {
   const int W = e->W, rows = sh.rows, act = e->act;
   TRY(gemm_ln_merged(act, CLIPK_EPI_BIAS, rows, 3 * W, W, X, f[0], (const float*)f[2], qkv, nullptr, lnst,
                      (const float*)f[1], m1, r1, rnb, st, text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE,
-                     text ? "text.qkv_fwd" : "vit.qkv_fwd", text));
+                     text ? "text.qkv_fwd" : "vit.qkv_fwd", text, gamma));
   const double ab = (double)rows * 4 * W * esize(act) + (lse ? 4.0 * rows * e->heads : 0.0);
   ProfScope ps(text ? CLIPK_PROF_ATTN : CLIPK_PROF_NONE, st, 0.0, text ? "text.attn_fwd" : "vit.attn_fwd", ab);
   return attn_fwd(e, sh, qkv, o, lse, st);
@@ -533,7 +537,8 @@ static int block_post_fold(const clipk_encoder* e, const std::array<const void*,
               nullptr, st, pg, text ? "text.out_fwd" : "vit.out_fwd"));
   TRY(gemm_ln_merged(act, CLIPK_EPI_BIAS_QGELU | (h && qgelu_deriv_on() ? CLIPK_QGELU_DERIV : 0), rows, 4 * W, W, Xm,
                      f[3], (const float*)f[5], g, h, lnst, (const float*)f[4], m2, r2, rnb, st,
-                     text ? CLIPK_PROF_GEMM_FC : CLIPK_PROF_NONE, text ? "text.fc_fwd" : "vit.fc_fwd", text));
+                     text ? CLIPK_PROF_GEMM_FC : CLIPK_PROF_NONE, text ? "text.fc_fwd" : "vit.fc_fwd", text,
+                     e->split == 2 ? (const float*)w[6] : nullptr));
   if (stats_next)
     return gemm_ln(act, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo, nullptr, lnst,
                    nullptr, nullptr, st, pg, text ? "text.proj_fwd" : "vit.proj_fwd");
@@ -793,7 +798,8 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
       TRY(block_attn_shared0(e, e->lw[l], sh, rd, cur, t.xn, t.qkv[l], t.o[l], t.lse[l], t.mean1[l], t.rstd1[l],
                              (int*)t.g, st));
     else if (fold && have_stats)
-      TRY(block_attn_fold(e, e->fold[l], sh, cur, t.qkv[l], t.o[l], t.lse[l], m1, r1, t.lnst, t.rnb, st, io.text));
+      TRY(block_attn_fold(e, e->fold[l], sh, cur, t.qkv[l], t.o[l], t.lse[l], m1, r1, t.lnst, t.rnb, st, io.text,
+                          e->split == 2 ? (const float*)e->lw[l][0] : nullptr));
     else
       TRY(block_attn(e, e->lw[l], sh, rd, cur, t.xn, t.qkv[l], t.o[l], t.lse[l], t.mean1[l], t.rstd1[l], st,
                      io.text, io.sk, io.skb));

@@ -60,7 +60,12 @@ struct GemmArgs {
   // LNM 3 (clipk_gemm_ln_merge): the fold reads the producer's partials (lnstats) and merges each
   // row's itself, exactly as clipk_ln_stats_merge; the column-0 tiles write mean / rstd / rnb
   float* lnmean; float* lnrstd; f32x2* lnrnb_out;
+  // LNM 4 (clipk_gemm_ln_gamma, PREC fp32s): LNM 2 with B = W itself and the LayerNorm weight
+  // applied to A instead, x[m, k] * gamma[k] in fp32 before the split (K <= kGammaMax); colsum =
+  // rowsums of W diag(gamma). Keeps W fp16-valued, so the fold runs CLIPK_F32S16's 2 MFMAs
+  const float* lngamma;
 };
+constexpr int kGammaMax = 1024;
 
 // Sum over the aligned 8-lane group (DPP: quad xor 1, quad xor 2, half-row mirror i <-> 7 - i).
 template <int CTRL>
@@ -384,6 +389,8 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
   // PREC fp32s: 4-byte elements (A fp32, B split-packed), staged as fp32; a 128-B K step is
   // one 32-deep k-window read as two 16-B chunks per fragment (2 fq, 2 fq + 1), 3 MFMAs each
   constexpr bool SPLIT = is_split_v<T>, W16 = __is_same(T, f32h);
+  constexpr bool LN_GAMMA = LNM == 4;
+  static_assert(!LN_GAMMA || SPLIT, "gamma-on-A fold: split GEMMs");
   [[maybe_unused]] constexpr bool TWO_TERMS =
       CLIPK_SPLIT_TERMS == 2 && (CLIPK_SPLIT_TERMS_EPI == 0 || EPI == CLIPK_EPI_NONE || EPI == CLIPK_EPI_DQGELU ||
                                  EPI == EPI_DMUL);
@@ -409,8 +416,9 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
   static_assert(BM % RPI == 0 && BN % RPI == 0 && NG >= NW, "tile/wave mismatch");
   static_assert(!AG || BLOCKED, "A-operand QuickGELU path: blocked unit split");
   // (+ 1 KiB: the CLIPK_GEMM_WARM junk area of the 192-row ping-pong loop)
-  __shared__ CLIPK_LDS_ALIGN char smem[DEPTH * STAGE + NW * EPI_SCRATCH +
-                                       (CLIPK_GEMM_WARM > 0 && PP && BM == 192 ? 1024 : 0)];  // one array (see header)
+  constexpr int WARM_B = CLIPK_GEMM_WARM > 0 && PP && BM == 192 ? 1024 : 0;
+  constexpr int GAM_OFF = DEPTH * STAGE + NW * EPI_SCRATCH + WARM_B;  // LNM 4: gamma[K] in LDS
+  __shared__ CLIPK_LDS_ALIGN char smem[GAM_OFF + (LN_GAMMA ? kGammaMax * 4 : 0)];  // one array (see header)
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
@@ -500,6 +508,11 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
   constexpr bool HAS_BIAS = EPI == CLIPK_EPI_BIAS || EPI == CLIPK_EPI_BIAS_RES || epi_qgelu(EPI);
   constexpr bool HAS_EXT = EPI == CLIPK_EPI_BIAS_RES || EPI == CLIPK_EPI_DQGELU || EPI == EPI_DMUL;
 
+  if constexpr (LN_GAMMA) {  // the LayerNorm weight, once per block (before any LDS-DMA is issued)
+    for (int k = threadIdx.x; k < g.K; k += NW * 64) reinterpret_cast<float*>(smem + GAM_OFF)[k] = g.lngamma[k];
+    __syncthreads();
+  }
+  [[maybe_unused]] const float* sgam = reinterpret_cast<const float*>(smem + GAM_OFF);
   set_tile(tile);
   // deep ring: wait until stage kt+1 has landed while `younger` later stages stay in flight
   // (this wave's glds per stage: PERL, or PERL + 1 for the first NREM waves)
@@ -584,7 +597,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
     // LN fold: mean / rstd of the lane's rows, two 16-row groups ahead of their use. (Merging the
     // producer's partials here instead of in clipk_ln_stats_merge -- 2 loads + 2 8-lane sums per
     // row -- measured slower: qkv 86 -> 110 us, c_fc 129 -> 158 us per launch.)
-    constexpr bool LN_IN = LNM == 2 || LNM == 3, LN_OUT = LNM == 1, LN_MERGE = LNM == 3;
+    constexpr bool LN_IN = LNM == 2 || LNM == 3 || LNM == 4, LN_OUT = LNM == 1, LN_MERGE = LNM == 3;
     // LN_MERGE: 16-bit out (8 lanes per row = the 8 partials of W = 512: lane ec merges partial
     // ec, the merge kernel's lane map and DPP order, so the same bits) on the 192-row ping-pong
     // tiles, whose free residual ring holds the tile's partials (loaded at the tile's start)
@@ -684,6 +697,8 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       };
       constexpr int NFB = CLIPK_GEMM_PPB0 ? 2 : 1;
       u32x4 fa[KK][TM2], fbs[NFB][KK][TN2];
+      int kga = 0;  // LNM 4: the absolute K step whose A fragments rd_a reads
+      [[maybe_unused]] f32x4 gam[2];
       auto rd_a = [&](int buf, int h) {
         const char* As = smem + buf * STAGE + (wm * (BM / WM) + h * (BM / WM / 2) + fr) * ROWB;
 #pragma unroll
@@ -691,6 +706,10 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
 #pragma unroll
           for (int i = 0; i < TM2; ++i)
             fa[kk][i] = *reinterpret_cast<const u32x4*>(As + i * 16 * ROWB + (((SPLIT ? 2 * fq + kk : kk * 4 + fq)) ^ sw) * 16);
+        if constexpr (LN_GAMMA) {  // gamma of the lane's 8 k (chunks 2 fq, 2 fq + 1 of the step)
+          gam[0] = *reinterpret_cast<const f32x4*>(sgam + kga * 32 + 8 * fq);
+          gam[1] = *reinterpret_cast<const f32x4*>(sgam + kga * 32 + 8 * fq + 4);
+        }
       };
       auto rd_b = [&](int buf, int q) {
         const char* Bs = smem + buf * STAGE + OPA + (wn * (BN / WN) + q * (BN / WN / 2) + fr) * ROWB;
@@ -727,7 +746,13 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       auto split_a = [&]() {
         if constexpr (SPLIT) {
 #pragma unroll
-          for (int i = 0; i < TM2; ++i) split8(fa[0][i], fa[1][i], fa[0][i], fa[1][i]);
+          for (int i = 0; i < TM2; ++i) {
+            if constexpr (LN_GAMMA) {
+              fa[0][i] = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, fa[0][i]) * gam[0]);
+              fa[1][i] = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, fa[1][i]) * gam[1]);
+            }
+            split8(fa[0][i], fa[1][i], fa[0][i], fa[1][i]);
+          }
         }
       };
       auto seg_end = [&](bool new_a = false) {  // memory segment done: fragments in registers, then the barrier
@@ -777,6 +802,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       if constexpr (PP2)
       for (int kt = 0; kt < nkc; ++kt, ++it) {
         const int b = it & 1;
+        kga = kt0c + kt;
         const bool in1 = kt + 1 < nkc, in2 = kt + 2 < nkc;
         const bool h1 = in1 || has_next, h2 = in2 || has_next;
         const int k1 = in1 ? kt0c + kt + 1 : kt0n + kt + 1 - nkc, k2 = in2 ? kt0c + kt + 2 : kt0n + kt + 2 - nkc;
@@ -813,6 +839,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
       else
       for (int kt = 0; kt < nkc; ++kt, ++it) {
         const int b = it & 1;
+        kga = kt0c + kt;
         const bool in1 = kt + 1 < nkc, in2 = kt + 2 < nkc;
         const bool h1 = in1 || has_next, h2 = in2 || has_next;
         const int k1 = in1 ? kt0c + kt + 1 : kt0n + kt + 1 - nkc, k2 = in2 ? kt0c + kt + 2 : kt0n + kt + 2 - nkc;
@@ -885,11 +912,20 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
           bh[j] = *reinterpret_cast<const u32x4*>(Bs + j * 16 * ROWB + p0);
           bl[j] = *reinterpret_cast<const u32x4*>(Bs + j * 16 * ROWB + p1);
         }
+        [[maybe_unused]] f32x4 gm0, gm1;
+        if constexpr (LN_GAMMA) {
+          gm0 = *reinterpret_cast<const f32x4*>(sgam + (kt0 + kt) * 32 + 8 * fq);
+          gm1 = *reinterpret_cast<const f32x4*>(sgam + (kt0 + kt) * 32 + 8 * fq + 4);
+        }
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-          u32x4 ah, al;
-          split8(*reinterpret_cast<const u32x4*>(As + i * 16 * ROWB + p0),
-                 *reinterpret_cast<const u32x4*>(As + i * 16 * ROWB + p1), ah, al);
+          u32x4 ah, al, x0 = *reinterpret_cast<const u32x4*>(As + i * 16 * ROWB + p0),
+                        x1 = *reinterpret_cast<const u32x4*>(As + i * 16 * ROWB + p1);
+          if constexpr (LN_GAMMA) {
+            x0 = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, x0) * gm0);
+            x1 = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, x1) * gm1);
+          }
+          split8(x0, x1, ah, al);
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = mma_split<TWO_TERMS, W16>(bh[j], bl[j], ah, al, acc[i][j]);
         }
@@ -1565,6 +1601,11 @@ static int dispatch_ln(int epi, const GemmArgs& g, hipStream_t st) {
 template <typename TS>
 static int dispatch_ln_split(int epi, const GemmArgs& g, hipStream_t st) {
   if (!g.colsum) return launch_gemm_split<CLIPK_EPI_BIAS_RES, 1, TS>(g, st);
+  if (g.lngamma) {  // clipk_gemm_ln_gamma
+    if (epi == CLIPK_EPI_BIAS) return launch_gemm_split<CLIPK_EPI_BIAS, 4, TS>(g, st);
+    if (epi == EPI_QGELU_D) return launch_gemm_split<EPI_QGELU_D, 4, TS>(g, st);
+    return launch_gemm_split<CLIPK_EPI_BIAS_QGELU, 4, TS>(g, st);
+  }
   if (epi == CLIPK_EPI_BIAS) return launch_gemm_split<CLIPK_EPI_BIAS, 2, TS>(g, st);
   if (epi == EPI_QGELU_D) return launch_gemm_split<EPI_QGELU_D, 2, TS>(g, st);
   return launch_gemm_split<CLIPK_EPI_BIAS_QGELU, 2, TS>(g, st);
@@ -1600,6 +1641,27 @@ extern "C" int clipk_gemm_ln(int in_dtype, int epi, int M, int N, int K, const v
   if (in_dtype == CLIPK_F32S) return dispatch_ln_split<f32s>(epi, g, st);
   if (in_dtype == CLIPK_F32S16) return dispatch_ln_split<f32h>(epi, g, st);
   return in_dtype == CLIPK_F16 ? dispatch_ln<f16>(epi, g, st) : dispatch_ln<bf16>(epi, g, st);
+}
+
+// the fold with the LayerNorm weight on A (LNM 4; include/clipk.h): PREC fp32s only
+extern "C" int clipk_gemm_ln_gamma(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B,
+                                   int ldb, const float* bias, void* out, int ldo, void* out2, const float* colsum,
+                                   const float* rnb, const float* gamma, void* stream) {
+  if (!A || !B || !out || !bias || !colsum || !rnb || !gamma) return CLIPK_EINVAL;
+  if (in_dtype != CLIPK_F32S && in_dtype != CLIPK_F32S16) return CLIPK_EDTYPE;
+  const bool deriv = (epi & CLIPK_QGELU_DERIV) != 0;
+  epi &= ~CLIPK_QGELU_DERIV;
+  if (epi != CLIPK_EPI_BIAS && epi != CLIPK_EPI_BIAS_QGELU) return CLIPK_EINVAL;
+  if (deriv && epi != CLIPK_EPI_BIAS_QGELU) return CLIPK_EINVAL;
+  if (M <= 0) return M == 0 ? CLIPK_OK : CLIPK_ESHAPE;
+  if (N <= 0 || K <= 0 || K > kGammaMax || N % GEMM_NMIN != 0 || (K * 4) % GEMM_ROWB != 0) return CLIPK_ESHAPE;
+  if (lda < K || ldb != K || lda % 8 || ldo < N || ldo % 8) return CLIPK_ESHAPE;
+  GemmArgs g{(const char*)A, (const char*)B, M, N, K, lda, ldb, bias, nullptr, 0, out, ldo, out2, nullptr,
+             0, nullptr, 1, 0, 0, nullptr, colsum, reinterpret_cast<const f32x2*>(rnb)};
+  g.lngamma = gamma;
+  hipStream_t st = (hipStream_t)stream;
+  if (deriv) epi = EPI_QGELU_D;
+  return in_dtype == CLIPK_F32S16 ? dispatch_ln_split<f32h>(epi, g, st) : dispatch_ln_split<f32s>(epi, g, st);
 }
 
 namespace clipk {

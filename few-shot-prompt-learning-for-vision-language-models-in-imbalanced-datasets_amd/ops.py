@@ -112,6 +112,23 @@ def gemm_ln(a, b, epi, bias, stats=None, res=None, colsum=None, rnb=None, want_o
     return (out, out2) if want_out2 else out
 
 
+def gemm_ln_gamma(a, b, epi, bias, colsum, rnb, gamma, want_out2=False, w16=False):
+    """clipk_gemm_ln_gamma (PREC fp32s): the LayerNorm fold with gamma applied to A: a fp32 x,
+    b = split_pack(W) (W itself), colsum = rowsums of W diag(gamma), bias = b + W beta, rnb =
+    (rstd, -rstd * mean) per row; ``w16``: CLIPK_F32S16 (W fp16-valued)."""
+    _need(a, "A", torch.float32)
+    _need(b, "B", torch.int32)
+    M, K = a.shape
+    Nn = b.shape[0]
+    out = torch.empty(M, Nn, device=a.device, dtype=torch.float32)
+    out2 = torch.empty_like(out) if want_out2 else None
+    for t, nm in ((bias, "bias"), (colsum, "colsum"), (rnb, "rnb"), (gamma, "gamma")):
+        _need(t, nm, torch.float32)
+    N.call("clipk_gemm_ln_gamma", N.F32S16 if w16 else N.F32S, epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias),
+           _p(out), Nn, _p(out2), _p(colsum), _p(rnb), _p(gamma), _stream())
+    return (out, out2) if want_out2 else out
+
+
 def gemm_ln_merge(a, b, epi, bias, stats, colsum, want_out2=False):
     """clipk_gemm_ln_merge: ln_stats_merge(stats, K) then the fold gemm_ln(a, b, epi, bias,
     colsum=colsum, rnb=...), as one launch where the library covers the shape. Returns

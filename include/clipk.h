@@ -144,6 +144,14 @@ int clipk_gemm_splitk(int in_dtype, int out_dtype, int epi, int M, int N, int K,
  * clipk_ln_stats_merge turns a producer's partials (width / 64 per row) into any of mean, rstd
  * (fp32 [rows]) and rnb (exact pairwise merge in a fixed order, eps 1e-5). Shape constraints as
  * clipk_gemm. */
+/* The fold with the LayerNorm weight on A (PREC fp32s, in_dtype CLIPK_F32S / CLIPK_F32S16; the
+ * consumer form of clipk_gemm_ln): A = x fp32 [M, K] (K <= 1024), B = W packed (ldb == K), each
+ * x[m, k] * gamma[k] rounded to fp32 before its split; colsum = rowsums of W diag(gamma) over the
+ * packed value / 64 (fp32 [N]), bias = b + W beta, rnb as in clipk_gemm_ln. Keeps an fp16-valued
+ * W fp16-valued, so CLIPK_F32S16's 2 MFMAs per product apply to the folded GEMMs too. */
+int clipk_gemm_ln_gamma(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B, int ldb,
+                        const float* bias, void* out, int ldo, void* out2, const float* colsum, const float* rnb,
+                        const float* gamma, void* stream);
 int clipk_gemm_ln(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B, int ldb,
                   const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
                   float* stats, const float* colsum, const float* rnb, void* stream);
@@ -397,7 +405,9 @@ int clipk_encoder_set_ln_fold(clipk_encoder* e, const void* const* fold_ptrs);
  * sit in fp16's normal range. Reference semantics: PromptSRC/clip/model.py:699 (fp32 model).
  * on = 2: as 1, and those weights are fp16-valued (clipk_split_lo_zero returned 1 for each; the
  * released CLIP checkpoints): their GEMMs run CLIPK_F32S16, 2 MFMAs per product, the same results.
- * The LayerNorm-folded W' (clipk_encoder_set_ln_fold) keep CLIPK_F32S. */
+ * With a LayerNorm fold (clipk_encoder_set_ln_fold after this call) the fold tables then hold W
+ * itself (packed) instead of W' = W diag(gamma), s = rowsums of W diag(gamma) over the packed
+ * values / 64, and the fold GEMMs apply the layer's LayerNorm weight to A (clipk_gemm_ln_gamma). */
 int clipk_encoder_set_split(clipk_encoder* e, int on);
 /* The split backward's scale target t (default 7): s puts max |s dtxt| in [2^(t-1), 2^t). A lower
  * target leaves more headroom below fp16's 65504 for gradient growth through the layers, at

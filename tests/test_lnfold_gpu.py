@@ -217,6 +217,52 @@ def test_gemm_ln_fold_split(dev, epi, Mr, Wd, Nn):
     assert e_fold <= 2.0 * amp * e_unf + 2e-6, f"fold {e_fold:.3e} vs un-fused {e_unf:.3e} (amp {amp:.2f})"
 
 
+@pytest.mark.parametrize("w16", [False, True])
+@pytest.mark.parametrize("epi", [N.EPI_BIAS, N.EPI_BIAS_QGELU])
+@pytest.mark.parametrize("Mr,Wd,Nn", [(47160, 512, 1536), (8000, 512, 2048), (300, 512, 2048), (3, 512, 1536),
+                                      (5000, 768, 2304)])
+def test_gemm_ln_gamma_split(dev, epi, Mr, Wd, Nn, w16):
+    """PREC fp32s fold with the LayerNorm weight on A (clipk_gemm_ln_gamma: B = W itself, x * gamma
+    in fp32 before the split), on an fp16-valued W (split mode 2's weights; w16: CLIPK_F32S16,
+    bitwise the 3-MFMA form on the tiles it runs on): the gates of test_gemm_ln_fold_split against
+    the fp64 LayerNorm -> Linear, on every tile path (ping-pong, 128x128, 64x128)."""
+    g = torch.Generator(device="cpu").manual_seed(Mr * 7 + Wd + Nn + epi)
+    x = torch.randn(Mr, Wd, generator=g) + 2.0 * torch.randn(Mr, 1, generator=g)
+    x[:, 5] *= 30.0
+    x = x.to(dev)
+    gamma = (1.0 + 0.2 * torch.randn(Wd, generator=g)).to(dev)
+    beta = (0.1 * torch.randn(Wd, generator=g)).to(dev)
+    w = (torch.randn(Nn, Wd, generator=g) / math.sqrt(Wd)).half().float().to(dev)
+    bias = (0.05 * torch.randn(Nn, generator=g)).to(dev)
+    wp, s, c = M.ln_fold_weights(w.cpu(), bias.cpu(), gamma.cpu(), beta.cpu(), torch.float32, dev, split=True,
+                                 gamma_on_a=True)
+    assert ops.split_lo_zero(wp)
+    xd = x.double()
+    ref = F.layer_norm(xd, (Wd,), gamma.double(), beta.double(), eps=1e-5) @ w.double().t() + bias.double()
+    xn = ops.layernorm(x, gamma, beta, out_dtype=torch.float32)
+    _, _, rnb = ops.ln_stats_merge(partials(x), Wd)
+    if epi == N.EPI_BIAS:
+        out = ops.gemm_ln_gamma(x, wp, epi, c, s, rnb, gamma, w16=w16)
+        unf = ops.gemm(xn, wp, N.EPI_BIAS, torch.float32, bias=bias)
+        e_fold, e_unf = _rel(out, ref), _rel(unf, ref)
+    else:
+        ref_g = ref * torch.sigmoid(1.702 * ref)
+        out, d = ops.gemm_ln_gamma(x, wp, epi | N.QGELU_DERIV, c, s, rnb, gamma, want_out2=True, w16=w16)
+        unf = ops.gemm(xn, wp, N.EPI_BIAS_QGELU, torch.float32, bias=bias)
+        sg = torch.sigmoid(1.702 * ref)
+        e_fold = max(_rel(out, ref_g), _rel(d, sg * (1 + 1.702 * ref * (1 - sg))))
+        e_unf = _rel(unf, ref_g)
+    if w16:  # the 2-MFMA form equals the 3-MFMA one
+        o3 = ops.gemm_ln_gamma(x, wp, epi, c, s, rnb, gamma)
+        o2 = out if epi == N.EPI_BIAS else ops.gemm_ln_gamma(x, wp, epi, c, s, rnb, gamma, w16=True)
+        assert torch.equal(o2, o3)
+    mu, var = xd.mean(1), xd.var(1, unbiased=False)
+    amp = float(torch.sqrt(1 + mu * mu / var).max())
+    print(f"gamma fold {Mr}x{Nn}x{Wd} w16={w16}: {e_fold:.2e} (un-fused {e_unf:.2e}, amp {amp:.2f})")
+    assert e_fold <= 2e-5, f"fold rel err {e_fold:.3e}"
+    assert e_fold <= 2.0 * amp * e_unf + 2e-6, f"fold {e_fold:.3e} vs un-fused {e_unf:.3e} (amp {amp:.2f})"
+
+
 def _encoder_pair(arch, prec, dev):
     sd = synth.make_state_dict(arch, seed=0)
     a = synth.ARCHS[arch]

@@ -88,8 +88,9 @@ def test_w16_on_fp32_weights_is_the_rounded_weight(dev):
     assert torch.equal(got, want)  # 300 rows: the 64x128 tiles, where the 2-MFMA kernel runs
 
 
-def _cocoop_c1000_b2(dev, fp16_values, monkeypatch, w16):
+def _cocoop_c1000_b2(dev, fp16_values, monkeypatch, w16, fold=True):
     monkeypatch.setenv("FSP_SPLIT_W16", "1" if w16 else "0")
+    monkeypatch.setenv("FSP_LN_FOLD", "1" if fold else "0")
     meta = {"arch": "ViT-B/16", "n_cls": 1000, "batch": 2, "n_ctx": 4, "ctx_init": "a photo of a", "focal": 0}
     return run_native(meta, {"ctx0": None, "tokenized": None}, "fp32s", cocoop=True, dev=str(dev),
                       fp16_values=fp16_values)
@@ -97,11 +98,12 @@ def _cocoop_c1000_b2(dev, fp16_values, monkeypatch, w16):
 
 def test_cocoop_headline_w16_bitwise(dev, monkeypatch):
     """The headline shape (CoCoOp ViT-B/16, C = 1000, B = 2, packed rows) in PREC fp32s on
-    fp16-valued weights: the encoders pick split mode 2 (CLIPK_F32S16 for every GEMM but the
-    LayerNorm-folded ones), and logits, loss, image features and every gradient are bitwise those
-    of split mode 1 (FSP_SPLIT_W16=0). On fp32-valued weights mode 1 stays."""
-    out2 = _cocoop_c1000_b2(dev, True, monkeypatch, True)
-    out1 = _cocoop_c1000_b2(dev, True, monkeypatch, False)
+    fp16-valued weights, without the LayerNorm fold (whose mode-2 form, gamma on A, rounds
+    differently from mode 1's W diag(gamma): test_cocoop_headline_w16_vs_oracle): the encoders pick
+    split mode 2 (CLIPK_F32S16 for every GEMM), and logits, loss, image features and every gradient
+    are bitwise those of split mode 1 (FSP_SPLIT_W16=0). On fp32-valued weights mode 1 stays."""
+    out2 = _cocoop_c1000_b2(dev, True, monkeypatch, True, fold=False)
+    out1 = _cocoop_c1000_b2(dev, True, monkeypatch, False, fold=False)
     assert out2["split_modes"] == (2, 2), out2["split_modes"]
     assert out1["split_modes"] == (1, 1), out1["split_modes"]
     for k in out1:
@@ -113,7 +115,8 @@ def test_cocoop_headline_w16_bitwise(dev, monkeypatch):
 
 
 def test_cocoop_headline_w16_vs_oracle(dev, monkeypatch):
-    """The same step against the CPU oracle run on the same fp16-valued weights: the fp32 gates."""
+    """The same step with the LayerNorm fold (mode 2: gamma on A, every GEMM CLIPK_F32S16) against
+    the CPU oracle run on the same fp16-valued weights: the fp32 gates."""
     from test_parity_gpu import _cocoop_oracle
     ref = _cocoop_oracle("ViT-B/16", 1000, 2, fp16_values=True)
     out = _cocoop_c1000_b2(dev, True, monkeypatch, True)
