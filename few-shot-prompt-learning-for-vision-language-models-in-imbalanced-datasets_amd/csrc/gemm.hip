@@ -1311,8 +1311,15 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
 // picks the 192- or 256-row tiles): the ping-pong loop on 192x256 tiles (256-row ones spill at
 // 256 VGPRs with the split's temporaries); otherwise 128x128 tiles (a 4-slot ring when the grid
 // is at most one tile per CU).
+// CLIPK_F32S16 runs the 2-MFMA kernel on the 192x256 ping-pong tiles only. On the other tile
+// paths (64x128, 128x128: the 2- / 4-slot loop) the 2-MFMA kernel measured not bit-identical to
+// the 3-MFMA one on some shapes and fold variants (up to 5e-2 relative at 4k-8k rows, varying run
+// to run, while the 3-MFMA, fp16 and bf16 kernels match the 2-slot loop bit for bit;
+// profiles/r05w16/ring.txt, tests_gamma.txt), cause not found -- so those paths keep the 3-MFMA
+// kernel (TB), where the weight-lo product adds exact zeros: the same results either way.
 template <int EPI, int LNM = 0, typename TS = f32s>
 static int launch_gemm_split(const GemmArgs& g, hipStream_t st) {
+  using TB = typename std::conditional<__is_same(TS, f32h), f32s, TS>::type;
   const int cus = num_cus();
   const_cast<GemmArgs&>(g).stamp = gemm_stamp_buf();
   const_cast<GemmArgs&>(g).skew = 0;
@@ -1320,10 +1327,10 @@ static int launch_gemm_split(const GemmArgs& g, hipStream_t st) {
   if (cfg == 7) {  // small M (the ViT): 64x128 tiles, twice the 128x128 grid
     const int nwg = ((g.M + 63) / 64) * (g.N / 128);
     if (nwg <= cus && deep_small())
-      hipLaunchKernelGGL((gemm_nt_kernel<TS, float, float, EPI, 64, 128, 2, 2, false, GEMM_ROWB, 4, false, false, LNM>), dim3(nwg),
+      hipLaunchKernelGGL((gemm_nt_kernel<TB, float, float, EPI, 64, 128, 2, 2, false, GEMM_ROWB, 4, false, false, LNM>), dim3(nwg),
                          dim3(256), 0, st, g);
     else
-      hipLaunchKernelGGL((gemm_nt_kernel<TS, float, float, EPI, 64, 128, 2, 2, false, GEMM_ROWB, 2, false, false, LNM>), dim3(nwg),
+      hipLaunchKernelGGL((gemm_nt_kernel<TB, float, float, EPI, 64, 128, 2, 2, false, GEMM_ROWB, 2, false, false, LNM>), dim3(nwg),
                          dim3(256), 0, st, g);
     CLIPK_CHECK_LAUNCH();
     return CLIPK_OK;
@@ -1334,12 +1341,6 @@ static int launch_gemm_split(const GemmArgs& g, hipStream_t st) {
       return CLIPK_OK;
     }
   }
-  // CLIPK_F32S16 keeps the 3-MFMA form on the 128x128 tiles: there the 2-MFMA kernel measured
-  // not bit-identical to it (outputs off by up to 5e-2 relative, varying run to run, while the
-  // 3-MFMA, fp16 and bf16 forms match the 2-slot loop bit for bit; profiles/r05w16/ring.txt),
-  // cause not found -- so CLIPK_F32S16 runs only where it is bitwise CLIPK_F32S (tests/
-  // test_split_w16_gpu.py): the 192x256 ping-pong and the 64x128 tiles
-  using TB = typename std::conditional<__is_same(TS, f32h), f32s, TS>::type;
   const int nwg = ((g.M + 127) / 128) * (g.N / 128);
   if (nwg <= cus && deep_small())
     hipLaunchKernelGGL((gemm_nt_kernel<TB, float, float, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 4, false, false, LNM>), dim3(nwg),

@@ -8,8 +8,9 @@ tools/lab/mfma_zero.hip, profiles/r05w16/mfma_zero.txt). CLIPK_F32S16 skips it. 
 bitwise: every output equals the 3-MFMA form's (torch.equal), GEMM by GEMM and through the whole
 CoCoOp step, and the step is within the fp32 gates of the oracle run on the same fp16-valued
 weights (|d logit| <= 1e-3, gradients rel <= 1e-3). The 2-MFMA kernel runs on the 192x256
-ping-pong and 64x128 tiles only: on the 128x128 tiles it measured not bit-identical (cause not
-found, profiles/r05w16/ring.txt), so CLIPK_F32S16 keeps the 3-MFMA kernel there."""
+ping-pong tiles only: on the 64x128 / 128x128 tiles it measured not bit-identical on some shapes
+(cause not found, profiles/r05w16/ring.txt, tests_gamma.txt), so CLIPK_F32S16 keeps the 3-MFMA
+kernel there."""
 import math
 import os
 
@@ -79,13 +80,13 @@ def test_w16_on_fp32_weights_is_the_rounded_weight(dev):
     prevents (the encoders' split_mode): the lo part is then dropped, i.e. the product is that of
     the weight rounded to fp16 (SPLIT_SCALE * W to fp16)."""
     g = torch.Generator(device="cpu").manual_seed(7)
-    a = torch.randn(300, 512, generator=g).to(dev)
-    b = (torch.randn(512, 512, generator=g) * 0.04).to(dev)
+    a = torch.randn(4600, 512, generator=g).to(dev)  # N = 2048 at 4.6k rows: the ping-pong tiles
+    b = (torch.randn(2048, 512, generator=g) * 0.04).to(dev)
     bp = ops.split_pack(b)
     assert not ops.split_lo_zero(bp)
     want = ops.gemm(a, ops.split_pack((b * N.SPLIT_SCALE).half().float() / N.SPLIT_SCALE), N.EPI_NONE)
     got = ops.gemm(a, bp, N.EPI_NONE, w16=True)
-    assert torch.equal(got, want)  # 300 rows: the 64x128 tiles, where the 2-MFMA kernel runs
+    assert torch.equal(got, want)
 
 
 def _cocoop_c1000_b2(dev, fp16_values, monkeypatch, w16, fold=True):
