@@ -123,6 +123,14 @@ __device__ __forceinline__ unsigned split_lo2(float a, float b, unsigned h) {
       : "v"(a), "v"(b), "v"(h));
   return l;
 }
+// MIX false: the lo part in compiler-visible cvt + sub + cvt form. The v_fma_mix pair is inline
+// asm, whose VGPR writes the compiler's hazard tracking does not see: an MFMA that reads them a
+// few instructions later (the 2- / 4-slot loop, where splits and MFMAs interleave) can read
+// stale values -- measured: the 2-MFMA split kernel on the 128x128 tiles off by up to 5e-2 at
+// 4k-8k rows, bit-exact with this form or with s_nop 7 after the split
+// (profiles/r05w16/hazard.txt). The ping-pong loop splits in its memory segment, a barrier
+// before the MFMAs that read the parts, and keeps the cheaper asm form.
+template <bool MIX = CLIPK_SPLIT_MIX != 0>
 __device__ __forceinline__ void split8(u32x4 a0, u32x4 a1, u32x4& hi, u32x4& lo) {
   const f32x4 x0 = __builtin_bit_cast(f32x4, a0), x1 = __builtin_bit_cast(f32x4, a1);
   f16x8 h;
@@ -132,16 +140,16 @@ __device__ __forceinline__ void split8(u32x4 a0, u32x4 a1, u32x4& hi, u32x4& lo)
     h[4 + c] = (f16)x1[c];
   }
   hi = __builtin_bit_cast(u32x4, h);
-#if CLIPK_SPLIT_MIX == 0  // A/B knob: the cvt + sub + cvt form
-  f16x8 l;
+  if constexpr (!MIX) {  // (also the A/B knob CLIPK_SPLIT_MIX=0 everywhere)
+    f16x8 l;
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    l[c] = (f16)(x0[c] - (float)h[c]);
-    l[4 + c] = (f16)(x1[c] - (float)h[4 + c]);
+    for (int c = 0; c < 4; ++c) {
+      l[c] = (f16)(x0[c] - (float)h[c]);
+      l[4 + c] = (f16)(x1[c] - (float)h[4 + c]);
+    }
+    lo = __builtin_bit_cast(u32x4, l);
+    return;
   }
-  lo = __builtin_bit_cast(u32x4, l);
-  return;
-#endif
   lo[0] = split_lo2(x0[0], x0[1], hi[0]);
   lo[1] = split_lo2(x0[2], x0[3], hi[1]);
   lo[2] = split_lo2(x1[0], x1[1], hi[2]);
@@ -161,12 +169,9 @@ __device__ __forceinline__ void split8(u32x4 a0, u32x4 a1, u32x4& hi, u32x4& lo)
 #endif
 // W16 (CLIPK_F32S16): lo(b) is zero, so the hi(a) lo(b) product adds exact zeros and is skipped
 // (the compiler then drops the lo(b) fragment reads from LDS too)
-#ifndef CLIPK_W16_SKIP  // diagnostic (A/B): 0 keeps the zero product in the CLIPK_F32S16 kernels
-#define CLIPK_W16_SKIP 1
-#endif
 template <bool TWO = false, bool W16 = false>
 __device__ __forceinline__ f32x4 mma_split(u32x4 bh, u32x4 bl, u32x4 ah, u32x4 al, f32x4 c) {
-  if constexpr (!W16 || !CLIPK_W16_SKIP)
+  if constexpr (!W16)
     c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, bl), __builtin_bit_cast(f16x8, ah), c, 0, 0, 0);
   if constexpr (!TWO)
     c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, bh), __builtin_bit_cast(f16x8, al), c, 0, 0, 0);
@@ -925,7 +930,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
             x0 = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, x0) * gm0);
             x1 = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, x1) * gm1);
           }
-          split8(x0, x1, ah, al);
+          split8<false>(x0, x1, ah, al);  // MFMAs follow within a few instructions
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = mma_split<TWO_TERMS, W16>(bh[j], bl[j], ah, al, acc[i][j]);
         }
@@ -1311,15 +1316,11 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
 // picks the 192- or 256-row tiles): the ping-pong loop on 192x256 tiles (256-row ones spill at
 // 256 VGPRs with the split's temporaries); otherwise 128x128 tiles (a 4-slot ring when the grid
 // is at most one tile per CU).
-// CLIPK_F32S16 runs the 2-MFMA kernel on the 192x256 ping-pong tiles only. On the other tile
-// paths (64x128, 128x128: the 2- / 4-slot loop) the 2-MFMA kernel measured not bit-identical to
-// the 3-MFMA one on some shapes and fold variants (up to 5e-2 relative at 4k-8k rows, varying run
-// to run, while the 3-MFMA, fp16 and bf16 kernels match the 2-slot loop bit for bit;
-// profiles/r05w16/ring.txt, tests_gamma.txt), cause not found -- so those paths keep the 3-MFMA
-// kernel (TB), where the weight-lo product adds exact zeros: the same results either way.
+// (Until the split8 hazard above was found, CLIPK_F32S16 ran the 2-MFMA kernel on the ping-pong
+// tiles only: on the 2- / 4-slot loop it measured not bit-identical. With the compiler-visible
+// split there it is bitwise the 3-MFMA kernel on every tile path, profiles/r05w16/hazard.txt.)
 template <int EPI, int LNM = 0, typename TS = f32s>
 static int launch_gemm_split(const GemmArgs& g, hipStream_t st) {
-  using TB = typename std::conditional<__is_same(TS, f32h), f32s, TS>::type;
   const int cus = num_cus();
   const_cast<GemmArgs&>(g).stamp = gemm_stamp_buf();
   const_cast<GemmArgs&>(g).skew = 0;
@@ -1327,10 +1328,10 @@ static int launch_gemm_split(const GemmArgs& g, hipStream_t st) {
   if (cfg == 7) {  // small M (the ViT): 64x128 tiles, twice the 128x128 grid
     const int nwg = ((g.M + 63) / 64) * (g.N / 128);
     if (nwg <= cus && deep_small())
-      hipLaunchKernelGGL((gemm_nt_kernel<TB, float, float, EPI, 64, 128, 2, 2, false, GEMM_ROWB, 4, false, false, LNM>), dim3(nwg),
+      hipLaunchKernelGGL((gemm_nt_kernel<TS, float, float, EPI, 64, 128, 2, 2, false, GEMM_ROWB, 4, false, false, LNM>), dim3(nwg),
                          dim3(256), 0, st, g);
     else
-      hipLaunchKernelGGL((gemm_nt_kernel<TB, float, float, EPI, 64, 128, 2, 2, false, GEMM_ROWB, 2, false, false, LNM>), dim3(nwg),
+      hipLaunchKernelGGL((gemm_nt_kernel<TS, float, float, EPI, 64, 128, 2, 2, false, GEMM_ROWB, 2, false, false, LNM>), dim3(nwg),
                          dim3(256), 0, st, g);
     CLIPK_CHECK_LAUNCH();
     return CLIPK_OK;
@@ -1343,10 +1344,10 @@ static int launch_gemm_split(const GemmArgs& g, hipStream_t st) {
   }
   const int nwg = ((g.M + 127) / 128) * (g.N / 128);
   if (nwg <= cus && deep_small())
-    hipLaunchKernelGGL((gemm_nt_kernel<TB, float, float, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 4, false, false, LNM>), dim3(nwg),
+    hipLaunchKernelGGL((gemm_nt_kernel<TS, float, float, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 4, false, false, LNM>), dim3(nwg),
                        dim3(256), 0, st, g);
   else
-    hipLaunchKernelGGL((gemm_nt_kernel<TB, float, float, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 2, false, false, LNM>), dim3(nwg),
+    hipLaunchKernelGGL((gemm_nt_kernel<TS, float, float, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 2, false, false, LNM>), dim3(nwg),
                        dim3(256), 0, st, g);
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
@@ -1851,8 +1852,8 @@ extern "C" int clipk_gemm_splitk(int in_dtype, int out_dtype, int epi, int M, in
       hipLaunchKernelGGL((gemm_nt_kernel<f32s, float, float, CLIPK_EPI_NONE, 128, 128, 2, 2, false>), dim3(nwg),
                          dim3(256), 0, st, p);
       break;
-    case CLIPK_F32S16:  // the 3-MFMA slices (128x128 tiles, see launch_gemm_split)
-      hipLaunchKernelGGL((gemm_nt_kernel<f32s, float, float, CLIPK_EPI_NONE, 128, 128, 2, 2, false>), dim3(nwg),
+    case CLIPK_F32S16:
+      hipLaunchKernelGGL((gemm_nt_kernel<f32h, float, float, CLIPK_EPI_NONE, 128, 128, 2, 2, false>), dim3(nwg),
                          dim3(256), 0, st, p);
       break;
     default: return CLIPK_EDTYPE;

@@ -45,9 +45,7 @@ extern "C" {
  * zero (clipk_split_lo_zero: W fp16-valued, as every released CLIP checkpoint's weights are --
  * the reference loads them from the fp16 archive, PromptSRC/clip/clip.py:154-180); the
  * hi(a) lo(b) product, exactly zero, is skipped: 2 MFMAs per product instead of 3, results
- * bitwise those of CLIPK_F32S. The 2-MFMA kernel runs on the 192x256 ping-pong tiles (the
- * large-M text GEMMs); the smaller tile paths, where it measured not bit-identical, keep the
- * 3-MFMA kernel. */
+ * bitwise those of CLIPK_F32S. */
 enum { CLIPK_F32 = 0, CLIPK_F16 = 1, CLIPK_BF16 = 2, CLIPK_F32S = 3, CLIPK_F32S16 = 4 };
 
 /* status codes (hipError_t values > 0 pass through) */

@@ -7,10 +7,9 @@ split GEMM is exactly zero (a v_mfma whose products are all zero returns C uncha
 tools/lab/mfma_zero.hip, profiles/r05w16/mfma_zero.txt). CLIPK_F32S16 skips it. The bar is
 bitwise: every output equals the 3-MFMA form's (torch.equal), GEMM by GEMM and through the whole
 CoCoOp step, and the step is within the fp32 gates of the oracle run on the same fp16-valued
-weights (|d logit| <= 1e-3, gradients rel <= 1e-3). The 2-MFMA kernel runs on the 192x256
-ping-pong tiles only: on the 64x128 / 128x128 tiles it measured not bit-identical on some shapes
-(cause not found, profiles/r05w16/ring.txt, tests_gamma.txt), so CLIPK_F32S16 keeps the 3-MFMA
-kernel there."""
+weights (|d logit| <= 1e-3, gradients rel <= 1e-3). On every tile path: the 2- / 4-slot loop's
+first 2-MFMA build was off by up to 5e-2 at 4k-8k rows -- an MFMA reading the split's
+inline-asm writes too early (profiles/r05w16/hazard.txt) -- which these cases caught."""
 import math
 import os
 
