@@ -161,6 +161,9 @@ __device__ __forceinline__ void split8(u32x4 a0, u32x4 a1, u32x4& hi, u32x4& lo)
 // lo(a) hi(b) term -- the activation operand rounded to fp16, the weight kept at ~22 bits -- in
 // the GEMMs of epilogue class `CLIPK_SPLIT_TERMS_EPI` (0: every GEMM, 1: the backward's input-grad
 // GEMMs, EPI_NONE / EPI_DMUL / EPI_DQGELU).
+#ifndef CLIPK_PP_SPLIT_NOP  // 0: none; n > 0: s_nop (n - 1) after the ping-pong loop's split (5: measured free, profiles/r05w16/ppnop_*.txt)
+#define CLIPK_PP_SPLIT_NOP 5
+#endif
 #ifndef CLIPK_SPLIT_TERMS
 #define CLIPK_SPLIT_TERMS 3
 #endif
@@ -758,6 +761,9 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
             }
             split8(fa[0][i], fa[1][i], fa[0][i], fa[1][i]);
           }
+          // wait states after the asm split's VGPR writes, independent of the barrier that
+          // follows (A/B knob CLIPK_PP_SPLIT_NOP; see split8)
+          if constexpr (CLIPK_PP_SPLIT_NOP > 0) asm volatile("s_nop %0" ::"n"(CLIPK_PP_SPLIT_NOP - 1));
         }
       };
       auto seg_end = [&](bool new_a = false) {  // memory segment done: fragments in registers, then the barrier
