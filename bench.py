@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Headline benchmark: CoCoOp ViT-B/16 16-shot train-step images/sec (+ eval images/sec)
-on the MI355X-native path (BASELINE.json metric, configs[2]).
+on the MI355X-native path (BASELINE.json metric, configs[2]), at PREC fp32s by default: the
+fp32-class mode that meets the north star's 1e-3 logit bar (the reference computes in fp32,
+PromptSRC/clip/model.py:699). The fp16 mode (|d logit| 0.026, outside that bar) is reported
+beside it as context (``fp16``).
 
     python bench.py --gpus N --steps K --warmup W
     (N > 1 without a torchrun environment: this process starts
@@ -31,8 +34,9 @@ The JSON line also carries (rank 0, N=1 unless noted):
   all-reduce of the prompt gradients), strong scaling of that step;
 * ``config4`` / ``config5`` (N = 1): BASELINE configs 4 (CoOp ViT-L/14 bf16, 32 images/step) and 5
   (CoCoOp ViT-L/14@336px bf16, 8 images/step) per GPU, train and eval images/sec;
-* ``fp32s`` / ``fp32``: the fp32-class precisions (the north-star 1e-3 logit bar) at the headline
-  workload: train over 10 steps, eval over 5,000 images, each with its own roofline;
+* ``fp16`` / ``fp32``: the headline workload at PREC fp16 (16-bit forward and gradients, the
+  fastest mode, outside the 1e-3 bar) and PREC fp32 (f32-input MFMA): train over 10 steps, eval
+  over 50,000 / 5,000 images, each with its own roofline;
 * ``cpu_baseline``: the oracle (fp32 restatement) on the host cores, with nproc stated, and the
   reference's own CPU path at 1,000 classes as measured in the build container
   (tools/ref_cpu_timing.py -> profiles/r03_ref_cpu_timing.jsonl; the reference does not travel
@@ -112,8 +116,11 @@ HBM_PEAK_GBS = 8000.0  # HBM3E, MI355X_MICROARCH.md
 # 3.32 ms in one round-4 run against 2.70 over 50 steps of tools/b1_time.py on the same build)
 B1_STEPS = 50
 # the latest round's PMC passes (tools/pmc_bench.sh), else the previous round's
-PMC_FILE = next((f for f in (os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r05_pmc", "r04_pmc", "r03_pmc"))
-                 if os.path.exists(f)), os.path.join(ROOT, "profiles", "r05_pmc", "traffic.json"))
+PMC_FILES = {  # per PREC: the latest round's PMC passes of that workload (tools/pmc_bench.sh)
+    "fp32s": os.path.join(ROOT, "profiles", "r06_pmc", "traffic.json"),
+    "fp16": next((f for f in (os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r06_pmc_fp16", "r05_pmc"))
+                  if os.path.exists(f)), os.path.join(ROOT, "profiles", "r05_pmc", "traffic.json")),
+}
 
 # kernel classes of the step: launch sites that run the same kernel instantiation (rocprofv3
 # kernel-name key, for the PMC traffic lookup) -- the text GEMMs by role, attention, LN. Each
@@ -139,10 +146,19 @@ KERNELS = {
 # input-grad GEMM, and the last layer's compact EOT-row launches (M = B*C)
 DX_SHAPES = {"fc_dx K=2048": ["text.fc_dx"], "qkv_dx K=1536": ["text.qkv_dx"], "out_dx K=512": ["text.out_dx"],
              "eot fc_dx+out_dx": ["text.fc_dx_eot", "text.out_dx_eot"]}
-ROOF_PMC_KEY = {"gemm_dx_n512": "gemm_nt_kernelIDF16_DF16_fLi4ELi192ELi256",
-                "gemm_dgelu": "gemm_nt_kernelIDF16_DF16_DF16_Li6E",
-                "gemm_proj_fwd": "gemm_nt_kernelIDF16_DF16_DF16_Li1ELi192ELi256ELi2ELi4ELb1ELi128ELi2ELb0ELb1E",
-                "attn_bwd": "attn_prefix_bwd_lds"}
+# rocprofv3 kernel-name keys of a class, per PREC (a class may run several instantiations: fp32s's
+# fc_dx reads its A pre-split, qkv_dx / out_dx do not)
+ROOF_PMC_KEY = {
+    "fp16": {"gemm_dx_n512": "gemm_nt_kernelIDF16_DF16_fLi4ELi192ELi256",
+             "gemm_dgelu": "gemm_nt_kernelIDF16_DF16_DF16_Li6E",
+             "gemm_proj_fwd": "gemm_nt_kernelIDF16_DF16_DF16_Li1ELi192ELi256ELi2ELi4ELb1ELi128ELi2ELb0ELb1E",
+             "attn_bwd": "attn_prefix_bwd_lds"},
+    "fp32s": {"gemm_dx_n512": "gemm_nt_kernelINS_4f32hEffLi4ELi192ELi256ELi2ELi4ELb1E",
+              "gemm_dgelu": "gemm_nt_kernelINS_4f32hEffLi6ELi192ELi256ELi2ELi4ELb1E",
+              "gemm_proj_fwd": "gemm_nt_kernelINS_4f32hEffLi1ELi192ELi256ELi2ELi4ELb1E",
+              "gemm_fc_fwd": "gemm_nt_kernelINS_4f32hEffLi5ELi192ELi256ELi2ELi4ELb1E",
+              "attn_bwd": "attn_prefix_bwd_f32"},
+}
 
 
 def flops(arch, n_cls, L):
@@ -155,17 +171,19 @@ def flops(arch, n_cls, L):
     return f_img, f_txt, b_txt
 
 
-def pmc_traffic(kernel_key):
-    """HBM bytes per launch of a kernel from the committed PMC passes of this workload
-    (tools/pmc_bench.sh: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of bench.py;
-    FETCH_SIZE doubled per the gfx950 note, MI355X_MICROARCH.md HBM). None if absent."""
+def pmc_traffic(kernel_key, prec="fp32s"):
+    """HBM bytes per launch of a kernel class from the committed PMC passes of this workload
+    (tools/pmc_bench.sh: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of bench.py at that
+    PREC; FETCH_SIZE doubled per the gfx950 note, MI355X_MICROARCH.md HBM): the launch-weighted
+    mean over the kernels whose name holds the key. None if absent."""
     try:
-        with open(PMC_FILE) as f:
+        with open(PMC_FILES[prec]) as f:
             d = json.load(f)
-    except OSError:
+    except (OSError, KeyError):
         return None
-    hits = [v["hbm_bytes"] for k, v in d.items() if kernel_key and kernel_key in k]
-    return hits[0] if hits else None
+    hits = [(v["hbm_bytes"], v.get("launches", 1)) for k, v in d.items() if kernel_key and kernel_key in k]
+    n = sum(c for _, c in hits)
+    return round(sum(b * c for b, c in hits) / n, 1) if n else None
 
 
 def cpu_baseline(arch_name, n_ctx_init, n_cls_full, sample_cls, threads):
@@ -270,10 +288,14 @@ def roofline_of(table, prec):
     else:
         ach = fl / avg / 1e12
         r = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4)}
-    r.update({"traffic": pmc_traffic(ROOF_PMC_KEY.get(name)) if prec == "fp16" else None,
+    base = "fp32s" if prec.startswith("fp32s") else prec
+    key = ROOF_PMC_KEY.get(base, {}).get(name)
+    r.update({"traffic": pmc_traffic(key, base) if key else None,
               "kernel_class": name, "kernel": k["kernel"], "avg_launch_ms": k["avg_launch_ms"],
-              "flops_per_launch": fl, "algorithmic_bytes": by,
-              "traffic_note": "HBM bytes/launch, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (" + os.path.relpath(os.path.dirname(PMC_FILE), ROOT) + ")"})
+              "flops_per_launch": fl, "algorithmic_bytes": by})
+    if key and base in PMC_FILES:
+        r["traffic_note"] = ("HBM bytes/launch, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, launch-weighted over the class's "
+                             "kernels (" + os.path.relpath(os.path.dirname(PMC_FILES[base]), ROOT) + ")")
     return r
 
 
@@ -402,6 +424,19 @@ def time_eval(trainer, dm, n_images):
     return dist.sum_over_ranks(n) / te, n
 
 
+# |d logit| of each PREC against the reference's own golden logits at the headline shape
+# (tests/test_parity_gpu.py test_headline_batch8_vs_golden, tests/golden/cocoop_vitb16_c1000_b8.npz)
+LOGIT_ERR = {"fp32s": "2.7e-5", "fp32": "2.7e-5", "fp16": "0.026 (outside the north star's 1e-3)"}
+
+
+def peak_key(prec, trainer):
+    """The PEAK entry a PREC's GEMM FLOPs are priced against: fp32s on fp16-valued weights (split
+    mode 2, CLIPK_F32S16) forms 2 fp16 MFMAs per product, else 3."""
+    if prec == "fp32s" and trainer.model.text_core.split_mode == 2:
+        return "fp32s16"
+    return prec
+
+
 def precision_line(args, prec, dev, rank, world, steps=10, warmup=2, n_eval=5000, prof=True):
     """The headline workload at another PREC: train img/s over `steps` timed steps, eval img/s
     over n_eval distinct resident images, and the roofline of its dominant kernel class
@@ -414,7 +449,7 @@ def precision_line(args, prec, dev, rank, world, steps=10, warmup=2, n_eval=5000
     t, sites = time_train(tr, dm, steps, warmup, prof_steps=2 if prof else 0)
     retries = TextEncoderCore.split_retries - retries0
     # the MFMA peak the dominant class is priced against: 3 or 2 fp16 MFMAs per product
-    pk = "fp32s16" if prec == "fp32s" and tr.model.text_core.split_mode == 2 else prec
+    pk = peak_key(prec, tr)
     table = kernel_table(sites, 2, pk) if sites else None
     e, n = time_eval(tr, dm, n_eval)
     roof = roofline_of(table, pk) if table else None
@@ -422,7 +457,7 @@ def precision_line(args, prec, dev, rank, world, steps=10, warmup=2, n_eval=5000
         roof = {k: roof[k] for k in ("bound", "achieved", "peak", "unit", "frac", "kernel_class", "avg_launch_ms")}
     line = {"images_per_sec": round(world * args.batch * steps / t, 3), "ms_per_step": round(1000 * t / steps, 3),
             "steps": steps, "eval_images_per_sec": round(e, 3), "eval_images": int(dist.sum_over_ranks(n)),
-            "roofline": roof,
+            "logit_err_vs_reference": LOGIT_ERR.get(prec), "roofline": roof,
             # the classes over 0.5 ms/step: [ms/step, bound, fraction of that roof]
             "kernels": ({k: [v["ms_per_step"], v["bound"], v["roof_frac"]] for k, v in table.items()
                          if v["ms_per_step"] >= 0.5} if table else None)}
@@ -472,7 +507,8 @@ def main():
     ap.add_argument("--batch", type=int, default=8, help="images per GPU per step")
     ap.add_argument("--classes", type=int, default=1000)
     ap.add_argument("--arch", default="ViT-B/16")
-    ap.add_argument("--prec", default="fp16")
+    ap.add_argument("--prec", default="fp32s",
+                    help="headline PREC (fp32s: the fp32-class mode meeting the 1e-3 logit bar)")
     ap.add_argument("--eval-images", type=int, default=50000)
     ap.add_argument("--cpu-classes", type=int, default=0,
                     help="classes in the CPU-baseline sample (0: all of --classes, no scaling)")
@@ -514,8 +550,9 @@ def main():
     L = lay.L
     n_prof = 0 if args.no_prof else args.prof_steps
     t, sites = time_train(trainer, dm, args.steps, args.warmup, prof_steps=n_prof)
-    table = kernel_table(sites, n_prof, args.prec) if sites else None
-    roof = roofline_of(table, args.prec) if table else None
+    pk = peak_key(args.prec, trainer)
+    table = kernel_table(sites, n_prof, pk) if sites else None
+    roof = roofline_of(table, pk) if table else None
     log(f"headline train {1000 * t / args.steps:.3f} ms/step; eval")
     eval_ips, n_eval = time_eval(trainer, dm, n_eval_rank)
     log(f"eval {eval_ips:.1f} img/s")
@@ -530,6 +567,12 @@ def main():
         "rccl_world": world, "backend": torch.distributed.get_backend() if dist.is_dist() else None,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * t / args.steps, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.prec,
+        "dtype_note": {"fp32s": "fp32-class: fp32 activations, residual stream, LayerNorm, softmax and attention; "
+                                "every GEMM product as fp16 hi / lo parts on the 16-bit MFMA (~22 significant "
+                                "bits per operand, fp32 accumulate) -- the reference computes in fp32 "
+                                "(PromptSRC/clip/model.py:699)",
+                       "fp16": "fp16 forward and gradients (outside the 1e-3 logit bar)"}.get(args.prec, args.prec),
+        "logit_err_vs_reference": LOGIT_ERR.get(args.prec),
         "data": "synthetic (seeded U[0,1) CLIP-normalised images, random-init CLIP weights%s)"
                 % (" rounded to fp16, as the released CLIP checkpoints hold them" if args.weights == "fp16" else ""),
         "config": {"workload": f"CoCoOp {args.arch} n_ctx=4 ctx_init='a photo of a', {args.classes} classes, "
@@ -553,11 +596,15 @@ def main():
         "model_tflops_per_gpu_l77": round(step_flops_77 * args.steps / t / 1e12, 2),
         "executed_gemm_tflops_per_gpu": executed_gemm_tflops(sites, n_prof, t / args.steps) if sites else None,
         "roofline": roof,
-        "dx_by_shape": dx_by_shape(sites, n_prof, args.prec) if sites else None,
+        "dx_by_shape": dx_by_shape(sites, n_prof, pk) if sites else None,
+        "peak_note": ("fp32s GEMM FLOPs priced at the fp16 MFMA peak / %d (%d fp16 MFMAs per fp32-class product)"
+                      % ((2, 2) if pk == "fp32s16" else (3, 3))) if args.prec == "fp32s" else None,
         # per kernel class: [launches/step, ms/step, bound, fraction of that roof, TF/s, GB/s]
         "kernels": ({k: [v["launches_per_step"], v["ms_per_step"], v["bound"], v["roof_frac"], v["tflops"], v["gbs"]]
                      for k, v in table.items()} if table else None),
     }
+    if args.prec == "fp32s":
+        out["split_mode"] = {"text": trainer.model.text_core.split_mode, "vision": trainer.model.image_encoder.split_mode}
     del trainer, dm
     torch.cuda.empty_cache()
     if not args.no_extra and world > 1:
@@ -572,47 +619,51 @@ def main():
         torch.cuda.empty_cache()
     if not args.no_extra and world == 1:  # the N > 1 scaling runs report the headline lines only
         # the reference's batch size for CoCoOp (configs/trainers/CoCoOp/*.yaml: 1 image/step)
-        log("batch1")
-        tr1, dm1 = build_trainer(args, args.prec, 1, dev, rank)
-        t1, _ = time_train(tr1, dm1, B1_STEPS, 5)
-        out["batch1"] = {"images_per_sec": round(world * B1_STEPS / t1, 3),
-                         "ms_per_step": round(1000 * t1 / B1_STEPS, 3), "steps": B1_STEPS,
-                         "images_per_gpu_per_step": 1}
-        del tr1, dm1
-        torch.cuda.empty_cache()
-        # single-GPU proxy of batch-1 class sharding at N = 2 / 4 / 8: one rank's work
-        # -- B = 1 at C / N classes -- timed alone, a lower bound on the N-GPU step (the logit
-        # all-gather and the gradient all-reduce come on top)
-        proxy = {}
-        for n in (2, 4, 8):
-            cls = args.classes // n
-            log(f"batch1 class-shard proxy n{n}")
-            trp, dmp = build_trainer(argparse.Namespace(**{**vars(args), "classes": cls}), args.prec, 1, dev, rank)
-            # two timed rounds, the faster reported
-            rounds = [time_train(trp, dmp, B1_STEPS, 5)[0] for _ in range(2)]
-            proxy[f"n{n}"] = {"classes": cls, "ms_per_step": round(1000 * min(rounds) / B1_STEPS, 3),
-                              "rounds_ms": [round(1000 * t / B1_STEPS, 3) for t in rounds]}
-            del trp, dmp
+        for bp in dict.fromkeys((args.prec, "fp16")):  # the headline PREC, then fp16 (context)
+            sfx = "" if bp == args.prec else "_" + bp
+            log(f"batch1 {bp}")
+            tr1, dm1 = build_trainer(args, bp, 1, dev, rank)
+            t1, _ = time_train(tr1, dm1, B1_STEPS, 5)
+            out["batch1" + sfx] = {"images_per_sec": round(world * B1_STEPS / t1, 3),
+                                   "ms_per_step": round(1000 * t1 / B1_STEPS, 3), "steps": B1_STEPS,
+                                   "images_per_gpu_per_step": 1, "dtype": bp}
+            del tr1, dm1
             torch.cuda.empty_cache()
-        out["batch1_class_shard_proxy"] = proxy
-        # BASELINE config 2: CoOp n_ctx 16, ViT-B/16 fp16, 1000 classes, batch 32
+            # single-GPU proxy of batch-1 class sharding at N = 2 / 4 / 8: one rank's
+            # work -- B = 1 at C / N classes -- timed alone, a lower bound on the N-GPU step (the
+            # logit all-gather and the gradient all-reduce come on top)
+            proxy = {"dtype": bp}
+            for n in (2, 4, 8):
+                cls = args.classes // n
+                log(f"batch1 class-shard proxy n{n} {bp}")
+                trp, dmp = build_trainer(argparse.Namespace(**{**vars(args), "classes": cls}), bp, 1, dev, rank)
+                # two timed rounds, the faster reported
+                rounds = [time_train(trp, dmp, B1_STEPS, 5)[0] for _ in range(2)]
+                proxy[f"n{n}"] = {"classes": cls, "ms_per_step": round(1000 * min(rounds) / B1_STEPS, 3),
+                                  "rounds_ms": [round(1000 * t / B1_STEPS, 3) for t in rounds]}
+                del trp, dmp
+                torch.cuda.empty_cache()
+            out["batch1_class_shard_proxy" + sfx] = proxy
+        # BASELINE config 2: CoOp n_ctx 16, ViT-B/16 fp16, 1000 classes, batch 32 (the config names fp16)
         log("coop config 2")
-        trc, dmc = build_coop_trainer(args, args.prec, 32, dev, rank, n_test_device=args.eval_images)
+        trc, dmc = build_coop_trainer(args, "fp16", 32, dev, rank, n_test_device=args.eval_images)
         tc, _ = time_train(trc, dmc, 10, 3)
         ec, nc = time_eval(trc, dmc, args.eval_images)
         out["coop"] = {"workload": f"CoOp {args.arch} n_ctx=16 end, {args.classes} classes, 32 images/GPU/step, "
-                                   f"{args.prec}", "images_per_sec": round(world * 32 * 10 / tc, 3),
+                                   "fp16 (BASELINE config 2)", "images_per_sec": round(world * 32 * 10 / tc, 3),
                        "ms_per_step": round(100 * tc, 3), "eval_images_per_sec": round(ec, 3),
                        "eval_images": int(dist.sum_over_ranks(nc)),
                        "text_layout": ("shared-prefix packed" if trc.model.prompt_learner.layout.pack is not None
                                        else "plain")}
         del trc, dmc
         torch.cuda.empty_cache()
-        # the fp32-class precisions, the paths that meet the north-star |d logit| <= 1e-3:
-        # PREC fp32s (split-fp16 MFMA GEMMs, fp32 elsewhere) and PREC fp32 (f32-input MFMA)
-        for p in ("fp32s", "fp32"):
+        # the other precisions at the headline workload: fp16 (the fastest mode, outside the 1e-3
+        # bar; full eval set) and PREC fp32 (f32-input MFMA), or fp32s when it is not the headline
+        for p in ("fp16", "fp32s", "fp32"):
+            if p == args.prec:
+                continue
             log(p)
-            out[p] = precision_line(args, p, dev, rank, world)
+            out[p] = precision_line(args, p, dev, rank, world, n_eval=args.eval_images if p != "fp32" else 5000)
         if args.weights == "fp16":
             # PREC fp32s on weights with fp32 mantissas (not a CLIP checkpoint: every GEMM keeps
             # the weight-lo product, split mode 1)

@@ -35,11 +35,12 @@ def source_digest():
     return h.hexdigest()
 
 F32, F16, BF16, F32S = 0, 1, 2, 3  # F32S: fp32 activations x split-packed weights (PREC fp32s)
-F32S16 = 4  # F32S with fp16-valued weights (every lo part zero): the weight-lo product skipped
+F32S16 = 4  # F32S for fp16-valued weights: B is the compact fp16 SPLIT_SCALE * W (clipk_split_hi16)
 SPLIT_SCALE = 64.0  # CLIPK_SPLIT_SCALE: clipk_split_pack stores SPLIT_SCALE * W
 EPI_BIAS, EPI_BIAS_RES, EPI_BIAS_QGELU, EPI_DQGELU, EPI_NONE = 0, 1, 2, 3, 4
 A_QGELU = 0x100  # OR-ed into epi: the GEMM consumes quickgelu(A) (include/clipk.h)
 QGELU_DERIV = 0x200  # OR-ed into epi: out2 = quickgelu' (EPI_BIAS_QGELU) / aux is quickgelu' (EPI_DQGELU)
+OUT_SPLIT, A_SPLIT = 0x400, 0x800  # PREC fp32s pre-split operands (include/clipk.h)
 PROF_NONE, PROF_GEMM_FC, PROF_GEMM_ALL, PROF_ATTN, PROF_LN, PROF_GEMM_DGELU = 0, 1, 2, 3, 4, 5
 
 _P = ctypes.c_void_p
@@ -61,10 +62,12 @@ SIGNATURES = {
     "clipk_gemm_splitk": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P, _S, _P]),
     "clipk_gemm_set_config": (_I, [_I]),
     "clipk_split_pack": (_I, [_I, _I, _P, _I, _P, _P]),
-    "clipk_split_lo_zero": (_I, [_I, _I, _P, _P]),
+    "clipk_split_lo_zero": (_I, [_I, _I, _P, _P, _P]),
+    "clipk_split_hi16": (_I, [_I, _I, _P, _P, _P]),
     "clipk_gemm_ln": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P]),
     "clipk_ln_stats_merge": (_I, [_I, _I, _P, _P, _P, _P, _P]),
     "clipk_gemm_ln_merge_fused": (_I, [_I, _I, _I, _I]),
+    "clipk_gemm_ln_stats_split": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P]),
     "clipk_gemm_ln_gamma": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P]),
     "clipk_gemm_ln_merge": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P]),
     "clipk_image_resample": (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P]),

@@ -75,12 +75,19 @@ def _mm_weight(x, device, act, split):
 def split_mode(weights) -> int:
     """clipk_encoder_set_split mode of a PREC fp32s encoder: 2 when every split-packed GEMM weight
     it was created with is fp16-valued (ops.split_lo_zero; the released CLIP checkpoints are fp16,
-    PromptSRC/clip/clip.py:154-180), so those GEMMs skip the weight-lo product (CLIPK_F32S16, the
-    same results); else 1. Knob FSP_SPLIT_W16=0 keeps 1 (A/B)."""
+    PromptSRC/clip/clip.py:154-180), so those GEMMs run CLIPK_F32S16 on the compact weights
+    (compact16: 2 MFMAs per product, half of B's bytes, the same results); else 1. Knob
+    FSP_SPLIT_W16=0 keeps 1 (A/B)."""
     if os.environ.get("FSP_SPLIT_W16", "1") == "0":
         return 1
     packed = [t for t in weights if isinstance(t, torch.Tensor) and t.dtype == torch.int32]
     return 2 if packed and all(ops.split_lo_zero(t) for t in packed) else 1
+
+
+def compact16(tensors):
+    """Split mode 2's weight tables: every split-packed (int32) weight replaced by its compact fp16
+    form (ops.split_hi16, the CLIPK_F32S16 B operand); other entries unchanged."""
+    return [ops.split_hi16(t) if isinstance(t, torch.Tensor) and t.dtype == torch.int32 else t for t in tensors]
 
 
 def _t(v):
@@ -145,8 +152,9 @@ def ln_fold_weights(w, b, gamma, beta, act, device, split=False, gamma_on_a=Fals
     s = W' summed over its input dimension (of the rounded W'), c = b + W beta.
     ``split`` (PREC fp32s): W' fp32, split-packed (ops.split_pack), and s summed over the value
     the split GEMM multiplies by, (hi + lo) / SPLIT_SCALE, so the mean term cancels against it.
-    ``gamma_on_a`` (split mode 2, clipk_gemm_ln_gamma): B = W itself, split-packed, gamma applied
-    to A in the kernel; s = rowsums of W diag(gamma) over W's packed value.
+    ``gamma_on_a`` (split mode 2, clipk_gemm_ln_gamma): B = W itself in its compact fp16 form
+    (ops.split_hi16), gamma applied to A in the kernel; s = rowsums of W diag(gamma) over W's
+    packed value.
     Returns (W', s, c) on ``device``, or None when W' does not fit the operand dtype."""
     wd = w.double()
     if gamma_on_a:
@@ -155,7 +163,7 @@ def ln_fold_weights(w, b, gamma, beta, act, device, split=False, gamma_on_a=Fals
         lo = (x - hi).half().float()
         s = (((hi.double() + lo.double()) / N.SPLIT_SCALE) * gamma.double()[None, :]).sum(1).float()
         c = (b.double() + wd @ beta.double()).float()
-        wdev = ops.split_pack(w.float().to(device).contiguous())
+        wdev = ops.split_hi16(ops.split_pack(w.float().to(device).contiguous()))
         return (wdev, s.to(device).contiguous(), c.to(device).contiguous())
     wp = (wd * gamma.double()[None, :]).to(act)
     if not bool(torch.isfinite(wp.float()).all()):
@@ -173,6 +181,56 @@ def ln_fold_weights(w, b, gamma, beta, act, device, split=False, gamma_on_a=Fals
         wdev = wp.to(device).contiguous()
     c = (b.double() + wd @ beta.double()).float()
     return (wdev, s.to(device).contiguous(), c.to(device).contiguous())
+
+
+class SplitStatus:
+    """The overflow flags of a device's PREC fp32s encoders (clipk_encoder_set_status): one device
+    int the text and image encoders OR into -- 1: a forward's features came out non-finite, 2: a
+    backward's gradients did. A backward reads them at once (its overflow re-runs at a lower scale,
+    TextEncoderCore.backward); inference forwards do not synchronise for them: they are read every
+    READ_EVERY forward-only calls and by check() (TrainerX.test calls it after its last batch), so a
+    non-finite forward still raises, within that many calls, without a host stall per batch."""
+    READ_EVERY = 64
+    _by_device = {}
+
+    def __init__(self, device):
+        self.flags = torch.zeros(1, dtype=torch.int32, device=device)
+        self.pending = 0  # forward-only calls since the last read
+
+    @classmethod
+    def of(cls, device):
+        key = str(torch.device(device))
+        if key not in cls._by_device:
+            cls._by_device[key] = cls(device)
+        return cls._by_device[key]
+
+    def read(self):
+        """Read and clear the flags (one synchronisation); a non-finite forward raises. Returns
+        the backward flag."""
+        st = int(self.flags.item())
+        self.flags.zero_()
+        self.pending = 0
+        if st & 1:
+            raise N.ClipkError("PREC fp32s encoder: non-finite features -- an activation exceeded fp16's range "
+                               "(65504) in the split-fp16 GEMM operands; use PREC fp32")
+        return bool(st & 2)
+
+    def forward_done(self):
+        self.pending += 1
+        if self.pending >= self.READ_EVERY:
+            self.read()
+
+    def check(self):
+        """The deferred read of the inference forwards' flags."""
+        if self.pending:
+            self.read()
+
+
+def check_split_status(device=None):
+    """SplitStatus.check() for every device with PREC fp32s encoders (or the given one)."""
+    for key, st in list(SplitStatus._by_device.items()):
+        if device is None or key == str(torch.device(device)):
+            st.check()
 
 
 class _Encoder:
@@ -227,6 +285,10 @@ class TextEncoderCore(_Encoder):
         # PREC fp32s split mode (2: fp16-valued weights, CLIPK_F32S16), decided before the fold:
         # mode 2 folds gamma into A (clipk_gemm_ln_gamma) so B stays the fp16-valued W
         self.split_mode = split_mode(keep) if split else 0
+        if self.split_mode == 2:  # the tables hold the compact weights (clipk_encoder_set_split)
+            table, head = compact16(table), compact16(head)
+            keep = table + head
+            self._keep = keep
         for p in params:
             if fold is None:
                 break
@@ -244,10 +306,10 @@ class TextEncoderCore(_Encoder):
         self._status = None
         if split:
             N.check(N.load().clipk_encoder_set_split(h, self.split_mode), "clipk_encoder_set_split(text)")
-            # overflow flags of the split calls (clipk_encoder_set_status): 1 = a forward's
-            # features, 2 = a backward's gradients came out non-finite
-            self._status = torch.zeros(1, dtype=torch.int32, device=self.device)
-            N.check(N.load().clipk_encoder_set_status(h, ops._p(self._status)), "clipk_encoder_set_status")
+            # overflow flags of the split calls (clipk_encoder_set_status; SplitStatus): 1 = a
+            # forward's features, 2 = a backward's gradients came out non-finite
+            self._status = SplitStatus.of(self.device)
+            N.check(N.load().clipk_encoder_set_status(h, ops._p(self._status.flags)), "clipk_encoder_set_status")
             N.check(N.load().clipk_encoder_set_split_target(h, self.SPLIT_TARGET), "clipk_encoder_set_split_target")
         if fold:
             self._keep += fold
@@ -294,22 +356,17 @@ class TextEncoderCore(_Encoder):
         else:
             N.check(lib.clipk_text_forward(h, shape.nseq, shape.L, *tail), "clipk_text_forward")
         if self._status is not None and not save:
-            self._check_status(forward_only=True)  # inference: no backward will look
+            self._status.forward_done()  # inference: read every READ_EVERY calls / SplitStatus.check
         return txt, saved
 
     # PREC fp32s: an overflowed backward is re-run once with this much lower scale target (10 more
     # bits of headroom below fp16's 65504 for gradient growth through the layers)
     SPLIT_TARGET, SPLIT_RETRY_TARGET = 7, -3
 
-    def _check_status(self, forward_only=False):
+    def _check_status(self):
         """Read and clear the split overflow flags (one host synchronisation); a non-finite
         forward raises. Returns the backward flag."""
-        st = int(self._status.item())
-        self._status.zero_()
-        if st & 1:
-            raise N.ClipkError("PREC fp32s text encoder: non-finite features -- an activation exceeded fp16's "
-                               "range (65504) in the split-fp16 GEMM operands; use PREC fp32")
-        return bool(st & 2) and not forward_only
+        return self._status.read()
 
     def backward(self, dtxt, shape, saved):
         lib = N.load()
@@ -460,6 +517,10 @@ class VisionEncoder(nn.Module, _Encoder):
                 f32(sd["visual.positional_embedding"])]
         # backward of the head: d ln_post(CLS) = dfeat . proj^T  (proj [D, E], B operand [N=D, K=E])
         self.proj_bwd = _mm_weight(_t(sd["visual.proj"]).float(), self.dev, act, split) if with_grad else None
+        self.split_mode = split_mode([t for t in table if t is not None] + head + [self.proj_bwd]) if split else 0
+        if self.split_mode == 2:  # the tables hold the compact weights (clipk_encoder_set_split)
+            table, head = compact16(table), compact16(head)
+            self.proj_bwd = compact16([self.proj_bwd])[0]
         self._keep = [t for t in table if t is not None] + head
         self.width, self.n_tokens = D, (arch.image_resolution // p) ** 2 + 1
         h = ctypes.c_void_p()
@@ -467,9 +528,13 @@ class VisionEncoder(nn.Module, _Encoder):
                                              ops.DT[act], _ptrs(table), _ptrs(head), ctypes.byref(h)),
                 "clipk_vision_create")
         self.handle = h
-        self.split_mode = split_mode(self._keep + [self.proj_bwd]) if split else 0
+        self._status = None
         if split:
             N.check(N.load().clipk_encoder_set_split(h, self.split_mode), "clipk_encoder_set_split(vision)")
+            # non-finite ViT features set flag 1 of the device's split status (the ViT's
+            # split_check had no status to report to)
+            self._status = SplitStatus.of(self.dev)
+            N.check(N.load().clipk_encoder_set_status(h, ops._p(self._status.flags)), "clipk_encoder_set_status")
         if fold:
             self._keep += fold
             N.check(N.load().clipk_encoder_set_ln_fold(h, _ptrs(fold)), "clipk_encoder_set_ln_fold")

@@ -147,9 +147,9 @@ struct ProfScope {
 // Algorithmic HBM bytes of one GEMM: A, B read once, out (+ out2) written, residual / aux
 // read once (epi without the CLIPK_A_QGELU flag).
 static double gemm_bytes(int in, int out, int epi, int M, int N, int K, bool has_o2, int auxdt) {
-  const double a = esize(in), o = esize(out);
-  double b = (double)M * K * a + (double)N * K * a + (double)M * N * o * (has_o2 ? 2 : 1);
-  const int e = epi & ~(CLIPK_A_QGELU | CLIPK_QGELU_DERIV);
+  const double a = esize(in), o = esize(out), wb = in == CLIPK_F32S16 ? 2.0 : a;  // compact weight
+  double b = (double)M * K * a + (double)N * K * wb + (double)M * N * o * (has_o2 ? 2 : 1);
+  const int e = epi & ~(CLIPK_A_QGELU | CLIPK_QGELU_DERIV | CLIPK_A_SPLIT | CLIPK_OUT_SPLIT | CLIPK_OUT2_SPLIT_GAMMA);
   if (e == CLIPK_EPI_BIAS_RES) b += (double)M * N * o;
   if (e == CLIPK_EPI_DQGELU) b += (double)M * N * esize(auxdt);
   return b;
@@ -429,6 +429,22 @@ static bool a_qgelu_on() {
   return v != 0;
 }
 
+// PREC fp32s: the MLP's hand-offs in pre-split form (include/clipk.h CLIPK_OUT_SPLIT / CLIPK_A_SPLIT):
+// c_fc stores QuickGELU(h) as the fp16 parts c_proj's split would form, and the backward's dgelu
+// stores dh as fc_dx's -- those GEMMs then run no split VALU in their K loop (23 % of their launch
+// on the headline shapes, profiles/r06b/). Bitwise the same results. Knob CLIPK_PRESPLIT=0 (A/B).
+static bool presplit_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char* s = getenv("CLIPK_PRESPLIT");
+    v = s ? atoi(s) : 1;
+  }
+  return v != 0;
+}
+// the operand flags of one hand-off on this call's path (split encoder calls only)
+static int ps_out() { return t_split && presplit_on() ? CLIPK_OUT_SPLIT : 0; }
+static int ps_a() { return t_split && presplit_on() ? CLIPK_A_SPLIT : 0; }
+
 // Training's c_fc saves quickgelu'(h) for the backward (CLIPK_QGELU_DERIV) instead of h itself;
 // knob CLIPK_QGELU_DERIV=0 (A/B) saves h and the backward recomputes the derivative.
 static bool qgelu_deriv_on() {
@@ -463,9 +479,10 @@ static int block_post(const clipk_encoder* e, const std::array<const void*, 16>&
     return CLIPK_OK;
   }
   // training (h given): h receives quickgelu'(xn Wfc^T + b) for the backward (CLIPK_QGELU_DERIV)
-  TRY(gemm(act, act, CLIPK_EPI_BIAS_QGELU | (h && qgelu_deriv_on() ? CLIPK_QGELU_DERIV : 0), rows, 4 * W, W, xn, w[8], (const float*)w[9],
+  const int pso = sk ? 0 : ps_out(), psa = sk ? 0 : ps_a();  // (split-K slices take no pre-split operands)
+  TRY(gemm(act, act, CLIPK_EPI_BIAS_QGELU | (h && qgelu_deriv_on() ? CLIPK_QGELU_DERIV : 0) | pso, rows, 4 * W, W, xn, w[8], (const float*)w[9],
            nullptr, g, h, nullptr, 0, st, text ? CLIPK_PROF_GEMM_FC : CLIPK_PROF_NONE, sk, skb, text ? "text.fc_fwd" : "vit.fc_fwd"));
-  TRY(gemm(act, rd, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo,
+  TRY(gemm(act, rd, CLIPK_EPI_BIAS_RES | psa, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo,
            nullptr, nullptr, 0, st, pg, sk, skb, text ? "text.proj_fwd" : "vit.proj_fwd"));
   return CLIPK_OK;
 }
@@ -535,15 +552,15 @@ static int block_post_fold(const clipk_encoder* e, const std::array<const void*,
   const int pg = text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE;
   TRY(gemm_ln(act, CLIPK_EPI_BIAS_RES, rows, W, W, o, w[4], (const float*)w[5], X, Xm, nullptr, lnst, nullptr,
               nullptr, st, pg, text ? "text.out_fwd" : "vit.out_fwd"));
-  TRY(gemm_ln_merged(act, CLIPK_EPI_BIAS_QGELU | (h && qgelu_deriv_on() ? CLIPK_QGELU_DERIV : 0), rows, 4 * W, W, Xm,
-                     f[3], (const float*)f[5], g, h, lnst, (const float*)f[4], m2, r2, rnb, st,
+  TRY(gemm_ln_merged(act, CLIPK_EPI_BIAS_QGELU | (h && qgelu_deriv_on() ? CLIPK_QGELU_DERIV : 0) | ps_out(), rows, 4 * W,
+                     W, Xm, f[3], (const float*)f[5], g, h, lnst, (const float*)f[4], m2, r2, rnb, st,
                      text ? CLIPK_PROF_GEMM_FC : CLIPK_PROF_NONE, text ? "text.fc_fwd" : "vit.fc_fwd", text,
                      e->split == 2 ? (const float*)w[6] : nullptr));
   if (stats_next)
-    return gemm_ln(act, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo, nullptr, lnst,
-                   nullptr, nullptr, st, pg, text ? "text.proj_fwd" : "vit.proj_fwd");
-  return gemm(act, act, CLIPK_EPI_BIAS_RES, rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo, nullptr, nullptr,
-              0, st, pg, nullptr, 0, text ? "text.proj_fwd" : "vit.proj_fwd");
+    return gemm_ln(act, CLIPK_EPI_BIAS_RES | ps_a(), rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo, nullptr,
+                   lnst, nullptr, nullptr, st, pg, text ? "text.proj_fwd" : "vit.proj_fwd");
+  return gemm(act, act, CLIPK_EPI_BIAS_RES | ps_a(), rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo, nullptr,
+              nullptr, 0, st, pg, nullptr, 0, text ? "text.proj_fwd" : "vit.proj_fwd");
 }
 
 }  // namespace clipk
@@ -557,7 +574,8 @@ extern "C" const char* clipk_strerror(int status) {
     case CLIPK_ESHAPE: return "shape violates a kernel constraint";
     case CLIPK_EDTYPE: return "unsupported dtype combination";
     case CLIPK_EWORKSPACE: return "workspace too small";
-    case CLIPK_ERANGE: return "input outside the supported range (clipk_split_pack: |W| >= 65504 / 64 or not finite)";
+    case CLIPK_ERANGE: return "input outside the supported range (clipk_split_pack: |W| >= 65504 / 64 or not finite; clipk_split_hi16: W not fp16-valued)";
+    case CLIPK_EHIP: return "a HIP runtime call of a synchronous check failed";
     default: return status > 0 ? hipGetErrorString((hipError_t)status) : "unknown error";
   }
 }
@@ -916,11 +934,13 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
     // in the act dtype (16-bit: rms 1.8e-4 on the derivative vs 2.9e-5 when recomputing it from a
     // 16-bit h -- under the 16-bit rounding of dh itself -- for no exp / rcp in this epilogue)
     // (the last layer's compact EOT-row launches are sites of their own: a different GEMM grid)
-    TRY(gemm(gd, gd, dgelu_epi, n, 4 * W, W, dA, w[15], nullptr, nullptr, b.dh, nullptr, t.h[l], act, st,
-             io.text ? CLIPK_PROF_GEMM_DGELU : CLIPK_PROF_NONE, nullptr, 0,
+    // (PREC fp32s: dh handed to fc_dx pre-split, presplit_on; the saved-derivative form only)
+    const bool dh_split = (dgelu_epi & CLIPK_QGELU_DERIV) != 0;
+    TRY(gemm(gd, gd, dgelu_epi | (dh_split ? ps_out() : 0), n, 4 * W, W, dA, w[15], nullptr, nullptr, b.dh, nullptr,
+             t.h[l], act, st, io.text ? CLIPK_PROF_GEMM_DGELU : CLIPK_PROF_NONE, nullptr, 0,
              compact ? SITE("proj_dx_dgelu_eot") : SITE("proj_dx_dgelu")));
-    TRY(gemm(gd, gd, CLIPK_EPI_NONE, n, W, 4 * W, b.dh, w[14], nullptr, nullptr, b.dxn, nullptr,
-             nullptr, 0, st, pg, nullptr, 0, compact ? SITE("fc_dx_eot") : SITE("fc_dx")));
+    TRY(gemm(gd, gd, CLIPK_EPI_NONE | (dh_split ? ps_a() : 0), n, W, 4 * W, b.dh, w[14], nullptr, nullptr, b.dxn,
+             nullptr, nullptr, 0, st, pg, nullptr, 0, compact ? SITE("fc_dx_eot") : SITE("fc_dx")));
     TRY(ln_bwd(n, t.Xm[l], (const float*)w[6], t.mean2[l], t.rstd2[l], false));
     // attention: do = dXm . Wout ; dqkv ; dxn1 = dqkv . Win
     TRY(gemm(gd, gd, CLIPK_EPI_NONE, n, W, W, dA, w[13], nullptr, nullptr, compact ? b.dh : b.do_,
@@ -1304,6 +1324,10 @@ extern "C" int clipk_encoder_set_ln_fold(clipk_encoder* e, const void* const* fo
 extern "C" int clipk_encoder_set_split(clipk_encoder* e, int on) {
   if (!e || on < 0 || on > 2) return CLIPK_EINVAL;
   if (on && (e->act != CLIPK_F32 || e->grad != CLIPK_F32)) return CLIPK_EDTYPE;
+  // the mode names the weight tables' format (packed / compact) and what a fold table holds
+  // (W diag(gamma) / W): fixed once set, and never changed under a fold
+  if (on == e->split) return CLIPK_OK;
+  if (e->split != 0 || !e->fold.empty()) return CLIPK_EINVAL;
   e->split = on;
   return CLIPK_OK;
 }

@@ -296,6 +296,9 @@ class TrainerX:
             batch = nxt
             preds.append(out.argmax(1).to(torch.int64))
             labels.append(y.to(torch.int64))
+        # PREC fp32s: the inference forwards' overflow flags, read once here (clip.model.SplitStatus)
+        from ..clip.model import check_split_status
+        check_split_status(self.device)
         dev = self.device
         p = torch.cat(preds) if preds else torch.zeros(0, dtype=torch.int64, device=dev)
         y = torch.cat(labels) if labels else torch.zeros(0, dtype=torch.int64, device=dev)

@@ -50,23 +50,43 @@ def split_pack(w):
 
 def split_lo_zero(packed) -> bool:
     """clipk_split_lo_zero: whether every lo part of a split_pack(...) weight is zero (the weight
-    is fp16-valued, so the GEMMs may run CLIPK_F32S16). Synchronises the stream."""
+    is fp16-valued, so split_hi16 compacts it for CLIPK_F32S16). Synchronises the stream."""
     _need(packed, "packed", torch.int32)
     n, k = packed.shape
-    rc = N.load().clipk_split_lo_zero(n, k, _p(packed), _stream())
-    if rc < 0 or rc > 1:
-        N.check(rc, "clipk_split_lo_zero")
-    return rc == 1
+    res = ctypes.c_int(-1)
+    N.call("clipk_split_lo_zero", n, k, _p(packed), ctypes.byref(res), _stream())
+    if res.value not in (0, 1):
+        raise N.ClipkError(f"clipk_split_lo_zero: no answer ({res.value})")
+    return res.value == 1
+
+
+def split_hi16(packed):
+    """clipk_split_hi16: the CLIPK_F32S16 B operand of an fp16-valued split_pack(...) weight -- fp16
+    [N, K] = SPLIT_SCALE * W exactly (2 B per element). Raises (CLIPK_ERANGE) when W is not
+    fp16-valued. Synchronises the stream."""
+    _need(packed, "packed", torch.int32)
+    n, k = packed.shape
+    out = torch.empty(n, k, dtype=torch.float16, device=packed.device)
+    N.call("clipk_split_hi16", n, k, _p(packed), _p(out), _stream())
+    return out
+
+
+def _split_kind(a, b):
+    """The GEMM input type for (a, b): PREC fp32s when a is fp32 and b a split weight -- int32
+    split_pack(...) (CLIPK_F32S) or fp16 split_hi16(...) (CLIPK_F32S16) -- else None."""
+    if a.dtype != torch.float32:
+        return None
+    return {torch.int32: N.F32S, torch.float16: N.F32S16}.get(b.dtype)
 
 
 def gemm(a, b, epi=N.EPI_NONE, out_dtype=torch.float32, bias=None, res=None, aux=None,
-         want_out2=False, out=None, w16=False):
+         want_out2=False, out=None):
     """out[M,N] = epi(a[M,K] @ b[N,K]^T); returns out (and out2 for EPI_BIAS_QGELU). With a
-    fp32 and b an int32 split_pack(...) weight: the fp32-class split-fp16 GEMM (CLIPK_F32S;
-    ``w16``: CLIPK_F32S16, b's lo parts all zero, see split_lo_zero)."""
+    fp32 and b a split weight: the fp32-class split-fp16 GEMM (b int32 split_pack(...):
+    CLIPK_F32S; b fp16 split_hi16(...) of an fp16-valued weight: CLIPK_F32S16)."""
     _need(a, "A")
-    split = a.dtype == torch.float32 and b.dtype == torch.int32
-    _need(b, "B", torch.int32 if split else a.dtype)
+    split = _split_kind(a, b)
+    _need(b, "B", b.dtype if split is not None else a.dtype)
     M, K = a.shape
     Nn = b.shape[0]
     if b.shape[1] != K:
@@ -80,23 +100,22 @@ def gemm(a, b, epi=N.EPI_NONE, out_dtype=torch.float32, bias=None, res=None, aux
         _need(res, "res", torch.float32 if out.dtype == torch.float32 else out.dtype)
     if aux is not None:
         _need(aux, "aux")
-    args = ((N.F32S16 if w16 else N.F32S) if split else DT[a.dtype], DT[out.dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias),
+    args = (split if split is not None else DT[a.dtype], DT[out.dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias),
             _p(res), Nn, _p(out), Nn, _p(out2), _p(aux), DT[aux.dtype] if aux is not None else 0, Nn)
     N.call("clipk_gemm", *args, _stream())
     return (out, out2) if want_out2 else out
 
 
-def gemm_ln(a, b, epi, bias, stats=None, res=None, colsum=None, rnb=None, want_out2=False, w16=False):
+def gemm_ln(a, b, epi, bias, stats=None, res=None, colsum=None, rnb=None, want_out2=False):
     """clipk_gemm_ln (include/clipk.h): 16-bit a[M,K] @ b[N,K]^T with the LayerNorm fold.
     Producer (EPI_BIAS_RES, colsum None): the statistics partials of the output are written to
     stats (fp32 [M, N/64, 2]). Fold (EPI_BIAS / EPI_BIAS_QGELU): a is the LayerNorm input x with
     per-row rnb = (rstd, -rstd * mean) (ln_stats_merge of its partials), b = W diag(gamma),
-    bias = b + W beta, colsum = row sums of b. Output in a's dtype. PREC fp32s: a fp32 and b an
-    int32 split_pack(...) weight (CLIPK_F32S; colsum summed over the packed value, see
-    clip.model.ln_fold_weights; ``w16``: CLIPK_F32S16)."""
+    bias = b + W beta, colsum = row sums of b. Output in a's dtype. PREC fp32s: a fp32 and b a
+    split weight as in gemm (colsum summed over the packed value, see clip.model.ln_fold_weights)."""
     _need(a, "A")
-    split = a.dtype == torch.float32 and b.dtype == torch.int32
-    _need(b, "B", torch.int32 if split else a.dtype)
+    split = _split_kind(a, b)
+    _need(b, "B", b.dtype if split is not None else a.dtype)
     M, K = a.shape
     Nn = b.shape[0]
     out = torch.empty(M, Nn, device=a.device, dtype=a.dtype)
@@ -107,26 +126,47 @@ def gemm_ln(a, b, epi, bias, stats=None, res=None, colsum=None, rnb=None, want_o
             _need(t, nm, torch.float32)
     if res is not None:
         _need(res, "res", a.dtype)
-    N.call("clipk_gemm_ln", (N.F32S16 if w16 else N.F32S) if split else DT[a.dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias), _p(res), Nn, _p(out), Nn,
-           _p(out2), _p(stats), _p(colsum), _p(rnb), _stream())
+    N.call("clipk_gemm_ln", split if split is not None else DT[a.dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias),
+           _p(res), Nn, _p(out), Nn, _p(out2), _p(stats), _p(colsum), _p(rnb), _stream())
     return (out, out2) if want_out2 else out
 
 
-def gemm_ln_gamma(a, b, epi, bias, colsum, rnb, gamma, want_out2=False, w16=False):
+def gemm_ln_gamma(a, b, epi, bias, colsum, rnb, gamma, want_out2=False):
     """clipk_gemm_ln_gamma (PREC fp32s): the LayerNorm fold with gamma applied to A: a fp32 x,
-    b = split_pack(W) (W itself), colsum = rowsums of W diag(gamma), bias = b + W beta, rnb =
-    (rstd, -rstd * mean) per row; ``w16``: CLIPK_F32S16 (W fp16-valued)."""
+    b = W itself as a split weight (int32 split_pack(W): CLIPK_F32S; fp16 split_hi16(...):
+    CLIPK_F32S16), colsum = rowsums of W diag(gamma), bias = b + W beta, rnb = (rstd, -rstd *
+    mean) per row."""
     _need(a, "A", torch.float32)
-    _need(b, "B", torch.int32)
+    split = _split_kind(a, b)
+    if split is None:
+        raise N.ClipkError(f"gemm_ln_gamma: B must be a split weight (int32 / fp16), got {b.dtype}")
+    _need(b, "B", b.dtype)
     M, K = a.shape
     Nn = b.shape[0]
     out = torch.empty(M, Nn, device=a.device, dtype=torch.float32)
     out2 = torch.empty_like(out) if want_out2 else None
     for t, nm in ((bias, "bias"), (colsum, "colsum"), (rnb, "rnb"), (gamma, "gamma")):
         _need(t, nm, torch.float32)
-    N.call("clipk_gemm_ln_gamma", N.F32S16 if w16 else N.F32S, epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias),
+    N.call("clipk_gemm_ln_gamma", split, epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias),
            _p(out), Nn, _p(out2), _p(colsum), _p(rnb), _p(gamma), _stream())
     return (out, out2) if want_out2 else out
+
+
+def gemm_ln_stats_split(a, b, epi, bias, stats, res, gamma):
+    """clipk_gemm_ln_stats_split (PREC fp32s, split mode 2): the LayerNorm-statistics producer
+    (EPI_BIAS_RES [| A_SPLIT], b a split_hi16 weight) that also writes the next fold's pre-split A,
+    split(out * gamma). Returns (out fp32 [M, N], out2 [M, N] fp32 storage of fp16 parts)."""
+    _need(a, "A", torch.float32)
+    _need(b, "B", torch.float16)
+    M, K = a.shape
+    Nn = b.shape[0]
+    out = torch.empty(M, Nn, device=a.device, dtype=torch.float32)
+    out2 = torch.empty_like(out)
+    for t, nm in ((bias, "bias"), (stats, "stats"), (res, "res"), (gamma, "gamma")):
+        _need(t, nm, torch.float32)
+    N.call("clipk_gemm_ln_stats_split", N.F32S16, epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias), _p(res), Nn,
+           _p(out), Nn, _p(stats), _p(gamma), _p(out2), _stream())
+    return out, out2
 
 
 def gemm_ln_merge(a, b, epi, bias, stats, colsum, want_out2=False):
@@ -167,16 +207,18 @@ def gemm_splitk(a, b, epi=N.EPI_NONE, out_dtype=torch.float32, bias=None, res=No
     """Split-K form of gemm (fp32 partials in a workspace, deterministic slice-order sum);
     splits <= 0 picks the library's choice for the shape."""
     _need(a, "A")
-    _need(b, "B", a.dtype)
+    split = _split_kind(a, b)
+    _need(b, "B", b.dtype if split is not None else a.dtype)
+    ind = split if split is not None else DT[a.dtype]
     M, K = a.shape
     Nn = b.shape[0]
     if splits <= 0:
-        splits = N.load().clipk_gemm_auto_splits(DT[a.dtype], M, Nn, K)
+        splits = N.load().clipk_gemm_auto_splits(ind, M, Nn, K)
     out = torch.empty(M, Nn, device=a.device, dtype=out_dtype)
     out2 = torch.empty_like(out) if want_out2 else None
     ws = torch.empty(max(N.load().clipk_gemm_splitk_ws_bytes(M, Nn, splits), 1), dtype=torch.uint8,
                      device=a.device)
-    N.call("clipk_gemm_splitk", DT[a.dtype], DT[out_dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias),
+    N.call("clipk_gemm_splitk", ind, DT[out_dtype], epi, M, Nn, K, _p(a), K, _p(b), K, _p(bias),
            _p(res), Nn, _p(out), Nn, _p(out2), splits, _p(ws), ws.numel(), _stream())
     return (out, out2) if want_out2 else out
 

@@ -41,11 +41,12 @@ extern "C" {
 
 /* element types. CLIPK_F32S (GEMM input type only): fp32 activations times a weight packed by
  * clipk_split_pack -- the fp32-class GEMM on 16-bit MFMA of PREC "fp32s" (clipk_gemm).
- * CLIPK_F32S16 (GEMM input type only): CLIPK_F32S for a packed weight whose lo parts are all
- * zero (clipk_split_lo_zero: W fp16-valued, as every released CLIP checkpoint's weights are --
- * the reference loads them from the fp16 archive, PromptSRC/clip/clip.py:154-180); the
- * hi(a) lo(b) product, exactly zero, is skipped: 2 MFMAs per product instead of 3, results
- * bitwise those of CLIPK_F32S. */
+ * CLIPK_F32S16 (GEMM input type only): the same product for an fp16-valued weight (every lo part
+ * of its clipk_split_pack output zero, as for every released CLIP checkpoint -- the reference
+ * loads them from the fp16 archive, PromptSRC/clip/clip.py:154-180), whose B operand is the
+ * COMPACT weight of clipk_split_hi16: fp16 [N, K] = CLIPK_SPLIT_SCALE * W exactly, 2 B per element
+ * (ldb == K). The hi(a) lo(b) product, exactly zero, is not formed: 2 MFMAs per product instead of
+ * 3, and half of B's bytes staged; results bitwise those of CLIPK_F32S on the packed weight. */
 enum { CLIPK_F32 = 0, CLIPK_F16 = 1, CLIPK_BF16 = 2, CLIPK_F32S = 3, CLIPK_F32S16 = 4 };
 
 /* status codes (hipError_t values > 0 pass through) */
@@ -55,7 +56,9 @@ enum {
   CLIPK_ESHAPE = -2,     /* shape violates a kernel constraint */
   CLIPK_EDTYPE = -3,     /* unsupported dtype combination */
   CLIPK_EWORKSPACE = -4, /* workspace too small */
-  CLIPK_ERANGE = -5      /* an input outside the range the kernel supports (clipk_split_pack) */
+  CLIPK_ERANGE = -5,     /* an input outside the range the kernel supports (clipk_split_pack,
+                            clipk_split_hi16) */
+  CLIPK_EHIP = -6        /* a HIP runtime call of a synchronous check failed (clipk_split_*) */
 };
 
 /* GEMM epilogues:  acc = A[M,K] . B[N,K]^T  (fp32 accumulate)                         */
@@ -78,6 +81,21 @@ enum { CLIPK_A_QGELU = 0x100 };
  * the backward epilogue drops its exp + rcp per element. Also accepted by clipk_gemm_ln (fold
  * form of EPI_BIAS_QGELU) and clipk_gemm_splitk (EPI_BIAS_QGELU). */
 enum { CLIPK_QGELU_DERIV = 0x200 };
+/* PREC fp32s operand flags OR-ed into epi (split in_dtype CLIPK_F32S / CLIPK_F32S16, fp32 out).
+ * The split GEMM forms each activation's fp16 parts hi = fp16(x), lo = fp16(x - hi) itself; a
+ * PRE-SPLIT operand holds them already: [rows, K] 4-byte elements, per 8 consecutive k 16 B of hi
+ * parts then 16 B of lo parts (clipk_split_pack's layout at scale 1).
+ *  CLIPK_OUT_SPLIT: out is stored pre-split (the fp32 result's parts; for the next GEMM's A).
+ *    clipk_gemm (EPI_BIAS_QGELU [| QGELU_DERIV], EPI_DQGELU | QGELU_DERIV) and the folds
+ *    clipk_gemm_ln / clipk_gemm_ln_gamma (c_fc).
+ *  CLIPK_A_SPLIT: A is given pre-split, as such a producer wrote it; the GEMM forms no split.
+ *    clipk_gemm (EPI_NONE, EPI_BIAS_RES, EPI_DQGELU | QGELU_DERIV), the producer form of
+ *    clipk_gemm_ln, clipk_gemm_ln_gamma (A = the split parts of x * gamma, which the call then
+ *    does not apply again: clipk_gemm_ln_stats_split writes them) and clipk_gemm_ln_stats_split.
+ *  (CLIPK_OUT2_SPLIT_GAMMA: internal to clipk_gemm_ln_stats_split.)
+ * Results are bitwise those of the same GEMMs on the fp32 values: the parts are the ones the GEMM
+ * would form (PREC fp32s: the split VALU leaves the K loop's critical path). */
+enum { CLIPK_OUT_SPLIT = 0x400, CLIPK_A_SPLIT = 0x800, CLIPK_OUT2_SPLIT_GAMMA = 0x1000 };
 
 const char* clipk_version(void);
 /* sha256 (hex) over the sources this library was built from: csrc/{*.hip,*.h,Makefile} and
@@ -109,10 +127,15 @@ int clipk_gemm(int in_dtype, int out_dtype, int epi, int M, int N, int K,
  * fp32 result to ~1e-6 relative. out / res / aux fp32 (epilogues as above). */
 #define CLIPK_SPLIT_SCALE 64.0f
 int clipk_split_pack(int N, int K, const float* W, int ldw, void* out, void* stream);
-/* 1 when every lo part of clipk_split_pack's output `packed` ([N, K] split elements) is zero
- * (the weight is fp16-valued: CLIPK_F32S16 may multiply it), 0 when not, < 0 on error. One
- * pass, then a stream synchronisation (checked once per weight, at model construction). */
-int clipk_split_lo_zero(int N, int K, const void* packed, void* stream);
+/* *result = 1 when every lo part of clipk_split_pack's output `packed` ([N, K] split elements) is
+ * zero (the weight is fp16-valued: clipk_split_hi16 may compact it for CLIPK_F32S16), 0 when not.
+ * Returns CLIPK_OK, or a negative status (CLIPK_EHIP for a failed HIP call; *result untouched).
+ * One pass, then a stream synchronisation (checked once per weight, at model construction). */
+int clipk_split_lo_zero(int N, int K, const void* packed, int* result, void* stream);
+/* The CLIPK_F32S16 B operand: out fp16 [N, K] = the hi parts of clipk_split_pack's output `packed`
+ * (= CLIPK_SPLIT_SCALE * W exactly). CLIPK_ERANGE when a lo part is nonzero (W is not fp16-valued;
+ * out is then unspecified). One pass, then a stream synchronisation. */
+int clipk_split_hi16(int N, int K, const void* packed, void* out, void* stream);
 
 /* Split-K form of clipk_gemm for small M (the ViT at training batch sizes, whose 128x128
  * tile grid would leave most CUs idle): the K range is cut into `splits` slices whose fp32
@@ -154,6 +177,13 @@ int clipk_gemm_ln_gamma(int in_dtype, int epi, int M, int N, int K, const void* 
 int clipk_gemm_ln(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B, int ldb,
                   const float* bias, const void* res, int ldr, void* out, int ldo, void* out2,
                   float* stats, const float* colsum, const float* rnb, void* stream);
+/* The statistics producer of clipk_gemm_ln (EPI_BIAS_RES [| CLIPK_A_SPLIT], colsum NULL), in_dtype
+ * CLIPK_F32S16, that also stores out2 [M, N] = the pre-split form (CLIPK_OUT_SPLIT) of out * gamma,
+ * the fp32 products the next fold (clipk_gemm_ln_gamma, gamma = its LayerNorm weight) would form:
+ * that fold then reads out2 with CLIPK_A_SPLIT. The residual stream out stays fp32. */
+int clipk_gemm_ln_stats_split(int in_dtype, int epi, int M, int N, int K, const void* A, int lda, const void* B,
+                              int ldb, const float* bias, const void* res, int ldr, void* out, int ldo, float* stats,
+                              const float* gamma, void* out2, void* stream);
 int clipk_ln_stats_merge(int rows, int width, const float* stats, float* mean, float* rstd, float* rnb,
                          void* stream);
 /* clipk_ln_stats_merge(M, K, stats, mean, rstd, rnb) followed by the fold clipk_gemm_ln(...,
@@ -402,11 +432,14 @@ int clipk_encoder_set_ln_fold(clipk_encoder* e, const void* const* fold_ptrs);
  * the residual stream stay fp32. The text backward then runs on s * dtxt with s a power of two
  * from max |dtxt| (exact, undone on dx0 and the deep-prompt gradients), so the gradient operands
  * sit in fp16's normal range. Reference semantics: PromptSRC/clip/model.py:699 (fp32 model).
- * on = 2: as 1, and those weights are fp16-valued (clipk_split_lo_zero returned 1 for each; the
- * released CLIP checkpoints): their GEMMs run CLIPK_F32S16, 2 MFMAs per product, the same results.
+ * on = 2: those weights are fp16-valued (clipk_split_lo_zero returned 1 for each; the released
+ * CLIP checkpoints) and the tables hold their COMPACT form (clipk_split_hi16) instead of the packed
+ * one: every GEMM runs CLIPK_F32S16, 2 MFMAs per product, the same results as mode 1.
  * With a LayerNorm fold (clipk_encoder_set_ln_fold after this call) the fold tables then hold W
- * itself (packed) instead of W' = W diag(gamma), s = rowsums of W diag(gamma) over the packed
- * values / 64, and the fold GEMMs apply the layer's LayerNorm weight to A (clipk_gemm_ln_gamma). */
+ * itself (compact) instead of W' = W diag(gamma), s = rowsums of W diag(gamma) over the packed
+ * values / 64, and the fold GEMMs apply the layer's LayerNorm weight to A (clipk_gemm_ln_gamma).
+ * The mode describes the tables' format, so it is fixed once set: a second call with another mode,
+ * or any call after clipk_encoder_set_ln_fold, returns CLIPK_EINVAL. */
 int clipk_encoder_set_split(clipk_encoder* e, int on);
 /* The split backward's scale target t (default 7): s puts max |s dtxt| in [2^(t-1), 2^t). A lower
  * target leaves more headroom below fp16's 65504 for gradient growth through the layers, at

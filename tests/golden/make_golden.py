@@ -91,9 +91,10 @@ def make_cfg(size, coop=None, cocoop=None, per_class=None):
 DESIGN = {"vision_depth": 0, "language_depth": 0, "vision_ctx": 0, "language_ctx": 0}
 
 
-def build_clip(arch):
-    from clip.model import build_model
-    sd = synth.make_state_dict(arch, seed=0)
+def build_clip(arch, fp16_values=False):
+    """The seeded synthetic CLIP (fp16_values: every weight rounded to fp16, as the released
+    checkpoints the reference loads from its fp16 archive, PromptSRC/clip/clip.py:154-180)."""
+    sd = synth.make_state_dict(arch, seed=0, fp16_values=fp16_values)
     digest = synth.state_dict_digest(sd)
     tsd = {k: torch.from_numpy(v.copy()) for k, v in sd.items()}
     return tsd, digest
@@ -274,7 +275,7 @@ def save(name, meta, arrays):
     print("wrote", name, {k: v.shape for k, v in arrays.items()})
 
 
-def run_cocoop_headline(arch, n_cls, batch, ctx_init, n_ctx, chunk=100):
+def run_cocoop_headline(arch, n_cls, batch, ctx_init, n_ctx, chunk=100, fp16_values=False):
     """run_cocoop at the benchmark's size (ViT-B/16, C = 1,000, B = 8), where the reference's
     one-shot autograd graph would hold ~40 GB of text activations per image: the same
     reference modules and the same arithmetic as CustomCLIP.forward (cocoop.py:235-260) --
@@ -284,10 +285,11 @@ def run_cocoop_headline(arch, n_cls, batch, ctx_init, n_ctx, chunk=100):
     (image, chunk) the text encoder re-run with a graph and back-propagated from its dlogits
     slice into the prompts, and finally prompts.backward(d prompts) into ctx and meta_net.
     Mathematically the reference's backward; only the fp32 summation order of the per-chunk
-    gradient accumulation differs."""
+    gradient accumulation differs. fp16_values: on fp16-valued weights (the benchmark's, as a
+    released checkpoint loads: PREC fp32s then runs split mode 2, CLIPK_F32S16)."""
     from clip.model import build_model
     import trainers.cocoop as cocoop
-    tsd, digest = build_clip(arch)
+    tsd, digest = build_clip(arch, fp16_values)
     a = synth.ARCHS[arch]
     design = dict(DESIGN, trainer="CoCoOp")
     model = build_model(dict(tsd), design).float()
@@ -307,7 +309,7 @@ def run_cocoop_headline(arch, n_cls, batch, ctx_init, n_ctx, chunk=100):
     lbl = torch.from_numpy(synth.make_labels(batch, n_cls, seed=2))
     tok = cc.tokenized_prompts
     out = dict(arch=arch, digest=digest, n_cls=n_cls, batch=batch, n_ctx=pl.n_ctx, ctx_init=ctx_init, focal=0,
-               chunked=chunk)
+               chunked=chunk, fp16_values=bool(fp16_values))
     cc.train()
     imf_raw = cc.image_encoder(img.type(cc.dtype))
     imf = imf_raw / imf_raw.norm(dim=-1, keepdim=True)
@@ -352,7 +354,7 @@ def run_cocoop_headline(arch, n_cls, batch, ctx_init, n_ctx, chunk=100):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also full-size ViT-B/L sets (slow)")
-    ap.add_argument("--only", choices=["tokenizer", "headline"],
+    ap.add_argument("--only", choices=["tokenizer", "headline", "headline_w16"],
                     help="tokenizer: the BPE probes alone; headline: the benchmark-size CoCoOp set alone "
                          "(ViT-B/16, C 1000, B 8: ~15 min on 8 threads)")
     args = ap.parse_args()
@@ -362,6 +364,10 @@ def main():
     if args.only == "headline":
         m, a = run_cocoop_headline("ViT-B/16", 1000, 8, "a photo of a", 4)
         save("cocoop_vitb16_c1000_b8", m, a)
+        return
+    if args.only == "headline_w16":  # the benched configuration exactly: fp16-valued weights
+        m, a = run_cocoop_headline("ViT-B/16", 1000, 8, "a photo of a", 4, fp16_values=True)
+        save("cocoop_vitb16_c1000_b8_w16", m, a)
         return
     table, enc = tokenizer_table()
     pkg = os.path.join(REPO, "few-shot-prompt-learning-for-vision-language-models-in-imbalanced-datasets_amd")

@@ -52,9 +52,10 @@ def test_stale_library_is_refused(monkeypatch, tmp_path):
     orig = dict(_native.source_files())["csrc/gemm.hip"]
     src.write_bytes(open(orig, "rb").read() + b"\n")
     monkeypatch.undo()
+    built = _native.library_digest()  # loads the real library first (the tree's digest)
     files = [(r, str(src) if r == "csrc/gemm.hip" else p) for r, p in _native.source_files()]
     monkeypatch.setattr(_native, "source_files", lambda: files)
-    assert _native.source_digest() != _native.library_digest()
+    assert _native.source_digest() != built
 
 
 def test_gemm_config_knob_range():

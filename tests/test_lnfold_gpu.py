@@ -153,6 +153,21 @@ def test_gemm_ln_merge_equals_two_launches(dev, dtype, epi, Mr, Nn, fused):
         assert torch.equal(u, v), f"{nm} differs from the two-launch form"
 
 
+def test_gemm_ln_merge_empty_and_negative_rows(dev, monkeypatch):
+    """clipk_gemm_ln_merge with M = 0 is a no-op (CLIPK_OK) and M < 0 a shape error, also when
+    the fused form is forced (the fused path launched a zero-block grid)."""
+    monkeypatch.setenv("CLIPK_GEMM_CFG", "6")
+    lib = N.load()
+    x = torch.zeros(8, 512, device=dev, dtype=torch.float16)
+    w = torch.zeros(512, 512, device=dev, dtype=torch.float16)
+    f = torch.zeros(4096, device=dev)
+    for m, want in ((0, 0), (-3, -2)):
+        rc = lib.clipk_gemm_ln_merge(N.F16, N.EPI_BIAS, m, 512, 512, ops._p(x), 512, ops._p(w), 512, ops._p(f),
+                                     ops._p(x), 512, None, ops._p(f), ops._p(f), ops._p(f), ops._p(f), ops._p(f),
+                                     ops._stream())
+        assert rc == want, (m, rc)
+
+
 @pytest.mark.parametrize("Mr,Nn,K", [(47160, 512, 2048), (8000, 512, 512), (300, 512, 2048), (1, 512, 512)])
 def test_gemm_ln_stats_split(dev, Mr, Nn, K):
     """PREC fp32s statistics producer (fp32 out, 16 lanes per 64-column group): the stored output
@@ -234,27 +249,31 @@ def test_gemm_ln_gamma_split(dev, epi, Mr, Wd, Nn, w16):
     beta = (0.1 * torch.randn(Wd, generator=g)).to(dev)
     w = (torch.randn(Nn, Wd, generator=g) / math.sqrt(Wd)).half().float().to(dev)
     bias = (0.05 * torch.randn(Nn, generator=g)).to(dev)
-    wp, s, c = M.ln_fold_weights(w.cpu(), bias.cpu(), gamma.cpu(), beta.cpu(), torch.float32, dev, split=True,
+    wh, s, c = M.ln_fold_weights(w.cpu(), bias.cpu(), gamma.cpu(), beta.cpu(), torch.float32, dev, split=True,
                                  gamma_on_a=True)
-    assert ops.split_lo_zero(wp)
+    assert wh.dtype == torch.float16  # mode 2's compact weight (ops.split_hi16)
+    wpk = ops.split_pack(w)  # the packed form (CLIPK_F32S, 3 MFMAs per product)
+    assert ops.split_lo_zero(wpk)
+    assert torch.equal(wh, ops.split_hi16(wpk))
+    wp = wh if w16 else wpk
     xd = x.double()
     ref = F.layer_norm(xd, (Wd,), gamma.double(), beta.double(), eps=1e-5) @ w.double().t() + bias.double()
     xn = ops.layernorm(x, gamma, beta, out_dtype=torch.float32)
     _, _, rnb = ops.ln_stats_merge(partials(x), Wd)
     if epi == N.EPI_BIAS:
-        out = ops.gemm_ln_gamma(x, wp, epi, c, s, rnb, gamma, w16=w16)
+        out = ops.gemm_ln_gamma(x, wp, epi, c, s, rnb, gamma)
         unf = ops.gemm(xn, wp, N.EPI_BIAS, torch.float32, bias=bias)
         e_fold, e_unf = _rel(out, ref), _rel(unf, ref)
     else:
         ref_g = ref * torch.sigmoid(1.702 * ref)
-        out, d = ops.gemm_ln_gamma(x, wp, epi | N.QGELU_DERIV, c, s, rnb, gamma, want_out2=True, w16=w16)
+        out, d = ops.gemm_ln_gamma(x, wp, epi | N.QGELU_DERIV, c, s, rnb, gamma, want_out2=True)
         unf = ops.gemm(xn, wp, N.EPI_BIAS_QGELU, torch.float32, bias=bias)
         sg = torch.sigmoid(1.702 * ref)
         e_fold = max(_rel(out, ref_g), _rel(d, sg * (1 + 1.702 * ref * (1 - sg))))
         e_unf = _rel(unf, ref_g)
-    if w16:  # the 2-MFMA form equals the 3-MFMA one
-        o3 = ops.gemm_ln_gamma(x, wp, epi, c, s, rnb, gamma)
-        o2 = out if epi == N.EPI_BIAS else ops.gemm_ln_gamma(x, wp, epi, c, s, rnb, gamma, w16=True)
+    if w16:  # the 2-MFMA form on the compact weight equals the 3-MFMA one on the packed weight
+        o3 = ops.gemm_ln_gamma(x, wpk, epi, c, s, rnb, gamma)
+        o2 = out if epi == N.EPI_BIAS else ops.gemm_ln_gamma(x, wh, epi, c, s, rnb, gamma)
         assert torch.equal(o2, o3)
     mu, var = xd.mean(1), xd.var(1, unbiased=False)
     amp = float(torch.sqrt(1 + mu * mu / var).max())

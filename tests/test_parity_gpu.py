@@ -50,9 +50,12 @@ SHOULD_PACK = {"coop_tiny_end_csc0_ce", "coop_tiny_middle_csc0_ce", "coop_tiny_e
                "cocoop_vitl14_336_c3"}
 
 
-def _check(name, cocoop, prec, dev, layout="packed"):
+def _check(name, cocoop, prec, dev, layout="packed", split_modes=None):
     meta, ref = load_fixture(name)
-    out = run_native(meta, ref, prec, cocoop=cocoop, dev=str(dev), shared=layout == "packed")
+    out = run_native(meta, ref, prec, cocoop=cocoop, dev=str(dev), shared=layout == "packed",
+                     fp16_values=bool(meta.get("fp16_values", False)))
+    if split_modes is not None:
+        assert out["split_modes"] == split_modes, out["split_modes"]
     assert out["packed"] == (layout == "packed" and name in SHOULD_PACK), (name, layout, out["packed"])
     grads = [k for k in ref if k.startswith("grad_")]
     report = {}
@@ -453,3 +456,20 @@ def test_fp32s_default_target_needs_no_rerun(dev):
     before = TextEncoderCore.split_retries
     _check("cocoop_vitb16_c4", True, "fp32s", dev)
     assert TextEncoderCore.split_retries == before
+
+
+HEADLINE_W16 = "cocoop_vitb16_c1000_b8_w16"
+
+
+@pytest.mark.parametrize("prec", ["fp32s", "fp16"])
+def test_headline_batch8_w16_vs_golden(dev, prec):
+    """The benched configuration exactly: CoCoOp ViT-B/16, C = 1,000, B = 8,
+    n_ctx 4 "a photo of a", on fp16-VALUED weights (as the released checkpoints load and as
+    bench.py's synthetic weights are made) against the reference's own outputs for those weights
+    (tests/golden/make_golden.py --only headline_w16). PREC fp32s runs split mode 2 on it -- every
+    GEMM CLIPK_F32S16 on the compact weights, the gamma-on-A fold, the pre-split MLP hand-offs --
+    and is held to the fp32 gates; fp16 to the 16-bit gates."""
+    if not os.path.exists(os.path.join(os.path.dirname(__file__), "golden", HEADLINE_W16 + ".npz")):
+        pytest.fail(f"fixture {HEADLINE_W16}.npz missing (tests/golden/make_golden.py --only headline_w16)")
+    SHOULD_PACK.add(HEADLINE_W16)
+    _check(HEADLINE_W16, True, prec, dev, split_modes=(2, 2) if prec == "fp32s" else None)

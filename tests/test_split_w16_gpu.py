@@ -4,7 +4,9 @@ The released CLIP checkpoints store fp16 weights (the reference loads them from 
 archive and copies them into its fp32 model: PromptSRC/clip/clip.py:154-180, model.py:699-701),
 so clipk_split_pack's lo parts of such a weight are all zero and the hi(a) lo(b) product of the
 split GEMM is exactly zero (a v_mfma whose products are all zero returns C unchanged:
-tools/lab/mfma_zero.hip, profiles/r05w16/mfma_zero.txt). CLIPK_F32S16 skips it. The bar is
+tools/lab/mfma_zero.hip, profiles/r05w16/mfma_zero.txt). CLIPK_F32S16 skips it and takes B in
+its compact form (clipk_split_hi16: fp16 SPLIT_SCALE * W, 2 B per element instead of the packed
+4), so its K loop stages B's rows at half the bytes. The bar is
 bitwise: every output equals the 3-MFMA form's (torch.equal), GEMM by GEMM and through the whole
 CoCoOp step, and the step is within the fp32 gates of the oracle run on the same fp16-valued
 weights (|d logit| <= 1e-3, gradients rel <= 1e-3). On every tile path: the 2- / 4-slot loop's
@@ -18,6 +20,7 @@ import pytest
 import torch
 
 from fsp_amd import ops, _native as N
+from fsp_amd.clip import model as M_
 from parity_util import run_native, rel_err
 
 pytestmark = pytest.mark.gpu
@@ -28,21 +31,65 @@ def _w16(shape, g, scale):
 
 
 def test_split_lo_zero(dev):
-    """clipk_split_lo_zero: 1 for an fp16-valued weight, 0 once one element is not."""
+    """clipk_split_lo_zero: 1 for an fp16-valued weight, 0 once one element is not; split_hi16
+    compacts the former (SPLIT_SCALE * W exactly in fp16) and refuses the latter (CLIPK_ERANGE)."""
     g = torch.Generator(device="cpu").manual_seed(0)
     w = _w16((512, 2048), g, 0.03).to(dev)
-    assert ops.split_lo_zero(ops.split_pack(w))
+    bp = ops.split_pack(w)
+    assert ops.split_lo_zero(bp)
+    wh = ops.split_hi16(bp)
+    assert wh.dtype == torch.float16 and wh.shape == w.shape
+    assert torch.equal(wh.float(), w * N.SPLIT_SCALE)
     w2 = w.clone()
     w2[511, 2047] += 2.0 ** -20
-    assert not ops.split_lo_zero(ops.split_pack(w2))
+    bp2 = ops.split_pack(w2)
+    assert not ops.split_lo_zero(bp2)
+    out = torch.empty(512, 2048, dtype=torch.float16, device=dev)
+    lib = N.load()
+    assert lib.clipk_split_hi16(512, 2048, ops._p(bp2), ops._p(out), ops._stream()) == -5  # CLIPK_ERANGE
+    with pytest.raises(N.ClipkError):
+        ops.split_hi16(bp2)
     assert not ops.split_lo_zero(ops.split_pack(torch.randn(128, 64, generator=g).to(dev)))
 
 
-@pytest.mark.parametrize("M", [300, 4600, 47160])
+def test_split_checks_report_errors_not_answers(dev):
+    """The weight checks report an argument error as a negative status and leave the answer
+    untouched: a failed check is never read as 'fp16-valued' (a positive HIP error
+    code from clipk_split_lo_zero used to equal its 'all lo parts zero' answer)."""
+    import ctypes
+    lib = N.load()
+    res = ctypes.c_int(7)
+    assert lib.clipk_split_lo_zero(128, 64, None, ctypes.byref(res), ops._stream()) < 0
+    assert lib.clipk_split_lo_zero(128, 60, ops._p(torch.zeros(128, 64, dtype=torch.int32, device=dev)),
+                                   ctypes.byref(res), ops._stream()) < 0
+    assert res.value == 7
+    ok = torch.zeros(128, 64, dtype=torch.int32, device=dev)
+    assert lib.clipk_split_lo_zero(128, 64, ops._p(ok), None, ops._stream()) < 0
+    assert lib.clipk_split_lo_zero(128, 64, ops._p(ok), ctypes.byref(res), ops._stream()) == 0
+    assert res.value == 1
+    # two threads checking different weights at once each get their own answer (per-call flags)
+    import threading
+    bad = ops.split_pack(torch.randn(256, 512, device=dev))
+    good = ops.split_pack(torch.randn(256, 512, device=dev).half().float())
+    answers = {}
+
+    def run(name, t):
+        with torch.cuda.stream(torch.cuda.Stream(dev)):
+            answers[name] = [ops.split_lo_zero(t) for _ in range(20)]
+    th = [threading.Thread(target=run, args=(n, t)) for n, t in (("bad", bad), ("good", good))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert answers == {"bad": [False] * 20, "good": [True] * 20}
+
+
+@pytest.mark.parametrize("M", [300, 4600, 8000, 47160])
 @pytest.mark.parametrize("Nn,K", [(512, 2048), (2048, 512), (1536, 512), (512, 512)])
 def test_gemm_w16_vs_f32s(dev, M, Nn, K):
-    """CLIPK_F32S16 == CLIPK_F32S bit for bit on an fp16-valued weight, every epilogue and the
-    LayerNorm-statistics producer, on the small-M, 128x128 and 192x256 ping-pong tiles."""
+    """CLIPK_F32S16 on the compact weight == CLIPK_F32S on the packed weight bit for bit (an
+    fp16-valued weight), every epilogue and the LayerNorm-statistics producer, on the small-M,
+    128x128 and 192x256 ping-pong tiles."""
     g = torch.Generator(device="cpu").manual_seed(M + Nn + K)
     a = torch.randn(M, K, generator=g).to(dev)
     b = _w16((Nn, K), g, 1 / math.sqrt(K)).to(dev)
@@ -51,41 +98,59 @@ def test_gemm_w16_vs_f32s(dev, M, Nn, K):
     aux = torch.randn(M, Nn, generator=g).to(dev)
     bp = ops.split_pack(b)
     assert ops.split_lo_zero(bp)
+    bh = ops.split_hi16(bp)
     cases = [(N.EPI_NONE, {}), (N.EPI_BIAS, {"bias": bias}), (N.EPI_BIAS_RES, {"bias": bias, "res": res}),
              (N.EPI_BIAS_QGELU, {"bias": bias, "want_out2": True}),
              (N.EPI_BIAS_QGELU | N.QGELU_DERIV, {"bias": bias, "want_out2": True}),
              (N.EPI_DQGELU, {"aux": aux}), (N.EPI_DQGELU | N.QGELU_DERIV, {"aux": aux})]
     for epi, kw in cases:
         o3 = ops.gemm(a, bp, epi, **kw)
-        o2 = ops.gemm(a, bp, epi, w16=True, **kw)
+        o2 = ops.gemm(a, bh, epi, **kw)
         o3 = o3 if isinstance(o3, tuple) else (o3,)
         o2 = o2 if isinstance(o2, tuple) else (o2,)
         for x, y in zip(o2, o3):
             assert torch.equal(x, y), f"epi {epi:#x}: {int((x != y).sum())} outputs differ"
     # the same product to fp64: the split's fp32-class accuracy holds
     ref = a.double() @ b.double().t()
-    o = ops.gemm(a, bp, N.EPI_NONE, w16=True)
+    o = ops.gemm(a, bh, N.EPI_NONE)
     assert ((o.double() - ref).abs().max() / ref.abs().max()).item() <= 4e-6
     if Nn % 64 == 0 and M >= 16:
         st3 = torch.empty(M, Nn // 64, 2, device=dev)
         st2 = torch.empty_like(st3)
         y3 = ops.gemm_ln(a, bp, N.EPI_BIAS_RES, bias, stats=st3, res=res)
-        y2 = ops.gemm_ln(a, bp, N.EPI_BIAS_RES, bias, stats=st2, res=res, w16=True)
+        y2 = ops.gemm_ln(a, bh, N.EPI_BIAS_RES, bias, stats=st2, res=res)
         assert torch.equal(y2, y3) and torch.equal(st2, st3)
+    if M <= 8000:  # split-K slices (the ViT's small-M path) on the compact weight
+        sk = ops.gemm_splitk(a, bh, N.EPI_NONE, splits=2) if K >= 512 else None
+        if sk is not None:
+            assert torch.equal(sk, ops.gemm_splitk(a, bp, N.EPI_NONE, splits=2))
 
 
-def test_w16_on_fp32_weights_is_the_rounded_weight(dev):
-    """CLIPK_F32S16 on a weight with nonzero lo parts is a caller error the split_lo_zero check
-    prevents (the encoders' split_mode): the lo part is then dropped, i.e. the product is that of
-    the weight rounded to fp16 (SPLIT_SCALE * W to fp16)."""
+def test_w16_refuses_fp32_weights(dev):
+    """A weight with nonzero lo parts has no compact form: split_hi16 refuses it, so CLIPK_F32S16
+    can never drop a weight's lo part (the encoders pick split mode 2 only when every weight passes
+    split_lo_zero, and then compact each one through split_hi16, which checks again)."""
     g = torch.Generator(device="cpu").manual_seed(7)
-    a = torch.randn(4600, 512, generator=g).to(dev)  # N = 2048 at 4.6k rows: the ping-pong tiles
     b = (torch.randn(2048, 512, generator=g) * 0.04).to(dev)
     bp = ops.split_pack(b)
     assert not ops.split_lo_zero(bp)
-    want = ops.gemm(a, ops.split_pack((b * N.SPLIT_SCALE).half().float() / N.SPLIT_SCALE), N.EPI_NONE)
-    got = ops.gemm(a, bp, N.EPI_NONE, w16=True)
-    assert torch.equal(got, want)
+    with pytest.raises(N.ClipkError):
+        ops.split_hi16(bp)
+
+
+def test_encoder_split_mode_is_fixed(dev):
+    """clipk_encoder_set_split: the mode names the tables' format, so it cannot change once set or
+    under a LayerNorm fold (a mode change after set_ln_fold applied gamma twice or
+    dropped it)."""
+    from fsp_amd.clip import synth, model as M
+    sd = synth.make_state_dict("tiny4", seed=0)
+    core = M.TextEncoderCore(sd, synth.ARCHS["tiny4"], "fp32s", dev)
+    lib = N.load()
+    mode = core.split_mode
+    assert mode in (1, 2)
+    assert lib.clipk_encoder_set_split(core.handle, mode) == 0        # idempotent
+    assert lib.clipk_encoder_set_split(core.handle, 3 - mode) == -1   # CLIPK_EINVAL
+    assert lib.clipk_encoder_set_split(core.handle, 0) == -1
 
 
 def _cocoop_c1000_b2(dev, fp16_values, monkeypatch, w16, fold=True):
@@ -126,3 +191,106 @@ def test_cocoop_headline_w16_vs_oracle(dev, monkeypatch):
     assert abs(out["loss"] - ref["loss"]) <= 1e-4 * max(1.0, abs(ref["loss"]))
     for g in [k for k in ref if k.startswith("grad_")]:
         assert rel_err(out[g], ref[g]) <= 1e-3, g
+
+
+def split_form(x):
+    """The pre-split operand form of fp32 x [M, K] (include/clipk.h CLIPK_OUT_SPLIT): per 8
+    consecutive k, 8 fp16 hi = fp16(x) then 8 fp16 lo = fp16(x - hi), viewed as fp32 [M, K]."""
+    M, K = x.shape
+    hi = x.half()
+    lo = (x - hi.float()).half()  # x - hi is exact in fp32
+    t = torch.stack([hi.view(M, K // 8, 8), lo.view(M, K // 8, 8)], 2)
+    return t.reshape(M, 2 * K).view(torch.float32)
+
+
+@pytest.mark.parametrize("M", [300, 4600, 8000, 47160])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_presplit_handoffs_bitwise(dev, M, mode):
+    """The MLP's pre-split hand-offs (CLIPK_OUT_SPLIT producers, CLIPK_A_SPLIT consumers) are
+    bitwise the fp32 hand-offs: c_fc (plain, W'-fold, gamma-fold) -> c_proj (plain and as the
+    statistics producer), dgelu (saved derivative) -> fc_dx, on every tile path (M 300: 64x128,
+    4,600 / 8,000: 128x128, 47,160: the 192x256 ping-pong tiles)."""
+    W = 512
+    g = torch.Generator(device="cpu").manual_seed(M + mode)
+    x = (torch.randn(M, W, generator=g) + 0.5 * torch.randn(M, 1, generator=g)).to(dev)
+    wfc = _w16((4 * W, W), g, 1 / math.sqrt(W)).to(dev)
+    wpj = _w16((W, 4 * W), g, 1 / math.sqrt(4 * W)).to(dev)
+    pk = lambda w: ops.split_hi16(ops.split_pack(w)) if mode == 2 else ops.split_pack(w)
+    bfc, bpj = pk(wfc), pk(wpj)
+    bias_fc = torch.randn(4 * W, generator=g).to(dev)
+    bias_pj = torch.randn(W, generator=g).to(dev)
+    res = torch.randn(M, W, generator=g).to(dev)
+    # c_fc (training form: QuickGELU(h) and the saved derivative) -> c_proj
+    for e in (N.EPI_BIAS_QGELU | N.QGELU_DERIV, N.EPI_BIAS_QGELU):
+        y, d = ops.gemm(x, bfc, e, bias=bias_fc, want_out2=True)
+        ys, ds = ops.gemm(x, bfc, e | N.OUT_SPLIT, bias=bias_fc, want_out2=True)
+        assert torch.equal(ys.view(torch.int32), split_form(y).view(torch.int32)), f"c_fc split output, epi {e:#x}"
+        assert torch.equal(ds, d)
+    o = ops.gemm(y, bpj, N.EPI_BIAS_RES, bias=bias_pj, res=res)
+    os_ = ops.gemm(ys, bpj, N.EPI_BIAS_RES | N.A_SPLIT, bias=bias_pj, res=res)
+    assert torch.equal(os_, o), "c_proj on the pre-split A"
+    st1, st2 = torch.empty(M, W // 64, 2, device=dev), torch.empty(M, W // 64, 2, device=dev)
+    o1 = ops.gemm_ln(y, bpj, N.EPI_BIAS_RES, bias_pj, stats=st1, res=res)
+    o2 = ops.gemm_ln(ys, bpj, N.EPI_BIAS_RES | N.A_SPLIT, bias_pj, stats=st2, res=res)
+    assert torch.equal(o1, o2) and torch.equal(st1, st2)
+    # dgelu (acc x the saved derivative) -> fc_dx
+    aux = torch.rand(M, 4 * W, generator=g).to(dev)
+    wfcT = pk(wfc.t().contiguous())
+    wpjT = pk(wpj.t().contiguous())
+    dh = ops.gemm(res, wpjT, N.EPI_DQGELU | N.QGELU_DERIV, aux=aux)
+    dhs = ops.gemm(res, wpjT, N.EPI_DQGELU | N.QGELU_DERIV | N.OUT_SPLIT, aux=aux)
+    assert torch.equal(dhs.view(torch.int32), split_form(dh).view(torch.int32)), "dgelu split output"
+    assert torch.equal(ops.gemm(dhs, wfcT, N.EPI_NONE | N.A_SPLIT), ops.gemm(dh, wfcT, N.EPI_NONE)), "fc_dx"
+    # the LayerNorm folds of c_fc with a split output
+    gamma = (1.0 + 0.2 * torch.randn(W, generator=g)).to(dev)
+    beta = (0.1 * torch.randn(W, generator=g)).to(dev)
+    _, _, rnb = ops.ln_stats_merge(_partials(x), W)
+    if mode == 2:
+        wh, s, c = M_.ln_fold_weights(wfc.cpu(), bias_fc.cpu(), gamma.cpu(), beta.cpu(), torch.float32, dev,
+                                      split=True, gamma_on_a=True)
+        f, fd = ops.gemm_ln_gamma(x, wh, N.EPI_BIAS_QGELU | N.QGELU_DERIV, c, s, rnb, gamma, want_out2=True)
+        fs, fds = ops.gemm_ln_gamma(x, wh, N.EPI_BIAS_QGELU | N.QGELU_DERIV | N.OUT_SPLIT, c, s, rnb, gamma,
+                                    want_out2=True)
+        assert torch.equal(fs.view(torch.int32), split_form(f).view(torch.int32)) and torch.equal(fds, fd)
+        # the fold reading A pre-split as split(x * gamma): clipk_gemm_ln_stats_split's out2
+        xs = split_form(x * gamma)
+        fa, fda = ops.gemm_ln_gamma(xs, wh, N.EPI_BIAS_QGELU | N.QGELU_DERIV | N.A_SPLIT, c, s, rnb, gamma,
+                                    want_out2=True)
+        assert torch.equal(fa, f) and torch.equal(fda, fd), "fold on the pre-split x * gamma"
+        q, _ = ops.gemm_ln_gamma(x, wh, N.EPI_BIAS, c, s, rnb, gamma), None
+        qa = ops.gemm_ln_gamma(xs, wh, N.EPI_BIAS | N.A_SPLIT, c, s, rnb, gamma)
+        assert torch.equal(qa, q)
+        st3 = torch.empty(M, W // 64, 2, device=dev)
+        o3, o3s = ops.gemm_ln_stats_split(ys, bpj, N.EPI_BIAS_RES | N.A_SPLIT, bias_pj, st3, res, gamma)
+        assert torch.equal(o3, o1) and torch.equal(st3, st1)
+        assert torch.equal(o3s.view(torch.int32), split_form(o1 * gamma).view(torch.int32)), "stats_split out2"
+    else:
+        wp, s, c = M_.ln_fold_weights(wfc.cpu(), bias_fc.cpu(), gamma.cpu(), beta.cpu(), torch.float32, dev,
+                                      split=True)
+        f, fd = ops.gemm_ln(x, wp, N.EPI_BIAS_QGELU | N.QGELU_DERIV, c, colsum=s, rnb=rnb, want_out2=True)
+        fs, fds = ops.gemm_ln(x, wp, N.EPI_BIAS_QGELU | N.QGELU_DERIV | N.OUT_SPLIT, c, colsum=s, rnb=rnb,
+                              want_out2=True)
+        assert torch.equal(fs.view(torch.int32), split_form(f).view(torch.int32)) and torch.equal(fds, fd)
+
+
+def _partials(x):
+    M, W = x.shape
+    v = x.view(M, W // 64, 64).double()
+    s = v.sum(2)
+    mu = s / 64
+    return torch.stack([s, ((v - mu[..., None]) ** 2).sum(2)], 2).float()
+
+
+def test_presplit_flags_refused_where_not_built(dev):
+    """Pre-split flags on a 16-bit / fp32 GEMM, on a 16-bit out, or with an epilogue no encoder
+    hands off are refused before any launch (CLIPK_EINVAL / EDTYPE), never run as a plain GEMM."""
+    lib = N.load()
+    a = torch.randn(256, 512, device=dev)
+    b16 = torch.randn(512, 512, device=dev).half()
+    out = torch.empty(256, 512, device=dev)
+    args = lambda ind, epi, b: (ind, N.F32, epi, 256, 512, 512, ops._p(a), 512, ops._p(b), 512, None, None, 512,
+                                ops._p(out), 512, None, None, 0, 512, ops._stream())
+    assert lib.clipk_gemm(*args(N.F16, N.EPI_NONE | N.A_SPLIT, b16)) < 0
+    assert lib.clipk_gemm(*args(N.F32, N.EPI_NONE | N.OUT_SPLIT, a[:, :512].contiguous())) < 0
+    assert lib.clipk_gemm(*args(N.F32S16, N.EPI_NONE | N.OUT_SPLIT, b16)) < 0  # EPI_NONE does not hand off split
+    assert lib.clipk_gemm(*args(N.F32S16, N.EPI_NONE | 0x1000, b16)) < 0
