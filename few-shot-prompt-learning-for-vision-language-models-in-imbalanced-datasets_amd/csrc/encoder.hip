@@ -509,6 +509,19 @@ static int gemm_ln(int act, int epi, int M, int N, int K, const void* A, const v
   if (gamma) return clipk_gemm_ln_gamma(act, epi, M, N, K, A, K, B, K, bias, o, N, o2, colsum, rnb, gamma, st);
   return clipk_gemm_ln(act, epi, M, N, K, A, K, B, K, bias, res, N, o, N, o2, stats, colsum, rnb, st);
 }
+// PREC fp32s split mode 2 with pre-split hand-offs: the residual-stream producer (out_proj ->
+// ln_2 -> c_fc, c_proj -> the next layer's ln_1 -> qkv) also stores the fold's A operand pre-split,
+// split(x * gamma) (clipk_gemm_ln_stats_split), into xs; the fold reads it with CLIPK_A_SPLIT
+static int gemm_ln_split2(int epi, int M, int N, int K, const void* A, const void* B, const float* bias,
+                          const void* res, void* o, float* stats, const float* gamma, void* xs, hipStream_t st,
+                          int prof_cls, const char* site) {
+  const double b = gemm_bytes(CLIPK_F32S16, CLIPK_F32, epi, M, N, K, false, CLIPK_F32) + (double)M * (N / 64) * 8 +
+                   4.0 * M * N + 4.0 * N;
+  ProfScope ps(prof_cls, st, 2.0 * M * N * K, site, b);
+  return clipk_gemm_ln_stats_split(CLIPK_F32S16, epi, M, N, K, A, K, B, K, bias, res, N, o, N, stats, gamma, xs, st);
+}
+// the fold-side hand-off of gemm_ln_split2 is on for this call: split mode 2, pre-split hand-offs
+static bool ps_fold(const clipk_encoder* e) { return t_split == 2 && e->split == 2 && presplit_on(); }
 // mean / rstd (kept for the LayerNorm backward) and the folding GEMM's (rstd, -rstd mean) pairs
 static int ln_merge(int rows, int W, const float* lnst, float* m, float* r, float* rnb, hipStream_t st, bool text) {
   ProfScope ps(CLIPK_PROF_NONE, st, 0.0, text ? "text.ln_stats" : "vit.ln_stats", (double)rows * (W / 64) * 8 + 16.0 * rows);
@@ -533,11 +546,13 @@ static int gemm_ln_merged(int act, int epi, int M, int N, int K, const void* A, 
 // (gamma: split mode 2, the fold's LayerNorm weight applied to A, f[0] = W itself)
 static int block_attn_fold(const clipk_encoder* e, const std::array<const void*, 6>& f, const SeqShape& sh,
                            const void* X, void* qkv, void* o, float* lse, float* m1, float* r1, const float* lnst,
-                           float* rnb, hipStream_t st, bool text, const float* gamma = nullptr) {
+                           float* rnb, hipStream_t st, bool text, const float* gamma = nullptr,
+                           const void* xs = nullptr) {
+  // xs: split(X * gamma), written by the previous layer's c_proj (gemm_ln_split2): the fold's A
   const int W = e->W, rows = sh.rows, act = e->act;
-  TRY(gemm_ln_merged(act, CLIPK_EPI_BIAS, rows, 3 * W, W, X, f[0], (const float*)f[2], qkv, nullptr, lnst,
-                     (const float*)f[1], m1, r1, rnb, st, text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE,
-                     text ? "text.qkv_fwd" : "vit.qkv_fwd", text, gamma));
+  TRY(gemm_ln_merged(act, CLIPK_EPI_BIAS | (xs ? CLIPK_A_SPLIT : 0), rows, 3 * W, W, xs ? xs : X, f[0],
+                     (const float*)f[2], qkv, nullptr, lnst, (const float*)f[1], m1, r1, rnb, st,
+                     text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE, text ? "text.qkv_fwd" : "vit.qkv_fwd", text, gamma));
   const double ab = (double)rows * 4 * W * esize(act) + (lse ? 4.0 * rows * e->heads : 0.0);
   ProfScope ps(text ? CLIPK_PROF_ATTN : CLIPK_PROF_NONE, st, 0.0, text ? "text.attn_fwd" : "vit.attn_fwd", ab);
   return attn_fwd(e, sh, qkv, o, lse, st);
@@ -547,15 +562,27 @@ static int block_attn_fold(const clipk_encoder* e, const std::array<const void*,
 static int block_post_fold(const clipk_encoder* e, const std::array<const void*, 16>& w,
                            const std::array<const void*, 6>& f, int rows, const void* X, const void* o, void* Xm,
                            void* Xo, void* h, void* g, float* m2, float* r2, float* lnst, float* rnb,
-                           bool stats_next, hipStream_t st, bool text) {
+                           bool stats_next, hipStream_t st, bool text, void* xs = nullptr,
+                           const float* gamma_next = nullptr) {
+  // xs (split mode 2, pre-split hand-offs): scratch [rows, W] for split(Xm * gamma2) -- c_fc's A --
+  // and then split(Xo * gamma_next), the next layer's qkv A (gamma_next: its ln_1 weight)
   const int W = e->W, act = e->act;
   const int pg = text ? CLIPK_PROF_GEMM_ALL : CLIPK_PROF_NONE;
-  TRY(gemm_ln(act, CLIPK_EPI_BIAS_RES, rows, W, W, o, w[4], (const float*)w[5], X, Xm, nullptr, lnst, nullptr,
-              nullptr, st, pg, text ? "text.out_fwd" : "vit.out_fwd"));
-  TRY(gemm_ln_merged(act, CLIPK_EPI_BIAS_QGELU | (h && qgelu_deriv_on() ? CLIPK_QGELU_DERIV : 0) | ps_out(), rows, 4 * W,
-                     W, Xm, f[3], (const float*)f[5], g, h, lnst, (const float*)f[4], m2, r2, rnb, st,
-                     text ? CLIPK_PROF_GEMM_FC : CLIPK_PROF_NONE, text ? "text.fc_fwd" : "vit.fc_fwd", text,
-                     e->split == 2 ? (const float*)w[6] : nullptr));
+  const float* g2 = e->split == 2 ? (const float*)w[6] : nullptr;
+  if (xs)
+    TRY(gemm_ln_split2(CLIPK_EPI_BIAS_RES, rows, W, W, o, w[4], (const float*)w[5], X, Xm, lnst, g2, xs, st, pg,
+                       text ? "text.out_fwd" : "vit.out_fwd"));
+  else
+    TRY(gemm_ln(act, CLIPK_EPI_BIAS_RES, rows, W, W, o, w[4], (const float*)w[5], X, Xm, nullptr, lnst, nullptr,
+                nullptr, st, pg, text ? "text.out_fwd" : "vit.out_fwd"));
+  TRY(gemm_ln_merged(act, CLIPK_EPI_BIAS_QGELU | (h && qgelu_deriv_on() ? CLIPK_QGELU_DERIV : 0) | ps_out() |
+                              (xs ? CLIPK_A_SPLIT : 0),
+                     rows, 4 * W, W, xs ? xs : Xm, f[3], (const float*)f[5], g, h, lnst, (const float*)f[4], m2, r2,
+                     rnb, st, text ? CLIPK_PROF_GEMM_FC : CLIPK_PROF_NONE, text ? "text.fc_fwd" : "vit.fc_fwd", text,
+                     g2));
+  if (stats_next && xs && gamma_next)
+    return gemm_ln_split2(CLIPK_EPI_BIAS_RES | ps_a(), rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo, lnst,
+                          gamma_next, xs, st, pg, text ? "text.proj_fwd" : "vit.proj_fwd");
   if (stats_next)
     return gemm_ln(act, CLIPK_EPI_BIAS_RES | ps_a(), rows, W, 4 * W, g, w[10], (const float*)w[11], Xm, Xo, nullptr,
                    lnst, nullptr, nullptr, st, pg, text ? "text.proj_fwd" : "vit.proj_fwd");
@@ -802,6 +829,7 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
   const int nl = e->layers, nout = sh.nout;
   const bool fold = ln_fold_on(e, io);
   bool have_stats = false;  // LN fold: t.lnst holds the statistics partials of cur
+  bool xs_ready = false;    // t.xn holds split(cur * the next ln_1 weight) (block_post_fold)
   for (int l = 0; l < nl; ++l) {
     void* Xo = t.X[l + 1];
     if (!save && Xo == cur) Xo = t.X[l];  // ping-pong (cur may be the caller's x0)
@@ -817,7 +845,7 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
                              (int*)t.g, st));
     else if (fold && have_stats)
       TRY(block_attn_fold(e, e->fold[l], sh, cur, t.qkv[l], t.o[l], t.lse[l], m1, r1, t.lnst, t.rnb, st, io.text,
-                          e->split == 2 ? (const float*)e->lw[l][0] : nullptr));
+                          e->split == 2 ? (const float*)e->lw[l][0] : nullptr, xs_ready ? t.xn : nullptr));
     else
       TRY(block_attn(e, e->lw[l], sh, rd, cur, t.xn, t.qkv[l], t.o[l], t.lse[l], t.mean1[l], t.rstd1[l], st,
                      io.text, io.sk, io.skb));
@@ -835,9 +863,14 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
       oin = t.oc;
     }
     const int n = compact ? nout : sh.rows;
+    // split mode 2, pre-split hand-offs: t.xn (free once layer 0's LayerNorm output is consumed)
+    // carries split(x * gamma) from each residual producer to its fold
+    void* xs = fold && ps_fold(e) ? t.xn : nullptr;
+    const float* gnext = l + 1 < nl ? (const float*)e->lw[l + 1][0] : nullptr;
+    xs_ready = xs && gnext;
     if (fold)
       TRY(block_post_fold(e, e->lw[l], e->fold[l], n, xin, oin, t.Xm[l], Xo, save ? t.h[l] : nullptr, t.g, m2, r2,
-                          t.lnst, t.rnb, l + 1 < nl, st, io.text));
+                          t.lnst, t.rnb, l + 1 < nl, st, io.text, xs, gnext));
     else
       TRY(block_post(e, e->lw[l], n, rd, xin, oin, t.Xm[l], Xo, t.xn, save ? t.h[l] : nullptr, t.g, t.mean2[l],
                      t.rstd2[l], st, io.text, compact ? nullptr : io.sk, compact ? 0 : io.skb));

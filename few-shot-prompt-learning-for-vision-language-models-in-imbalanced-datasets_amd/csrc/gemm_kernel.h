@@ -136,6 +136,10 @@ __device__ __forceinline__ unsigned split_lo2(float a, float b, unsigned h) {
 // before the MFMAs that read the parts, and keeps the cheaper asm form.
 template <bool MIX = CLIPK_SPLIT_MIX != 0>
 __device__ __forceinline__ void split8(u32x4 a0, u32x4 a1, u32x4& hi, u32x4& lo) {
+  // the inputs as materialised fp32 values: a caller's x * gamma (the fold's LayerNorm weight) must
+  // not contract with the x - hi below into one fma (the parts of the unrounded product), so every
+  // path -- this one, the asm form, a producer's pre-split store -- splits the same rounded value
+  asm volatile("" : "+v"(a0), "+v"(a1));
   const f32x4 x0 = __builtin_bit_cast(f32x4, a0), x1 = __builtin_bit_cast(f32x4, a1);
   f16x8 h;
 #pragma unroll

@@ -254,9 +254,10 @@ def test_presplit_handoffs_bitwise(dev, M, mode):
         assert torch.equal(fs.view(torch.int32), split_form(f).view(torch.int32)) and torch.equal(fds, fd)
         # the fold reading A pre-split as split(x * gamma): clipk_gemm_ln_stats_split's out2
         xs = split_form(x * gamma)
-        fa, fda = ops.gemm_ln_gamma(xs, wh, N.EPI_BIAS_QGELU | N.QGELU_DERIV | N.A_SPLIT, c, s, rnb, gamma,
-                                    want_out2=True)
-        assert torch.equal(fa, f) and torch.equal(fda, fd), "fold on the pre-split x * gamma"
+        fa, fda = ops.gemm_ln_gamma(xs, wh, N.EPI_BIAS_QGELU | N.QGELU_DERIV | N.A_SPLIT | N.OUT_SPLIT, c, s, rnb,
+                                    gamma, want_out2=True)
+        assert torch.equal(fa.view(torch.int32), fs.view(torch.int32)) and torch.equal(fda, fd), \
+            "fold on the pre-split x * gamma"
         q, _ = ops.gemm_ln_gamma(x, wh, N.EPI_BIAS, c, s, rnb, gamma), None
         qa = ops.gemm_ln_gamma(xs, wh, N.EPI_BIAS | N.A_SPLIT, c, s, rnb, gamma)
         assert torch.equal(qa, q)
