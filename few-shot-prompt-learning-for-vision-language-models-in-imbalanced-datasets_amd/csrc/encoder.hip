@@ -923,8 +923,14 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
   // the ViT's residual stream is fp32: its gradient stays fp32 too
   const bool r16 = io.rd != CLIPK_F32 && text_dres16(e);
   // fp32 gradients with the fp32 stream (PREC fp32 / fp32s): the input-grad GEMMs read dX itself
-  // (a second fp32 copy in dX_lp would be 4 B/element more per LayerNorm backward, unread)
-  const bool lp_alias = !r16 && gd == CLIPK_F32;
+  // (a second fp32 copy in dX_lp would be 4 B/element more per LayerNorm backward, unread).
+  // PREC fp32s with pre-split hand-offs: the LayerNorm backwards also write dX_lp in the pre-split
+  // form (lp dtype CLIPK_F32S), which proj_dx / out_dx read with CLIPK_A_SPLIT (no split VALU in
+  // their K loops; +4 B/element written per LayerNorm backward)
+  const bool a_split = e->split == 2 && presplit_on() && !r16 && gd == CLIPK_F32;  // (split mode 2: the kernels built)
+  const bool lp_alias = !r16 && gd == CLIPK_F32 && !a_split;
+  const int lpd = a_split ? CLIPK_F32S : gd;  // dX_lp's dtype
+  const int dA_split = a_split ? CLIPK_A_SPLIT : 0;
   void* const dA = lp_alias ? (void*)dX : b.dX_lp;  // the A operand of proj_dx / out_dx
   const bool eotl = text_eot_last(sh);
   auto zero = [&](void* p, size_t bytes) {
@@ -938,7 +944,7 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
   const int rd = io.rd;
   const int* frows = eotl ? nullptr : eot_rows;  // EOT-last: the last layer's rows are compact
   TRY(clipk_layernorm_bwd_x2(rd, CLIPK_F32, nout, W, b.dlnf, W, t.Xf, W, frows, io.lnf_w, t.meanf,
-                             t.rstdf, nullptr, CLIPK_F32, W, r16 ? nullptr : dX, lp_alias ? nullptr : b.dX_lp, gd,
+                             t.rstdf, nullptr, CLIPK_F32, W, r16 ? nullptr : dX, lp_alias ? nullptr : b.dX_lp, lpd,
                              frows, W, st));
   // residual-gradient update of one LayerNorm backward over n rows: dres (fp32 dX or the
   // 16-bit dX_lp, in place) + LN'(dxn); last: the encoder input's gradient, always fp32 into dX
@@ -949,7 +955,7 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
     ProfScope ps(CLIPK_PROF_NONE, st, 0.0, SITE("ln_bwd"), lnbb);
     if (!r16)
       return clipk_layernorm_bwd_x(rd, gd, n, W, b.dxn, W, x, W, nullptr, gamma, mean, rstd, dX, W, dX,
-                                   last || lp_alias ? nullptr : b.dX_lp, gd, nullptr, W, st);
+                                   last || lp_alias ? nullptr : b.dX_lp, lpd, nullptr, W, st);
     return clipk_layernorm_bwd_x2(rd, gd, n, W, b.dxn, W, x, W, nullptr, gamma, mean, rstd, b.dX_lp, gd, W,
                                   last ? dX : nullptr, b.dX_lp, gd, nullptr, W, st);
   };
@@ -969,14 +975,14 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
     // (the last layer's compact EOT-row launches are sites of their own: a different GEMM grid)
     // (PREC fp32s: dh handed to fc_dx pre-split, presplit_on; the saved-derivative form only)
     const bool dh_split = (dgelu_epi & CLIPK_QGELU_DERIV) != 0;
-    TRY(gemm(gd, gd, dgelu_epi | (dh_split ? ps_out() : 0), n, 4 * W, W, dA, w[15], nullptr, nullptr, b.dh, nullptr,
-             t.h[l], act, st, io.text ? CLIPK_PROF_GEMM_DGELU : CLIPK_PROF_NONE, nullptr, 0,
+    TRY(gemm(gd, gd, dgelu_epi | (dh_split ? ps_out() | dA_split : 0), n, 4 * W, W, dA, w[15], nullptr, nullptr,
+             b.dh, nullptr, t.h[l], act, st, io.text ? CLIPK_PROF_GEMM_DGELU : CLIPK_PROF_NONE, nullptr, 0,
              compact ? SITE("proj_dx_dgelu_eot") : SITE("proj_dx_dgelu")));
     TRY(gemm(gd, gd, CLIPK_EPI_NONE | (dh_split ? ps_a() : 0), n, W, 4 * W, b.dh, w[14], nullptr, nullptr, b.dxn,
              nullptr, nullptr, 0, st, pg, nullptr, 0, compact ? SITE("fc_dx_eot") : SITE("fc_dx")));
     TRY(ln_bwd(n, t.Xm[l], (const float*)w[6], t.mean2[l], t.rstd2[l], false));
     // attention: do = dXm . Wout ; dqkv ; dxn1 = dqkv . Win
-    TRY(gemm(gd, gd, CLIPK_EPI_NONE, n, W, W, dA, w[13], nullptr, nullptr, compact ? b.dh : b.do_,
+    TRY(gemm(gd, gd, CLIPK_EPI_NONE | dA_split, n, W, W, dA, w[13], nullptr, nullptr, compact ? b.dh : b.do_,
              nullptr, nullptr, 0, st, pg, nullptr, 0, compact ? SITE("out_dx_eot") : SITE("out_dx")));
     if (compact) {
       // back to the full row layout: do and the residual gradient (the one LN1's backward

@@ -42,7 +42,37 @@ __device__ __forceinline__ void ldv(const T* p, float* o) {
 }
 template <typename T, int VW>
 __device__ __forceinline__ void stv(T* p, const float* v) {
-  if constexpr (VW == 4) {
+  if constexpr (__is_same(T, f32s)) {
+    // the pre-split operand form of a split GEMM's A (include/clipk.h CLIPK_A_SPLIT): per 8
+    // consecutive elements 16 B of fp16 hi = fp16(v) then 16 B of lo = fp16(v - hi), of the
+    // ROUNDED fp32 v (opaque copy: no contraction with v's producing arithmetic). VW 8 = one whole
+    // group; VW 4 = half a group (hi and lo 8 B each, 16 B apart).
+    float x[VW];
+#pragma unroll
+    for (int i = 0; i < VW; ++i) {
+      x[i] = v[i];
+      asm volatile("" : "+v"(x[i]));
+    }
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    h4 hi[VW / 4], lo[VW / 4];
+#pragma unroll
+    for (int i = 0; i < VW; ++i) {
+      hi[i / 4][i % 4] = (_Float16)x[i];
+      lo[i / 4][i % 4] = (_Float16)(x[i] - (float)hi[i / 4][i % 4]);
+    }
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);  // element offset within its 8-group: 0 or 4
+    char* g = reinterpret_cast<char*>(a & ~uintptr_t(31));
+    const int half = (int)((a >> 4) & 1);
+    if constexpr (VW == 8) {
+      *reinterpret_cast<uint4*>(g) = __builtin_bit_cast(uint4, (f16x8){hi[0][0], hi[0][1], hi[0][2], hi[0][3],
+                                                                       hi[1][0], hi[1][1], hi[1][2], hi[1][3]});
+      *reinterpret_cast<uint4*>(g + 16) = __builtin_bit_cast(uint4, (f16x8){lo[0][0], lo[0][1], lo[0][2], lo[0][3],
+                                                                            lo[1][0], lo[1][1], lo[1][2], lo[1][3]});
+    } else {
+      *reinterpret_cast<uint2*>(g + 8 * half) = __builtin_bit_cast(uint2, hi[0]);
+      *reinterpret_cast<uint2*>(g + 16 + 8 * half) = __builtin_bit_cast(uint2, lo[0]);
+    }
+  } else if constexpr (VW == 4) {
     store4<T>(p, v[0], v[1], v[2], v[3]);
   } else if constexpr (sizeof(T) == 2) {
 #if CLIPK_LN_NT & 2
@@ -354,6 +384,9 @@ static int ln_bwd_launch(int rows, int width, const void* dy, int lddy, const TX
   if (!dx_lp || lp_dtype == CLIPK_F32) {
     if (dres_lp) return CLIPK_EDTYPE;
     CLIPK_LNB(float, false)
+  } else if (lp_dtype == CLIPK_F32S) {  // dx_lp: the next split GEMMs' pre-split A (fp32 gradients)
+    if (dres_lp || ldo % 8) return CLIPK_EDTYPE;
+    CLIPK_LNB(f32s, false)
   } else if (lp_dtype == CLIPK_BF16) {
     if (dres_lp) { CLIPK_LNB(bf16, true) } else { CLIPK_LNB(bf16, false) }
   } else if (lp_dtype == CLIPK_F16) {

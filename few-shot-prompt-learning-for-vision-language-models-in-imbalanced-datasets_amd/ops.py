@@ -239,13 +239,18 @@ def layernorm(x, w, b, out_dtype=torch.float32, rows=None, stats=False):
 
 
 def layernorm_bwd(dy, x, w, mean, rstd, dres=None, lp_dtype=None):
+    """LayerNorm input-grad (+ dres) into fp32 dx and, with lp_dtype, a second copy dx_lp; lp_dtype
+    "split": dx_lp in the pre-split operand form (CLIPK_A_SPLIT; fp32 storage of fp16 parts)."""
     _need(dy, "dy")
     R, W = dy.shape
     dx = torch.empty(R, W, device=dy.device, dtype=torch.float32)
-    lp = torch.empty(R, W, device=dy.device, dtype=lp_dtype) if lp_dtype is not None else None
+    split = lp_dtype == "split"
+    lp = (torch.empty(R, W, device=dy.device, dtype=torch.float32 if split else lp_dtype)
+          if lp_dtype is not None else None)
+    lpd = N.F32S if split else (DT[lp_dtype] if lp_dtype is not None else 0)
     _need(x, "x")
     N.call("clipk_layernorm_bwd_x", DT[x.dtype], DT[dy.dtype], R, W, _p(dy), W, _p(x), W, None, _p(w), _p(mean),
-           _p(rstd), _p(dres), W, _p(dx), _p(lp), DT[lp_dtype] if lp_dtype is not None else 0, None, W, _stream())
+           _p(rstd), _p(dres), W, _p(dx), _p(lp), lpd, None, W, _stream())
     return (dx, lp) if lp is not None else dx
 
 

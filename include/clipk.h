@@ -244,7 +244,8 @@ int clipk_layernorm_fwd_x(int x_dtype, int out_dtype, int rows, int width, const
                           void* out, int ldo, float* mean, float* rstd, void* stream);
 
 /* dx = LN-input-grad(dy; x, gamma, mean, rstd) (+ dres). dy of dy_dtype; x row = x_rows ? x_rows[r] : r;
- * outputs written at row out_rows ? out_rows[r] : r of dx (f32) and dx_lp (lp_dtype, optional). */
+ * outputs written at row out_rows ? out_rows[r] : r of dx (f32) and dx_lp (lp_dtype, optional;
+ * lp_dtype CLIPK_F32S: dx_lp in the pre-split form of CLIPK_A_SPLIT, the next split GEMMs' A). */
 int clipk_layernorm_bwd(int dy_dtype, int rows, int width, const void* dy, int lddy, const float* x, int ldx,
                         const int* x_rows, const float* gamma, const float* mean, const float* rstd,
                         const float* dres, int lddres, float* dx, void* dx_lp, int lp_dtype,

@@ -295,3 +295,21 @@ def test_presplit_flags_refused_where_not_built(dev):
     assert lib.clipk_gemm(*args(N.F32, N.EPI_NONE | N.OUT_SPLIT, a[:, :512].contiguous())) < 0
     assert lib.clipk_gemm(*args(N.F32S16, N.EPI_NONE | N.OUT_SPLIT, b16)) < 0  # EPI_NONE does not hand off split
     assert lib.clipk_gemm(*args(N.F32S16, N.EPI_NONE | 0x1000, b16)) < 0
+
+
+@pytest.mark.parametrize("rows,W", [(47160, 512), (300, 512), (257, 768)])
+def test_layernorm_bwd_split_copy(dev, rows, W):
+    """The LayerNorm backward's pre-split copy of its fp32 output (lp dtype CLIPK_F32S: the A of
+    proj_dx / out_dx under PREC fp32s) is bitwise split_form(dx), and dx itself is unchanged; at
+    W 768 the 4-element lanes store half groups."""
+    g = torch.Generator(device="cpu").manual_seed(rows + W)
+    x = (torch.randn(rows, W, generator=g) + torch.randn(rows, 1, generator=g)).to(dev)
+    dy = torch.randn(rows, W, generator=g).to(dev)
+    dres = torch.randn(rows, W, generator=g).to(dev)
+    w = (1 + 0.1 * torch.randn(W, generator=g)).to(dev)
+    mean = x.mean(1)
+    rstd = torch.rsqrt(x.var(1, unbiased=False) + 1e-5)
+    dx0 = ops.layernorm_bwd(dy, x, w, mean, rstd, dres=dres)
+    dx, lp = ops.layernorm_bwd(dy, x, w, mean, rstd, dres=dres, lp_dtype="split")
+    assert torch.equal(dx, dx0)
+    assert torch.equal(lp.view(torch.int32), split_form(dx).view(torch.int32))
