@@ -148,16 +148,24 @@ DX_SHAPES = {"fc_dx K=2048": ["text.fc_dx"], "qkv_dx K=1536": ["text.qkv_dx"], "
              "eot fc_dx+out_dx": ["text.fc_dx_eot", "text.out_dx_eot"]}
 # rocprofv3 kernel-name keys of a class, per PREC (a class may run several instantiations: fp32s's
 # fc_dx reads its A pre-split, qkv_dx / out_dx do not)
+# (rocprofv3 writes the kernel names mangled or demangled depending on its build: each class lists
+# both forms)
 ROOF_PMC_KEY = {
-    "fp16": {"gemm_dx_n512": "gemm_nt_kernelIDF16_DF16_fLi4ELi192ELi256",
-             "gemm_dgelu": "gemm_nt_kernelIDF16_DF16_DF16_Li6E",
-             "gemm_proj_fwd": "gemm_nt_kernelIDF16_DF16_DF16_Li1ELi192ELi256ELi2ELi4ELb1ELi128ELi2ELb0ELb1E",
-             "attn_bwd": "attn_prefix_bwd_lds"},
-    "fp32s": {"gemm_dx_n512": "gemm_nt_kernelINS_4f32hEffLi4ELi192ELi256ELi2ELi4ELb1E",
-              "gemm_dgelu": "gemm_nt_kernelINS_4f32hEffLi6ELi192ELi256ELi2ELi4ELb1E",
-              "gemm_proj_fwd": "gemm_nt_kernelINS_4f32hEffLi1ELi192ELi256ELi2ELi4ELb1E",
-              "gemm_fc_fwd": "gemm_nt_kernelINS_4f32hEffLi5ELi192ELi256ELi2ELi4ELb1E",
-              "attn_bwd": "attn_prefix_bwd_f32"},
+    "fp16": {"gemm_dx_n512": ("gemm_nt_kernelIDF16_DF16_fLi4ELi192ELi256",
+                              "gemm_nt_kernel<_Float16, _Float16, float, 4, 192, 256,"),
+             "gemm_dgelu": ("gemm_nt_kernelIDF16_DF16_DF16_Li6E", "gemm_nt_kernel<_Float16, _Float16, _Float16, 6,"),
+             "gemm_proj_fwd": ("gemm_nt_kernelIDF16_DF16_DF16_Li1ELi192ELi256ELi2ELi4ELb1ELi128ELi2ELb0ELb1E",
+                               "gemm_nt_kernel<_Float16, _Float16, _Float16, 1, 192, 256, 2, 4, true, 128, 2, false, true,"),
+             "attn_bwd": ("attn_prefix_bwd_lds",)},
+    "fp32s": {"gemm_dx_n512": ("gemm_nt_kernelINS_4f32hEffLi4ELi192ELi256ELi2ELi4ELb1E",
+                               "gemm_nt_kernel<clipk::f32h, float, float, 4, 192, 256, 2, 4, true,"),
+              "gemm_dgelu": ("gemm_nt_kernelINS_4f32hEffLi6ELi192ELi256ELi2ELi4ELb1E",
+                             "gemm_nt_kernel<clipk::f32h, float, float, 6, 192, 256, 2, 4, true,"),
+              "gemm_proj_fwd": ("gemm_nt_kernelINS_4f32hEffLi1ELi192ELi256ELi2ELi4ELb1E",
+                                "gemm_nt_kernel<clipk::f32h, float, float, 1, 192, 256, 2, 4, true,"),
+              "gemm_fc_fwd": ("gemm_nt_kernelINS_4f32hEffLi5ELi192ELi256ELi2ELi4ELb1E",
+                              "gemm_nt_kernel<clipk::f32h, float, float, 5, 192, 256, 2, 4, true,"),
+              "attn_bwd": ("attn_prefix_bwd_f32",)},
 }
 
 
@@ -175,13 +183,15 @@ def pmc_traffic(kernel_key, prec="fp32s"):
     """HBM bytes per launch of a kernel class from the committed PMC passes of this workload
     (tools/pmc_bench.sh: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of bench.py at that
     PREC; FETCH_SIZE doubled per the gfx950 note, MI355X_MICROARCH.md HBM): the launch-weighted
-    mean over the kernels whose name holds the key. None if absent."""
+    mean over the kernels whose name holds the key (a string, or a tuple of alternative forms).
+    None if absent."""
     try:
         with open(PMC_FILES[prec]) as f:
             d = json.load(f)
     except (OSError, KeyError):
         return None
-    hits = [(v["hbm_bytes"], v.get("launches", 1)) for k, v in d.items() if kernel_key and kernel_key in k]
+    keys = (kernel_key,) if isinstance(kernel_key, str) else tuple(kernel_key or ())
+    hits = [(v["hbm_bytes"], v.get("launches", 1)) for k, v in d.items() if any(x and x in k for x in keys)]
     n = sum(c for _, c in hits)
     return round(sum(b * c for b, c in hits) / n, 1) if n else None
 

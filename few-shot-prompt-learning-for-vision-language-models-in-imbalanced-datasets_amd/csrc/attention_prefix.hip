@@ -940,7 +940,9 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
 // dK, dV over the unit's queries (the prefix unit's own keys ARE the prefix rows: accumulated).
 // Phase 3 (lane = prefix key): the prefix rows' dK, dV partial of this unit, accumulated over
 // the chunk in registers and written once per chunk (prefix_kv_reduce sums the chunks).
-template <int WPB>
+// OS (grad dtype CLIPK_F32S): dQ / dK / dV stored in the pre-split form of the qkv input-grad
+// GEMM's A (st16x_split; the prefix rows' dK / dV by prefix_kv_reduce_split), the same bytes
+template <int WPB, bool OS = false>
 __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 waves per SIMD (<= 256 VGPRs)
     int G, int P, int R, int ntiles, const int* __restrict__ tiles, const int* __restrict__ row_first, int H,
     int nchunk, int uc, const float* __restrict__ qkv, int ldq, const float* __restrict__ o_fwd, int ldof,
@@ -1023,7 +1025,8 @@ __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 wav
     if (qok) {
 #pragma unroll
       for (int d = 0; d < 16; ++d) dq[d] *= kScale;
-      st16x(dqkv + row * lddq + h * 64 + kSl * s, dq);
+      if constexpr (OS) st16x_split(dqkv + row * lddq + h * 64 + kSl * s, dq, s);
+      else st16x(dqkv + row * lddq + h * 64 + kSl * s, dq);
     }
     // sA / sB: the unit's scaled q and dO rows for the key phases (after every lane's phase-1
     // reads of K / V: program order)
@@ -1052,8 +1055,13 @@ __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 wav
       for (int d = 0; d < 16; ++d) { dk[d] = 0.f; dv[d] = 0.f; }
       keysum(16 + r, dk, dv);
       if (qok) {
-        st16x(dqkv + row * lddq + W + h * 64 + kSl * s, dk);
-        st16x(dqkv + row * lddq + 2 * W + h * 64 + kSl * s, dv);
+        if constexpr (OS) {
+          st16x_split(dqkv + row * lddq + W + h * 64 + kSl * s, dk, s);
+          st16x_split(dqkv + row * lddq + 2 * W + h * 64 + kSl * s, dv, s);
+        } else {
+          st16x(dqkv + row * lddq + W + h * 64 + kSl * s, dk);
+          st16x(dqkv + row * lddq + 2 * W + h * 64 + kSl * s, dv);
+        }
       }
       keysum(r, akp, avp);  // prefix key r (zero columns past pre)
     }
@@ -1101,6 +1109,45 @@ __global__ __launch_bounds__(256) void prefix_kv_reduce(int P, int R, int W, int
   for (; k < nchunk; ++k) a0 += src[k * cs];
   const float acc = (a0 + a1) + (a2 + a3);
   dqkv[((size_t)g * R + p) * lddq + W + col] = (TG)acc;
+}
+
+// prefix_kv_reduce for the pre-split dQ|dK|dV (grad dtype CLIPK_F32S): column col's fp16 hi / lo
+// parts at byte 2 (col % 8) of its 8-column group's hi / lo halves (the same sums, fixed order)
+__global__ __launch_bounds__(256) void prefix_kv_reduce_split(int P, int R, int W, int nchunk,
+                                                              const float* __restrict__ part,
+                                                              float* __restrict__ dqkv, int lddq) {
+  const int g = blockIdx.x / P, p = blockIdx.x % P;
+  const int col = blockIdx.y * 256 + threadIdx.x;
+  if (col >= 2 * W) return;
+  const float* src = part + ((size_t)g * nchunk * 16 + p) * 2 * W + col;
+  const size_t cs = (size_t)16 * 2 * W;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // prefix_kv_reduce's chains and order
+  int k = 0;
+  for (; k + 16 <= nchunk; k += 16) {
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = src[(k + i) * cs];
+#pragma unroll
+    for (int i = 0; i < 16; i += 4) {
+      a0 += v[i];
+      a1 += v[i + 1];
+      a2 += v[i + 2];
+      a3 += v[i + 3];
+    }
+  }
+  for (; k + 4 <= nchunk; k += 4) {
+    a0 += src[k * cs];
+    a1 += src[(k + 1) * cs];
+    a2 += src[(k + 2) * cs];
+    a3 += src[(k + 3) * cs];
+  }
+  for (; k < nchunk; ++k) a0 += src[k * cs];
+  _Float16 hi, lo;
+  split_parts((a0 + a1) + (a2 + a3), hi, lo);
+  const int c = W + col;  // column within the q|k|v row
+  _Float16* grp = reinterpret_cast<_Float16*>(dqkv + ((size_t)g * R + p) * lddq + (c & ~7));
+  grp[c & 7] = hi;
+  grp[8 + (c & 7)] = lo;
 }
 
 template <typename T>
@@ -1157,10 +1204,11 @@ static int prefix_fwd(int G, int P, int R, int ntiles, const int* tiles, const i
   return CLIPK_OK;
 }
 
-template <typename T, typename TG>
+template <typename T, typename TG, bool OS = false>
 static int prefix_bwd(int G, int P, int R, int ntiles, const int* tiles, const int* row_first, int H,
                       const void* qkv, int ldq, const void* ofwd, int ldof, const void* dout, int lddo,
                       const float* lse, void* dqkv, int lddq, float* part, hipStream_t st) {
+  static_assert(!OS || (sizeof(T) == 4 && sizeof(TG) == 4), "pre-split dQ|dK|dV: the fp32 backward");
   constexpr bool mfma = sizeof(TG) == 2 && sizeof(T) == 2;
   const int uc = mfma ? bwd_uc(G, ntiles, H) : f32_uc(G, ntiles, H, kF32BwdWpc);
   const int nchunk = n_chunks(ntiles, uc);
@@ -1205,14 +1253,18 @@ static int prefix_bwd(int G, int P, int R, int ntiles, const int* tiles, const i
                          (float*)dqkv, lddq, part);
     };
     const int wpb = f32_wpb();
-    if (wpb == 2) go(attn_prefix_bwd_f32<2>, 2);
-    else if (wpb == 8) go(attn_prefix_bwd_f32<8>, 8);
-    else go(attn_prefix_bwd_f32<4>, 4);
+    if (wpb == 2) go(attn_prefix_bwd_f32<2, OS>, 2);
+    else if (wpb == 8) go(attn_prefix_bwd_f32<8, OS>, 8);
+    else go(attn_prefix_bwd_f32<4, OS>, 4);
   }
   CLIPK_CHECK_LAUNCH();
   const int W = H * 64;
-  hipLaunchKernelGGL((prefix_kv_reduce<TG>), dim3(G * P, (2 * W + 255) / 256), dim3(256), 0, st, P, R, W,
-                     nchunk, part, (TG*)dqkv, lddq);
+  if constexpr (OS)
+    hipLaunchKernelGGL(prefix_kv_reduce_split, dim3(G * P, (2 * W + 255) / 256), dim3(256), 0, st, P, R, W,
+                       nchunk, part, (float*)dqkv, lddq);
+  else
+    hipLaunchKernelGGL((prefix_kv_reduce<TG>), dim3(G * P, (2 * W + 255) / 256), dim3(256), 0, st, P, R, W,
+                       nchunk, part, (TG*)dqkv, lddq);
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
 }
@@ -1268,6 +1320,11 @@ extern "C" int clipk_attention_prefix_bwd(int dtype, int grad_dtype, int G, int 
   if (dtype == CLIPK_F16 && grad_dtype == CLIPK_F16) CLIPK_PBWD(f16, f16);
   if (dtype == CLIPK_BF16 && grad_dtype == CLIPK_BF16) CLIPK_PBWD(bf16, bf16);
   if (dtype == CLIPK_F32 && grad_dtype == CLIPK_F32) CLIPK_PBWD(float, float);
+  if (dtype == CLIPK_F32 && grad_dtype == CLIPK_F32S) {
+    if (lddqkv % 8) return CLIPK_ESHAPE;  // whole 8-column groups per row
+    return prefix_bwd<float, float, true>(G, P, R, ntiles, tiles, row_first, heads, qkv, ldqkv, ofwd, ldof, dout,
+                                          lddo, lse, dqkv, lddqkv, part, st);
+  }
 #undef CLIPK_PBWD
   return CLIPK_EDTYPE;
 }

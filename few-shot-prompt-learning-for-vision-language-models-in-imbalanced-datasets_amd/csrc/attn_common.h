@@ -85,6 +85,52 @@ __device__ __forceinline__ void st16x(float* __restrict__ p, const float* v) {
   for (int c = 0; c < 4; ++c)
     *reinterpret_cast<f32x4*>(p + kCs * c) = (f32x4){v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]};
 }
+// The parts of one fp32 value as a split GEMM forms them (gemm_kernel.h split8): hi = fp16(x),
+// lo = fp16(x - hi), of the ROUNDED x (opaque copy: no contraction with x's producing arithmetic)
+__device__ __forceinline__ void split_parts(float v, _Float16& hi, _Float16& lo) {
+  float x = v;
+  asm volatile("" : "+v"(x));
+  hi = (_Float16)x;
+  lo = (_Float16)(x - (float)hi);
+}
+// st16x in the pre-split operand form of a split GEMM's A (include/clipk.h CLIPK_A_SPLIT: per 8
+// consecutive columns 16 B of hi parts then 16 B of lo parts, 4 B per element as the fp32 row).
+// Called by all 4 lanes of a row (lane = 4 r + s, the slice map above, interleaved only): chunk c
+// of lanes s = 2j, 2j + 1 is the 8-column group 2c + j, so the pair trades halves over one DPP
+// quad_perm [1,0,3,2] -- the even lane sends its lo parts and gets its partner's hi parts -- and
+// each lane stores one whole 16-B half (even: the group's hi parts, odd: its lo parts), the store
+// count of st16x. The lo parts are v_fma_mix, as gemm_kernel.h split_lo8 (their consumers here
+// are a VALU select and a store: no MFMA reads them, so no wait states in the statement).
+static_assert(CLIPK_F32_IL, "st16x_split: the interleaved slice map");
+__device__ __forceinline__ void st16x_split(float* __restrict__ p, const float* v, int s) {
+  const bool odd = s & 1;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    float x[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      x[e] = v[4 * c + e];
+      asm volatile("" : "+v"(x[e]));  // the rounded fp32 value (no contraction with its producer)
+    }
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const unsigned h0 = __builtin_bit_cast(unsigned, (h2){(_Float16)x[0], (_Float16)x[1]});
+    const unsigned h1 = __builtin_bit_cast(unsigned, (h2){(_Float16)x[2], (_Float16)x[3]});
+    unsigned l0, l1;
+    asm("v_fma_mixlo_f16 %0, %2, 1.0, -%6 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %0, %3, 1.0, -%6 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixlo_f16 %1, %4, 1.0, -%7 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %1, %5, 1.0, -%7 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "=&v"(l0), "=&v"(l1)
+        : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(h0), "v"(h1));
+    const unsigned s0 = odd ? h0 : l0, s1 = odd ? h1 : l1;  // the half the partner stores
+    const unsigned y0 = (unsigned)__builtin_amdgcn_mov_dpp((int)s0, 0xB1, 0xF, 0xF, false);
+    const unsigned y1 = (unsigned)__builtin_amdgcn_mov_dpp((int)s1, 0xB1, 0xF, 0xF, false);
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p + kCs * c);
+    uint4* grp = reinterpret_cast<uint4*>(a & ~uintptr_t(31));
+    // even: hi parts (own columns 0-3, partner's 4-7); odd: lo parts (partner's 0-3, own 4-7)
+    grp[odd] = odd ? (uint4){y0, y1, l0, l1} : (uint4){h0, h1, y0, y1};
+  }
+}
 
 __device__ __forceinline__ float dot16(const float* a, const float* b) {
   float s0 = 0.f, s1 = 0.f;

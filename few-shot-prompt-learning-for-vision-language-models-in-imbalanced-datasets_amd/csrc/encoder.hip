@@ -378,11 +378,14 @@ static int attn_fwd(const clipk_encoder* e, const SeqShape& sh, const void* qkv,
   return clipk_attention_fwd(e->act, sh.nseq, sh.L, e->heads, sh.causal, qkv, 3 * W, o, W, lse, st);
 }
 
+// dqkv_split (shared-prefix packed rows, fp32 gradients): dq|dk|dv stored in the pre-split form the
+// qkv input-grad GEMM reads with CLIPK_A_SPLIT (grad dtype CLIPK_F32S of the prefix backward)
 static int attn_bwd(const clipk_encoder* e, const SeqShape& sh, const void* qkv, const void* o,
-                    const void* dout, const float* lse, void* dqkv, void* part, hipStream_t st) {
+                    const void* dout, const float* lse, void* dqkv, void* part, hipStream_t st,
+                    bool dqkv_split = false) {
   const int W = e->W;
   if (sh.packed)
-    return clipk_attention_prefix_bwd(e->act, e->grad, sh.G, sh.P, sh.R, sh.ntiles, sh.tiles, sh.row_first,
+    return clipk_attention_prefix_bwd(e->act, dqkv_split ? CLIPK_F32S : e->grad, sh.G, sh.P, sh.R, sh.ntiles, sh.tiles, sh.row_first,
                                       e->heads, qkv, 3 * W, o, W, dout, W, lse, dqkv, 3 * W, part,
                                       sh.part_bytes(e->heads), st);
   return clipk_attention_bwd(e->act, e->grad, sh.nseq, sh.L, e->heads, sh.causal, qkv, 3 * W, o, W, dout, W,
@@ -931,6 +934,15 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
   const bool lp_alias = !r16 && gd == CLIPK_F32 && !a_split;
   const int lpd = a_split ? CLIPK_F32S : gd;  // dX_lp's dtype
   const int dA_split = a_split ? CLIPK_A_SPLIT : 0;
+  // ... and the shared-prefix attention backward writes dq|dk|dv pre-split for qkv_dx (+23 % on
+  // that GEMM's launch when it splits them itself, as fc_dx before its pre-split A)
+  // (knob CLIPK_PRESPLIT_QKV=0: qkv_dx splits them itself, A/B)
+  static const bool qkv_knob = [] {
+    const char* s = getenv("CLIPK_PRESPLIT_QKV");
+    return s ? atoi(s) != 0 : true;
+  }();
+  const bool qkv_split = a_split && sh.packed && qkv_knob;
+  const int dqkv_split = qkv_split ? CLIPK_A_SPLIT : 0;
   void* const dA = lp_alias ? (void*)dX : b.dX_lp;  // the A operand of proj_dx / out_dx
   const bool eotl = text_eot_last(sh);
   auto zero = [&](void* p, size_t bytes) {
@@ -1003,7 +1015,7 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
       const double ab = (double)rows * W * ((act == CLIPK_F32 ? 4.0 : 3.0) * esize(act) + 4.0 * esize(gd)) +
                         4.0 * rows * e->heads;
       ProfScope ps(io.text ? CLIPK_PROF_ATTN : CLIPK_PROF_NONE, st, 0.0, SITE("attn_bwd"), ab);
-      TRY(attn_bwd(e, sh, t.qkv[l], t.o[l], b.do_, t.lse[l], b.dqkv, b.part, st));
+      TRY(attn_bwd(e, sh, t.qkv[l], t.o[l], b.do_, t.lse[l], b.dqkv, b.part, st, qkv_split));
     }
     if (l == 0 && io.text && prefix_mode(e, sh)) {
       // the input gradient on the prefix rows only: dqkv gathered to G*P compact rows, their
@@ -1014,8 +1026,8 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
       float* rc = mc + np;
       TRY(prefix_tables(sh, sh.G >= 2, prow, t.mean1[0], t.rstd1[0], mc, rc, st));
       TRY(clipk_rows_copy(3 * W * (int)esize(gd), np, b.dqkv, prow, b.dh, nullptr, st));
-      TRY(gemm(gd, gd, CLIPK_EPI_NONE, np, W, 3 * W, b.dh, w[12], nullptr, nullptr, b.dxn, nullptr, nullptr, 0, st,
-               pg, nullptr, 0, SITE("qkv_dx_prefix")));
+      TRY(gemm(gd, gd, CLIPK_EPI_NONE | dqkv_split, np, W, 3 * W, b.dh, w[12], nullptr, nullptr, b.dxn, nullptr,
+               nullptr, 0, st, pg, nullptr, 0, SITE("qkv_dx_prefix")));
       const float* g0 = (const float*)w[0];
       if (!r16)
         TRY(clipk_layernorm_bwd_x(rd, gd, np, W, b.dxn, W, t.X[0], W, prow, g0, mc, rc, dX, W, dX, nullptr, gd, prow,
@@ -1025,7 +1037,7 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
                                    gd, prow, W, st));
       continue;
     }
-    TRY(gemm(gd, gd, CLIPK_EPI_NONE, rows, W, 3 * W, b.dqkv, w[12], nullptr, nullptr, b.dxn,
+    TRY(gemm(gd, gd, CLIPK_EPI_NONE | dqkv_split, rows, W, 3 * W, b.dqkv, w[12], nullptr, nullptr, b.dxn,
              nullptr, nullptr, 0, st, pg, nullptr, 0, SITE("qkv_dx")));
     TRY(ln_bwd(rows, t.X[l], (const float*)w[0], t.mean1[l], t.rstd1[l], l == 0));
     const DeepPrompts& d = e->deep;

@@ -116,24 +116,35 @@ __device__ __forceinline__ f32x4 mma(u32x4 a, u32x4 b, f32x4 c) {
 // from the packed fp16 register and rounds once (exact: x - hi is representable in fp32), so
 // a pair costs 1 cvt_pk + 2 fma_mix instead of cvt_pk + 2 cvt + sub + cvt_pk (the split sits in
 // the ping-pong loop's memory segment, where its VALU count is on the critical path).
+// The 8 v_fma_mix of a split are ONE inline-asm statement that ends with its own wait states:
+// hipcc's hazard recognizer does not see the VGPRs an asm statement writes, and the ISA rule for
+// a VALU write of a VGPR that an MFMA then reads as SrcA / SrcB is 2 wait states (the guide's
+// inline-asm rule, cdna_hip_programming.md §5.7 item 2: "a just-written "v" operand -> MFMA
+// operand (s_nop 1)"; hipcc applies the same rule to the compiler-visible form of this sequence:
+// the v_fma_mixhi_f16 -> v_mfma_f32_16x16x32_f16 pair gets its s_nop, tools/lab/split_hazard.hip).
+// With `s_nop 1` inside the string the parts are safe for any consumer hipcc schedules after
+// the statement, so no caller counts wait states (round 5 counted them by hand: an MFMA two
+// instructions after the split read stale parts, off by up to 5.8e-2, profiles/r05w16/hazard.txt).
 #ifndef CLIPK_SPLIT_MIX
 #define CLIPK_SPLIT_MIX 1
 #endif
-__device__ __forceinline__ unsigned split_lo2(float a, float b, unsigned h) {
-  unsigned l;
-  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%3 op_sel_hi:[0,0,1]\n\t"
-      "v_fma_mixhi_f16 %0, %2, 1.0, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
-      : "=&v"(l)
-      : "v"(a), "v"(b), "v"(h));
-  return l;
+__device__ __forceinline__ void split_lo8(const f32x4& x0, const f32x4& x1, const u32x4& hi, u32x4& lo) {
+  unsigned l0, l1, l2, l3;
+  asm("v_fma_mixlo_f16 %0, %4, 1.0, -%12 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %5, 1.0, -%12 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %1, %6, 1.0, -%13 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %7, 1.0, -%13 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %2, %8, 1.0, -%14 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %2, %9, 1.0, -%14 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %3, %10, 1.0, -%15 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %3, %11, 1.0, -%15 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "s_nop 1"
+      : "=&v"(l0), "=&v"(l1), "=&v"(l2), "=&v"(l3)
+      : "v"(x0[0]), "v"(x0[1]), "v"(x0[2]), "v"(x0[3]), "v"(x1[0]), "v"(x1[1]), "v"(x1[2]), "v"(x1[3]),
+        "v"(hi[0]), "v"(hi[1]), "v"(hi[2]), "v"(hi[3]));
+  lo = (u32x4){l0, l1, l2, l3};
 }
-// MIX false: the lo part in compiler-visible cvt + sub + cvt form. The v_fma_mix pair is inline
-// asm, whose VGPR writes the compiler's hazard tracking does not see: an MFMA that reads them a
-// few instructions later (the 2- / 4-slot loop, where splits and MFMAs interleave) can read
-// stale values -- measured: the 2-MFMA split kernel on the 128x128 tiles off by up to 5e-2 at
-// 4k-8k rows, bit-exact with this form or with s_nop 7 after the split
-// (profiles/r05w16/hazard.txt). The ping-pong loop splits in its memory segment, a barrier
-// before the MFMAs that read the parts, and keeps the cheaper asm form.
+// MIX false: the lo part in compiler-visible cvt + sub + cvt form (A/B knob CLIPK_SPLIT_MIX=0).
 template <bool MIX = CLIPK_SPLIT_MIX != 0>
 __device__ __forceinline__ void split8(u32x4 a0, u32x4 a1, u32x4& hi, u32x4& lo) {
   // the inputs as materialised fp32 values: a caller's x * gamma (the fold's LayerNorm weight) must
@@ -148,7 +159,7 @@ __device__ __forceinline__ void split8(u32x4 a0, u32x4 a1, u32x4& hi, u32x4& lo)
     h[4 + c] = (f16)x1[c];
   }
   hi = __builtin_bit_cast(u32x4, h);
-  if constexpr (!MIX) {  // (also the A/B knob CLIPK_SPLIT_MIX=0 everywhere)
+  if constexpr (!MIX) {
     f16x8 l;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -158,10 +169,7 @@ __device__ __forceinline__ void split8(u32x4 a0, u32x4 a1, u32x4& hi, u32x4& lo)
     lo = __builtin_bit_cast(u32x4, l);
     return;
   }
-  lo[0] = split_lo2(x0[0], x0[1], hi[0]);
-  lo[1] = split_lo2(x0[2], x0[3], hi[1]);
-  lo[2] = split_lo2(x1[0], x1[1], hi[2]);
-  lo[3] = split_lo2(x1[2], x1[3], hi[3]);
+  split_lo8(x0, x1, hi, lo);
 }
 // a . b ~= hi(a) hi(b) + hi(a) lo(b) + lo(a) hi(b) (lo . lo ~ 2^-22 relative is dropped); the
 // weight's parts (packed, clipk_split_pack) are the instruction's A operand (swapped operands)
@@ -169,9 +177,6 @@ __device__ __forceinline__ void split8(u32x4 a0, u32x4 a1, u32x4& hi, u32x4& lo)
 // lo(a) hi(b) term -- the activation operand rounded to fp16, the weight kept at ~22 bits -- in
 // the GEMMs of epilogue class `CLIPK_SPLIT_TERMS_EPI` (0: every GEMM, 1: the backward's input-grad
 // GEMMs, EPI_NONE / EPI_DMUL / EPI_DQGELU).
-#ifndef CLIPK_PP_SPLIT_NOP  // 0: none; n > 0: s_nop (n - 1) after the ping-pong loop's split (5: measured free, profiles/r05w16/ppnop_*.txt)
-#define CLIPK_PP_SPLIT_NOP 5
-#endif
 #ifndef CLIPK_SPLIT_TERMS
 #define CLIPK_SPLIT_TERMS 3
 #endif
@@ -820,9 +825,6 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
             }
             if constexpr (!CLIPK_GEMM_NOSPLIT) split8(fa[0][i], fa[1][i], fa[0][i], fa[1][i]);
           }
-          // wait states after the asm split's VGPR writes, independent of the barrier that
-          // follows (A/B knob CLIPK_PP_SPLIT_NOP; see split8)
-          if constexpr (CLIPK_PP_SPLIT_NOP > 0) asm volatile("s_nop %0" ::"n"(CLIPK_PP_SPLIT_NOP - 1));
         }
       };
       auto seg_end = [&](bool new_a = false) {  // memory segment done: fragments in registers, then the barrier
@@ -1004,7 +1006,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
               x0 = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, x0) * gm0);
               x1 = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, x1) * gm1);
             }
-            split8<false>(x0, x1, ah, al);  // MFMAs follow within a few instructions
+            split8(x0, x1, ah, al);  // (the MFMAs right after it: split_lo8 carries their wait states)
           }
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = mma_split<TWO_TERMS, W16>(bh[j], bl[j], ah, al, acc[i][j]);

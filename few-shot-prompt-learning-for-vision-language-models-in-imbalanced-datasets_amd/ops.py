@@ -329,13 +329,16 @@ def attention_prefix(qkv, G, P, R, tiles, row_first, heads, lse=False):
     return (out, l) if lse else out
 
 
-def attention_prefix_bwd(qkv, o, dout, lse, G, P, R, tiles, row_first, heads, grad_dtype):
+def attention_prefix_bwd(qkv, o, dout, lse, G, P, R, tiles, row_first, heads, grad_dtype, split=False):
+    """split (fp32 qkv / dout / grad_dtype): dq|dk|dv in the pre-split operand form of CLIPK_A_SPLIT
+    (grad dtype CLIPK_F32S), viewed as fp32 [G*R, 3W]."""
     W = heads * 64
     nt = tiles.numel() // 2
     dqkv = torch.zeros(G * R, 3 * W, device=qkv.device, dtype=grad_dtype)
     nb = N.load().clipk_attention_prefix_ws_bytes(G, nt, heads)
     ws = torch.empty(nb, dtype=torch.uint8, device=qkv.device)
-    N.call("clipk_attention_prefix_bwd", DT[qkv.dtype], DT[grad_dtype], G, P, R, nt, _p(tiles), _p(row_first),
+    gdt = N.F32S if split else DT[grad_dtype]
+    N.call("clipk_attention_prefix_bwd", DT[qkv.dtype], gdt, G, P, R, nt, _p(tiles), _p(row_first),
            heads, _p(qkv), 3 * W, _p(o), W, _p(dout), W, _p(lse), _p(dqkv), 3 * W, _p(ws), nb, _stream())
     return dqkv
 

@@ -289,7 +289,9 @@ int clipk_attention_prefix_fwd(int dtype, int G, int P, int R, int ntiles, const
                                const int* row_first, int heads, const void* qkv, int ldqkv, void* out,
                                int ldo, float* lse, void* stream);
 /* Backward; ws >= clipk_attention_prefix_ws_bytes(G, ntiles, heads) holds the per-chunk fp32
- * partial dK/dV of the prefix rows (reduced in a fixed order). */
+ * partial dK/dV of the prefix rows (reduced in a fixed order). grad_dtype CLIPK_F32S (dtype
+ * CLIPK_F32, PREC fp32s): fp32 dout, dqkv stored in the pre-split form of CLIPK_A_SPLIT (the qkv
+ * input-grad GEMM's A; ldqkv % 8 == 0), the parts of the same fp32 values. */
 size_t clipk_attention_prefix_ws_bytes(int G, int ntiles, int heads);
 int clipk_attention_prefix_bwd(int dtype, int grad_dtype, int G, int P, int R, int ntiles,
                                const int* tiles, const int* row_first, int heads, const void* qkv,

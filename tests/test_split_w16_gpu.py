@@ -313,3 +313,24 @@ def test_layernorm_bwd_split_copy(dev, rows, W):
     dx, lp = ops.layernorm_bwd(dy, x, w, mean, rstd, dres=dres, lp_dtype="split")
     assert torch.equal(dx, dx0)
     assert torch.equal(lp.view(torch.int32), split_form(dx).view(torch.int32))
+
+
+@pytest.mark.parametrize("G,C,P,H,max_q", [(2, 37, 5, 8, 6), (1, 19, 16, 2, 7), (24, 300, 5, 8, 7)])
+def test_attention_prefix_bwd_split_copy(dev, G, C, P, H, max_q):
+    """The fp32 shared-prefix attention backward with grad dtype CLIPK_F32S (PREC fp32s: dq|dk|dv
+    handed to the qkv input-grad GEMM pre-split) stores bitwise split_form of the fp32 backward's
+    dq|dk|dv -- the rows the attention kernel writes and the prefix rows' reduced dK / dV -- and
+    that GEMM on it (CLIPK_A_SPLIT) equals the GEMM on the fp32 values."""
+    from test_kernels_gpu import prefix_case
+    R, tiles, row_first, off, qlen, g = prefix_case(G, C, P, H, max_q, seed=G * 100 + C + P)
+    W = H * 64
+    qkv = torch.randn(G * R, 3 * W, generator=g).to(dev)
+    tiles, row_first = tiles.to(dev), row_first.to(dev)
+    o, lse = ops.attention_prefix(qkv, G, P, R, tiles, row_first, H, lse=True)
+    dout = torch.randn(G * R, W, generator=g).to(dev)
+    d32 = ops.attention_prefix_bwd(qkv, o, dout, lse, G, P, R, tiles, row_first, H, torch.float32)
+    ds = ops.attention_prefix_bwd(qkv, o, dout, lse, G, P, R, tiles, row_first, H, torch.float32, split=True)
+    assert torch.equal(ds.view(torch.int32), split_form(d32).view(torch.int32))
+    w = _w16((W, 3 * W), g, 1 / math.sqrt(3 * W)).to(dev)
+    wh = ops.split_hi16(ops.split_pack(w))
+    assert torch.equal(ops.gemm(ds, wh, N.EPI_NONE | N.A_SPLIT), ops.gemm(d32, wh, N.EPI_NONE))
