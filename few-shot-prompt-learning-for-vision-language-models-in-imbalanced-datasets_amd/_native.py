@@ -35,6 +35,7 @@ def source_digest():
     return h.hexdigest()
 
 F32, F16, BF16, F32S = 0, 1, 2, 3  # F32S: fp32 activations x split-packed weights (PREC fp32s)
+PREFIX_CLS_GROUP0 = 1  # clipk_attention_prefix_*_ex flag
 F32S16 = 4  # F32S for fp16-valued weights: B is the compact fp16 SPLIT_SCALE * W (clipk_split_hi16)
 SPLIT_SCALE = 64.0  # CLIPK_SPLIT_SCALE: clipk_split_pack stores SPLIT_SCALE * W
 EPI_BIAS, EPI_BIAS_RES, EPI_BIAS_QGELU, EPI_DQGELU, EPI_NONE = 0, 1, 2, 3, 4
@@ -85,17 +86,26 @@ SIGNATURES = {
     "clipk_ctx_grad": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "clipk_prompt_assemble_rows": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _L, _L, _P, _P, _P, _P]),
     "clipk_ctx_grad_rows": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P]),
+    "clipk_ctx_bias_grad_rows": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "clipk_attention_prefix_fwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _I, _P, _I, _P, _I, _P, _P]),
     "clipk_attention_prefix_ws_bytes": (_S, [_I, _I, _I]),
     "clipk_attention_prefix_bwd": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I, _P, _I, _P, _I, _P, _P,
                                         _I, _P, _S, _P]),
+    "clipk_attention_prefix_fwd_ex": (_I, [_I, _I, _I, _I, _I, _P, _P, _I, _P, _I, _P, _I, _P, _I, _P]),
+    "clipk_attention_prefix_bwd_ex": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I, _P, _I, _P, _I, _P, _P,
+                                           _I, _P, _S, _I, _P]),
     "clipk_cosine_logits_fwd": (_I, [_I, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P]),
     "clipk_cosine_logits_bwd": (_I, [_I, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P]),
     "clipk_ce_loss": (_I, [_I, _I, _P, _P, _P, _F, _I, _F, _P, _P, _P]),
+    "clipk_ce_loss_reduce": (_I, [_I, _I, _P, _P, _P, _F, _I, _F, _I, _P, _P, _P, _P]),
     "clipk_meta_net_fwd": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "clipk_meta_net_fwd_norm": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "clipk_status_take": (_I, [_P, _P, _P]),
     "clipk_meta_net_bwd": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "clipk_sgd_step": (_I, [_L, _P, _P, _P, _F, _F, _F, _I, _P]),
     "clipk_sgd_step_multi": (_I, [_I, _P, _P, _P, _P, _P, _F, _F, _F, _P]),
+    "clipk_sgd_step_multi_scaled": (_I, [_I, _P, _P, _P, _P, _P, _F, _F, _F, _F, _P]),
+    "clipk_sgd_step_multi_if": (_I, [_I, _P, _P, _P, _P, _P, _F, _F, _F, _F, _P, _I, _P]),
     "clipk_cast": (_I, [_I, _L, _P, _P, _P]),
     "clipk_rows_copy": (_I, [_I, _I, _P, _P, _P, _P, _P]),
     "clipk_vit_embed_ln_vpt": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),

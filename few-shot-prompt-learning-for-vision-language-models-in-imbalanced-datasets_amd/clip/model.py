@@ -195,6 +195,9 @@ class SplitStatus:
 
     def __init__(self, device):
         self.flags = torch.zeros(1, dtype=torch.int32, device=device)
+        # the host-visible word clipk_status_take hands the flags to (pinned: the kernel writes it,
+        # no runtime copy or fill launch per read)
+        self.host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         self.pending = 0  # forward-only calls since the last read
 
     @classmethod
@@ -207,13 +210,31 @@ class SplitStatus:
     def read(self):
         """Read and clear the flags (one synchronisation); a non-finite forward raises. Returns
         the backward flag."""
-        st = int(self.flags.item())
-        self.flags.zero_()
+        ops.status_take(self.flags, self.host)  # host <- flags, flags <- 0 (one clipk launch)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.flags.device))
+        ev.synchronize()
+        st = int(self.host[0])
         self.pending = 0
         if st & 1:
             raise N.ClipkError("PREC fp32s encoder: non-finite features -- an activation exceeded fp16's range "
                                "(65504) in the split-fp16 GEMM operands; use PREC fp32")
         return bool(st & 2)
+
+    def take_async(self):
+        """Hand the flags to a pinned word and clear them at this point of the current stream,
+        without waiting: returns a handle whose result() waits for that point only (a ring of
+        two words: the previous step's handle stays valid while the next one is taken)."""
+        ring = getattr(self, "_ring", None)
+        if ring is None:
+            ring = self._ring = [torch.zeros(1, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+            self._ri = 0
+        host = ring[self._ri]
+        self._ri ^= 1
+        ops.status_take(self.flags, host)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.flags.device))
+        return _StatusHandle(ev, host)
 
     def forward_done(self):
         self.pending += 1
@@ -224,6 +245,22 @@ class SplitStatus:
         """The deferred read of the inference forwards' flags."""
         if self.pending:
             self.read()
+
+
+class _StatusHandle:
+    """SplitStatus.take_async's result: the flags as of that stream point (a non-finite forward
+    raises, as SplitStatus.read)."""
+
+    def __init__(self, ev, host):
+        self.ev, self.host = ev, host
+
+    def result(self):
+        self.ev.synchronize()
+        st = int(self.host[0])
+        if st & 1:
+            raise N.ClipkError("PREC fp32s encoder: non-finite features -- an activation exceeded fp16's range "
+                               "(65504) in the split-fp16 GEMM operands; use PREC fp32")
+        return st
 
 
 def check_split_status(device=None):
@@ -390,7 +427,9 @@ class TextEncoderCore(_Encoder):
                 N.check(lib.clipk_text_backward(h, shape.nseq, shape.L, *tail), "clipk_text_backward")
 
         run()
-        if self._status is not None and self._check_status():
+        # (defer_check: the trainer reads the flag later, its SGD launch guarded by it on the
+        # device -- CoCoOp._settle_pending re-runs an overflowed step with this check on)
+        if self._status is not None and not self.defer_check and self._check_status():
             # the gradients overflowed the split operands' fp16 range: once more at a lower scale
             # target (exact: the backward is linear in dtxt and the scale a power of two)
             type(self).split_retries += 1
@@ -405,6 +444,7 @@ class TextEncoderCore(_Encoder):
         return dx0
 
     split_retries = 0  # PREC fp32s backwards re-run at the lower scale target (overflow), all instances
+    defer_check = False
 
 
 class TextEncodeFn(torch.autograd.Function):

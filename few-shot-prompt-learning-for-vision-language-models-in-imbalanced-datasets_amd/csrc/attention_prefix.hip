@@ -138,7 +138,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_mfma(int G, int P, i
                                                             const int* __restrict__ row_first, int H,
                                                             int nchunk, int uc, const T* __restrict__ qkv,
                                                             int ldq, T* __restrict__ out, int ldo,
-                                                            float* __restrict__ lse) {
+                                                            float* __restrict__ lse, int cls0) {
   __shared__ CLIPK_LDS_ALIGN short sm[WPB][2][16 * TRS];  // per wave: prefix V, own V
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_mfma(int G, int P, i
   auto load = [&](int u, TileRows& f) {
     tile_info(tab, P, u, u_begin, f.t0, f.n, f.pre);
     const int rl = f.t0 + min(r16, f.n - 1);
-    const T* qp = qh + (gR + rl) * ldq;
+    const T* qp = qh + ((cls0 && u > 0 ? 0 : gR) + rl) * ldq;  // cls0: class rows read from group 0
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int c = 8 * g4 + 32 * kk;
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_bwd_mfma(int G, int P, i
                                                             int ldq, const TG* __restrict__ dout,
                                                             int lddo, const float* __restrict__ lse,
                                                             TG* __restrict__ dqkv, int lddq,
-                                                            float* __restrict__ part) {
+                                                            float* __restrict__ part, int cls0) {
   static_assert(sizeof(T) == 2 && sizeof(TG) == 2, "MFMA attention backward: 16-bit operands, math in TG");
   __shared__ CLIPK_LDS_ALIGN short sm[WPB][4][16 * TRS];  // per wave: K_pre, K_own, Q, dO
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_bwd_mfma(int G, int P, i
   auto load = [&](int u, TileRowsB& f) {
     tile_info(tab, P, u, u_begin, f.t0, f.n, f.pre);
     const int rl = f.t0 + min(r16, f.n - 1);
-    const T* qp = qh + (gR + rl) * ldq;
+    const T* qp = qh + ((cls0 && u > 0 ? 0 : gR) + rl) * ldq;  // cls0: class rows read from group 0
     const TG* dp = dh + (gR + rl) * lddo;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -509,7 +509,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_lds(int G, int P, in
                                                            const int* __restrict__ row_first, int H,
                                                            int nchunk, int uc, const T* __restrict__ qkv,
                                                            int ldq, T* __restrict__ out, int ldo,
-                                                           float* __restrict__ lse) {
+                                                           float* __restrict__ lse, int cls0) {
   constexpr int SLOT = 3 * 2048 + 256;  // q | k | v tiles, row_first of the 16 rows (+ lane copies)
   constexpr int PER = 7;                // global_load_lds per tile
   __shared__ CLIPK_LDS_ALIGN char sm[WPB][NS * SLOT + 16 * TRS * 2];
@@ -530,7 +530,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_lds(int G, int P, in
     tile_info(tab, P, u, u_begin, t0, n, pre);
     char* b = ring + slot * SLOT;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) stage_slice<T>(qh + j * W, ldq, gR + t0, n, b + j * 2048, lane);
+    for (int j = 0; j < 3; ++j) stage_slice<T>(qh + j * W, ldq, (cls0 && u > 0 ? 0 : gR) + t0, n, b + j * 2048, lane);
     glds_b(row_first + t0 + min(r16, n - 1), b + 3 * 2048, 4);
   };
   const bool pok = r16 < P;
@@ -614,7 +614,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_bwd_lds(int G, int P, in
                                                            int ldq, const T* __restrict__ dout, int lddo,
                                                            const float* __restrict__ lse,
                                                            T* __restrict__ dqkv, int lddq,
-                                                           float* __restrict__ part) {
+                                                           float* __restrict__ part, int cls0) {
   static_assert(sizeof(T) == 2, "MFMA attention backward: 16-bit operands");
   constexpr int SLOT = 4 * 2048 + 2 * 256;  // q | k | v | dO tiles, row_first, lse
   constexpr int PER = 10;
@@ -636,7 +636,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_bwd_lds(int G, int P, in
     tile_info(tab, P, u, u_begin, t0, n, pre);
     char* b = ring + slot * SLOT;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) stage_slice<T>(qh + j * W, ldq, gR + t0, n, b + j * 2048, lane);
+    for (int j = 0; j < 3; ++j) stage_slice<T>(qh + j * W, ldq, (cls0 && u > 0 ? 0 : gR) + t0, n, b + j * 2048, lane);
     stage_slice<T>(dout + h * 64, lddo, gR + t0, n, b + 3 * 2048, lane);
     const int rr = t0 + min(r16, n - 1);
     glds_b(row_first + rr, b + 4 * 2048, 4);
@@ -841,7 +841,7 @@ template <int WPB>
 __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
     int G, int P, int R, int ntiles, const int* __restrict__ tiles, const int* __restrict__ row_first, int H,
     int nchunk, int uc, const float* __restrict__ qkv, int ldq, float* __restrict__ out, int ldo,
-    float* __restrict__ lse) {
+    float* __restrict__ lse, int cls0) {
   __shared__ CLIPK_LDS_ALIGN float sKp[16 * 64], sVp[16 * 64];
   __shared__ CLIPK_LDS_ALIGN float sK[WPB][16 * 64], sV[WPB][16 * 64];
   int g, h, k, w;
@@ -860,7 +860,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
   int t0n, nn, pren, rrn, firstn;
   auto fetch = [&](int u) {
     f32_unit(tiles, row_first, P, u, r, t0n, nn, pren, rrn, firstn);
-    const float* qp = qkv + ((size_t)g * R + t0n + rrn) * ldq + h * 64 + kSl * s;
+    const float* qp = qkv + ((cls0 && u > 0 ? 0 : (size_t)g * R) + t0n + rrn) * ldq + h * 64 + kSl * s;
     ld16x(qp, qn);
     ld16x(qp + W, kn);
     ld16x(qp + 2 * W, vn);
@@ -947,7 +947,7 @@ __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 wav
     int G, int P, int R, int ntiles, const int* __restrict__ tiles, const int* __restrict__ row_first, int H,
     int nchunk, int uc, const float* __restrict__ qkv, int ldq, const float* __restrict__ o_fwd, int ldof,
     const float* __restrict__ dout, int lddo, const float* __restrict__ lse, float* __restrict__ dqkv, int lddq,
-    float* __restrict__ part) {
+    float* __restrict__ part, int cls0) {
   __shared__ CLIPK_LDS_ALIGN float sKp[16 * 64], sVp[16 * 64];
   // padded rows (bank-conflict-free stores): K|V then Q|dO rows at stride RS floats; P / dS at
   // stride PS (a column of 16 query rows written by one lane per row hit 2 banks at stride 32)
@@ -976,7 +976,7 @@ __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 wav
   auto fetch = [&](int u) {
     f32_unit(tiles, row_first, P, u, r, t0n, nn, pren, rrn, firstn);
     const size_t rw = (size_t)g * R + t0n + rrn;
-    const float* qp = qkv + rw * ldq + h * 64 + kSl * s;
+    const float* qp = qkv + ((cls0 && u > 0 ? 0 : (size_t)g * R) + t0n + rrn) * ldq + h * 64 + kSl * s;
     ld16x(qp, qn);
     ld16x(dout + rw * lddo + h * 64 + kSl * s, dOn);
     ld16x(o_fwd + rw * ldof + h * 64 + kSl * s, on);
@@ -1152,7 +1152,7 @@ __global__ __launch_bounds__(256) void prefix_kv_reduce_split(int P, int R, int 
 
 template <typename T>
 static int prefix_fwd(int G, int P, int R, int ntiles, const int* tiles, const int* row_first, int H,
-                      const void* qkv, int ldq, void* out, int ldo, float* lse, hipStream_t st) {
+                      const void* qkv, int ldq, void* out, int ldo, float* lse, hipStream_t st, int cls0) {
   if constexpr (sizeof(T) == 2) {
     const int uc = fwd_chunk();
     const int nchunk = n_chunks(ntiles, uc);
@@ -1161,7 +1161,7 @@ static int prefix_fwd(int G, int P, int R, int ntiles, const int* tiles, const i
       const int wpb = lds_wpb();
       auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3((waves + wpb - 1) / wpb), dim3(64 * wpb), 0, st, G, P, R, ntiles, tiles,
-                           row_first, H, nchunk, uc, (const T*)qkv, ldq, (T*)out, ldo, lse);
+                           row_first, H, nchunk, uc, (const T*)qkv, ldq, (T*)out, ldo, lse, cls0);
       };
 #define CLIPK_LDS_GO(K, T_, ...)                                                               \
   if (ns == 2) { if (wpb == 1) go(K<T_, 2, 1 __VA_ARGS__>); else if (wpb == 2) go(K<T_, 2, 2 __VA_ARGS__>); \
@@ -1176,7 +1176,7 @@ static int prefix_fwd(int G, int P, int R, int ntiles, const int* tiles, const i
     const int wpb = prefix_wpb();
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3((waves + wpb - 1) / wpb), dim3(64 * wpb), 0, st, G, P, R, ntiles, tiles,
-                         row_first, H, nchunk, uc, (const T*)qkv, ldq, (T*)out, ldo, lse);
+                         row_first, H, nchunk, uc, (const T*)qkv, ldq, (T*)out, ldo, lse, cls0);
     };
     if (wpb == 8) {
       if (b == 1) go(attn_prefix_fwd_mfma<T, 1, 8>);
@@ -1193,7 +1193,7 @@ static int prefix_fwd(int G, int P, int R, int ntiles, const int* tiles, const i
     auto go = [&](auto kern, int wpb) {
       const long blocks = (long)G * ((nchunk + wpb - 1) / wpb) * H;
       hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * wpb), 0, st, G, P, R, ntiles, tiles, row_first, H, nchunk,
-                         uc, (const float*)qkv, ldq, (float*)out, ldo, lse);
+                         uc, (const float*)qkv, ldq, (float*)out, ldo, lse, cls0);
     };
     const int wpb = f32_wpb();
     if (wpb == 2) go(attn_prefix_fwd_f32<2>, 2);
@@ -1207,7 +1207,7 @@ static int prefix_fwd(int G, int P, int R, int ntiles, const int* tiles, const i
 template <typename T, typename TG, bool OS = false>
 static int prefix_bwd(int G, int P, int R, int ntiles, const int* tiles, const int* row_first, int H,
                       const void* qkv, int ldq, const void* ofwd, int ldof, const void* dout, int lddo,
-                      const float* lse, void* dqkv, int lddq, float* part, hipStream_t st) {
+                      const float* lse, void* dqkv, int lddq, float* part, hipStream_t st, int cls0) {
   static_assert(!OS || (sizeof(T) == 4 && sizeof(TG) == 4), "pre-split dQ|dK|dV: the fp32 backward");
   constexpr bool mfma = sizeof(TG) == 2 && sizeof(T) == 2;
   const int uc = mfma ? bwd_uc(G, ntiles, H) : f32_uc(G, ntiles, H, kF32BwdWpc);
@@ -1219,7 +1219,7 @@ static int prefix_bwd(int G, int P, int R, int ntiles, const int* tiles, const i
       auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3((waves + wpb - 1) / wpb), dim3(64 * wpb), 0, st, G, P, R, ntiles, tiles,
                            row_first, H, nchunk, uc, (const T*)qkv, ldq, (const T*)dout, lddo, lse, (T*)dqkv,
-                           lddq, part);
+                           lddq, part, cls0);
       };
       CLIPK_LDS_GO(attn_prefix_bwd_lds, T)
       CLIPK_CHECK_LAUNCH();
@@ -1235,7 +1235,7 @@ static int prefix_bwd(int G, int P, int R, int ntiles, const int* tiles, const i
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3((waves + wpb - 1) / wpb), dim3(64 * wpb), 0, st, G, P, R, ntiles, tiles,
                          row_first, H, nchunk, uc, (const T*)qkv, ldq, (const TG*)dout, lddo, lse, (TG*)dqkv,
-                         lddq, part);
+                         lddq, part, cls0);
     };
     if (wpb == 8) {
       if (bwd_batch() == 1) go(attn_prefix_bwd_mfma<T, TG, 1, 8>);
@@ -1250,7 +1250,7 @@ static int prefix_bwd(int G, int P, int R, int ntiles, const int* tiles, const i
       const long blocks = (long)G * ((nchunk + wpb - 1) / wpb) * H;
       hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * wpb), 0, st, G, P, R, ntiles, tiles, row_first, H, nchunk,
                          uc, (const float*)qkv, ldq, (const float*)ofwd, ldof, (const float*)dout, lddo, lse,
-                         (float*)dqkv, lddq, part);
+                         (float*)dqkv, lddq, part, cls0);
     };
     const int wpb = f32_wpb();
     if (wpb == 2) go(attn_prefix_bwd_f32<2, OS>, 2);
@@ -1285,37 +1285,55 @@ extern "C" size_t clipk_attention_prefix_ws_bytes(int G, int ntiles, int heads) 
   return (size_t)G * n_chunks(ntiles, uc) * 16 * 2 * heads * 64 * sizeof(float);
 }
 
-extern "C" int clipk_attention_prefix_fwd(int dtype, int G, int P, int R, int ntiles, const int* tiles,
-                                          const int* row_first, int heads, const void* qkv, int ldqkv,
-                                          void* out, int ldo, float* lse, void* stream) {
+// flags (the _ex entry points): CLIPK_PREFIX_CLS_GROUP0 -- the class rows' q|k|v are read from
+// group 0 for every group (the text encoder's layer 0, whose class rows are the same in every
+// group: no per-group copies of them are materialised); prefix rows and every output per group
+static int prefix_fwd_call(int dtype, int G, int P, int R, int ntiles, const int* tiles, const int* row_first,
+                           int heads, const void* qkv, int ldqkv, void* out, int ldo, float* lse, int flags,
+                           void* stream) {
   if (!tiles || !row_first || !qkv || !out) return CLIPK_EINVAL;
+  if (flags & ~CLIPK_PREFIX_CLS_GROUP0) return CLIPK_EINVAL;
   if (!prefix_shape_ok(G, P, R, ntiles, heads, ldqkv) || ldqkv < 3 * heads * 64 || ldo < heads * 64 ||
       ldqkv % 8 || ldo % 8)
     return CLIPK_ESHAPE;
   hipStream_t st = (hipStream_t)stream;
+  const int c0 = (flags & CLIPK_PREFIX_CLS_GROUP0) ? 1 : 0;
   switch (dtype) {
-    case CLIPK_F16: return prefix_fwd<f16>(G, P, R, ntiles, tiles, row_first, heads, qkv, ldqkv, out, ldo, lse, st);
-    case CLIPK_BF16: return prefix_fwd<bf16>(G, P, R, ntiles, tiles, row_first, heads, qkv, ldqkv, out, ldo, lse, st);
-    case CLIPK_F32: return prefix_fwd<float>(G, P, R, ntiles, tiles, row_first, heads, qkv, ldqkv, out, ldo, lse, st);
+    case CLIPK_F16: return prefix_fwd<f16>(G, P, R, ntiles, tiles, row_first, heads, qkv, ldqkv, out, ldo, lse, st, c0);
+    case CLIPK_BF16: return prefix_fwd<bf16>(G, P, R, ntiles, tiles, row_first, heads, qkv, ldqkv, out, ldo, lse, st, c0);
+    case CLIPK_F32: return prefix_fwd<float>(G, P, R, ntiles, tiles, row_first, heads, qkv, ldqkv, out, ldo, lse, st, c0);
     default: return CLIPK_EDTYPE;
   }
 }
 
-extern "C" int clipk_attention_prefix_bwd(int dtype, int grad_dtype, int G, int P, int R, int ntiles,
-                                          const int* tiles, const int* row_first, int heads,
-                                          const void* qkv, int ldqkv, const void* ofwd, int ldof,
-                                          const void* dout, int lddo, const float* lse, void* dqkv,
-                                          int lddqkv, void* ws, size_t ws_bytes, void* stream) {
+extern "C" int clipk_attention_prefix_fwd(int dtype, int G, int P, int R, int ntiles, const int* tiles,
+                                          const int* row_first, int heads, const void* qkv, int ldqkv,
+                                          void* out, int ldo, float* lse, void* stream) {
+  return prefix_fwd_call(dtype, G, P, R, ntiles, tiles, row_first, heads, qkv, ldqkv, out, ldo, lse, 0, stream);
+}
+
+extern "C" int clipk_attention_prefix_fwd_ex(int dtype, int G, int P, int R, int ntiles, const int* tiles,
+                                             const int* row_first, int heads, const void* qkv, int ldqkv,
+                                             void* out, int ldo, float* lse, int flags, void* stream) {
+  return prefix_fwd_call(dtype, G, P, R, ntiles, tiles, row_first, heads, qkv, ldqkv, out, ldo, lse, flags, stream);
+}
+
+static int prefix_bwd_call(int dtype, int grad_dtype, int G, int P, int R, int ntiles, const int* tiles,
+                           const int* row_first, int heads, const void* qkv, int ldqkv, const void* ofwd, int ldof,
+                           const void* dout, int lddo, const float* lse, void* dqkv, int lddqkv, void* ws,
+                           size_t ws_bytes, int flags, void* stream) {
   if (!tiles || !row_first || !qkv || !ofwd || !dout || !lse || !dqkv || !ws) return CLIPK_EINVAL;
+  if (flags & ~CLIPK_PREFIX_CLS_GROUP0) return CLIPK_EINVAL;
   if (!prefix_shape_ok(G, P, R, ntiles, heads, lddqkv) || ldqkv < 3 * heads * 64 || lddqkv < 3 * heads * 64 ||
       ldof < heads * 64 || lddo < heads * 64)
     return CLIPK_ESHAPE;
   if (ws_bytes < clipk_attention_prefix_ws_bytes(G, ntiles, heads)) return CLIPK_EWORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)ws;
+  const int c0 = (flags & CLIPK_PREFIX_CLS_GROUP0) ? 1 : 0;
 #define CLIPK_PBWD(TT, TGG)                                                                            \
   return prefix_bwd<TT, TGG>(G, P, R, ntiles, tiles, row_first, heads, qkv, ldqkv, ofwd, ldof, dout, lddo, \
-                             lse, dqkv, lddqkv, part, st)
+                             lse, dqkv, lddqkv, part, st, c0)
   if (dtype == CLIPK_F16 && grad_dtype == CLIPK_BF16) CLIPK_PBWD(f16, bf16);
   if (dtype == CLIPK_F16 && grad_dtype == CLIPK_F16) CLIPK_PBWD(f16, f16);
   if (dtype == CLIPK_BF16 && grad_dtype == CLIPK_BF16) CLIPK_PBWD(bf16, bf16);
@@ -1323,8 +1341,26 @@ extern "C" int clipk_attention_prefix_bwd(int dtype, int grad_dtype, int G, int 
   if (dtype == CLIPK_F32 && grad_dtype == CLIPK_F32S) {
     if (lddqkv % 8) return CLIPK_ESHAPE;  // whole 8-column groups per row
     return prefix_bwd<float, float, true>(G, P, R, ntiles, tiles, row_first, heads, qkv, ldqkv, ofwd, ldof, dout,
-                                          lddo, lse, dqkv, lddqkv, part, st);
+                                          lddo, lse, dqkv, lddqkv, part, st, c0);
   }
 #undef CLIPK_PBWD
   return CLIPK_EDTYPE;
+}
+
+extern "C" int clipk_attention_prefix_bwd(int dtype, int grad_dtype, int G, int P, int R, int ntiles,
+                                          const int* tiles, const int* row_first, int heads,
+                                          const void* qkv, int ldqkv, const void* ofwd, int ldof,
+                                          const void* dout, int lddo, const float* lse, void* dqkv,
+                                          int lddqkv, void* ws, size_t ws_bytes, void* stream) {
+  return prefix_bwd_call(dtype, grad_dtype, G, P, R, ntiles, tiles, row_first, heads, qkv, ldqkv, ofwd, ldof, dout,
+                         lddo, lse, dqkv, lddqkv, ws, ws_bytes, 0, stream);
+}
+
+extern "C" int clipk_attention_prefix_bwd_ex(int dtype, int grad_dtype, int G, int P, int R, int ntiles,
+                                             const int* tiles, const int* row_first, int heads,
+                                             const void* qkv, int ldqkv, const void* ofwd, int ldof,
+                                             const void* dout, int lddo, const float* lse, void* dqkv,
+                                             int lddqkv, void* ws, size_t ws_bytes, int flags, void* stream) {
+  return prefix_bwd_call(dtype, grad_dtype, G, P, R, ntiles, tiles, row_first, heads, qkv, ldqkv, ofwd, ldof, dout,
+                         lddo, lse, dqkv, lddqkv, ws, ws_bytes, flags, stream);
 }

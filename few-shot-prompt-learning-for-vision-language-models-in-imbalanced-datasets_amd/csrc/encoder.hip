@@ -369,12 +369,13 @@ struct SeqShape {
   size_t part_bytes(int heads) const { return packed ? clipk_attention_prefix_ws_bytes(G, ntiles, heads) : 0; }
 };
 
+// pflags: clipk_attention_prefix_*_ex flags (CLIPK_PREFIX_CLS_GROUP0: layer 0 under forward sharing)
 static int attn_fwd(const clipk_encoder* e, const SeqShape& sh, const void* qkv, void* o, float* lse,
-                    hipStream_t st) {
+                    hipStream_t st, int pflags = 0) {
   const int W = e->W;
   if (sh.packed)
-    return clipk_attention_prefix_fwd(e->act, sh.G, sh.P, sh.R, sh.ntiles, sh.tiles, sh.row_first, e->heads,
-                                      qkv, 3 * W, o, W, lse, st);
+    return clipk_attention_prefix_fwd_ex(e->act, sh.G, sh.P, sh.R, sh.ntiles, sh.tiles, sh.row_first, e->heads,
+                                         qkv, 3 * W, o, W, lse, pflags, st);
   return clipk_attention_fwd(e->act, sh.nseq, sh.L, e->heads, sh.causal, qkv, 3 * W, o, W, lse, st);
 }
 
@@ -382,12 +383,12 @@ static int attn_fwd(const clipk_encoder* e, const SeqShape& sh, const void* qkv,
 // qkv input-grad GEMM reads with CLIPK_A_SPLIT (grad dtype CLIPK_F32S of the prefix backward)
 static int attn_bwd(const clipk_encoder* e, const SeqShape& sh, const void* qkv, const void* o,
                     const void* dout, const float* lse, void* dqkv, void* part, hipStream_t st,
-                    bool dqkv_split = false) {
+                    bool dqkv_split = false, int pflags = 0) {
   const int W = e->W;
   if (sh.packed)
-    return clipk_attention_prefix_bwd(e->act, dqkv_split ? CLIPK_F32S : e->grad, sh.G, sh.P, sh.R, sh.ntiles, sh.tiles, sh.row_first,
+    return clipk_attention_prefix_bwd_ex(e->act, dqkv_split ? CLIPK_F32S : e->grad, sh.G, sh.P, sh.R, sh.ntiles, sh.tiles, sh.row_first,
                                       e->heads, qkv, 3 * W, o, W, dout, W, lse, dqkv, 3 * W, part,
-                                      sh.part_bytes(e->heads), st);
+                                      sh.part_bytes(e->heads), pflags, st);
   return clipk_attention_bwd(e->act, e->grad, sh.nseq, sh.L, e->heads, sh.causal, qkv, 3 * W, o, W, dout, W,
                              lse, dqkv, 3 * W, st);
 }
@@ -771,7 +772,18 @@ static int prefix_tables(const SeqShape& sh, bool shared, int* prow, const float
 }
 
 // Layer 0's attention half under forward sharing (prefix_mode, G >= 2): LN1 + qkv on group 0's
-// rows and, compactly, on the other groups' prefix rows; qkv class rows copied to every group.
+// rows and, compactly, on the other groups' prefix rows. The attention reads every group's class
+// rows from group 0 (CLIPK_PREFIX_CLS_GROUP0), forward and backward: no per-group copies of them
+// (127 MB per step at the 16-bit headline; 253 MB at fp32). Knob CLIPK_SHARE0_INDEX=0 copies them
+// to every group (group_bcast_kernel) and reads them in place (A/B).
+static bool share0_index_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char* s = getenv("CLIPK_SHARE0_INDEX");
+    v = s ? atoi(s) : 1;
+  }
+  return v != 0;
+}
 static int block_attn_shared0(const clipk_encoder* e, const std::array<const void*, 16>& w, const SeqShape& sh,
                               int rd, const void* X, void* xn, void* qkv, void* o, float* lse, float* m1, float* r1,
                               int* prow, hipStream_t st) {
@@ -791,18 +803,21 @@ static int block_attn_shared0(const clipk_encoder* e, const std::array<const voi
   TRY(gemm(act, act, CLIPK_EPI_BIAS, R + n, 3 * W, W, xn, w[2], (const float*)w[3], nullptr, qkv, nullptr, nullptr,
            0, st, CLIPK_PROF_GEMM_ALL, nullptr, 0, "text.qkv_fwd"));
   {
-    ProfScope ps(CLIPK_PROF_NONE, st, 0.0, "text.qkv_bcast", (double)(G - 1) * (R - P) * qa * 2.0);
+    ProfScope ps(CLIPK_PROF_NONE, st, 0.0, "text.qkv_bcast",
+                 (double)(G - 2 > 0 ? G - 2 : 0) * P * qa * 2.0 + (share0_index_on() ? 0.0 : (double)(G - 1) * (R - P) * qa * 2.0));
     if (G > 2) TRY(clipk_rows_copy((int)qa, (G - 2) * P, (char*)qkv + (size_t)(R + P) * qa, nullptr, qkv, prow + 2 * P, st));
-    const int chunks = (int)(qa / 16);
-    const long total = (long)(R - P) * chunks;
-    hipLaunchKernelGGL(group_bcast_kernel, dim3((unsigned)std::min<long>((total + 255) / 256, 4096)), dim3(256), 0, st,
-                       G, P, R, chunks, (uint4*)qkv);
-    CLIPK_CHECK_LAUNCH();
+    if (!share0_index_on()) {
+      const int chunks = (int)(qa / 16);
+      const long total = (long)(R - P) * chunks;
+      hipLaunchKernelGGL(group_bcast_kernel, dim3((unsigned)std::min<long>((total + 255) / 256, 4096)), dim3(256), 0,
+                         st, G, P, R, chunks, (uint4*)qkv);
+      CLIPK_CHECK_LAUNCH();
+    }
   }
   {
     const double ab = (double)sh.rows * 4 * W * esize(act) + (lse ? 4.0 * sh.rows * e->heads : 0.0);
     ProfScope ps(CLIPK_PROF_ATTN, st, 0.0, "text.attn_fwd", ab);
-    TRY(attn_fwd(e, sh, qkv, o, lse, st));
+    TRY(attn_fwd(e, sh, qkv, o, lse, st, share0_index_on() ? CLIPK_PREFIX_CLS_GROUP0 : 0));
   }
   return CLIPK_OK;
 }
@@ -821,8 +836,7 @@ static int text_forward_impl(const clipk_encoder* e, const SeqShape& sh, const f
   const void* cur = x0;
   if (save || rd != CLIPK_F32) {
     if (rd == CLIPK_F32) {
-      if (hipMemcpyAsync(t.X[0], x0, (size_t)rows * W * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
-        return (int)hipGetLastError();
+      TRY(clipk_rows_copy(W * 4, rows, x0, nullptr, t.X[0], nullptr, st));  // (a clipk kernel, not a runtime blit)
     } else {
       TRY(clipk_cast(rd, (long)rows * W, x0, t.X[0], st));
     }
@@ -904,6 +918,21 @@ static bool text_dres16(const clipk_encoder* e) {
   return v > 0 || e->grad == CLIPK_F16;
 }
 
+// zero fill of 16-B aligned buffers of a multiple of 16 bytes (every text-backward buffer) as a
+// clipk kernel instead of a runtime fill
+__global__ __launch_bounds__(256) void zero16_kernel(long n, uint4* __restrict__ p) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) p[i] = make_uint4(0, 0, 0, 0);
+}
+static int zero_bytes(void* p, size_t bytes, hipStream_t st) {
+  if (bytes == 0) return CLIPK_OK;
+  if ((bytes | (uintptr_t)p) & 15) return CLIPK_ESHAPE;
+  const long n = (long)(bytes / 16);
+  hipLaunchKernelGGL(zero16_kernel, dim3((unsigned)std::min<long>((n + 255) / 256, 4096)), dim3(256), 0, st, n,
+                     (uint4*)p);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
 static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const int* eot_rows,
                               const float* dtxt, const void* saved, size_t saved_bytes, float* dx0,
                               void* ws, size_t ws_bytes, hipStream_t st, const EncIO& io) {
@@ -945,9 +974,7 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
   const int dqkv_split = qkv_split ? CLIPK_A_SPLIT : 0;
   void* const dA = lp_alias ? (void*)dX : b.dX_lp;  // the A operand of proj_dx / out_dx
   const bool eotl = text_eot_last(sh);
-  auto zero = [&](void* p, size_t bytes) {
-    return hipMemsetAsync(p, 0, bytes, st) == hipSuccess ? CLIPK_OK : (int)hipGetLastError();
-  };
+  auto zero = [&](void* p, size_t bytes) { return zero_bytes(p, bytes, st); };
   if (!eotl) {
     // ln_final's gradient lands on the EOT rows of zeroed full-row streams
     if (!r16) TRY(zero(dX, (size_t)rows * W * 4));
@@ -1015,7 +1042,10 @@ static int text_backward_impl(const clipk_encoder* e, const SeqShape& sh, const 
       const double ab = (double)rows * W * ((act == CLIPK_F32 ? 4.0 : 3.0) * esize(act) + 4.0 * esize(gd)) +
                         4.0 * rows * e->heads;
       ProfScope ps(io.text ? CLIPK_PROF_ATTN : CLIPK_PROF_NONE, st, 0.0, SITE("attn_bwd"), ab);
-      TRY(attn_bwd(e, sh, t.qkv[l], t.o[l], b.do_, t.lse[l], b.dqkv, b.part, st, qkv_split));
+      // layer 0 under forward sharing: its class rows of q|k|v exist in group 0 only
+      const bool shared0 = l == 0 && io.text && sh.G >= 2 && prefix_mode(e, sh) && share0_index_on();
+      TRY(attn_bwd(e, sh, t.qkv[l], t.o[l], b.do_, t.lse[l], b.dqkv, b.part, st, qkv_split,
+                   shared0 ? CLIPK_PREFIX_CLS_GROUP0 : 0));
     }
     if (l == 0 && io.text && prefix_mode(e, sh)) {
       // the input gradient on the prefix rows only: dqkv gathered to G*P compact rows, their

@@ -197,6 +197,32 @@ __global__ __launch_bounds__(256) void ctx_grad_rows_kernel(int R, int W, int n_
   if (wv == 0 && wcol < W) dctx[(size_t)o * W + wcol] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
+// CoCoOp's ctx_shifted = ctx + bias_g on packed prompts (PromptAssembleFn.backward): the two sums
+// of the per-(g, k) slot gradients in one launch, one thread per column w:
+//   dctx[k, w] = sum_g d(g, k)[w]   (the shared ctx, summed over the images in g order)
+//   dbias[g, w] = sum_k d(g, k)[w]  (the Meta-Net output of image g, summed over the slots)
+// with d(g, k) = the ctx_grad_rows_kernel sum of slot k's rows of group g
+__global__ __launch_bounds__(256) void ctx_bias_grad_rows_kernel(int G, int R, int W, int n_ctx,
+                                                                 const int* __restrict__ slot_ptr,
+                                                                 const int* __restrict__ slot_rows,
+                                                                 const float* __restrict__ dx0,
+                                                                 float* __restrict__ dctx,
+                                                                 float* __restrict__ dbias) {
+  const int w = blockIdx.x * 256 + threadIdx.x;
+  if (w >= W) return;
+  for (int k = 0; k < n_ctx; ++k) {
+    const int i0 = slot_ptr[k], i1 = slot_ptr[k + 1];
+    float sk = 0.f;
+    for (int g = 0; g < G; ++g) {
+      float d = 0.f;
+      for (int i = i0; i < i1; ++i) d += dx0[((size_t)g * R + slot_rows[i]) * W + w];
+      sk += d;
+      if (dbias) dbias[(size_t)g * W + w] = (k == 0 ? 0.f : dbias[(size_t)g * W + w]) + d;
+    }
+    dctx[(size_t)k * W + w] = sk;
+  }
+}
+
 // ---------------------------------------------------------------- cosine logits
 // coop.py:356-363 / cocoop.py:238-251: logits = exp(logit_scale) * (imf/|imf|) . (txt/|txt|)
 __global__ __launch_bounds__(256) void cos_logits_fwd_kernel(int B, int C, int E, int per_image,
@@ -309,6 +335,51 @@ __global__ __launch_bounds__(64) void ce_loss_kernel(int B, int C, const float* 
   }
 }
 
+// The loss reduced in the same launch (clipk_ce_loss_reduce): one block, wave w takes rows w,
+// w + 4, ...; the row losses are summed in row order by one thread (deterministic)
+__global__ __launch_bounds__(256) void ce_loss_reduce_kernel(int B, int C, const float* __restrict__ logits,
+                                                             const int64_t* __restrict__ labels,
+                                                             const float* __restrict__ alpha, float gamma,
+                                                             int focal, float grad_scale, int mean,
+                                                             float* __restrict__ row_loss,
+                                                             float* __restrict__ loss,
+                                                             float* __restrict__ dlogits) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int b = wv; b < B; b += 4) {
+    const float* z = logits + (size_t)b * C;
+    const int y = (int)labels[b];
+    float mx = -INFINITY;
+    for (int c = lane; c < C; c += 64) mx = fmaxf(mx, z[c]);
+    mx = wave_max(mx);
+    float se = 0.f;
+    for (int c = lane; c < C; c += 64) se += __expf(z[c] - mx);
+    se = wave_sum(se);
+    const float lse = mx + __logf(se);
+    const float ce = lse - z[y];
+    float wgt = 1.f, l = ce;
+    if (focal) {
+      const float p = __expf(-ce);
+      const float a = alpha ? alpha[y] : 1.f;
+      const float om = 1.f - p;
+      l = a * powf(om, gamma) * ce;
+      wgt = a * (powf(om, gamma) + (gamma != 0.f ? gamma * p * powf(om, gamma - 1.f) * ce : 0.f));
+    }
+    if (lane == 0) row_loss[b] = l;
+    if (dlogits)
+      for (int c = lane; c < C; c += 64) {
+        const float pc = __expf(z[c] - lse);
+        dlogits[(size_t)b * C + c] = grad_scale * wgt * (pc - (c == y ? 1.f : 0.f));
+      }
+  }
+  __threadfence_block();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += row_loss[b];
+    loss[0] = mean ? s * (1.0f / (float)B) : s;  // (torch's mean: the sum times 1 / B)
+  }
+}
+
 // ---------------------------------------------------------------- Meta-Net (cocoop.py:139-143)
 // Block (image b, 64-output block ob): every block of an image recomputes the Hd hidden units
 // (W1 stays in L2). Lane l of a wave holds x[b, 4 l .. 4 l + 3 (+ 256 i)] and the matching W1
@@ -318,11 +389,16 @@ __global__ __launch_bounds__(64) void ce_loss_kernel(int B, int C, const float* 
 // per output split the Hd-long second dot product (fixed order: 4 interleaved partial sums, then
 // the quad sum). V % 256 == 0, V <= 1024, Hd <= 64, 16-B aligned x / W1 (the CLIP widths);
 // other shapes run meta_net_fwd_generic_kernel.
+// NORM (clipk_meta_net_fwd_norm): x is the raw image feature; every wave holds the whole row, so
+// each forms |x| itself and the Meta-Net runs on x / |x| (cocoop.py:238's imf / imf.norm(), the
+// row also written to xn by one wave for the cosine logits and the backward)
+template <bool NORM>
 __global__ __launch_bounds__(256) void meta_net_fwd_kernel(int V, int Hd, int Wd, const float* __restrict__ x,
                                                            const float* __restrict__ w1,
                                                            const float* __restrict__ b1,
                                                            const float* __restrict__ w2,
                                                            const float* __restrict__ b2,
+                                                           float* __restrict__ xn,
                                                            float* __restrict__ h, float* __restrict__ y) {
   extern __shared__ float sh[];  // Hd floats
   const int b = blockIdx.x, ob = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -332,6 +408,22 @@ __global__ __launch_bounds__(256) void meta_net_fwd_kernel(int V, int Hd, int Wd
 #pragma unroll
   for (int c = 0; c < 4; ++c)
     if (c < nc) xv[c] = *reinterpret_cast<const f32x4*>(xb + 4 * lane + 256 * c);
+  if constexpr (NORM) {
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (c < nc)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ss = fmaf(xv[c][e], xv[c][e], ss);
+    const float nrm = sqrtf(wave_sum(ss));
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (c < nc) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xv[c][e] = xv[c][e] / nrm;
+        if (ob == 0 && wv == 0) *reinterpret_cast<f32x4*>(xn + (size_t)b * V + 4 * lane + 256 * c) = xv[c];
+      }
+  }
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const int k = wv + 4 * j;
@@ -369,15 +461,28 @@ __global__ __launch_bounds__(256) void meta_net_fwd_kernel(int V, int Hd, int Wd
 }
 
 // any V / Hd (tiny test models): one block per image, a dependent load + wave sum per hidden unit
+// (NORM: x / |x| written to xn first, then read back: the block's own rows)
+template <bool NORM>
 __global__ __launch_bounds__(256) void meta_net_fwd_generic_kernel(int V, int Hd, int Wd, const float* __restrict__ x,
                                                                    const float* __restrict__ w1,
                                                                    const float* __restrict__ b1,
                                                                    const float* __restrict__ w2,
                                                                    const float* __restrict__ b2,
+                                                                   float* __restrict__ xn,
                                                                    float* __restrict__ h, float* __restrict__ y) {
   extern __shared__ float sh[];  // Hd floats
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const float* xb = x + (size_t)b * V;
+  if constexpr (NORM) {
+    float ss = 0.f;
+    for (int v = lane; v < V; v += 64) ss = fmaf(xb[v], xb[v], ss);
+    const float nrm = sqrtf(wave_sum(ss));
+    if (wv == 0)
+      for (int v = lane; v < V; v += 64) xn[(size_t)b * V + v] = xb[v] / nrm;
+    __threadfence_block();
+    __syncthreads();
+    xb = xn + (size_t)b * V;
+  }
   for (int k = wv; k < Hd; k += 4) {
     float a = 0.f;
     for (int v = lane; v < V; v += 64) a += w1[(size_t)k * V + v] * xb[v];
@@ -468,7 +573,16 @@ struct SgdTensors {
   long n[kSgdMaxTensors];
   int has[kSgdMaxTensors];
 };
-__global__ __launch_bounds__(256) void sgd_multi_kernel(SgdTensors t, float lr, float mom, float wd) {
+// gs (clipk_sgd_step_multi_scaled): the gradient scale, e.g. the 1 / world of a SUM all-reduce
+// (dist.allreduce_grads folds its average here instead of a separate division launch); 1.0 is
+// bitwise the unscaled update
+// guard (clipk_sgd_step_multi_if): the whole update is skipped when guard[0] & mask != 0 -- the
+// PREC fp32s backward's overflow flag, read on the device so the host need not wait for the
+// backward before queueing the step (a skipped step leaves p and buf untouched)
+template <bool SCALED>
+__global__ __launch_bounds__(256) void sgd_multi_kernel(SgdTensors t, float lr, float mom, float wd, float gs,
+                                                        const int* __restrict__ guard, int mask) {
+  if (guard && (guard[0] & mask)) return;
   const int k = blockIdx.y;
   const long n = t.n[k];
   float* __restrict__ p = t.p[k];
@@ -476,10 +590,22 @@ __global__ __launch_bounds__(256) void sgd_multi_kernel(SgdTensors t, float lr, 
   float* __restrict__ buf = t.buf[k];
   const int has_buf = t.has[k];
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const float d = g[i] + wd * p[i];
+    // d = fma(wd, p, g) spelled out (the form hipcc contracts the unscaled update to), with the
+    // scaled gradient rounded on its own: a power-of-two scale is bitwise the update on
+    // pre-scaled gradients
+    const float d = __builtin_fmaf(wd, p[i], SCALED ? __fmul_rn(g[i], gs) : g[i]);
     const float bb = has_buf ? mom * buf[i] + d : d;
     buf[i] = bb;
     p[i] -= lr * bb;
+  }
+}
+
+// clipk_status_take: the status word handed to host-visible memory and cleared, one thread
+__global__ __launch_bounds__(64) void status_take_kernel(int* __restrict__ flags, int* __restrict__ host) {
+  if (threadIdx.x == 0) {
+    const int v = atomicExch(flags, 0);  // (a concurrent stream's OR is never lost between read and clear)
+    host[0] = v;
+    __threadfence_system();
   }
 }
 
@@ -678,20 +804,70 @@ extern "C" int clipk_ce_loss(int B, int C, const float* logits, const int64_t* l
   return CLIPK_OK;
 }
 
-extern "C" int clipk_meta_net_fwd(int B, int V, int Hd, int Wd, const float* x, const float* w1,
-                                  const float* b1, const float* w2, const float* b2, float* h,
-                                  float* y, void* stream) {
-  if (!x || !w1 || !b1 || !w2 || !b2 || !y) return CLIPK_EINVAL;
+static int meta_net_fwd_launch(bool norm, int B, int V, int Hd, int Wd, const float* x, const float* w1,
+                               const float* b1, const float* w2, const float* b2, float* xn, float* h, float* y,
+                               void* stream) {
+  if (!x || !w1 || !b1 || !w2 || !b2 || !y || (norm && !xn)) return CLIPK_EINVAL;
   if (B < 0 || V <= 0 || Hd <= 0 || Wd <= 0) return CLIPK_ESHAPE;
   if (B == 0) return CLIPK_OK;
-  if (V % 256 || V > 1024 || Hd > 64 || ((uintptr_t)x | (uintptr_t)w1) % 16) {
-    hipLaunchKernelGGL(meta_net_fwd_generic_kernel, dim3(B), dim3(256), Hd * sizeof(float), (hipStream_t)stream, V,
-                       Hd, Wd, x, w1, b1, w2, b2, h, y);
+  hipStream_t st = (hipStream_t)stream;
+  if (V % 256 || V > 1024 || Hd > 64 || ((uintptr_t)x | (uintptr_t)w1 | (uintptr_t)xn) % 16) {
+    if (norm)
+      hipLaunchKernelGGL(meta_net_fwd_generic_kernel<true>, dim3(B), dim3(256), Hd * sizeof(float), st, V, Hd, Wd, x,
+                         w1, b1, w2, b2, xn, h, y);
+    else
+      hipLaunchKernelGGL(meta_net_fwd_generic_kernel<false>, dim3(B), dim3(256), Hd * sizeof(float), st, V, Hd, Wd, x,
+                         w1, b1, w2, b2, xn, h, y);
     CLIPK_CHECK_LAUNCH();
     return CLIPK_OK;
   }
-  hipLaunchKernelGGL(meta_net_fwd_kernel, dim3(B, (Wd + 63) / 64), dim3(256), Hd * sizeof(float), (hipStream_t)stream,
-                     V, Hd, Wd, x, w1, b1, w2, b2, h, y);
+  if (norm)
+    hipLaunchKernelGGL(meta_net_fwd_kernel<true>, dim3(B, (Wd + 63) / 64), dim3(256), Hd * sizeof(float), st, V, Hd,
+                       Wd, x, w1, b1, w2, b2, xn, h, y);
+  else
+    hipLaunchKernelGGL(meta_net_fwd_kernel<false>, dim3(B, (Wd + 63) / 64), dim3(256), Hd * sizeof(float), st, V, Hd,
+                       Wd, x, w1, b1, w2, b2, xn, h, y);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_meta_net_fwd(int B, int V, int Hd, int Wd, const float* x, const float* w1,
+                                  const float* b1, const float* w2, const float* b2, float* h,
+                                  float* y, void* stream) {
+  return meta_net_fwd_launch(false, B, V, Hd, Wd, x, w1, b1, w2, b2, nullptr, h, y, stream);
+}
+
+extern "C" int clipk_meta_net_fwd_norm(int B, int V, int Hd, int Wd, const float* x, const float* w1,
+                                       const float* b1, const float* w2, const float* b2, float* xn, float* h,
+                                       float* y, void* stream) {
+  return meta_net_fwd_launch(true, B, V, Hd, Wd, x, w1, b1, w2, b2, xn, h, y, stream);
+}
+
+extern "C" int clipk_ce_loss_reduce(int B, int C, const float* logits, const int64_t* labels, const float* alpha,
+                                    float gamma, int focal, float grad_scale, int reduction, float* row_loss,
+                                    float* loss, float* dlogits, void* stream) {
+  if (!logits || !labels || !row_loss || !loss) return CLIPK_EINVAL;
+  if (reduction != 1 && reduction != 2) return CLIPK_EINVAL;
+  if (B <= 0 || C <= 0) return CLIPK_ESHAPE;
+  hipLaunchKernelGGL(ce_loss_reduce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, C, logits, labels, alpha,
+                     gamma, focal, grad_scale, reduction == 1 ? 1 : 0, row_loss, loss, dlogits);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_ctx_bias_grad_rows(int G, int R, int W, int n_ctx, const int* slot_ptr, const int* slot_rows,
+                                        const float* dx0, float* dctx, float* dbias, void* stream) {
+  if (!slot_ptr || !slot_rows || !dx0 || !dctx) return CLIPK_EINVAL;
+  if (G <= 0 || R <= 0 || n_ctx <= 0 || W <= 0) return CLIPK_ESHAPE;
+  hipLaunchKernelGGL(ctx_bias_grad_rows_kernel, dim3((W + 255) / 256), dim3(256), 0, (hipStream_t)stream, G, R, W,
+                     n_ctx, slot_ptr, slot_rows, dx0, dctx, dbias);
+  CLIPK_CHECK_LAUNCH();
+  return CLIPK_OK;
+}
+
+extern "C" int clipk_status_take(int* flags, int* host_word, void* stream) {
+  if (!flags || !host_word) return CLIPK_EINVAL;
+  hipLaunchKernelGGL(status_take_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, flags, host_word);
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
 }
@@ -713,9 +889,33 @@ extern "C" int clipk_meta_net_bwd(int B, int V, int Hd, int Wd, const float* x, 
   return CLIPK_OK;
 }
 
+static int sgd_multi(int count, float* const* p, const float* const* g, float* const* buf, const long* n,
+                     const int* has_buf, float lr, float momentum, float weight_decay, float grad_scale,
+                     const int* guard, int mask, void* stream);
+
 extern "C" int clipk_sgd_step_multi(int count, float* const* p, const float* const* g, float* const* buf,
                                     const long* n, const int* has_buf, float lr, float momentum,
                                     float weight_decay, void* stream) {
+  return sgd_multi(count, p, g, buf, n, has_buf, lr, momentum, weight_decay, 1.0f, nullptr, 0, stream);
+}
+
+extern "C" int clipk_sgd_step_multi_scaled(int count, float* const* p, const float* const* g, float* const* buf,
+                                           const long* n, const int* has_buf, float lr, float momentum,
+                                           float weight_decay, float grad_scale, void* stream) {
+  return sgd_multi(count, p, g, buf, n, has_buf, lr, momentum, weight_decay, grad_scale, nullptr, 0, stream);
+}
+
+extern "C" int clipk_sgd_step_multi_if(int count, float* const* p, const float* const* g, float* const* buf,
+                                       const long* n, const int* has_buf, float lr, float momentum,
+                                       float weight_decay, float grad_scale, const int* guard, int mask,
+                                       void* stream) {
+  if (!guard) return CLIPK_EINVAL;
+  return sgd_multi(count, p, g, buf, n, has_buf, lr, momentum, weight_decay, grad_scale, guard, mask, stream);
+}
+
+static int sgd_multi(int count, float* const* p, const float* const* g, float* const* buf, const long* n,
+                     const int* has_buf, float lr, float momentum, float weight_decay, float grad_scale,
+                     const int* guard, int mask, void* stream) {
   if (count < 0 || count > kSgdMaxTensors || (count && (!p || !g || !buf || !n || !has_buf))) return CLIPK_EINVAL;
   SgdTensors t{};
   long nmax = 0;
@@ -730,8 +930,12 @@ extern "C" int clipk_sgd_step_multi(int count, float* const* p, const float* con
     nmax = n[k] > nmax ? n[k] : nmax;
   }
   if (nmax == 0) return CLIPK_OK;
-  hipLaunchKernelGGL(sgd_multi_kernel, dim3(grid_for(nmax), count), dim3(256), 0, (hipStream_t)stream, t, lr,
-                     momentum, weight_decay);
+  if (grad_scale == 1.0f)
+    hipLaunchKernelGGL(sgd_multi_kernel<false>, dim3(grid_for(nmax), count), dim3(256), 0, (hipStream_t)stream, t, lr,
+                       momentum, weight_decay, 1.0f, guard, mask);
+  else
+    hipLaunchKernelGGL(sgd_multi_kernel<true>, dim3(grid_for(nmax), count), dim3(256), 0, (hipStream_t)stream, t, lr,
+                       momentum, weight_decay, grad_scale, guard, mask);
   CLIPK_CHECK_LAUNCH();
   return CLIPK_OK;
 }

@@ -87,11 +87,14 @@ def _grad_bucket(ps):
     return b[1], b[2]
 
 
-def allreduce_grads(params, average: bool = True):
+def allreduce_grads(params, average: bool = True, optimizer=None):
     """Sum (mean) the gradients of ``params`` across ranks in ONE fused bucket: the gradients are
     copied into a persistent flat buffer (one multi-tensor copy, or none when they already are its
     views), reduced in place, and each ``p.grad`` is rebound to its view of the result (no
-    per-step concatenation, no copy back)."""
+    per-step concatenation, no copy back). ``optimizer`` with ``defer_grad_scale`` (FusedSGD):
+    the mean's 1 / world is folded into its next step (clipk_sgd_step_multi_scaled) instead of a
+    division launch -- the grads then hold the SUM, tagged with the pending scale, until that step
+    (a step skipped by the amp finite check leaves the tag to the next all-reduce, which resets it)."""
     if not is_dist():
         return
     ps = [p for p in params if p.grad is not None]
@@ -105,7 +108,10 @@ def allreduce_grads(params, average: bool = True):
         torch._foreach_copy_([v for v, _ in todo], [g for _, g in todo])
     _all_reduce(flat)
     if average and world_size() > 1:
-        flat.div_(world_size())
+        if optimizer is not None and hasattr(optimizer, "defer_grad_scale"):
+            optimizer.defer_grad_scale(views, 1.0 / world_size())
+        else:
+            flat.div_(world_size())
     for p, v in zip(ps, views):
         p.grad = v
 

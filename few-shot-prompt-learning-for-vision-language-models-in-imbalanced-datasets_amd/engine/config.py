@@ -149,5 +149,9 @@ def get_cfg_default() -> CfgNode:
                    "OVERLAP_VISION": True,
                    # PREFETCH_VISION: CoCoOp starts the next batch's image encoder (frozen) on a side
                    # stream between a step's forward and backward (the loop names the next batch)
-                   "PREFETCH_VISION": True},
+                   "PREFETCH_VISION": True,
+                   # DEFER_SPLIT_CHECK: PREC fp32s CoCoOp (one process) reads a step's overflow flag
+                   # in the next step instead of waiting for it in the backward (same updates:
+                   # CoCoOp.forward_backward)
+                   "DEFER_SPLIT_CHECK": True},
     })

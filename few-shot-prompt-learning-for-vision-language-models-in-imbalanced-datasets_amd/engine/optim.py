@@ -20,6 +20,8 @@ class FusedSGD(torch.optim.Optimizer):
     """Param groups carry every key of torch.optim.SGD's groups, so ``state_dict()`` loads
     into the reference's torch.optim.SGD (and a reference SGD state into this one)."""
 
+    created_last = ()
+
     def __init__(self, params, lr=0.002, momentum=0.9, weight_decay=5e-4, dampening=0.0,
                  nesterov=False):
         if dampening != 0 or nesterov:
@@ -28,13 +30,25 @@ class FusedSGD(torch.optim.Optimizer):
                                       nesterov=False, maximize=False, foreach=None, differentiable=False,
                                       fused=None))
 
+    @staticmethod
+    def defer_grad_scale(grads, s):
+        """The next step updates with s * g for these gradient tensors (dist.allreduce_grads folds
+        the average of a SUM all-reduce here: one launch less per step). A tag on each tensor,
+        set (not multiplied) per all-reduce and consumed by step()."""
+        for g in grads:
+            g._clipk_grad_scale = s
+
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, guard=None):
+        """guard = (int32 device flags, mask): the update is skipped on the device when
+        flags[0] & mask (clipk_sgd_step_multi_if); ``created_last`` lists the parameters whose
+        momentum buffer this call created (a skipped step's are never written)."""
         loss = closure() if closure is not None else None
+        self.created_last = []
         for grp in self.param_groups:
             # the group's tensors in one launch per 16 (clipk_sgd_step_multi): at the reference's
             # batch of 1 the five per-tensor launches were kernel boundaries on the critical path
-            ps, gs, bufs, has = [], [], [], []
+            ps, gs, bufs, has, scales = [], [], [], [], []
             for p in grp["params"]:
                 if p.grad is None:
                     continue
@@ -49,15 +63,23 @@ class FusedSGD(torch.optim.Optimizer):
                 h = buf is not None
                 if not h:
                     buf = st["momentum_buffer"] = torch.empty_like(p)
+                    self.created_last.append(p)
                 elif buf.device != p.device or not buf.is_contiguous():
                     buf = st["momentum_buffer"] = buf.to(p.device).contiguous()
                 ps.append(p.data)
+                scales.append(getattr(p.grad, "_clipk_grad_scale", 1.0))
+                if hasattr(p.grad, "_clipk_grad_scale"):
+                    del p.grad._clipk_grad_scale
                 gs.append(p.grad if p.grad.is_contiguous() else p.grad.contiguous())
                 bufs.append(buf)
                 has.append(h)
                 p._clipk_gen = getattr(p, "_clipk_gen", 0) + 1  # invalidates cached text features
             if ps:
-                ops.sgd_step_multi(ps, gs, bufs, grp["lr"], grp["momentum"], grp["weight_decay"], has)
+                if len(set(scales)) > 1:  # (mixed tags: scaled here, then one unscaled launch)
+                    gs = [g * sc if sc != 1.0 else g for g, sc in zip(gs, scales)]
+                    scales = [1.0]
+                ops.sgd_step_multi(ps, gs, bufs, grp["lr"], grp["momentum"], grp["weight_decay"], has,
+                                   grad_scale=scales[0], guard=guard)
         return loss
 
 

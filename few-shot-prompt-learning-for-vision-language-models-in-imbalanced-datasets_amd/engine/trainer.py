@@ -124,7 +124,9 @@ class TrainerX:
             dist.broadcast_params(self.trainable_params(), src=0)
 
     def allreduce_grads(self, module):
-        dist.allreduce_grads([p for p in module.parameters() if p.requires_grad])
+        # the average's 1 / world folded into the fused SGD step (FusedSGD.defer_grad_scale)
+        dist.allreduce_grads([p for p in module.parameters() if p.requires_grad],
+                             optimizer=getattr(self, "optim", None))
 
     @staticmethod
     def batch_weight(batch, n_local):
@@ -164,6 +166,7 @@ class TrainerX:
         module.load_state_dict(keep, strict=False)
 
     def save_model(self, epoch, directory, is_best=False, val_result=None, model_name=""):
+        self.flush_deferred()
         if dist.rank() != 0:
             return
         for name in self.get_model_names():
@@ -261,12 +264,18 @@ class TrainerX:
             if (self.batch_idx + 1) % self.cfg.TRAIN.PRINT_FREQ == 0 and dist.rank() == 0:
                 print(f"epoch [{self.epoch + 1}/{self.max_epoch}] batch [{self.batch_idx + 1}/"
                       f"{self.num_batches}] {summary} lr {self.get_current_lr():.4e}")
+        self.flush_deferred()
+
+    def flush_deferred(self):
+        """Settle a check the last step left pending (PREC fp32s, CoCoOp.forward_backward); a
+        no-op for trainers that check in the step."""
 
     @torch.no_grad()
     def test(self, split=None, return_pred=False):
         """trainer.py:446-486. Each rank evaluates its shard of the split (the loader is
         rank-aware); labels and predictions are gathered so every rank evaluates the union.
         Returns (y_true, y_pred) numpy arrays with ``return_pred``, else the first metric."""
+        self.flush_deferred()
         self.set_model_mode("eval")
         self.evaluator.reset()
         if split is None:

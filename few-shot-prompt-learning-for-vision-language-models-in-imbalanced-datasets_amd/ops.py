@@ -309,27 +309,38 @@ def prompt_assemble_rows(G, R, C, L, row_tab, src_map, emb, ctx, ctx_sg, ctx_sc,
     return x0
 
 
+def ctx_bias_grad_rows(G, R, W, n_ctx, slot_ptr, slot_rows, dx0, bias=True):
+    """clipk_ctx_bias_grad_rows: (dctx [n_ctx, W] summed over the G groups, dbias [G, W] summed
+    over the slots, or None)."""
+    dctx = torch.empty(n_ctx, W, device=dx0.device, dtype=torch.float32)
+    dbias = torch.empty(G, W, device=dx0.device, dtype=torch.float32) if bias else None
+    N.call("clipk_ctx_bias_grad_rows", G, R, W, n_ctx, _p(slot_ptr), _p(slot_rows), _p(dx0), _p(dctx), _p(dbias),
+           _stream())
+    return dctx, dbias
+
+
 def ctx_grad_rows(G, R, W, n_ctx, slot_ptr, slot_rows, dx0):
     d = torch.empty(G * n_ctx, W, device=dx0.device, dtype=torch.float32)
     N.call("clipk_ctx_grad_rows", G, R, W, n_ctx, _p(slot_ptr), _p(slot_rows), _p(dx0), _p(d), _stream())
     return d
 
 
-def attention_prefix(qkv, G, P, R, tiles, row_first, heads, lse=False):
-    """Shared-prefix packed causal attention (clipk_attention_prefix_fwd); tiles int32
-    [ntiles*2] (first row, rows), row_first int32 [R]."""
+def attention_prefix(qkv, G, P, R, tiles, row_first, heads, lse=False, flags=0):
+    """Shared-prefix packed causal attention (clipk_attention_prefix_fwd_ex); tiles int32
+    [ntiles*2] (first row, rows), row_first int32 [R]; flags N.PREFIX_CLS_GROUP0: class rows'
+    q|k|v read from group 0."""
     _need(qkv, "qkv")
     _need(tiles, "tiles", torch.int32)
     _need(row_first, "row_first", torch.int32)
     W = heads * 64
     out = torch.zeros(G * R, W, device=qkv.device, dtype=qkv.dtype)
     l = torch.zeros(G * R, heads, device=qkv.device) if lse else None
-    N.call("clipk_attention_prefix_fwd", DT[qkv.dtype], G, P, R, tiles.numel() // 2, _p(tiles), _p(row_first),
-           heads, _p(qkv), 3 * W, _p(out), W, _p(l), _stream())
+    N.call("clipk_attention_prefix_fwd_ex", DT[qkv.dtype], G, P, R, tiles.numel() // 2, _p(tiles), _p(row_first),
+           heads, _p(qkv), 3 * W, _p(out), W, _p(l), int(flags), _stream())
     return (out, l) if lse else out
 
 
-def attention_prefix_bwd(qkv, o, dout, lse, G, P, R, tiles, row_first, heads, grad_dtype, split=False):
+def attention_prefix_bwd(qkv, o, dout, lse, G, P, R, tiles, row_first, heads, grad_dtype, split=False, flags=0):
     """split (fp32 qkv / dout / grad_dtype): dq|dk|dv in the pre-split operand form of CLIPK_A_SPLIT
     (grad dtype CLIPK_F32S), viewed as fp32 [G*R, 3W]."""
     W = heads * 64
@@ -338,8 +349,8 @@ def attention_prefix_bwd(qkv, o, dout, lse, G, P, R, tiles, row_first, heads, gr
     nb = N.load().clipk_attention_prefix_ws_bytes(G, nt, heads)
     ws = torch.empty(nb, dtype=torch.uint8, device=qkv.device)
     gdt = N.F32S if split else DT[grad_dtype]
-    N.call("clipk_attention_prefix_bwd", DT[qkv.dtype], gdt, G, P, R, nt, _p(tiles), _p(row_first),
-           heads, _p(qkv), 3 * W, _p(o), W, _p(dout), W, _p(lse), _p(dqkv), 3 * W, _p(ws), nb, _stream())
+    N.call("clipk_attention_prefix_bwd_ex", DT[qkv.dtype], gdt, G, P, R, nt, _p(tiles), _p(row_first),
+           heads, _p(qkv), 3 * W, _p(o), W, _p(dout), W, _p(lse), _p(dqkv), 3 * W, _p(ws), nb, int(flags), _stream())
     return dqkv
 
 
@@ -388,14 +399,46 @@ def ce_loss(logits, labels, alpha=None, gamma=2.0, focal=False, grad=True, grad_
     return row, dl
 
 
-def meta_net(x, w1, b1, w2, b2):
+def meta_net(x, w1, b1, w2, b2, normalize=False):
+    """(h, y); normalize: the Meta-Net on x / |x| (clipk_meta_net_fwd_norm) -> (xn, h, y)."""
     B, V = x.shape
     Hd, Wd = w1.shape[0], w2.shape[0]
     h = torch.empty(B, Hd, device=x.device)
     y = torch.empty(B, Wd, device=x.device)
+    if normalize:
+        xn = torch.empty(B, V, device=x.device)
+        N.call("clipk_meta_net_fwd_norm", B, V, Hd, Wd, _p(x), _p(w1), _p(b1), _p(w2), _p(b2), _p(xn), _p(h),
+               _p(y), _stream())
+        return xn, h, y
     N.call("clipk_meta_net_fwd", B, V, Hd, Wd, _p(x), _p(w1), _p(b1), _p(w2), _p(b2), _p(h), _p(y),
            _stream())
     return h, y
+
+
+def ce_loss_reduce(logits, labels, alpha=None, gamma=2.0, focal=False, grad=True, reduction="mean"):
+    """clipk_ce_loss_reduce: (loss [] = mean / sum of the row losses, dlogits = d loss / d logits)
+    in one launch."""
+    _need(logits, "logits", torch.float32)
+    _need(labels, "labels", torch.int64)
+    B, C = logits.shape
+    if labels.shape != (B,):
+        raise N.ClipkError(f"labels must be [{B}], got {tuple(labels.shape)}")
+    if alpha is not None:
+        _need(alpha, "alpha", torch.float32)
+        if alpha.numel() < C:
+            raise N.ClipkError(f"alpha must hold {C} class weights, got {alpha.numel()}")
+    red = {"mean": 1, "sum": 2}[reduction]
+    row = torch.empty(B, device=logits.device)
+    loss = torch.empty((), device=logits.device)
+    dl = torch.empty_like(logits) if grad else None
+    N.call("clipk_ce_loss_reduce", B, C, _p(logits), _p(labels), _p(alpha), float(gamma), int(focal),
+           1.0 / B if reduction == "mean" else 1.0, red, _p(row), _p(loss), _p(dl), _stream())
+    return loss, dl
+
+
+def status_take(flags, host_word):
+    """clipk_status_take: flags -> host_word (pinned int32), flags cleared (stream-ordered)."""
+    N.call("clipk_status_take", _p(flags), _p(host_word), _stream())
 
 
 def meta_net_bwd(x, h, w2, dy, V, Hd, Wd):
@@ -415,17 +458,25 @@ def sgd_step(p, g, buf, lr, momentum, weight_decay, has_buf):
            float(weight_decay), int(has_buf), _stream())
 
 
-def sgd_step_multi(ps, gs, bufs, lr, momentum, weight_decay, has_bufs):
-    """clipk_sgd_step_multi: one launch per 16 tensors (fp32, contiguous, on one device)."""
+def sgd_step_multi(ps, gs, bufs, lr, momentum, weight_decay, has_bufs, grad_scale=1.0, guard=None):
+    """clipk_sgd_step_multi(_scaled / _if): one launch per 16 tensors (fp32, contiguous, on one
+    device); grad_scale multiplies every gradient (1.0: the unscaled entry point); guard = (int32
+    device flags, mask): the update is skipped on the device when flags[0] & mask."""
     import ctypes
     for i in range(0, len(ps), 16):
         P_, G_, B_ = ps[i:i + 16], gs[i:i + 16], bufs[i:i + 16]
         c = len(P_)
         VP = ctypes.c_void_p * c
-        N.call("clipk_sgd_step_multi", c, VP(*[t.data_ptr() for t in P_]), VP(*[t.data_ptr() for t in G_]),
-               VP(*[t.data_ptr() for t in B_]), (ctypes.c_long * c)(*[t.numel() for t in P_]),
-               (ctypes.c_int * c)(*[int(h) for h in has_bufs[i:i + 16]]), float(lr), float(momentum),
-               float(weight_decay), _stream())
+        args = (c, VP(*[t.data_ptr() for t in P_]), VP(*[t.data_ptr() for t in G_]),
+                VP(*[t.data_ptr() for t in B_]), (ctypes.c_long * c)(*[t.numel() for t in P_]),
+                (ctypes.c_int * c)(*[int(h) for h in has_bufs[i:i + 16]]), float(lr), float(momentum),
+                float(weight_decay))
+        if guard is not None:
+            N.call("clipk_sgd_step_multi_if", *args, float(grad_scale), _p(guard[0]), int(guard[1]), _stream())
+        elif grad_scale == 1.0:
+            N.call("clipk_sgd_step_multi", *args, _stream())
+        else:
+            N.call("clipk_sgd_step_multi_scaled", *args, float(grad_scale), _stream())
 
 
 def cast(x, dtype):

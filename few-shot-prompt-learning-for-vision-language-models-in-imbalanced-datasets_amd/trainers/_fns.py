@@ -69,6 +69,12 @@ class PromptAssembleFn(torch.autograd.Function):
         lay = ctx.lay
         W = ctx.shape[-1]
         if lay.pack is not None:
+            if not ctx.csc and (ctx.B > 1 or ctx.has_bias):
+                # the per-image slot gradients summed into d ctx and d bias in the same launch (no
+                # separate reductions; clipk_ctx_bias_grad_rows)
+                dctx, dbias = ops.ctx_bias_grad_rows(ctx.B, lay.R, W, lay.n_ctx, lay.slot_ptr, lay.slot_rows,
+                                                     dx0.contiguous(), bias=ctx.has_bias)
+                return dctx.view(ctx.shape), dbias, None
             d = ops.ctx_grad_rows(ctx.B, lay.R, W, lay.n_ctx, lay.slot_ptr, lay.slot_rows, dx0.contiguous())
         else:
             d = ops.ctx_grad(ctx.B, lay.n_cls, lay.L, W, lay.n_ctx, ctx.csc, lay.ctx_pos, dx0.contiguous())
@@ -106,10 +112,16 @@ class CrossEntropyFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, labels, alpha, gamma, focal, reduction="mean"):
         B = logits.shape[0]
+        ctx.reduction = reduction
+        if reduction in ("mean", "sum") and B > 0:
+            # the batch reduction in the loss launch itself (clipk_ce_loss_reduce)
+            loss, ctx.dl = ops.ce_loss_reduce(logits.contiguous(), labels, alpha, gamma, focal,
+                                              grad=logits.requires_grad, reduction=reduction)
+            return loss
         scale = 1.0 / B if reduction == "mean" else 1.0
         row, dl = ops.ce_loss(logits.contiguous(), labels, alpha, gamma, focal, grad=logits.requires_grad,
                               grad_scale=scale)
-        ctx.dl, ctx.reduction = dl, reduction
+        ctx.dl = dl
         if reduction == "mean":
             return row.mean()
         if reduction == "sum":
@@ -118,9 +130,56 @@ class CrossEntropyFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        # 'none': g is [B], each row's gradient scales its own row of d(row loss)/d logits
+        # 'none': g is [B], each row's gradient scales its own row of d(row loss)/d logits. A
+        # scalar loss back-propagated from backward_unit's cached 1.0 (every trainer step) needs
+        # no multiply launch
+        if ctx.reduction != "none" and g.data_ptr() == unit_grad(g.device).data_ptr():
+            return ctx.dl, None, None, None, None, None
         dl = ctx.dl * (g[:, None] if ctx.reduction == "none" else g)
         return dl, None, None, None, None, None
+
+
+_UNIT = {}
+
+
+def unit_grad(device):
+    """The cached scalar 1.0 a trainer step back-propagates from (backward_unit); read-only."""
+    key = str(device)
+    t = _UNIT.get(key)
+    if t is None:
+        t = _UNIT[key] = torch.ones((), device=device)
+    return t
+
+
+def backward_unit(loss):
+    """loss.backward() from the cached unit gradient: no per-step fill launch for the seed, and
+    CrossEntropyFn.backward skips its multiply by it (bitwise loss.backward())."""
+    loss.backward(unit_grad(loss.device))
+
+
+class MetaNetNormFn(torch.autograd.Function):
+    """MetaNetFn on the L2-normalised rows of x (cocoop.py:238 imf / imf.norm(dim=-1) folded into
+    the Meta-Net launch, clipk_meta_net_fwd_norm): returns (y, xn); xn (the normalised features,
+    for the cosine logits) carries no gradient (the image encoder is frozen)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        xn, h, y = ops.meta_net(x.contiguous(), w1.contiguous(), b1.contiguous(), w2.contiguous(), b2.contiguous(),
+                                normalize=True)
+        ctx.save_for_backward(xn, h, w2)
+        ctx.dims = (x.shape[1], w1.shape[0], w2.shape[0])
+        ctx.mark_non_differentiable(xn)
+        ctx.set_materialize_grads(False)  # (no zero-filled gradient launched for xn)
+        return y, xn
+
+    @staticmethod
+    def backward(ctx, dy, dxn):
+        if dy is None:
+            return None, None, None, None, None
+        xn, h, w2 = ctx.saved_tensors
+        V, Hd, Wd = ctx.dims
+        dw1, db1, dw2, db2 = ops.meta_net_bwd(xn, h, w2.contiguous(), dy, V, Hd, Wd)
+        return None, dw1, db1, dw2, db2
 
 
 class MetaNetFn(torch.autograd.Function):

@@ -79,10 +79,16 @@ class ImageFeatureSchedule:
             side = self._side_stream = side_stream(device)
         return side
 
-    def prefetch_image_features(self, image):
+    def prefetch_image_features(self, image, after=None):
+        """after: an event recorded on the main stream once `image` is ready there; the side
+        stream waits for it instead of for everything queued on main so far (a caller may queue
+        the current step's work first and start the prefetch behind it on the host)."""
         main = torch.cuda.current_stream(image.device)
         side = self._side(image.device)
-        side.wait_stream(main)
+        if after is not None:
+            side.wait_event(after)
+        else:
+            side.wait_stream(main)
         with torch.cuda.stream(side):
             imf = self.image_encoder(image)
             done = torch.cuda.Event()

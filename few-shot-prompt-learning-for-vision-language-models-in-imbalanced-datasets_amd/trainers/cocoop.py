@@ -32,7 +32,7 @@ from ..engine.trainer import TrainerX, load_clip
 from ..engine.optim import build_optimizer, build_lr_scheduler
 from ..engine.metrics import LossSummary
 from ..clip.model import TextEncodeFn
-from ._fns import PromptAssembleFn, CosineLogitsFn, MetaNetFn
+from ._fns import PromptAssembleFn, CosineLogitsFn, MetaNetFn, MetaNetNormFn, backward_unit
 from .losses import CrossEntropyLoss, MultiClassFocalLoss, focal_alpha
 from ._vision import ImageFeatureSchedule
 from .prompt_base import init_prompts, grads_finite
@@ -50,6 +50,11 @@ class MetaNet(nn.Module):
     def forward(self, x):
         return MetaNetFn.apply(x, self.linear1.weight, self.linear1.bias, self.linear2.weight,
                                self.linear2.bias)
+
+    def forward_normalized(self, x):
+        """(meta_net(x / |x|), x / |x|) in one launch (MetaNetNormFn)."""
+        return MetaNetNormFn.apply(x, self.linear1.weight, self.linear1.bias, self.linear2.weight,
+                                   self.linear2.bias)
 
 
 class PromptLearner(nn.Module):
@@ -72,6 +77,12 @@ class PromptLearner(nn.Module):
         """im_features [B, V] (L2-normalised) -> x0 [B*C*L, W] with ctx + meta_net(imf_b)."""
         bias = self.meta_net(im_features)
         return PromptAssembleFn.apply(self.ctx, bias, self.layout)
+
+    def assemble_raw(self, im_features):
+        """im_features [B, V] as the image encoder returns them -> (x0, imf / |imf|): the
+        normalisation of cocoop.py:238 inside the Meta-Net launch."""
+        bias, imf_n = self.meta_net.forward_normalized(im_features)
+        return PromptAssembleFn.apply(self.ctx, bias, self.layout), imf_n
 
     def construct_prompts(self, ctx, prefix, suffix, label=None):
         if label is not None:
@@ -129,10 +140,11 @@ class CustomCLIP(ImageFeatureSchedule, nn.Module):
             print(">> Use Cross Entropy Loss!")
             self.criterion = CrossEntropyLoss()
 
-    def logits_for(self, imf_n):
+    def logits_for(self, imf):
+        """imf: the raw image features (normalised with the Meta-Net, assemble_raw)."""
         pl = self.prompt_learner
-        B = imf_n.shape[0]
-        x0 = pl.assemble(imf_n)
+        B = imf.shape[0]
+        x0, imf_n = pl.assemble_raw(imf)
         txt = TextEncodeFn.apply(x0, self.text_core, pl.layout.shape(B))
         logits = CosineLogitsFn.apply(imf_n, txt, self.logit_scale_value, 1, pl.layout.n_cls)
         if self.class_counts is not None:
@@ -146,7 +158,7 @@ class CustomCLIP(ImageFeatureSchedule, nn.Module):
             # eval: the next test batch's image encoder beside this batch's text encoder (the test
             # loop names it, TrainerX.test)
             self.prefetch_image_features(nxt)
-        imf = imf / imf.norm(dim=-1, keepdim=True)
+        # imf / imf.norm(dim=-1, keepdim=True) (cocoop.py:238) happens in logits_for's Meta-Net launch
         pl = self.prompt_learner
         chunk = max(1, self.max_rows // self._rows_per_img)
         if imf.shape[0] <= chunk:
@@ -196,31 +208,106 @@ class CoCoOp(TrainerX):
         self.register_model("prompt_learner", self.model.prompt_learner, self.optim, self.sched)
 
     def forward_backward(self, batch):
-        """cocoop.py:313-338 (multi-GPU weighting and the amp skip test as CoOp's)."""
+        """cocoop.py:313-338 (multi-GPU weighting and the amp skip test as CoOp's).
+        PREC fp32s, one process: the text backward's overflow flag (a retry at a lower gradient
+        scale, TextEncoderCore.backward) is not waited for inside the step. The SGD launch skips
+        itself on the device when the flag is set, and the flag of step i is read in step i + 1
+        once its forward is queued (the GPU is busy meanwhile): an overflowed step i is then re-run
+        at the lower scale and step i + 1's forward again -- the same updates as the waiting form
+        (0.6 ms/step of host synchronisation at B = 8, 0.3 at B = 1: tools/lab/step_parts.py)."""
         image, label = self.parse_batch_train(batch)
         nb, self.next_batch = getattr(self, "next_batch", None), None
+        nxt = ready = None
         if nb is not None and image.is_cuda and self.cfg.get("NATIVE", {}).get("PREFETCH_VISION", False):
-            # the next step's image features on a side stream for the whole of this step
-            # (run_epoch / bench set next_batch to the batch the loop will pass next;
-            # trainers/_vision.py)
-            self.model.prefetch_image_features(self.parse_batch_train(nb)[0])
+            # the next step's image features on a side stream beside this step (run_epoch /
+            # bench set next_batch to the batch the loop will pass next; trainers/_vision.py),
+            # from this point of the main stream on
+            nxt = self.parse_batch_train(nb)[0]
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream(image.device))
+        defer = self._deferred_status()
         loss = self.model(image, label)
+        if nxt is not None:
+            # issued after this step's forward, so that the host queues the main stream's work
+            # first after a synchronisation
+            self.model.prefetch_image_features(nxt, after=ready)
+        if self._settle_pending():
+            loss = self.model(image, label)  # the re-run step before changed the prompts
+        return self._finish_step(batch, image, loss, defer)
+
+    def _finish_step(self, batch, image, loss, defer, redo=False):
+        """Backward, gradient all-reduce, SGD and the LR update of forward_backward; defer: the
+        split status whose check is left to the next step (None: checked in the backward)."""
         self.optim.zero_grad()
         if self.class_sharded:  # full loss on every rank, partial gradients: summed
-            loss.backward()
+            backward_unit(loss)
             dist.allreduce_grads([p for p in self.model.prompt_learner.parameters() if p.requires_grad],
                                  average=False)
         else:
             w = self.batch_weight(batch, image.shape[0])
-            (loss * w if w != 1.0 else loss).backward()
+            if w != 1.0:
+                (loss * w).backward()
+            else:
+                backward_unit(loss)  # loss.backward() without the seed fill / multiply launches
             self.allreduce_grads(self.model.prompt_learner)
+        lrs = [g["lr"] for g in self.optim.param_groups]
         if self.cfg.TRAINER.COCOOP.PREC != "amp" or grads_finite(self.model.prompt_learner):
-            self.optim.step()
+            if defer is not None:
+                self.optim.step(guard=(defer.flags, 2))  # skipped on the device after an overflow
+                self._pending = (defer.take_async(), batch, lrs, getattr(self.optim, "created_last", []))
+            else:
+                self.optim.step()
         loss_summary = LossSummary()
         loss_summary["loss"] = loss
-        if (self.batch_idx + 1) == self.num_batches:
+        if not redo and (self.batch_idx + 1) == self.num_batches:
             self.update_lr()
         return loss_summary
+
+    def _deferred_status(self):
+        """The text encoder's split status when its check may be deferred (PREC fp32s, one
+        process, NATIVE.DEFER_SPLIT_CHECK), else None (the backward checks it itself)."""
+        core = self.model.text_core
+        st = getattr(core, "_status", None)
+        on = (st is not None and not dist.is_dist() and self.cfg.get("NATIVE", {}).get("DEFER_SPLIT_CHECK", True)
+              and hasattr(self.optim, "created_last"))
+        core.defer_check = bool(on)
+        return st if on else None
+
+    def _settle_pending(self):
+        """Read the previous step's deferred overflow flag (waits for that step only). On an
+        overflow -- its SGD was skipped on the device -- re-run that step with the check in the
+        backward (lower-scale retry), at its own LR. Returns whether a step was re-run."""
+        pend, self._pending = getattr(self, "_pending", None), None
+        if pend is None:
+            return False
+        handle, batch, lrs, created = pend
+        if not handle.result() & 2:
+            return False
+        torch.cuda.synchronize()
+        for p in created:  # momentum buffers the skipped step created: never written
+            self.optim.state.pop(p, None)
+        now = [g["lr"] for g in self.optim.param_groups]
+        core = self.model.text_core
+        was = core.defer_check
+        try:
+            for g, lr in zip(self.optim.param_groups, lrs):
+                g["lr"] = lr
+            core.defer_check = False
+            image, label = self.parse_batch_train(batch)
+            self._finish_step(batch, image, self.model(image, label), None, redo=True)
+        finally:
+            for g, lr in zip(self.optim.param_groups, now):
+                g["lr"] = lr
+            core.defer_check = was  # (this step's own backward defers again)
+        type(self).deferred_redos += 1
+        return True
+
+    deferred_redos = 0  # steps re-run after a deferred overflow check, all instances
+
+    def flush_deferred(self):
+        """Settle the last step's deferred check (end of an epoch, before a test or a save)."""
+        with torch.enable_grad():  # (test() runs under no_grad; a re-run step needs autograd)
+            self._settle_pending()
 
     def parse_batch_train(self, batch):
         return batch["img"].to(self.device), batch["label"].to(self.device)

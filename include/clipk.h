@@ -299,6 +299,20 @@ int clipk_attention_prefix_bwd(int dtype, int grad_dtype, int G, int P, int R, i
                                const float* lse, void* dqkv, int lddqkv, void* ws, size_t ws_bytes,
                                void* stream);
 
+/* The same with flags: CLIPK_PREFIX_CLS_GROUP0 -- every group's class rows read their q|k|v from
+ * group 0's rows (the text encoder's layer 0, where the class rows enter every group with the
+ * same values: clipk_encoder_set_input_rows; rows [P, R) of groups >= 1 of qkv are then never
+ * read, so no copies of group 0's are written). Prefix rows, outputs, dout, lse per group. */
+enum { CLIPK_PREFIX_CLS_GROUP0 = 1 };
+int clipk_attention_prefix_fwd_ex(int dtype, int G, int P, int R, int ntiles, const int* tiles,
+                                  const int* row_first, int heads, const void* qkv, int ldqkv, void* out,
+                                  int ldo, float* lse, int flags, void* stream);
+int clipk_attention_prefix_bwd_ex(int dtype, int grad_dtype, int G, int P, int R, int ntiles,
+                                  const int* tiles, const int* row_first, int heads, const void* qkv,
+                                  int ldqkv, const void* ofwd, int ldof, const void* dout, int lddo,
+                                  const float* lse, void* dqkv, int lddqkv, void* ws, size_t ws_bytes,
+                                  int flags, void* stream);
+
 /* Patch extraction: img fp32 [B,3,R,R] -> out [B*G*G, Kp] (out_dtype), K index c*p*p+ky*p+kx,
  * zero padded to Kp >= 3*p*p. */
 int clipk_im2col(int out_dtype, int B, int res, int patch, int Kp, const float* img, void* out,
@@ -333,6 +347,13 @@ int clipk_prompt_assemble_rows(int G, int R, int C, int L, int W, const int* row
 int clipk_ctx_grad_rows(int G, int R, int W, int n_ctx, const int* slot_ptr, const int* slot_rows,
                         const float* dx0, float* dctx, void* stream);
 
+/* CoCoOp's two prompt-parameter gradients of packed prompts in one launch (PromptAssembleFn
+ * backward, cocoop.py:189-197 ctx_shifted = ctx + bias): with d(g, k) = the clipk_ctx_grad_rows
+ * sum of slot k's rows of group g, dctx[k*W + w] = sum_g d(g, k)[w] (g order) and, when dbias is
+ * given, dbias[g*W + w] = sum_k d(g, k)[w] (k order). Replaces the per-(g, k) output + two sums. */
+int clipk_ctx_bias_grad_rows(int G, int R, int W, int n_ctx, const int* slot_ptr, const int* slot_rows,
+                             const float* dx0, float* dctx, float* dbias, void* stream);
+
 /* logits[b,c] = scale * <imf[b], txt[row]> / |txt[row]| / |imf[b]|,
  * row = per_image ? b*C + c : c.  tnorm[row] (optional out) = |txt[row]|. */
 int clipk_cosine_logits_fwd(int B, int C, int E, int per_image, float scale, const float* imf,
@@ -349,12 +370,24 @@ int clipk_ce_loss(int B, int C, const float* logits, const int64_t* labels, cons
                   float gamma, int focal, float grad_scale, float* row_loss, float* dlogits,
                   void* stream);
 
+/* clipk_ce_loss with the batch reduction in the same launch (one block): reduction 1 = mean,
+ * 2 = sum of the row losses (summed in row order), into loss[0]; row_loss [B] is still written.
+ * Replaces the separate mean / sum launch after clipk_ce_loss (coop.py:158-163 reductions). */
+int clipk_ce_loss_reduce(int B, int C, const float* logits, const int64_t* labels, const float* alpha,
+                         float gamma, int focal, float grad_scale, int reduction, float* row_loss,
+                         float* loss, float* dlogits, void* stream);
+
 /* CoCoOp Meta-Net: h = relu(x W1^T + b1); y = h W2^T + b2. x [B,V], W1 [Hd,V], W2 [Wd,Hd].
  * The CLIP widths (V % 256 == 0, V <= 1024, Hd <= 64, x / W1 16-B aligned) take the
  * many-block form; other shapes one block per image. */
 int clipk_meta_net_fwd(int B, int V, int Hd, int Wd, const float* x, const float* w1,
                        const float* b1, const float* w2, const float* b2, float* h, float* y,
                        void* stream);
+/* clipk_meta_net_fwd on the L2-normalised rows of x: xn [B,V] = x / |x| (written; cocoop.py:238
+ * imf / imf.norm(dim=-1)), then the Meta-Net on xn -- the normalisation's two launches folded in. */
+int clipk_meta_net_fwd_norm(int B, int V, int Hd, int Wd, const float* x, const float* w1,
+                            const float* b1, const float* w2, const float* b2, float* xn, float* h,
+                            float* y, void* stream);
 /* grads of W1,b1,W2,b2 from dy (x has no grad). dh_ws: caller scratch of B*Hd floats. */
 int clipk_meta_net_bwd(int B, int V, int Hd, int Wd, const float* x, const float* h,
                        const float* w2, const float* dy, float* dw1, float* db1, float* dw2,
@@ -368,6 +401,22 @@ int clipk_sgd_step(long n, float* p, const float* g, float* buf, float lr, float
 int clipk_sgd_step_multi(int count, float* const* p, const float* const* g, float* const* buf,
                          const long* n, const int* has_buf, float lr, float momentum,
                          float weight_decay, void* stream);
+
+/* clipk_sgd_step_multi on grad_scale * g (e.g. 1 / world after a SUM all-reduce: the average
+ * folded into the update instead of a division launch; 1.0 is bitwise clipk_sgd_step_multi). */
+int clipk_sgd_step_multi_scaled(int count, float* const* p, const float* const* g, float* const* buf,
+                                const long* n, const int* has_buf, float lr, float momentum,
+                                float weight_decay, float grad_scale, void* stream);
+/* clipk_sgd_step_multi_scaled skipped entirely (p, buf untouched) when guard[0] & mask != 0, read on
+ * the device: the PREC fp32s trainer queues the step without waiting for its backward's overflow
+ * flag (clipk_encoder_set_status bit 2) and re-runs an overflowed step later. */
+int clipk_sgd_step_multi_if(int count, float* const* p, const float* const* g, float* const* buf,
+                            const long* n, const int* has_buf, float lr, float momentum,
+                            float weight_decay, float grad_scale, const int* guard, int mask, void* stream);
+/* Status word hand-off (PREC fp32s overflow flags, clipk_encoder_set_status): host_word[0] =
+ * flags[0], then flags[0] = 0, in one stream-ordered launch; host_word is host-visible memory
+ * (pinned). The caller synchronises the stream (or an event after it) before reading it. */
+int clipk_status_take(int* flags, int* host_word, void* stream);
 
 /* Row gather / scatter: dst row (dst_rows ? dst_rows[i] : i) = src row (src_rows ? src_rows[i] : i)
  * for i < n; rows of row_bytes (multiple of 16) bytes, 16-B aligned. The text encoder's last

@@ -335,6 +335,68 @@ def test_meta_net_and_sgd(dev, B, V, Wd):
         ops.sgd_step_multi(pb, gs, bb, 0.002, 0.9, 5e-4, [step > 0] * len(sizes))
     for t1, t2, m1, m2 in zip(pa, pb, ba, bb):
         assert torch.equal(t1, t2) and torch.equal(m1, m2)
+    # the gradient scale of a SUM all-reduce folded into the update (clipk_sgd_step_multi_scaled):
+    # bitwise the update on the pre-scaled gradients for a power-of-two scale
+    pc, bc = [t.clone() for t in ps], [torch.zeros_like(t) for t in ps]
+    pd, bd = [t.clone() for t in ps], [torch.zeros_like(t) for t in ps]
+    for step in range(3):
+        ops.sgd_step_multi(pc, [gt * 0.125 for gt in gs], bc, 0.002, 0.9, 5e-4, [step > 0] * len(sizes))
+        ops.sgd_step_multi(pd, gs, bd, 0.002, 0.9, 5e-4, [step > 0] * len(sizes), grad_scale=0.125)
+    for t1, t2, m1, m2 in zip(pc, pd, bc, bd):
+        assert torch.equal(t1, t2) and torch.equal(m1, m2)
+
+
+@pytest.mark.parametrize("B,V,Wd", [(4, 512, 512), (8, 512, 512), (1, 768, 768), (2, 96, 80)])
+def test_meta_net_fwd_norm(dev, B, V, Wd):
+    """clipk_meta_net_fwd_norm: xn = x / |x| (cocoop.py:238) and the Meta-Net on it in one launch,
+    against torch's imf / imf.norm() and the un-normalised entry point on that."""
+    g = torch.Generator().manual_seed(5)
+    Hd = V // 16
+    x = (torch.randn(B, V, generator=g) * 3).to(dev)
+    w1 = (torch.randn(Hd, V, generator=g) * 0.05).to(dev)
+    b1 = (torch.randn(Hd, generator=g) * 0.05).to(dev)
+    w2 = (torch.randn(Wd, Hd, generator=g) * 0.1).to(dev)
+    b2 = (torch.randn(Wd, generator=g) * 0.05).to(dev)
+    xn, h, y = ops.meta_net(x, w1, b1, w2, b2, normalize=True)
+    ref = x / x.norm(dim=-1, keepdim=True)
+    torch.testing.assert_close(xn, ref, rtol=2e-6, atol=1e-7)
+    h2, y2 = ops.meta_net(ref, w1, b1, w2, b2)
+    torch.testing.assert_close(y, y2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(h, h2, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,C", [(8, 1000), (1, 1000), (13, 37)])
+@pytest.mark.parametrize("reduction", ["mean", "sum"])
+def test_ce_loss_reduce(dev, B, C, reduction):
+    """clipk_ce_loss_reduce: the batch reduction in the loss launch -- dlogits bitwise the
+    per-row kernel's, the loss = the row-order sum (/ B) of its row losses."""
+    g = torch.Generator().manual_seed(B + C)
+    logits = (torch.randn(B, C, generator=g) * 4).to(dev)
+    y = torch.randint(0, C, (B,), generator=g).to(dev)
+    alpha = (torch.rand(C, generator=g) + 0.5).to(dev)
+    for focal in (False, True):
+        a = alpha if focal else None
+        scale = 1.0 / B if reduction == "mean" else 1.0
+        row, dl = ops.ce_loss(logits, y, a, 2.0, focal, grad_scale=scale)
+        loss, dl2 = ops.ce_loss_reduce(logits, y, a, 2.0, focal, reduction=reduction)
+        assert torch.equal(dl, dl2)
+        s = row[0].clone()
+        for b in range(1, B):
+            s = s + row[b]
+        ref = s * (1.0 / B) if reduction == "mean" else s
+        assert torch.equal(loss, ref), (loss.item(), ref.item())
+
+
+def test_status_take(dev):
+    """clipk_status_take: the flags reach the pinned host word and are cleared, stream-ordered."""
+    flags = torch.tensor([6], dtype=torch.int32, device=dev)
+    host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+    ops.status_take(flags, host)
+    torch.cuda.synchronize()
+    assert int(host[0]) == 6 and int(flags.item()) == 0
+    ops.status_take(flags, host)
+    torch.cuda.synchronize()
+    assert int(host[0]) == 0
 
 
 @pytest.mark.parametrize("cfg", [0, 1, 2, 3, 6])
@@ -677,6 +739,32 @@ def test_attention_prefix_fwd_bwd(dev, dtype, gdtype, G, C, P, H, max_q):
         close(dq[:, sl], ref[:, sl], gdtype if dtype != torch.float32 else dtype, f"prefix attn {part}")
 
 
+@pytest.mark.parametrize("dtype,gdtype", [(torch.float16, torch.float16), (torch.bfloat16, torch.bfloat16),
+                                          (torch.float32, torch.float32)])
+@pytest.mark.parametrize("G,C,P,H,max_q", [(3, 37, 5, 8, 6), (2, 19, 16, 2, 7), (24, 300, 5, 8, 7)])
+def test_attention_prefix_cls_group0(dev, dtype, gdtype, G, C, P, H, max_q):
+    """CLIPK_PREFIX_CLS_GROUP0 (the text encoder's shared layer 0): with every group's class rows
+    of q|k|v read from group 0, forward and backward are bitwise the plain calls on a qkv whose
+    class rows were copied into every group -- here the other groups' class rows hold NaN, so a
+    read of them would show."""
+    R, tiles, row_first, off, qlen, g = prefix_case(G, C, P, H, max_q, seed=G * 100 + C + P + 7)
+    W = H * 64
+    qkv = torch.randn(G * R, 3 * W, generator=g).to(dev).to(dtype)
+    for gg in range(1, G):
+        qkv[gg * R + P:(gg + 1) * R] = qkv[P:R]
+    hole = qkv.clone()
+    for gg in range(1, G):
+        hole[gg * R + P:(gg + 1) * R] = float("nan")
+    tiles, row_first = tiles.to(dev), row_first.to(dev)
+    o, lse = ops.attention_prefix(qkv, G, P, R, tiles, row_first, H, lse=True)
+    o2, lse2 = ops.attention_prefix(hole, G, P, R, tiles, row_first, H, lse=True, flags=N.PREFIX_CLS_GROUP0)
+    assert torch.equal(o, o2) and torch.equal(lse, lse2)
+    dout = torch.randn(G * R, W, generator=g).to(dev).to(gdtype)
+    d1 = ops.attention_prefix_bwd(qkv, o, dout, lse, G, P, R, tiles, row_first, H, gdtype)
+    d2 = ops.attention_prefix_bwd(hole, o, dout, lse, G, P, R, tiles, row_first, H, gdtype, flags=N.PREFIX_CLS_GROUP0)
+    assert torch.equal(d1, d2)
+
+
 @pytest.mark.parametrize("knobs", [
     {"CLIPK_PREFIX_LDS": "0"},
     {"CLIPK_PREFIX_LDS": "3", "CLIPK_PREFIX_LDS_WPB": "1"},
@@ -733,3 +821,14 @@ def test_prompt_rows_and_ctx_grad_rows(dev):
     d = d.view(G, n_ctx, W)
     torch.testing.assert_close(d.sum(0), ctx_r.grad, rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(d.sum(1), bias_r.grad, rtol=1e-5, atol=1e-4)
+    # the same two sums in one launch (clipk_ctx_bias_grad_rows): d ctx in g order, d bias in k order
+    dctx, dbias = ops.ctx_bias_grad_rows(G, R, W, n_ctx, t(pk["slot_ptr"]), t(pk["slot_rows"]), dx)
+    sg = d[0].clone()
+    for gg in range(1, G):
+        sg = sg + d[gg]
+    sk = d[:, 0].clone()
+    for k in range(1, n_ctx):
+        sk = sk + d[:, k]
+    assert torch.equal(dctx, sg) and torch.equal(dbias, sk)
+    dctx2, none = ops.ctx_bias_grad_rows(G, R, W, n_ctx, t(pk["slot_ptr"]), t(pk["slot_rows"]), dx, bias=False)
+    assert none is None and torch.equal(dctx2, dctx)

@@ -27,7 +27,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "golden"))
 
 
-def _setup(trainer, outdir, dev, batches_on_dev=True, cocoop_shard="image"):
+def _setup(trainer, outdir, dev, batches_on_dev=True, cocoop_shard="image", prec=None, native=None):
     import make_golden_trainer as MT
     from fsp_amd.clip import synth
     from fsp_amd.engine.registry import TRAINER_REGISTRY
@@ -35,6 +35,10 @@ def _setup(trainer, outdir, dev, batches_on_dev=True, cocoop_shard="image"):
     cfg = MT.make_cfg(trainer, str(outdir))
     cfg.TEST.NO_TEST = True
     cfg.NATIVE.COCOOP_SHARD = cocoop_shard
+    if prec is not None:
+        getattr(cfg.TRAINER, trainer.upper()).PREC = prec
+    for k, v in (native or {}).items():
+        cfg.NATIVE[k] = v
     names = synth.synthetic_classnames(MT.N_CLS)
     train, test = MT.batches()
     mv = (lambda b: {k: v.to(dev) for k, v in b.items()}) if batches_on_dev else (lambda b: b)
@@ -111,6 +115,54 @@ def test_trainer_matches_reference(dev, tmp_path, trainer):
     assert isinstance(acc, float)
     if ok.all():
         assert acc == meta["test_acc"]
+
+
+def _fp32s_run(dev, outdir, defer, target=None, monkeypatch=None):
+    from fsp_amd.clip.model import TextEncoderCore
+    meta, ref = load_fixture("trainer_cocoop")
+    if target is not None:
+        monkeypatch.setattr(TextEncoderCore, "SPLIT_TARGET", target)
+    tr, _ = _setup("CoCoOp", outdir, dev, prec="fp32s", native={"DEFER_SPLIT_CHECK": defer})
+    _init_like_fixture(tr, "CoCoOp", ref)
+    losses = []
+    fb = tr.forward_backward
+    tr.forward_backward = lambda b: losses.append(float(fb(b)["loss"])) or {}
+    tr.max_epoch = meta["epochs"]
+    for tr.epoch in range(meta["epochs"]):
+        tr.run_epoch()
+        tr.after_epoch()
+    pl = tr.model.prompt_learner
+    params = {k: p.detach().cpu().clone() for k, p in pl.named_parameters()}
+    bufs = [tr.optim.state[p]["momentum_buffer"].detach().cpu().clone() for p in pl.parameters()]
+    return losses, params, bufs, tr.get_current_lr()
+
+
+def test_cocoop_fp32s_deferred_check(dev, tmp_path, monkeypatch):
+    """PREC fp32s CoCoOp with the text backward's overflow check deferred to the next step
+    (CoCoOp.forward_backward: the SGD launch guarded on the device, the flag read once the next
+    forward is queued) trains exactly as with the check inside the backward -- bitwise losses,
+    prompts, momentum buffers and LR over 2 epochs -- and, with every step forced to overflow
+    (scale target 2^20), each skipped step is re-run (at the next step, or by the epoch-end
+    flush) to the same bits as the in-backward retry."""
+    from fsp_amd.trainers.cocoop import CoCoOp
+    from fsp_amd.clip.model import TextEncoderCore
+    a = _fp32s_run(dev, tmp_path / "a", False)
+    b = _fp32s_run(dev, tmp_path / "b", True)
+    for x, y in ((a[0], b[0]), (a[3], b[3])):
+        assert x == y
+    for k in a[1]:
+        assert torch.equal(a[1][k], b[1][k]), k
+    assert all(torch.equal(x, y) for x, y in zip(a[2], b[2]))
+    r0, d0 = TextEncoderCore.split_retries, CoCoOp.deferred_redos
+    c = _fp32s_run(dev, tmp_path / "c", False, 20, monkeypatch)
+    n_steps = len(c[0])
+    assert TextEncoderCore.split_retries == r0 + n_steps
+    d = _fp32s_run(dev, tmp_path / "d", True, 20, monkeypatch)
+    assert CoCoOp.deferred_redos == d0 + n_steps
+    assert c[0] == d[0] and c[3] == d[3]
+    for k in c[1]:
+        assert torch.equal(c[1][k], d[1][k]), k
+    assert all(torch.equal(x, y) for x, y in zip(c[2], d[2]))
 
 
 @pytest.mark.parametrize("trainer", ["CoOp", "CoCoOp"])
