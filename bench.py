@@ -436,7 +436,10 @@ def time_eval(trainer, dm, n_images):
 
 # |d logit| of each PREC against the reference's own golden logits at the headline shape
 # (tests/test_parity_gpu.py test_headline_batch8_vs_golden, tests/golden/cocoop_vitb16_c1000_b8.npz)
-LOGIT_ERR = {"fp32s": "2.7e-5", "fp32": "2.7e-5", "fp16": "0.026 (outside the north star's 1e-3)"}
+# (fp32s on the benched fp16-valued weights: test_headline_batch8_w16_vs_golden, cocoop_vitb16_c1000_b8_w16.npz;
+# profiles/r06h/t_headline_reports.txt)
+LOGIT_ERR = {"fp32s": "2.3e-5 (fp16-valued weights, as benched; 2.7e-5 on fp32-valued ones)", "fp32": "2.9e-5",
+             "fp16": "0.024 (outside the north star's 1e-3)"}
 
 
 def peak_key(prec, trainer):

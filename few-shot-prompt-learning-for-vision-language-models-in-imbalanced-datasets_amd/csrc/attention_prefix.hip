@@ -810,7 +810,10 @@ __device__ __forceinline__ void f32_unit(const int* __restrict__ tiles, const in
 }
 
 // block (g, h, chunk block kb): waves take chunks kb * WPB + w; stages the prefix K / V rows
-// of (g, h) (P <= 16 rows x 64 fp32) into sKp / sVp
+// of (g, h) (P <= 16 rows x 64 fp32) into sKp / sVp. These sit in DYNAMIC LDS sized to P rows
+// (2 x P x 256 B, f32_prefix_lds): at the CoCoOp P of 5 a block takes 2.5 KiB for them instead of
+// 8, which lets 5 backward blocks (10 waves) and 8 forward blocks (16 waves) share a CU instead
+// of 4 and 6 (LDS was the occupancy limit: 34 / 24 KiB per 2-wave block)
 template <int WPB>
 __device__ __forceinline__ void f32_block(int H, int nchunk, int& g, int& h, int& k, int& w) {
   const int nkb = (nchunk + WPB - 1) / WPB;
@@ -824,25 +827,23 @@ __device__ __forceinline__ void f32_block(int H, int nchunk, int& g, int& h, int
 template <int WPB>
 __device__ __forceinline__ void f32_stage_prefix(const float* __restrict__ qkv, size_t row0, int P, int ldq, int col,
                                                  int W, float* sKp, float* sVp) {
-  for (int i = threadIdx.x; i < 16 * 16; i += WPB * 64) {  // 16 rows x 16 float4
+  for (int i = threadIdx.x; i < P * 16; i += WPB * 64) {  // P rows x 16 float4
     const int j = i >> 4, c = i & 15;
-    f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = kv;
-    if (j < P) {
-      const float* b = qkv + (row0 + j) * ldq + col + 4 * c;
-      kv = *reinterpret_cast<const f32x4*>(b + W);
-      vv = *reinterpret_cast<const f32x4*>(b + 2 * W);
-    }
-    reinterpret_cast<f32x4*>(sKp)[i] = kv;
-    reinterpret_cast<f32x4*>(sVp)[i] = vv;
+    const float* b = qkv + (row0 + j) * ldq + col + 4 * c;
+    reinterpret_cast<f32x4*>(sKp)[i] = *reinterpret_cast<const f32x4*>(b + W);
+    reinterpret_cast<f32x4*>(sVp)[i] = *reinterpret_cast<const f32x4*>(b + 2 * W);
   }
 }
+static size_t f32_prefix_lds(int P) { return (size_t)2 * P * 64 * sizeof(float); }
 
 template <int WPB>
 __global__ __launch_bounds__(WPB * 64) void attn_prefix_fwd_f32(
     int G, int P, int R, int ntiles, const int* __restrict__ tiles, const int* __restrict__ row_first, int H,
     int nchunk, int uc, const float* __restrict__ qkv, int ldq, float* __restrict__ out, int ldo,
     float* __restrict__ lse, int cls0) {
-  __shared__ CLIPK_LDS_ALIGN float sKp[16 * 64], sVp[16 * 64];
+  extern __shared__ CLIPK_LDS_ALIGN float sPre[];  // prefix K | V rows, P x 64 each (f32_prefix_lds)
+  float* const sKp = sPre;
+  float* const sVp = sPre + P * 64;
   __shared__ CLIPK_LDS_ALIGN float sK[WPB][16 * 64], sV[WPB][16 * 64];
   int g, h, k, w;
   f32_block<WPB>(H, nchunk, g, h, k, w);
@@ -948,7 +949,9 @@ __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 wav
     int nchunk, int uc, const float* __restrict__ qkv, int ldq, const float* __restrict__ o_fwd, int ldof,
     const float* __restrict__ dout, int lddo, const float* __restrict__ lse, float* __restrict__ dqkv, int lddq,
     float* __restrict__ part, int cls0) {
-  __shared__ CLIPK_LDS_ALIGN float sKp[16 * 64], sVp[16 * 64];
+  extern __shared__ CLIPK_LDS_ALIGN float sPre[];  // prefix K | V rows, P x 64 each (f32_prefix_lds)
+  float* const sKp = sPre;
+  float* const sVp = sPre + P * 64;
   // padded rows (bank-conflict-free stores): K|V then Q|dO rows at stride RS floats; P / dS at
   // stride PS (a column of 16 query rows written by one lane per row hit 2 banks at stride 32)
   constexpr int RS = 68, PS = 33;
@@ -1053,7 +1056,22 @@ __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 wav
       float dk[16], dv[16];
 #pragma unroll
       for (int d = 0; d < 16; ++d) { dk[d] = 0.f; dv[d] = 0.f; }
-      keysum(16 + r, dk, dv);
+      // own key 16 + r and prefix key r in one pass over the unit's queries: each q / dO row is
+      // read from LDS once for both (the same per-accumulator FMA order as two keysum passes)
+      for (int i = 0; i < n; ++i) {
+        const float pv = sp[i * PS + 16 + r], dsv = ss[i * PS + 16 + r];
+        const float pp = sp[i * PS + r], dsp = ss[i * PS + r];
+        float a[16], b[16];
+        ld16x(sa + i * RS + kSl * s, a);
+        ld16x(sb + i * RS + kSl * s, b);
+#pragma unroll
+        for (int d = 0; d < 16; ++d) {
+          dk[d] = fmaf(dsv, a[d], dk[d]);
+          dv[d] = fmaf(pv, b[d], dv[d]);
+          akp[d] = fmaf(dsp, a[d], akp[d]);
+          avp[d] = fmaf(pp, b[d], avp[d]);
+        }
+      }
       if (qok) {
         if constexpr (OS) {
           st16x_split(dqkv + row * lddq + W + h * 64 + kSl * s, dk, s);
@@ -1063,7 +1081,6 @@ __global__ __launch_bounds__(WPB * 64, 2) void attn_prefix_bwd_f32(  // >= 2 wav
           st16x(dqkv + row * lddq + 2 * W + h * 64 + kSl * s, dv);
         }
       }
-      keysum(r, akp, avp);  // prefix key r (zero columns past pre)
     }
     lds_sync();
   }
@@ -1192,8 +1209,8 @@ static int prefix_fwd(int G, int P, int R, int ntiles, const int* tiles, const i
     const int nchunk = n_chunks(ntiles, uc);
     auto go = [&](auto kern, int wpb) {
       const long blocks = (long)G * ((nchunk + wpb - 1) / wpb) * H;
-      hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * wpb), 0, st, G, P, R, ntiles, tiles, row_first, H, nchunk,
-                         uc, (const float*)qkv, ldq, (float*)out, ldo, lse, cls0);
+      hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * wpb), f32_prefix_lds(P), st, G, P, R, ntiles, tiles, row_first,
+                         H, nchunk, uc, (const float*)qkv, ldq, (float*)out, ldo, lse, cls0);
     };
     const int wpb = f32_wpb();
     if (wpb == 2) go(attn_prefix_fwd_f32<2>, 2);
@@ -1248,9 +1265,9 @@ static int prefix_bwd(int G, int P, int R, int ntiles, const int* tiles, const i
     static_assert(mfma || (sizeof(T) == 4 && sizeof(TG) == 4), "fp32 backward");
     auto go = [&](auto kern, int wpb) {
       const long blocks = (long)G * ((nchunk + wpb - 1) / wpb) * H;
-      hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * wpb), 0, st, G, P, R, ntiles, tiles, row_first, H, nchunk,
-                         uc, (const float*)qkv, ldq, (const float*)ofwd, ldof, (const float*)dout, lddo, lse,
-                         (float*)dqkv, lddq, part, cls0);
+      hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * wpb), f32_prefix_lds(P), st, G, P, R, ntiles, tiles, row_first,
+                         H, nchunk, uc, (const float*)qkv, ldq, (const float*)ofwd, ldof, (const float*)dout, lddo,
+                         lse, (float*)dqkv, lddq, part, cls0);
     };
     const int wpb = f32_wpb();
     if (wpb == 2) go(attn_prefix_bwd_f32<2, OS>, 2);
