@@ -527,18 +527,14 @@ class VisionEncoder(nn.Module, _Encoder):
         G = lambda x: _mm_weight(_t(x).float().t(), self.dev, act, split) if with_grad else None
         self.with_grad = with_grad
         table = []
-        # LayerNorm fold of ln_1 / ln_2 for the 16-bit-residual forward (clipk_vit_forward)
-        fold = [] if act != torch.float32 and ln_fold_enabled() else None
+        # LayerNorm fold of ln_1 / ln_2 for the layer-loop forward (clipk_vit_forward: 16-bit
+        # residual stream, or PREC fp32s's fp32 one), built once the split mode is known
+        fparams = [] if (act != torch.float32 or split) and ln_fold_enabled() else None
         for i in range(nl):
             pre = f"visual.transformer.resblocks.{i}."
             q = {k: sd[pre + k] for k in _LAYER_KEYS}
-            if fold is not None:
-                qf = {k: _t(v).float() for k, v in q.items()}
-                f_in = ln_fold_weights(qf["attn.in_proj_weight"], qf["attn.in_proj_bias"], qf["ln_1.weight"],
-                                       qf["ln_1.bias"], act, self.dev)
-                f_fc = ln_fold_weights(qf["mlp.c_fc.weight"], qf["mlp.c_fc.bias"], qf["ln_2.weight"],
-                                       qf["ln_2.bias"], act, self.dev)
-                fold = fold + list(f_in) + list(f_fc) if f_in and f_fc else None
+            if fparams is not None:
+                fparams.append({k: _t(v).float() for k, v in q.items()})
             table += [f32(q["ln_1.weight"]), f32(q["ln_1.bias"]), A(q["attn.in_proj_weight"]),
                       f32(q["attn.in_proj_bias"]), A(q["attn.out_proj.weight"]), f32(q["attn.out_proj.bias"]),
                       f32(q["ln_2.weight"]), f32(q["ln_2.bias"]), A(q["mlp.c_fc.weight"]), f32(q["mlp.c_fc.bias"]),
@@ -562,6 +558,19 @@ class VisionEncoder(nn.Module, _Encoder):
             table, head = compact16(table), compact16(head)
             self.proj_bwd = compact16([self.proj_bwd])[0]
         self._keep = [t for t in table if t is not None] + head
+        fold = None
+        if fparams is not None:
+            ga = self.split_mode == 2  # mode 2: gamma on A, B = W itself (clipk_gemm_ln_gamma)
+            fold = []
+            for qf in fparams:
+                f_in = ln_fold_weights(qf["attn.in_proj_weight"], qf["attn.in_proj_bias"], qf["ln_1.weight"],
+                                       qf["ln_1.bias"], act, self.dev, split, gamma_on_a=ga)
+                f_fc = ln_fold_weights(qf["mlp.c_fc.weight"], qf["mlp.c_fc.bias"], qf["ln_2.weight"],
+                                       qf["ln_2.bias"], act, self.dev, split, gamma_on_a=ga)
+                if not (f_in and f_fc):
+                    fold = None
+                    break
+                fold += list(f_in) + list(f_fc)
         self.width, self.n_tokens = D, (arch.image_resolution // p) ** 2 + 1
         h = ctypes.c_void_p()
         N.check(N.load().clipk_vision_create(D, nl, D // 64, arch.embed_dim, arch.image_resolution, p,

@@ -1318,13 +1318,20 @@ __global__ void cls_rows_kernel(int B, int Lp, int* rows) {
 // gets the LayerNorm fold of ln_1 / ln_2 (when set on the handle) and the last layer's
 // post-attention half on the CLS rows alone (the only rows ln_post reads; exact). ln_pre stays in
 // clipk_vit_embed_ln (fp32 out, cast into the stream by the layer loop).
+// Round 6: PREC fp32s (fp32 stream, split GEMMs) takes the same layer loop -- with the fp32
+// residual stream, the LayerNorm fold (gamma on A in split mode 2) and its pre-split hand-offs,
+// and the last layer's post-attention half on the CLS rows -- instead of block_fwd's LayerNorm
+// passes over every row (knob CLIPK_VIT_LOOP32=0: the block_fwd form)
 static bool vit_res16(const clipk_encoder* e) {
-  static int v = -1;
+  static int v = -1, v32 = -1;
   if (v < 0) {
     const char* s = getenv("CLIPK_VIT_RES16");
     v = s ? atoi(s) : 1;
+    const char* s32 = getenv("CLIPK_VIT_LOOP32");
+    v32 = s32 ? atoi(s32) : 1;
   }
-  return v != 0 && e->act != CLIPK_F32;
+  if (e->act == CLIPK_F32) return v32 != 0 && e->split != 0;
+  return v != 0;
 }
 // parts: patches, pout, x0, cls_rows, sk, rest (the layer loop's workspace); returns the bytes
 static size_t vit16_bytes(const clipk_encoder* e, int B, void* ws, void** parts) {
@@ -1349,6 +1356,7 @@ static int vit16_forward(const clipk_encoder* e, int B, const float* img, float*
   void* p[6];
   const size_t need = vit16_bytes(e, B, ws, p);
   if (ws_bytes < need) return CLIPK_EWORKSPACE;
+  SplitScope split_scope(e);  // (PREC fp32s: the patch embedding's split GEMM, before the layer loop's own scope)
   const int D = e->W, L = e->Limg, np = B * (L - 1), act = e->act;
   const size_t skb = p[4] ? (size_t)((char*)p[5] - (char*)p[4]) : 0;
   TRY(clipk_im2col(act, B, e->res, e->patch, e->Kp, img, p[0], st));
