@@ -95,6 +95,26 @@ bool deep_small() {
 }
 
 static int g_skew = -1;
+int gemm_skew() {
+  if (g_skew < 0) {
+    const char* e = getenv("CLIPK_GEMM_SKEW");
+    g_skew = e ? atoi(e) : 0;
+  }
+  return g_skew;
+}
+// Diagnostic filter (tools/lab/step_stamps.py): stamp only launches of one epilogue id and at
+// least this many rows, so the buffer holds the last such launch of a whole train step
+unsigned long long* gemm_stamp_for(int epi, int M) {
+  static int fe = -2, fm = 0;
+  if (fe == -2) {
+    const char* e = getenv("CLIPK_GEMM_STAMP_EPI");
+    const char* m = getenv("CLIPK_GEMM_STAMP_MINM");
+    fe = e ? atoi(e) : -1;
+    fm = m ? atoi(m) : 0;
+  }
+  if ((fe >= 0 && epi != fe) || M < fm) return nullptr;
+  return gemm_stamp_buf();
+}
 static int g_num_cus = 0;
 int num_cus() {
   if (!g_num_cus) {

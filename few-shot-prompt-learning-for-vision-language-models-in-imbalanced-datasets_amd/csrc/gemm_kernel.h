@@ -1252,6 +1252,9 @@ int num_cus();
 bool deep_small();                      // 4-slot ring for grids of at most one tile per CU
 int pp_grid(int nwg, int cus);          // ping-pong launches: blocks per grid
 unsigned long long* gemm_stamp_buf();   // CLIPK_GEMM_STAMP diagnostic buffer (or null)
+// the same, for this launch only when it passes CLIPK_GEMM_STAMP_EPI / CLIPK_GEMM_STAMP_MINM
+unsigned long long* gemm_stamp_for(int epi, int M);
+int gemm_skew();                        // CLIPK_GEMM_SKEW (us), 0 when unset
 // PREC fp32s launches with pre-split operands (gemm_presplit.hip): spf = the kernel's SPF bits,
 // epi the internal epilogue id, lnm the LayerNorm mode; CLIPK_EINVAL for a combination not built
 int presplit_launch(bool w16, int spf, int epi, int lnm, const GemmArgs& g, hipStream_t st);
@@ -1280,8 +1283,8 @@ static bool try_pp(const GemmArgs& g, int nwg, hipStream_t st) {
 template <int EPI, int LNM = 0, typename TS = f32s, int SPF = 0>
 static int launch_gemm_split(const GemmArgs& g, hipStream_t st) {
   const int cus = num_cus();
-  const_cast<GemmArgs&>(g).stamp = gemm_stamp_buf();
-  const_cast<GemmArgs&>(g).skew = 0;
+  const_cast<GemmArgs&>(g).stamp = gemm_stamp_for(EPI, g.M);
+  const_cast<GemmArgs&>(g).skew = gemm_skew();
   const int cfg = pick_cfg(g.M, g.N, 2);
   if (cfg == 7) {  // small M (the ViT): 64x128 tiles, twice the 128x128 grid
     const int nwg = ((g.M + 63) / 64) * (g.N / 128);
