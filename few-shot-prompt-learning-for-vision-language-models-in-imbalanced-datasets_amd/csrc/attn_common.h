@@ -116,12 +116,7 @@ __device__ __forceinline__ void st16x_split(float* __restrict__ p, const float* 
     const unsigned h0 = __builtin_bit_cast(unsigned, (h2){(_Float16)x[0], (_Float16)x[1]});
     const unsigned h1 = __builtin_bit_cast(unsigned, (h2){(_Float16)x[2], (_Float16)x[3]});
     unsigned l0, l1;
-    asm("v_fma_mixlo_f16 %0, %2, 1.0, -%6 op_sel_hi:[0,0,1]\n\t"
-        "v_fma_mixhi_f16 %0, %3, 1.0, -%6 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
-        "v_fma_mixlo_f16 %1, %4, 1.0, -%7 op_sel_hi:[0,0,1]\n\t"
-        "v_fma_mixhi_f16 %1, %5, 1.0, -%7 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
-        : "=&v"(l0), "=&v"(l1)
-        : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(h0), "v"(h1));
+    split_lo4(x[0], x[1], x[2], x[3], h0, h1, l0, l1);
     const unsigned s0 = odd ? h0 : l0, s1 = odd ? h1 : l1;  // the half the partner stores
     const unsigned y0 = (unsigned)__builtin_amdgcn_mov_dpp((int)s0, 0xB1, 0xF, 0xF, false);
     const unsigned y1 = (unsigned)__builtin_amdgcn_mov_dpp((int)s1, 0xB1, 0xF, 0xF, false);

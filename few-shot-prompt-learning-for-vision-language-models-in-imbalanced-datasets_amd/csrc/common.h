@@ -143,6 +143,21 @@ __device__ __forceinline__ float quick_gelu_grad(float x) {
   return s * fmaf(1.702f * x, 1.0f - s, 1.0f);  // s + 1.702 x s (1 - s)
 }
 
+// The lo parts of a split (hi = fp16(x), lo = fp16(x - hi)) of 4 fp32 values whose hi parts are
+// the fp16 pairs h01 = (x0, x1), h23 = (x2, x3): v_fma_mix forms x - hi exactly in fp32 and
+// rounds once, bitwise (_Float16)(x - (float)hi), in 4 instructions instead of cvt + sub + cvt
+// per value. Consumers must not be MFMA operands without their own wait states (gemm_kernel.h
+// split_lo8 carries them for that case).
+__device__ __forceinline__ void split_lo4(float x0, float x1, float x2, float x3, unsigned h01, unsigned h23,
+                                          unsigned& l01, unsigned& l23) {
+  asm("v_fma_mixlo_f16 %0, %2, 1.0, -%6 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %3, 1.0, -%6 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %1, %4, 1.0, -%7 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %5, 1.0, -%7 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(l01), "=&v"(l23)
+      : "v"(x0), "v"(x1), "v"(x2), "v"(x3), "v"(h01), "v"(h23));
+}
+
 }  // namespace clipk
 
 #define CLIPK_CHECK_LAUNCH()                                  \

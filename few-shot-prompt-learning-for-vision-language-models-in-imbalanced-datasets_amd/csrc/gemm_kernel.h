@@ -194,6 +194,12 @@ __device__ __forceinline__ f32x4 mma_split(u32x4 bh, u32x4 bl, u32x4 ah, u32x4 a
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, bh), __builtin_bit_cast(f16x8, ah), c, 0,
                                                 0, 0);
 }
+// Split-form epilogue stores form the lo parts by v_fma_mix, and the LayerNorm fold carries the
+// weights' scale on the row's rstd (A/B knob: 0 = the convert / subtract form and a multiply per
+// element; bitwise the same outputs)
+#ifndef CLIPK_EPI_MIXSPLIT
+#define CLIPK_EPI_MIXSPLIT 1
+#endif
 constexpr float kSplitAlpha = 1.0f / CLIPK_SPLIT_SCALE;  // the packed weights' scale, undone
 
 // Training's QuickGELU pair with the derivative saved (CLIPK_QGELU_DERIV, include/clipk.h):
@@ -1094,14 +1100,19 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
 #pragma unroll
         for (int c = 0; c < 4; ++c) asm volatile("" : "+v"(x[c]));
         const f16x2 h01 = {(f16)x[0], (f16)x[1]}, h23 = {(f16)x[2], (f16)x[3]};
-        const f16x2 l01 = {(f16)(x[0] - (float)h01[0]), (f16)(x[1] - (float)h01[1])};
-        const f16x2 l23 = {(f16)(x[2] - (float)h23[0]), (f16)(x[3] - (float)h23[1])};
+        const unsigned hu01 = __builtin_bit_cast(unsigned, h01), hu23 = __builtin_bit_cast(unsigned, h23);
+        unsigned l01, l23;  // lo = fp16(x - hi) by v_fma_mix (common.h split_lo4; bitwise the cvt form)
+        if constexpr (CLIPK_EPI_MIXSPLIT) {
+          split_lo4(x[0], x[1], x[2], x[3], hu01, hu23, l01, l23);
+        } else {  // A/B: convert, subtract, convert
+          l01 = __builtin_bit_cast(unsigned, (f16x2){(f16)(x[0] - (float)h01[0]), (f16)(x[1] - (float)h01[1])});
+          l23 = __builtin_bit_cast(unsigned, (f16x2){(f16)(x[2] - (float)h23[0]), (f16)(x[3] - (float)h23[1])});
+        }
         const bool odd = (ec & 1) != 0;
-        const int s0 = __builtin_bit_cast(int, odd ? h01 : l01), s1 = __builtin_bit_cast(int, odd ? h23 : l23);
+        const int s0 = (int)(odd ? hu01 : l01), s1 = (int)(odd ? hu23 : l23);
         const unsigned r0 = (unsigned)__builtin_amdgcn_update_dpp(0, s0, 0xB1, 0xF, 0xF, false);
         const unsigned r1 = (unsigned)__builtin_amdgcn_update_dpp(0, s1, 0xB1, 0xF, 0xF, false);
-        const u32x4 d = odd ? (u32x4){r0, r1, __builtin_bit_cast(unsigned, l01), __builtin_bit_cast(unsigned, l23)}
-                            : (u32x4){__builtin_bit_cast(unsigned, h01), __builtin_bit_cast(unsigned, h23), r0, r1};
+        const u32x4 d = odd ? (u32x4){r0, r1, l01, l23} : (u32x4){hu01, hu23, r0, r1};
         const int offs = ((m - m0) * g.ldo + (ncol & ~7)) * 4 + (odd ? 16 : 0);
         if (keep) __builtin_amdgcn_raw_buffer_store_b128(d, rs, offs, 0, CLIPK_GEMM_SPOL_LN);
         else __builtin_amdgcn_raw_buffer_store_b128(d, rs, offs, 0, CLIPK_GEMM_SPOL_CHAIN);
@@ -1134,9 +1145,11 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
           v[4 * c] = t[0]; v[4 * c + 1] = t[1]; v[4 * c + 2] = t[2]; v[4 * c + 3] = t[3];
         }
         const int off = ((m - m0) * g.ldo + ncol) * (int)sizeof(TO);  // rows >= M: out of range, dropped
-        if constexpr (SPLIT) {
+        // the packed weights' scale undone: exact (a power of 2), so under the LayerNorm fold it
+        // rides on the row's rstd (fma(rs * alpha, v, t) == fma(rs, v * alpha, t) bitwise)
+        if constexpr (SPLIT && (!LN_IN || !CLIPK_EPI_MIXSPLIT)) {
 #pragma unroll
-          for (int c = 0; c < CW; ++c) v[c] *= kSplitAlpha;  // exact (power of 2)
+          for (int c = 0; c < CW; ++c) v[c] *= kSplitAlpha;
         }
         if constexpr (LN_MERGE) {
           // clipk_ln_stats_merge's arithmetic on the row's 8 partials (ln_stats_merge_kernel)
@@ -1153,7 +1166,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] = fmaf(rs, v[c], fmaf(nb, csum[c], bia[c]));
         } else if constexpr (LN_IN) {
-          const float rs = lnp[i & 1][q][0], nb = lnp[i & 1][q][1];
+          const float rs = lnp[i & 1][q][0] * (SPLIT && CLIPK_EPI_MIXSPLIT ? kSplitAlpha : 1.0f), nb = lnp[i & 1][q][1];
 #pragma unroll
           for (int c = 0; c < CW; ++c) v[c] = fmaf(rs, v[c], fmaf(nb, csum[c], bia[c]));
         } else if constexpr (HAS_BIAS) {
