@@ -1,6 +1,6 @@
 """Which main-stream kernels the side-stream ViT slows: K CoCoOp bench steps with the ViT
 prefetch (MODE=vit, the bench step) or with the image encoder replaced by cached features
-(MODE=novit, a diagnostic), meant to run under `rocprofv3 --kernel-trace --stats` once per mode;
+(MODE=novit, a diagnostic) or with the ViT run in line on the main stream (MODE=serial), meant to run under `rocprofv3 --kernel-trace --stats` once per mode;
 compare the per-kernel totals of the two summaries.
     MODE=vit PREC=fp32s python tools/lab/vit_contention.py [steps]"""
 import argparse
@@ -29,6 +29,8 @@ def main():
             def forward(self, x):
                 return feats
         tr.model.image_encoder = Cached()
+        tr.cfg.NATIVE["PREFETCH_VISION"] = False
+    elif mode == "serial":
         tr.cfg.NATIVE["PREFETCH_VISION"] = False
     t, _ = bench.time_train(tr, dm, steps, 3)
     print(f"{prec} {mode}: {1000 * t / steps:.3f} ms/step over {steps} steps", flush=True)
