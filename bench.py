@@ -434,6 +434,35 @@ def time_eval(trainer, dm, n_images):
     return dist.sum_over_ranks(n) / te, n
 
 
+def time_grad_allreduce(params, iters=50, warmup=10):
+    """The step's gradient all-reduce alone (dist.allreduce_grads over the prompt learner's
+    trainable parameters: one flat fp32 bucket, RCCL over xGMI at N > 1), barrier + sync around
+    `iters` calls, max over ranks. Run after the timed region; it sums into the grads."""
+    import torch
+    from fsp_amd import dist
+    ps = [p for p in params if p.requires_grad]
+    for p in ps:
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+    cuda = ps[0].is_cuda
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+        dist.barrier()
+
+    for _ in range(warmup):
+        dist.allreduce_grads(ps, average=False)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dist.allreduce_grads(ps, average=False)
+    sync()
+    t = dist.max_over_ranks(time.perf_counter() - t0)
+    return {"bytes": 4 * sum(p.numel() for p in ps), "us_per_call": round(1e6 * t / iters, 1), "iters": iters,
+            "backend": torch.distributed.get_backend() if dist.is_dist() else None}
+
+
 # |d logit| of each PREC against the reference's own golden logits at the headline shape
 # (tests/test_parity_gpu.py test_headline_batch8_vs_golden, tests/golden/cocoop_vitb16_c1000_b8.npz)
 # (fp32s on the benched fp16-valued weights: test_headline_batch8_w16_vs_golden, cocoop_vitb16_c1000_b8_w16.npz;
@@ -618,6 +647,8 @@ def main():
     }
     if args.prec == "fp32s":
         out["split_mode"] = {"text": trainer.model.text_core.split_mode, "vision": trainer.model.image_encoder.split_mode}
+    if world > 1:  # the step's gradient all-reduce measured on its own (part of ms_per_step above)
+        out["grad_allreduce"] = time_grad_allreduce(list(trainer.model.prompt_learner.parameters()))
     del trainer, dm
     torch.cuda.empty_cache()
     if not args.no_extra and world > 1:

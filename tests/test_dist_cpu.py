@@ -74,6 +74,26 @@ def test_collectives_gloo_ws2():
     assert out[0]["shard"] == (0, 5) and out[1]["shard"] == (5, 10)
 
 
+def _grad_allreduce_timer(rank, world):
+    import bench
+    p1 = torch.nn.Parameter(torch.ones(3, 4))
+    p2 = torch.nn.Parameter(torch.ones(5))
+    frozen = torch.nn.Parameter(torch.ones(2), requires_grad=False)
+    r = bench.time_grad_allreduce([p1, p2, frozen], iters=3, warmup=1)
+    return r, p1.grad.clone().numpy()
+
+
+def test_bench_grad_allreduce_timer_gloo_ws2():
+    """bench.py's N > 1 field grad_allreduce: the trainable parameters' bytes, a positive time
+    equal on every rank (max over ranks), the collective really summing (zeros in, zeros out)."""
+    out = _run(_grad_allreduce_timer)
+    for rk in (0, 1):
+        r, g = out[rk]
+        assert r["bytes"] == 4 * 17 and r["iters"] == 3 and r["backend"] == "gloo" and r["us_per_call"] > 0
+        np.testing.assert_array_equal(g, np.zeros((3, 4)))
+    assert out[0][0]["us_per_call"] == out[1][0]["us_per_call"]
+
+
 def _bucket_steps(rank, world):
     """Three steps through one persistent gradient bucket: fresh grads (zero_grad to None), then
     grads accumulated in place into the bucket's views (zero_grad(set_to_none=False))."""

@@ -60,6 +60,9 @@ def suite():
     dist.broadcast_params([p])
     out["bcast_params"] = p.detach().cpu().tolist()
     out["varlen"] = dist.all_gather_varlen(x[:3]).cpu().tolist()
+    import bench  # its N > 1 grad_allreduce field, through this backend
+    r = bench.time_grad_allreduce([torch.nn.Parameter(torch.zeros(7, device=dev))], iters=3, warmup=1)
+    out["ar_timer"] = [r["bytes"], r["iters"], r["us_per_call"] > 0]
     dist.barrier()
     torch.cuda.synchronize()
     return out
@@ -97,3 +100,4 @@ def test_rccl_branches_one_rank_match_gloo():
     np.testing.assert_array_equal(np.asarray(nc["gcc_bwd"]), np.full((4, 5), 3.0))
     assert nc["bcast_int"] == 41 and nc["max"] == 2.5 and nc["sum"] == 1.5
     assert nc["allreduce"] == [4.0, 4.0, 4.0]
+    assert nc["ar_timer"] == [28, 3, True]
