@@ -2,7 +2,7 @@
 prefetch (MODE=vit, the bench step) or with the image encoder replaced by cached features
 (MODE=novit, a diagnostic) or with the ViT run in line on the main stream (MODE=serial), meant to run under `rocprofv3 --kernel-trace --stats` once per mode;
 compare the per-kernel totals of the two summaries.
-    MODE=vit PREC=fp32s python tools/lab/vit_contention.py [steps]"""
+    MODE=vit PREC=fp32s [BATCH=8] python tools/lab/vit_contention.py [steps]"""
 import argparse
 import os
 import sys
@@ -19,7 +19,8 @@ def main():
     mode = os.environ.get("MODE", "vit")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    tr, dm = bench.build_trainer(argparse.Namespace(arch="ViT-B/16", classes=1000), prec, 8, dev, 0)
+    batch = int(os.environ.get("BATCH", "8"))
+    tr, dm = bench.build_trainer(argparse.Namespace(arch="ViT-B/16", classes=1000), prec, batch, dev, 0)
     if mode == "novit":
         enc = tr.model.image_encoder
         with torch.no_grad():
