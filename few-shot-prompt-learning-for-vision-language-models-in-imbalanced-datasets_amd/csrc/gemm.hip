@@ -115,6 +115,15 @@ unsigned long long* gemm_stamp_for(int epi, int M) {
   if ((fe >= 0 && epi != fe) || M < fm) return nullptr;
   return gemm_stamp_buf();
 }
+// (knob CLIPK_GEMM_T96=0: the 128x128 deep ring instead, A/B)
+bool gemm_t96() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLIPK_GEMM_T96");
+    v = e ? atoi(e) : 1;
+  }
+  return v != 0;
+}
 static int g_num_cus = 0;
 int num_cus() {
   if (!g_num_cus) {

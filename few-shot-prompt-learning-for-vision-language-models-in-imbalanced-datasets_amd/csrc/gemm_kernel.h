@@ -1263,6 +1263,7 @@ __global__ __launch_bounds__(WM * WN * 64, DEPTH == 2 ? 2 : 1) void gemm_nt_kern
 int pick_cfg(int M, int N, int esz);   // tile configuration for a 16-bit GEMM shape
 int num_cus();
 bool deep_small();                      // 4-slot ring for grids of at most one tile per CU
+bool gemm_t96();                        // PREC fp32s: 96-row tiles for better-filled one-round grids
 int pp_grid(int nwg, int cus);          // ping-pong launches: blocks per grid
 unsigned long long* gemm_stamp_buf();   // CLIPK_GEMM_STAMP diagnostic buffer (or null)
 // the same, for this launch only when it passes CLIPK_GEMM_STAMP_EPI / CLIPK_GEMM_STAMP_MINM
@@ -1317,7 +1318,13 @@ static int launch_gemm_split(const GemmArgs& g, hipStream_t st) {
     }
   }
   const int nwg = ((g.M + 127) / 128) * (g.N / 128);
-  if (nwg <= cus && deep_small())
+  // 96-row tiles where they still fit one round of CUs and fill more of it (the batch-1 text
+  // encoder's N = 512 GEMMs at 5.9k rows: 188 -> 248 blocks on 256 CUs); knob CLIPK_GEMM_T96
+  const int nwg96 = ((g.M + 95) / 96) * (g.N / 128);
+  if (nwg < cus && nwg96 <= cus && nwg96 > nwg && deep_small() && gemm_t96())
+    hipLaunchKernelGGL((gemm_nt_kernel<TS, float, float, EPI, 96, 128, 2, 2, false, GEMM_ROWB, 4, false, false, LNM, SPF>), dim3(nwg96),
+                       dim3(256), 0, st, g);
+  else if (nwg <= cus && deep_small())
     hipLaunchKernelGGL((gemm_nt_kernel<TS, float, float, EPI, 128, 128, 2, 2, false, GEMM_ROWB, 4, false, false, LNM, SPF>), dim3(nwg),
                        dim3(256), 0, st, g);
   else

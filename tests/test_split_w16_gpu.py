@@ -334,3 +334,42 @@ def test_attention_prefix_bwd_split_copy(dev, G, C, P, H, max_q):
     w = _w16((W, 3 * W), g, 1 / math.sqrt(3 * W)).to(dev)
     wh = ops.split_hi16(ops.split_pack(w))
     assert torch.equal(ops.gemm(ds, wh, N.EPI_NONE | N.A_SPLIT), ops.gemm(d32, wh, N.EPI_NONE))
+
+
+_T96_PROBE = r"""
+import os, sys, math, torch
+sys.path.insert(0, os.environ["FSP_ROOT"])
+from fsp_amd import ops, _native as N
+dev = torch.device("cuda", 0)
+out = {}
+for M in (4600, 5895):
+    g = torch.Generator(device="cpu").manual_seed(M)
+    a = torch.randn(M, 2048, generator=g).to(dev)
+    b = (torch.randn(512, 2048, generator=g) / math.sqrt(2048)).half().float().to(dev)
+    bias = torch.randn(512, generator=g).to(dev)
+    res = torch.randn(M, 512, generator=g).to(dev)
+    bh = ops.split_hi16(ops.split_pack(b))
+    st = torch.empty(M, 8, 2, device=dev)
+    out[M] = [ops.gemm(a, bh, N.EPI_NONE).cpu(), ops.gemm(a, bh, N.EPI_BIAS_RES, bias=bias, res=res).cpu(),
+              ops.gemm_ln(a, bh, N.EPI_BIAS_RES, bias, stats=st, res=res).cpu(), st.cpu()]
+torch.save(out, sys.argv[1])
+"""
+
+
+def test_gemm_t96_bitwise_t128(tmp_path):
+    """The 96-row deep-ring tiles (batch-1 text N = 512 GEMMs: 188 -> 248 blocks) give the
+    128x128 tiles' outputs bit for bit (the same per-element K order): the same GEMMs in two
+    child processes, CLIPK_GEMM_T96 on and off (the knob is read once per process)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for t96 in ("1", "0"):
+        f = str(tmp_path / f"t96_{t96}.pt")
+        env = dict(os.environ, FSP_ROOT=root, CLIPK_GEMM_T96=t96)
+        p = subprocess.run([sys.executable, "-c", _T96_PROBE, f], env=env, capture_output=True, text=True, timeout=240)
+        assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+        res[t96] = torch.load(f, weights_only=True)
+    for M in (4600, 5895):
+        for i, (x, y) in enumerate(zip(res["1"][M], res["0"][M])):
+            assert torch.equal(x, y), f"M {M} output {i}: {int((x != y).sum())} differ"
